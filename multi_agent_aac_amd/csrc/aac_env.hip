@@ -1,0 +1,893 @@
+// aac_env.hip -- gfx950 kernels + C ABI for the one_model_att environment hot path.
+//
+// One thread per (env, agent); a 256-thread workgroup owns floor(256/N) whole envs, so every
+// neighbour interaction (radar vs other drones, tdCPA, collisions, team reward) stays inside the
+// workgroup and goes through LDS -- no inter-workgroup communication at all.  State is SoA double2
+// in HBM (16 B per lane, coalesced), observations are written as fp32.  No MFMA: this is byte- and
+// fp64-branch work bounded by HBM.
+//
+// Arithmetic contract (shared with oracle/aac_oracle.c, compiled -ffp-contract=off):
+//   np.linalg.norm([x,y]) = sqrt(fma(y,y,x*x)); np.dot = fma(a1,b1,a0*b0); GEOS distance has no FMA;
+//   np.sum over the N team rewards = numpy pairwise summation.
+// Reference: ATT/env:2627-2713 kinematics, :758-773 neighbours, :1051-1170 radar (drones),
+// OM/env:1049-1148 radar (obstacles), :1285-1469 observation, ATT/util:308-329 tdCPA,
+// ATT/env:2105-2618 ss_reward, ATT/main:448-462 termination, ATT/env:199-405 reset.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/aac_env.h"
+
+#define NRAY 18
+#define BLOCK 256
+#define MAX_MAP_BYTES 8192
+
+namespace {
+
+struct Tab {
+    double circ_c[64], circ_s[64];   // GEOS createCircle unit vectors, angle 0 - i*inc
+    double nrm_c[64], nrm_s[64];     // 64-gon edge normals, angle (k + 1/2) pi/32
+    double ray_c[NRAY], ray_s[NRAY]; // cos/sin(math.radians(20 r))
+    double apothem;                  // cos(pi/64)
+    double quantum;                  // GEOS filletAngleQuantum = pi/2/16
+};
+
+__constant__ Tab c_tab;
+
+constexpr double PI_GEOS = 3.14159265358979323846;
+
+struct Args {
+    int E, N, K, D0, W, radar_mode, compat, team_reward, episode_length, gw, gh, n_maps, epb;
+    double bound[4];
+    double gx0, gy0, xs, ys;
+    double dt, acc_max, vmax, pb, radar_len;
+    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp;
+    int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx;
+    uint8_t *reach;
+    const uint8_t *occ;  // n_maps * gw * gh
+    float *own, *radar, *nei, *reward;
+    uint8_t *done, *mask, *env_done, *bbc;
+    double *tcpa, *dcpa;
+    int32_t *conf_cur, *conf_pre;
+};
+
+struct ResetArgs {
+    int mode;                 // 0 explicit OD, 1 bank
+    const uint8_t *mask;      // env mask (explicit) or env_done (bank); NULL = all
+    const double2 *start;     // explicit [E][N]
+    const double2 *wps;       // explicit [E][N][W]
+    const int32_t *cnt;       // explicit [E][N]
+    const int32_t *map_idx;   // explicit [E] or NULL
+    const double2 *bank_start, *bank_wp;
+    const int32_t *bank_cnt;
+    int32_t bank_n;
+    uint64_t seed;
+    int32_t *episode;         // [E] per-env episode counter (bank mode)
+};
+
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ inline double npnorm(double x, double y) { return sqrt(__builtin_fma(y, y, x * x)); }
+__device__ inline double gdist(double ax, double ay, double bx, double by) {
+    double dx = ax - bx, dy = ay - by;
+    return sqrt(dx * dx + dy * dy);
+}
+
+// ------------------------------------------------------------------ GEOS-shape predicates
+__device__ inline void upd(double x, double y, double &mnx, double &mxx, double &mny, double &mxy) {
+    mnx = x < mnx ? x : mnx;
+    mxx = x > mxx ? x : mxx;
+    mny = y < mny ? y : mny;
+    mxy = y > mxy ? y : mxy;
+}
+
+__device__ void fillet_ext(double px, double py, double start, double end, double r, double &mnx, double &mxx,
+                           double &mny, double &mxy) {
+    double total = fabs(start - end);
+    int nseg = (int)(total / c_tab.quantum + 0.5);
+    double inc = total / nseg;
+    for (int i = 1; i < nseg; ++i) {  // i = 0 is redundant with the offset point (GEOS isRedundant)
+        double a = start + (double)(-1 * i) * inc;
+        upd(px + r * cos(a), py + r * sin(a), mnx, mxx, mny, mxy);
+    }
+}
+
+// LineString([p0,p1]).buffer(r) meets one of the 4 infinite bound lines (ATT/env:2507)
+__device__ bool bound_crash(const Args &A, double x0, double y0, double x1, double y1) {
+    const double r = A.pb;
+    const double *b = A.bound;
+    // every capsule vertex lies within r (1 + 1e-15) of p0 or p1: cheap exact pre-filter
+    const double m = r + 1e-6;
+    double lx = fmin(x0, x1), hx = fmax(x0, x1), ly = fmin(y0, y1), hy = fmax(y0, y1);
+    if (lx - m > b[0] && hx + m < b[1] && ly - m > b[2] && hy + m < b[3]) return false;
+    double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
+    if (x0 == x1 && y0 == y1) {
+        for (int i = 0; i < 64; ++i) upd(x0 + r * c_tab.circ_c[i], y0 + r * c_tab.circ_s[i], mnx, mxx, mny, mxy);
+    } else {
+        double dx = x1 - x0, dy = y1 - y0;
+        double len = sqrt(dx * dx + dy * dy);
+        double ux = 1 * r * dx / len, uy = 1 * r * dy / len;
+        upd(x1 - uy, y1 + ux, mnx, mxx, mny, mxy);
+        upd(x1 + uy, y1 - ux, mnx, mxx, mny, mxy);
+        upd(x0 + uy, y0 - ux, mnx, mxx, mny, mxy);
+        upd(x0 - uy, y0 + ux, mnx, mxx, mny, mxy);
+        double a1 = atan2(dy, dx);
+        fillet_ext(x1, y1, a1 + PI_GEOS / 2.0, a1 - PI_GEOS / 2.0, r, mnx, mxx, mny, mxy);
+        double a0 = atan2(y0 - y1, x0 - x1);
+        fillet_ext(x0, y0, a0 + PI_GEOS / 2.0, a0 - PI_GEOS / 2.0, r, mnx, mxx, mny, mxy);
+    }
+    return (mnx <= b[0] && b[0] <= mxx) || (mnx <= b[1] && b[1] <= mxx) || (mny <= b[2] && b[2] <= mxy) ||
+           (mny <= b[3] && b[3] <= mxy);
+}
+
+// 64-gon(pos, pB) meets 64-gon(goal, 1): Minkowski closed form (ATT/env:2266-2269)
+__device__ bool goal_reached(double px, double py, double gx, double gy, double pb) {
+    double dx = gx - px, dy = gy - py;
+    double thr = (pb + 1.0) * c_tab.apothem;
+    double m = -INFINITY;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) {
+        double v = dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k];
+        m = v > m ? v : m;
+    }
+    return m <= thr;
+}
+
+// 64-gon(pos, pB) meets the closed square cell (ATT/env:2243-2250): separating axes
+__device__ bool building_hit(double px, double py, double cx, double cy, double pb) {
+    double dx = cx - px, dy = cy - py;
+    if (fabs(dx) > 5.0 + pb || fabs(dy) > 5.0 + pb) return false;
+    for (int k = 0; k < 32; ++k) {
+        double proj = fabs(dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k]);
+        double lim = 5.0 * (fabs(c_tab.nrm_c[k]) + fabs(c_tab.nrm_s[k])) + pb * c_tab.apothem;
+        if (proj > lim) return false;
+    }
+    return true;
+}
+
+// Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p
+__device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
+                               double &tout) {
+    double ddx = ex - cx, ddy = ey - cy;
+    double tlo = 0.0, thi = 1.0;
+    double vx = px + r * c_tab.circ_c[0], vy = py + r * c_tab.circ_s[0];
+    for (int k = 0; k < 64; ++k) {
+        int k1 = (k + 1) & 63;
+        double wx = px + r * c_tab.circ_c[k1], wy = py + r * c_tab.circ_s[k1];
+        double exx = wx - vx, eyy = wy - vy;
+        double a = exx * (cy - vy) - eyy * (cx - vx);
+        double b = exx * ddy - eyy * ddx;
+        if (b == 0.0) {
+            if (a > 0.0) return false;
+        } else if (b < 0.0) {
+            double t = -a / b;
+            tlo = t > tlo ? t : tlo;
+        } else {
+            double t = -a / b;
+            thi = t < thi ? t : thi;
+        }
+        if (tlo > thi) return false;
+        vx = wx;
+        vy = wy;
+    }
+    tout = tlo;
+    return true;
+}
+
+__device__ bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1,
+                           double &dout) {
+    double ddx = ex - cx, ddy = ey - cy;
+    double tx0, tx1, ty0, ty1;
+    if (ddx == 0.0) {
+        if (cx < x0 || cx > x1) return false;
+        tx0 = -INFINITY;
+        tx1 = INFINITY;
+    } else {
+        double ta = (x0 - cx) / ddx, tb = (x1 - cx) / ddx;
+        if (ta < tb) { tx0 = ta; tx1 = tb; } else { tx0 = tb; tx1 = ta; }
+    }
+    if (ddy == 0.0) {
+        if (cy < y0 || cy > y1) return false;
+        ty0 = -INFINITY;
+        ty1 = INFINITY;
+    } else {
+        double ta = (y0 - cy) / ddy, tb = (y1 - cy) / ddy;
+        if (ta < tb) { ty0 = ta; ty1 = tb; } else { ty0 = tb; ty1 = ta; }
+    }
+    double tin = tx0 > ty0 ? tx0 : ty0;
+    double tout = tx1 < ty1 ? tx1 : ty1;
+    if (tin > tout || tout < 0.0 || tin > 1.0) return false;
+    double t = tin >= 0.0 ? tin : tout;
+    if (t > 1.0) return false;
+    dout = gdist(cx + t * ddx, cy + t * ddy, cx, cy);
+    return true;
+}
+
+__device__ bool ray_vline(double cx, double cy, double ex, double ey, double lx, double &dout) {
+    if (cx == lx && ex == lx) { dout = 0.0; return true; }
+    if ((cx - lx) * (ex - lx) > 0.0) return false;
+    double t = (lx - cx) / (ex - cx);
+    dout = gdist(lx, cy + t * (ey - cy), cx, cy);
+    return true;
+}
+
+__device__ bool ray_hline(double cx, double cy, double ex, double ey, double ly, double &dout) {
+    if (cy == ly && ey == ly) { dout = 0.0; return true; }
+    if ((cy - ly) * (ey - ly) > 0.0) return false;
+    double t = (ly - cy) / (ey - cy);
+    dout = gdist(cx + t * (ex - cx), ly, cx, cy);
+    return true;
+}
+
+__device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, double cy, double ex, double ey,
+                                  double len) {
+    double mind = len, d;
+    int i0 = (int)floor((cx - 20.0 - A.gx0) / 10.0), i1 = (int)ceil((cx + 20.0 - A.gx0) / 10.0);
+    int j0 = (int)floor((cy - 20.0 - A.gy0) / 10.0), j1 = (int)ceil((cy + 20.0 - A.gy0) / 10.0);
+    i0 = i0 < 0 ? 0 : i0;
+    j0 = j0 < 0 ? 0 : j0;
+    i1 = i1 > A.gw - 1 ? A.gw - 1 : i1;
+    j1 = j1 > A.gh - 1 ? A.gh - 1 : j1;
+    for (int i = i0; i <= i1; ++i)
+        for (int j = j0; j <= j1; ++j) {
+            if (!occ[i * A.gh + j]) continue;
+            double qx = A.gx0 + 10.0 * i, qy = A.gy0 + 10.0 * j;
+            if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
+        }
+    if (ray_vline(cx, cy, ex, ey, A.bound[0], d) && d < mind) mind = d;
+    if (ray_vline(cx, cy, ex, ey, A.bound[1], d) && d < mind) mind = d;
+    if (ray_hline(cx, cy, ex, ey, A.bound[2], d) && d < mind) mind = d;
+    if (ray_hline(cx, cy, ex, ey, A.bound[3], d) && d < mind) mind = d;
+    return mind;
+}
+
+__device__ void tdcpa(double ox, double oy, double hx, double hy, double ovx, double ovy, double hvx, double hvy,
+                      double pb, double &tcpa, double &dcpa, int &total) {
+    double rx = -1 * (ox - hx), ry = -1 * (oy - hy);
+    double wx = ovx - hvx, wy = ovy - hvy;
+    double nw = npnorm(wx, wy);
+    double sq = nw * nw;
+    double t, d;
+    if (sq == 0) {
+        t = -10;
+        double nnx = ox + ovx * 1, nny = oy + ovy * 1;
+        double nhx = hx + hvx * 1, nhy = hy + hvy * 1;
+        d = npnorm(nhx - nnx, nhy - nny);
+        if (d < pb + pb) total += 1;
+    } else {
+        t = __builtin_fma(ry, wy, rx * wx) / sq;
+        d = npnorm((rx * -1) + (wx * t), (ry * -1) + (wy * t));
+    }
+    if (t <= 1 && t >= 0 && d < pb + pb) total += 1;
+    tcpa = t;
+    dcpa = d;
+}
+
+__device__ double pairwise_sum(const double *a, int n) {
+    if (n < 8) {
+        double s = a[0];
+        for (int i = 1; i < n; ++i) s += a[i];
+        return s;
+    }
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+}
+
+// LDS image of one workgroup's envs
+struct Lds {
+    double2 pos[BLOCK], vel[BLOCK], ppos[BLOCK], pvel[BLOCK], goal[BLOCK];
+    double rew[BLOCK];
+    uint8_t flags[BLOCK];   // bit0 done, bit1 check_goal, bit2 reach (after step), bit3 bound, bit4 drone, bit5 last==nearest
+    int32_t idx[BLOCK];
+    uint8_t occ[MAX_MAP_BYTES];
+};
+
+// observation of agent i of env e (cur_state_norm_state_v3, ATT/env:837-1493)
+__device__ void observe(const Args &A, const Lds &S, int e, int i, int base, const uint8_t *occ) {
+    const int N = A.N, K = A.K;
+    const size_t ai = (size_t)e * N + i;
+    const double *b = A.bound;
+    const double pb = A.pb, vmax = A.vmax;
+    const double2 p = S.pos[base + i], v = S.vel[base + i];
+    const double px = p.x, py = p.y;
+    float *own = A.own + ai * A.D0;
+    double npx = -1 + (px - b[0]) * A.xs, npy = -1 + (py - b[2]) * A.ys;
+    const double2 g = S.goal[base + i];
+    double ngx = 2 * ((g.x - b[0]) / (b[1] - b[0])) - 1, ngy = 2 * ((g.y - b[2]) / (b[3] - b[2])) - 1;
+    own[0] = (float)npx;
+    own[1] = (float)npy;
+    own[2] = (float)(v.x / vmax);
+    own[3] = (float)(v.y / vmax);
+    own[4] = (float)(ngx - npx);
+    own[5] = (float)(ngy - npy);
+    const double dxm = b[0] - b[1], dxM = b[1] - b[0], dym = b[2] - b[3], dyM = b[3] - b[2];
+    int kk = 0, cc = 0, cp = 0;
+    const double2 hp = S.ppos[base + i], hv = S.pvel[base + i];
+    for (int j = 0; j < N; ++j) {
+        if (j == i) continue;
+        const double2 q = S.pos[base + j], w = S.vel[base + j];
+        double dx = q.x - px, dy = q.y - py;
+        if (A.compat) {
+            own[6 + 4 * kk] = (float)(-1 + (dx - b[0]) * A.xs);
+            own[7 + 4 * kk] = (float)(-1 + (dy - b[2]) * A.ys);
+        } else {
+            own[6 + 4 * kk] = (float)(A.xs * dx);
+            own[7 + 4 * kk] = (float)(A.ys * dy);
+        }
+        own[8 + 4 * kk] = (float)(w.x / vmax);
+        own[9 + 4 * kk] = (float)(w.y / vmax);
+        float *nb = A.nei + (ai * K + kk) * 6;
+        nb[0] = (float)(2 * ((dx - dxm) / (dxM - dxm)) - 1);
+        nb[1] = (float)(2 * ((dy - dym) / (dyM - dym)) - 1);
+        double g0, g1;
+        if (A.compat) {
+            g0 = w.y - q.x;
+            g1 = pb - q.y;
+        } else {
+            g0 = S.goal[base + j].x - q.x;
+            g1 = S.goal[base + j].y - q.y;
+        }
+        nb[2] = (float)(2 * ((g0 - dxm) / (dxM - dxm)) - 1);
+        nb[3] = (float)(2 * ((g1 - dym) / (dyM - dym)) - 1);
+        nb[4] = (float)(w.x / vmax);
+        nb[5] = (float)(w.y / vmax);
+        if (A.tcpa || A.conf_cur) {
+            double t, d, t2, d2;
+            tdcpa(q.x, q.y, px, py, w.x, w.y, v.x, v.y, pb, t, d, cc);
+            const double2 qp = S.ppos[base + j], wp = S.pvel[base + j];
+            tdcpa(qp.x, qp.y, hp.x, hp.y, wp.x, wp.y, hv.x, hv.y, pb, t2, d2, cp);
+            if (A.tcpa) {
+                A.tcpa[ai * K + kk] = t;
+                A.dcpa[ai * K + kk] = d;
+            }
+        }
+        ++kk;
+    }
+    if (A.conf_cur) {
+        A.conf_cur[ai] = cc;
+        A.conf_pre[ai] = cp;
+    }
+    // radar (18 rays from the centre, length radar_len)
+    float *rad = A.radar + ai * NRAY;
+    const double reach2 = (pb + 1e-6) * (pb + 1e-6);
+    for (int r = 0; r < NRAY; ++r) {
+        double ex = px + A.radar_len * c_tab.ray_c[r], ey = py + A.radar_len * c_tab.ray_s[r];
+        double len = gdist(ex, ey, px, py);
+        double dd = len, dob = len;
+        if (A.radar_mode != AAC_RADAR_OBSTACLES) {
+            double shortest = INFINITY;
+            double ddx = ex - px, ddy = ey - py;
+            double inv = 1.0 / (ddx * ddx + ddy * ddy);
+            for (int j = 0; j < N; ++j) {
+                if (j == i) continue;
+                const double2 q = S.pos[base + j];
+                // exact pre-filter: the 64-gon lies inside the circle of radius pb (+1e-15)
+                double wx = q.x - px, wy = q.y - py;
+                double tt = (wx * ddx + wy * ddy) * inv;
+                tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
+                double qx = tt * ddx - wx, qy = tt * ddy - wy;
+                if (qx * qx + qy * qy > reach2) continue;
+                double t;
+                if (!ray_poly_entry(px, py, ex, ey, q.x, q.y, pb, t)) continue;
+                double ix = px + t * (ex - px), iy = py + t * (ey - py);
+                double d = gdist(ix, iy, px, py);
+                if (d < shortest) {
+                    shortest = d;
+                    dd = d;
+                }
+            }
+        }
+        if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, px, py, ex, ey, len);
+        double val = A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
+        rad[r] = (float)val;
+    }
+}
+
+__device__ inline void load_maps(const Args &A, Lds &S) {
+    const int bytes = A.n_maps * A.gw * A.gh;
+    for (int k = threadIdx.x; k < bytes; k += BLOCK) S.occ[k] = A.occ[k];
+}
+
+// --------------------------------------------------------------------------------- step
+__global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__restrict__ act) {
+    __shared__ Lds S;
+    const int N = A.N;
+    const int le = threadIdx.x / N, i = threadIdx.x - le * N;
+    const int e = blockIdx.x * A.epb + le;
+    const bool active = (le < A.epb) && (e < A.E);
+    const int base = le * N;
+    const size_t ai = (size_t)e * N + i;
+    load_maps(A, S);
+
+    // ---- a1: kinematics (ATT/env:2639-2713)
+    double2 np = make_double2(0.0, 0.0), nv = np, pp = np, pv = np;
+    if (active) {
+        pp = A.pos[ai];
+        pv = A.vel[ai];
+        float2 a = act[ai];
+        double ax = (double)a.x * A.acc_max, ay = (double)a.y * A.acc_max;
+        double cvx = pv.x + ax * A.dt, cvy = pv.y + ay * A.dt;
+        if (npnorm(cvx, cvy) >= A.vmax) {
+            double h = atan2(cvy, cvx);
+            nv = make_double2(A.vmax * cos(h), A.vmax * sin(h));
+        } else {
+            nv = make_double2(cvx, cvy);
+        }
+        np = make_double2(pp.x + nv.x * A.dt, pp.y + nv.y * A.dt);
+        A.pre_pos[ai] = pp;
+        A.pre_vel[ai] = pv;
+        A.pos[ai] = np;
+        A.vel[ai] = nv;
+        S.pos[threadIdx.x] = np;
+        S.vel[threadIdx.x] = nv;
+        S.ppos[threadIdx.x] = pp;
+        S.pvel[threadIdx.x] = pv;
+        S.goal[threadIdx.x] = A.goal[ai];
+    }
+    __syncthreads();
+    if (active) {
+        const uint8_t *occ = S.occ + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
+        observe(A, S, e, i, base, occ);
+
+        // ---- ss_reward (ATT/env:2133-2603)
+        const double px = np.x, py = np.y, pb = A.pb;
+        int ncoll = 0, last_coll = -1, nearest = -1;
+        double shortest = INFINITY;
+        for (int j = 0; j < N; ++j) {
+            if (j == i) continue;
+            const double2 q = S.pos[base + j];
+            double d = npnorm(px - q.x, py - q.y);
+            if (d < shortest) {
+                shortest = d;
+                nearest = j;
+            }
+            if (d <= pb * 2) {
+                ++ncoll;
+                last_coll = j;
+            }
+        }
+        const double c_drone = 1 + (2.5 / (10 - 2.5)), m_drone = (0 - 1) / (10 - 2.5);
+        double pen = 0;
+        for (int j = 0; j < N; ++j) {
+            if (j == i) continue;
+            const double2 q = S.pos[base + j];
+            double d = npnorm(px - q.x, py - q.y);
+            if (d >= 2.5 && d <= 10) pen = pen + (1 * (m_drone * shortest + c_drone));
+            else pen = pen + 0;
+        }
+        int building = 0;
+        {
+            int ci = (int)floor((px - A.gx0) / 10.0 + 0.5), cj = (int)floor((py - A.gy0) / 10.0 + 0.5);
+            for (int ii = ci - 1; ii <= ci + 1 && !building; ++ii)
+                for (int jj = cj - 1; jj <= cj + 1; ++jj) {
+                    if (ii < 0 || jj < 0 || ii >= A.gw || jj >= A.gh) continue;
+                    if (!occ[ii * A.gh + jj]) continue;
+                    if (building_hit(px, py, A.gx0 + 10.0 * ii, A.gy0 + 10.0 * jj, pb)) {
+                        building = 1;
+                        break;
+                    }
+                }
+        }
+        if (building) A.wall[ai] += 1;
+        const double2 g = S.goal[threadIdx.x];
+        const int goal = goal_reached(px, py, g.x, g.y, pb);
+        const int cur = A.wp_cur[ai];
+        const double2 w0 = A.wp[(size_t)ai * A.W + cur];
+        const int wpf = gdist(px, py, w0.x, w0.y) < 5;
+        double before = npnorm(pp.x - g.x, pp.y - g.y);
+        double after = npnorm(px - g.x, py - g.y);
+        double dtg = (1 * (before - after)) / A.vmax;
+        const int bnd = bound_crash(A, pp.x, pp.y, px, py);
+        uint8_t m = (uint8_t)(bnd | ((ncoll > 0) << 1) | (goal << 2) | (building << 3) | (wpf << 4));
+        int done = 0, cg = 0;
+        uint8_t fl = 0;
+        double r;
+        uint8_t reach = A.reach[ai];
+        if (bnd) {
+            r = ((0.0 - 20) - 0.0) - 0;
+            done = 1;
+            fl |= 8;
+        } else if (ncoll > 0) {
+            r = ((0.0 - 20) - 0.0) - pen;
+            done = 1;
+            fl |= 16;
+            if (last_coll == nearest) fl |= 32;
+        } else if (goal) {
+            r = (0.0 + 20) + 0.0;
+            cg = 1;
+            reach = 1;
+            A.reach[ai] = 1;
+        } else {
+            if (wpf && A.wp_cnt[ai] - cur > 1) A.wp_cur[ai] = cur + 1;
+            r = dtg - pen;
+        }
+        if (cg) m |= 32;
+        fl |= (uint8_t)(done | (cg << 1) | (reach << 2));
+        S.rew[threadIdx.x] = r;
+        S.flags[threadIdx.x] = fl;
+        A.done[ai] = (uint8_t)done;
+        A.mask[ai] = m;
+    }
+    __syncthreads();
+    if (active) {
+        double team = A.team_reward ? pairwise_sum(&S.rew[base], N) : S.rew[threadIdx.x];
+        A.reward[ai] = (float)team;
+        if (i == 0) {
+            int any_done = 0, all_goal = 1, all_reach = 1, b0 = 0, b2 = 0, b3 = 0;
+            for (int j = 0; j < N; ++j) {
+                uint8_t f = S.flags[base + j];
+                any_done |= f & 1;
+                all_goal &= (f >> 1) & 1;
+                all_reach &= (f >> 2) & 1;
+                b0 |= (f >> 3) & 1;
+                b2 |= (f >> 4) & 1;
+                b3 |= (f >> 5) & 1;
+            }
+            A.bbc[4 * e + 0] = (uint8_t)b0;
+            A.bbc[4 * e + 1] = 0;
+            A.bbc[4 * e + 2] = (uint8_t)b2;
+            A.bbc[4 * e + 3] = (uint8_t)b3;
+            int st = A.step[e] + 1;
+            A.step[e] = st;
+            A.env_done[e] = (uint8_t)((A.episode_length < st) || any_done || all_goal || all_reach);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------- reset / auto-reset
+__global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
+    __shared__ Lds S;
+    const int N = A.N;
+    const int le = threadIdx.x / N, i = threadIdx.x - le * N;
+    const int e = blockIdx.x * A.epb + le;
+    const bool in_range = (le < A.epb) && (e < A.E);
+    const bool active = in_range && (R.mask == nullptr || R.mask[e] != 0);
+    const int base = le * N;
+    const size_t ai = (size_t)e * N + i;
+    load_maps(A, S);
+    if (R.mode == 1 && active && i == 0) {
+        // draw N OD entries; starts pairwise > 2 pB apart (ATT/env:258-268)
+        int ep = R.episode[e] + 1;
+        R.episode[e] = ep;
+        for (int a = 0; a < N; ++a) {
+            int idx = 0;
+            for (int att = 0; att < 4096; ++att) {
+                uint64_t key = mix64(mix64(mix64(R.seed ^ (uint64_t)e) ^ (uint64_t)ep) ^ ((uint64_t)a * 65536ull + att));
+                idx = (int)(key % (uint64_t)R.bank_n);
+                double2 s = R.bank_start[idx];
+                bool ok = true;
+                for (int b = 0; b < a; ++b) {
+                    double2 o = R.bank_start[S.idx[base + b]];
+                    if (!(npnorm(s.x - o.x, s.y - o.y) > A.pb * 2)) { ok = false; break; }
+                }
+                if (ok) break;
+            }
+            S.idx[base + a] = idx;
+        }
+    }
+    __syncthreads();
+    if (active) {
+        double2 st;
+        int cnt;
+        if (R.mode == 1) {
+            int idx = S.idx[base + i];
+            st = R.bank_start[idx];
+            cnt = R.bank_cnt[idx];
+            for (int k = 0; k < A.W; ++k) A.wp[ai * A.W + k] = R.bank_wp[(size_t)idx * A.W + k];
+            A.goal[ai] = R.bank_wp[(size_t)idx * A.W + cnt - 1];
+        } else {
+            st = R.start[ai];
+            cnt = R.cnt[ai];
+            for (int k = 0; k < A.W; ++k) A.wp[ai * A.W + k] = R.wps[ai * A.W + k];
+            A.goal[ai] = R.wps[ai * A.W + cnt - 1];
+            if (i == 0 && A.map_idx) A.map_idx[e] = R.map_idx ? R.map_idx[e] : 0;
+        }
+        const double2 z = make_double2(0.0, 0.0);
+        A.pos[ai] = st;
+        A.pre_pos[ai] = st;
+        A.vel[ai] = z;
+        A.pre_vel[ai] = z;
+        A.wp_cnt[ai] = cnt;
+        A.wp_cur[ai] = 0;
+        A.reach[ai] = 0;
+        A.wall[ai] = 0;
+        if (i == 0) A.step[e] = 0;
+        S.pos[threadIdx.x] = st;
+        S.ppos[threadIdx.x] = st;
+        S.vel[threadIdx.x] = z;
+        S.pvel[threadIdx.x] = z;
+        S.goal[threadIdx.x] = A.goal[ai];
+    }
+    __syncthreads();
+    if (active) {
+        int mi = A.map_idx ? A.map_idx[e] : 0;
+        if (R.mode == 0 && R.map_idx) mi = R.map_idx[e];
+        observe(A, S, e, i, base, S.occ + mi * A.gw * A.gh);
+    }
+}
+
+// ------------------------------------------------------------------------------ host side
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                           \
+    do {                                                                                                    \
+        hipError_t _e = (x);                                                                                \
+        if (_e != hipSuccess) return fail(AAC_E_HIP, std::string(#x) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+}  // namespace
+
+struct aac_env {
+    aac_env_cfg cfg;
+    int device;
+    int K, D0, W, epb, blocks;
+    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp;
+    int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx, *episode;
+    uint8_t *reach, *occ;
+    double2 *bank_start, *bank_wp;
+    int32_t *bank_cnt;
+    int32_t bank_n;
+    uint64_t bank_seed;
+};
+
+static void fill_tables(Tab &t) {
+    const double quantum = PI_GEOS / 2.0 / 16;
+    const double total = std::fabs(0.0 - 2.0 * PI_GEOS);
+    const int nseg = (int)(total / quantum + 0.5);
+    const double inc = total / nseg;
+    for (int i = 0; i < 64; ++i) {
+        double a = 0.0 + (double)(-1 * i) * inc;
+        t.circ_c[i] = std::cos(a);
+        t.circ_s[i] = std::sin(a);
+        t.nrm_c[i] = std::cos((i + 0.5) * PI_GEOS / 32.0);
+        t.nrm_s[i] = std::sin((i + 0.5) * PI_GEOS / 32.0);
+    }
+    for (int r = 0; r < NRAY; ++r) {
+        double rad = (double)(20 * r) * (PI_GEOS / 180.0);
+        t.ray_c[r] = std::cos(rad);
+        t.ray_s[r] = std::sin(rad);
+    }
+    t.apothem = std::cos(PI_GEOS / 64.0);
+    t.quantum = quantum;
+}
+
+static Args make_args(const aac_env *h, const aac_step_out *o) {
+    Args A;
+    const aac_env_cfg &c = h->cfg;
+    A.E = c.E;
+    A.N = c.N;
+    A.K = h->K;
+    A.D0 = h->D0;
+    A.W = h->W;
+    A.radar_mode = c.radar_mode;
+    A.compat = c.compat;
+    A.team_reward = c.team_reward;
+    A.episode_length = c.episode_length;
+    A.gw = c.grid_w;
+    A.gh = c.grid_h;
+    A.n_maps = c.n_maps;
+    A.epb = h->epb;
+    for (int k = 0; k < 4; ++k) A.bound[k] = c.bound[k];
+    A.gx0 = std::ceil(c.bound[0] / c.cell) * c.cell;
+    A.gy0 = std::ceil(c.bound[2] / c.cell) * c.cell;
+    A.xs = (1.0 - (-1.0)) / (c.bound[1] - c.bound[0]);
+    A.ys = (1.0 - (-1.0)) / (c.bound[3] - c.bound[2]);
+    A.dt = c.dt;
+    A.acc_max = c.acc_max;
+    A.vmax = c.vmax;
+    A.pb = c.pB;
+    A.radar_len = c.radar_len;
+    A.pos = h->pos;
+    A.vel = h->vel;
+    A.pre_pos = h->pre_pos;
+    A.pre_vel = h->pre_vel;
+    A.goal = h->goal;
+    A.wp = h->wp;
+    A.wp_cur = h->wp_cur;
+    A.wp_cnt = h->wp_cnt;
+    A.wall = h->wall;
+    A.step = h->step;
+    A.map_idx = h->map_idx;
+    A.reach = h->reach;
+    A.occ = h->occ;
+    A.own = o->own;
+    A.radar = o->radar;
+    A.nei = o->nei;
+    A.reward = o->reward;
+    A.done = o->done;
+    A.mask = o->mask;
+    A.env_done = o->env_done;
+    A.bbc = o->bbc;
+    A.tcpa = o->tcpa;
+    A.dcpa = o->dcpa;
+    A.conf_cur = o->conf_cur;
+    A.conf_pre = o->conf_pre;
+    return A;
+}
+
+extern "C" {
+
+const char *aac_last_error(void) { return g_err.c_str(); }
+
+int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
+    if (!cfg || !out) return fail(AAC_E_INVALID, "null argument");
+    const aac_env_cfg &c = *cfg;
+    if (c.E <= 0 || c.N < 2 || c.N > BLOCK) return fail(AAC_E_INVALID, "need E > 0 and 2 <= N <= 256");
+    if (c.R != NRAY) return fail(AAC_E_INVALID, "R must be 18 (range(0, 360, 20))");
+    if (c.radar_mode < 0 || c.radar_mode > 2) return fail(AAC_E_INVALID, "bad radar_mode");
+    if (c.max_wp < 1) return fail(AAC_E_INVALID, "max_wp must be >= 1");
+    if (c.n_maps < 1 || !c.occ || c.grid_w < 1 || c.grid_h < 1) return fail(AAC_E_INVALID, "bad occupancy maps");
+    if ((size_t)c.n_maps * c.grid_w * c.grid_h > MAX_MAP_BYTES) return fail(AAC_E_INVALID, "maps exceed LDS budget");
+    if (c.cell != 10.0) return fail(AAC_E_INVALID, "cell must be 10 m (grid geometry of ATT/grid:138)");
+    HIPCHK(hipSetDevice(device));
+    aac_env *h = new aac_env();
+    std::memset(h, 0, sizeof(*h));
+    h->cfg = c;
+    h->cfg.occ = nullptr;
+    h->device = device;
+    h->K = c.N - 1;
+    h->D0 = 6 + 4 * h->K;
+    h->W = c.max_wp;
+    h->epb = BLOCK / c.N;
+    h->blocks = (c.E + h->epb - 1) / h->epb;
+    const size_t EN = (size_t)c.E * c.N;
+    hipError_t st = hipSuccess;
+#define ALLOC(p, n)                                                       \
+    if (st == hipSuccess) st = hipMalloc((void **)&h->p, (n) * sizeof(*h->p)); \
+    if (st == hipSuccess) st = hipMemset(h->p, 0, (n) * sizeof(*h->p));
+    ALLOC(pos, EN) ALLOC(vel, EN) ALLOC(pre_pos, EN) ALLOC(pre_vel, EN) ALLOC(goal, EN)
+    ALLOC(wp, EN * h->W) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
+    ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
+    ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
+#undef ALLOC
+    if (st == hipSuccess) st = hipMemcpy(h->occ, c.occ, (size_t)c.n_maps * c.grid_w * c.grid_h, hipMemcpyHostToDevice);
+    if (st == hipSuccess) {
+        Tab t;
+        fill_tables(t);
+        st = hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &t, sizeof(Tab));
+    }
+    if (st != hipSuccess) {
+        aac_env_destroy(h);
+        return fail(AAC_E_HIP, std::string("aac_env_create: ") + hipGetErrorString(st));
+    }
+    *out = h;
+    return AAC_OK;
+}
+
+void aac_env_destroy(aac_env *h) {
+    if (!h) return;
+    void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->wp, h->wp_cur, h->wp_cnt, h->wall,
+                    h->reach, h->step, h->map_idx, h->episode, h->occ, h->bank_start, h->bank_wp, h->bank_cnt};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    delete h;
+}
+
+static int check_out(const aac_step_out *o) {
+    if (!o || !o->own || !o->radar || !o->nei) return fail(AAC_E_INVALID, "observation outputs required");
+    if ((o->tcpa == nullptr) != (o->dcpa == nullptr)) return fail(AAC_E_INVALID, "tcpa/dcpa must be both set");
+    if ((o->conf_cur == nullptr) != (o->conf_pre == nullptr)) return fail(AAC_E_INVALID, "conf_cur/pre both");
+    return AAC_OK;
+}
+
+int aac_env_step(aac_env *h, const float *actions, const aac_step_out *o, void *stream) {
+    if (!h || !actions) return fail(AAC_E_INVALID, "null argument");
+    int rc = check_out(o);
+    if (rc) return rc;
+    if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return fail(AAC_E_INVALID, "step outputs");
+    Args A = make_args(h, o);
+    hipLaunchKernelGGL(step_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A,
+                       reinterpret_cast<const float2 *>(actions));
+    HIPCHK(hipGetLastError());
+    return AAC_OK;
+}
+
+int aac_env_reset(aac_env *h, const uint8_t *mask, const double *start, const double *wps, const int32_t *cnt,
+                  const int32_t *map_idx, const aac_step_out *o, void *stream) {
+    if (!h || !start || !wps || !cnt) return fail(AAC_E_INVALID, "null argument");
+    int rc = check_out(o);
+    if (rc) return rc;
+    Args A = make_args(h, o);
+    ResetArgs R{};
+    R.mode = 0;
+    R.mask = mask;
+    R.start = reinterpret_cast<const double2 *>(start);
+    R.wps = reinterpret_cast<const double2 *>(wps);
+    R.cnt = cnt;
+    R.map_idx = map_idx;
+    R.episode = h->episode;
+    hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A, R);
+    HIPCHK(hipGetLastError());
+    return AAC_OK;
+}
+
+int aac_env_set_od_bank(aac_env *h, const double *start, const double *wps, const int32_t *cnt, int32_t n,
+                        uint64_t seed) {
+    if (!h || !start || !wps || !cnt || n <= 0) return fail(AAC_E_INVALID, "bad OD bank");
+    for (int32_t k = 0; k < n; ++k)
+        if (cnt[k] < 1 || cnt[k] > h->W) return fail(AAC_E_INVALID, "OD bank waypoint count out of [1, W]");
+    HIPCHK(hipSetDevice(h->device));
+    if (h->bank_start) { (void)hipFree(h->bank_start); (void)hipFree(h->bank_wp); (void)hipFree(h->bank_cnt); }
+    h->bank_start = nullptr; h->bank_wp = nullptr; h->bank_cnt = nullptr;
+    HIPCHK(hipMalloc((void **)&h->bank_start, sizeof(double2) * n));
+    HIPCHK(hipMalloc((void **)&h->bank_wp, sizeof(double2) * (size_t)n * h->W));
+    HIPCHK(hipMalloc((void **)&h->bank_cnt, sizeof(int32_t) * n));
+    HIPCHK(hipMemcpy(h->bank_start, start, sizeof(double2) * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->bank_wp, wps, sizeof(double2) * (size_t)n * h->W, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->bank_cnt, cnt, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+    h->bank_n = n;
+    h->bank_seed = seed;
+    return AAC_OK;
+}
+
+int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *o, void *stream) {
+    if (!h) return fail(AAC_E_INVALID, "null handle");
+    if (!h->bank_n) return fail(AAC_E_STATE, "no OD bank installed (aac_env_set_od_bank)");
+    int rc = check_out(o);
+    if (rc) return rc;
+    Args A = make_args(h, o);
+    ResetArgs R{};
+    R.mode = 1;
+    R.mask = env_done;
+    R.bank_start = h->bank_start;
+    R.bank_wp = h->bank_wp;
+    R.bank_cnt = h->bank_cnt;
+    R.bank_n = h->bank_n;
+    R.seed = h->bank_seed;
+    R.episode = h->episode;
+    hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A, R);
+    HIPCHK(hipGetLastError());
+    return AAC_OK;
+}
+
+#define CPY(dst, src, n)                                                                                  \
+    if (dst && src) HIPCHK(hipMemcpyAsync((void *)(dst), (const void *)(src), (n), hipMemcpyDeviceToDevice, \
+                                          (hipStream_t)stream));
+
+int aac_env_get_state(aac_env *h, double *pos, double *vel, double *pre_pos, double *pre_vel, double *goal, double *wp,
+                      int32_t *wp_cur, int32_t *wp_cnt, uint8_t *reach, int32_t *wall, int32_t *step,
+                      int32_t *map_idx, void *stream) {
+    if (!h) return fail(AAC_E_INVALID, "null handle");
+    const size_t EN = (size_t)h->cfg.E * h->cfg.N, E = h->cfg.E;
+    CPY(pos, h->pos, EN * 16) CPY(vel, h->vel, EN * 16) CPY(pre_pos, h->pre_pos, EN * 16)
+    CPY(pre_vel, h->pre_vel, EN * 16) CPY(goal, h->goal, EN * 16) CPY(wp, h->wp, EN * h->W * 16)
+    CPY(wp_cur, h->wp_cur, EN * 4) CPY(wp_cnt, h->wp_cnt, EN * 4) CPY(reach, h->reach, EN)
+    CPY(wall, h->wall, EN * 4) CPY(step, h->step, E * 4) CPY(map_idx, h->map_idx, E * 4)
+    return AAC_OK;
+}
+
+int aac_env_set_state(aac_env *h, const double *pos, const double *vel, const double *pre_pos, const double *pre_vel,
+                      const double *goal, const double *wp, const int32_t *wp_cur, const int32_t *wp_cnt,
+                      const uint8_t *reach, const int32_t *wall, const int32_t *step, const int32_t *map_idx,
+                      void *stream) {
+    if (!h) return fail(AAC_E_INVALID, "null handle");
+    const size_t EN = (size_t)h->cfg.E * h->cfg.N, E = h->cfg.E;
+    CPY(h->pos, pos, EN * 16) CPY(h->vel, vel, EN * 16) CPY(h->pre_pos, pre_pos, EN * 16)
+    CPY(h->pre_vel, pre_vel, EN * 16) CPY(h->goal, goal, EN * 16) CPY(h->wp, wp, EN * h->W * 16)
+    CPY(h->wp_cur, wp_cur, EN * 4) CPY(h->wp_cnt, wp_cnt, EN * 4) CPY(h->reach, reach, EN)
+    CPY(h->wall, wall, EN * 4) CPY(h->step, step, E * 4) CPY(h->map_idx, map_idx, E * 4)
+    return AAC_OK;
+}
+#undef CPY
+
+}  // extern "C"

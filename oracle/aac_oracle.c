@@ -1,0 +1,508 @@
+/* aac_oracle.c -- batched CPU restatement of the one_model_att environment step.
+ *
+ * TEST INFRASTRUCTURE ONLY: built by oracle/Makefile into oracle/_build/libaac_oracle.so and
+ * loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker or
+ * the timed CPU baseline.  Never linked into the product.
+ *
+ * It is the same algorithm as oracle/env_ref.py (which follows the reference line by line) and
+ * is tested bit-identical to it; it exists because env_ref is per-agent Python and too slow to
+ * check the GPU at full sizes.  Arithmetic contract (compile with -ffp-contract=off -O2):
+ *   np.linalg.norm([x, y])  == sqrt(fma(y, y, x*x))   (cblas_ddot FMA tail; verified on numpy 2.2)
+ *   np.dot(a, b)            == fma(a1, b1, a0*b0)
+ *   GEOS Coordinate distance == sqrt(dx*dx + dy*dy)   (no FMA)
+ *   np.sum over N agents    == numpy pairwise_sum (sequential below 8, 8 accumulators above)
+ * Reference lines: ATT/env:2627-2713 (kinematics), :758-773 (neighbours), :1051-1170 + OM/env:
+ * 1049-1148 (radar), :1285-1469 (obs), ATT/util:308-329 (tdCPA), ATT/env:2105-2618 (ss_reward),
+ * ATT/main:448-462 (termination).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PI_GEOS 3.14159265358979323846
+#define NRAY 18
+
+typedef struct {
+    int32_t E, N, W;            /* envs, agents, waypoint capacity */
+    int32_t radar_mode;         /* 0 drones, 1 obstacles, 2 combined */
+    int32_t compat;             /* 1: bug-compatible observation quirks */
+    int32_t team_reward;        /* 1: full_observable_critic_flag team sum (ATT/env:2602-2603) */
+    int32_t episode_length;
+    int32_t gw, gh;             /* occupancy grid (x-major [i*gh + j]) */
+    double bound[4];
+    const uint8_t *occ;
+} oc_cfg;
+
+typedef struct {
+    double *pos, *vel, *pre_pos, *pre_vel;   /* E*N*2 */
+    double *goal;                            /* E*N*2 : goal[-1] */
+    double *wp;                              /* E*N*W*2 */
+    int32_t *wp_cur, *wp_cnt;                /* E*N */
+    uint8_t *reach;                          /* E*N reach_target latch */
+    int32_t *wall;                           /* E*N collide_wall_count */
+    int32_t *step;                           /* E */
+} oc_state;
+
+typedef struct {
+    float *own, *radar, *nei, *reward;       /* E*N*D0, E*N*18, E*N*K*6, E*N */
+    uint8_t *done, *mask, *env_done, *bbc;   /* E*N, E*N, E, E*4 */
+    double *tcpa, *dcpa;                     /* optional E*N*K (current state) */
+    int32_t *conf_cur, *conf_pre;            /* optional E*N */
+} oc_out;
+
+/* ------------------------------------------------------------------ tables */
+static double circ_c[64], circ_s[64], nrm_c[64], nrm_s[64], ray_c[NRAY], ray_s[NRAY];
+static double apothem;
+static int tables_ready = 0;
+
+static void init_tables(void) {
+    if (tables_ready) return;
+    double quantum = PI_GEOS / 2.0 / 16;
+    double total = fabs(0.0 - 2.0 * PI_GEOS);
+    int nseg = (int)(total / quantum + 0.5);
+    double inc = total / nseg;
+    for (int i = 0; i < 64; ++i) {
+        double a = 0.0 + (double)(-1 * i) * inc;
+        circ_c[i] = cos(a);
+        circ_s[i] = sin(a);
+        nrm_c[i] = cos((i + 0.5) * PI_GEOS / 32.0);
+        nrm_s[i] = sin((i + 0.5) * PI_GEOS / 32.0);
+    }
+    for (int r = 0; r < NRAY; ++r) {
+        double rad = (double)(20 * r) * (PI_GEOS / 180.0);   /* math.radians */
+        ray_c[r] = cos(rad);
+        ray_s[r] = sin(rad);
+    }
+    apothem = cos(PI_GEOS / 64.0);
+    tables_ready = 1;
+}
+
+static inline double npnorm(double x, double y) { return sqrt(fma(y, y, x * x)); }
+static inline double gdist(double ax, double ay, double bx, double by) {
+    double dx = ax - bx, dy = ay - by;
+    return sqrt(dx * dx + dy * dy);
+}
+
+/* ----------------------------------------------------------- GEOS shapes */
+/* min/max over the vertices of LineString([p0,p1]).buffer(r) (see oracle/geos.py) */
+static void fillet_ext(double px, double py, double start, double end, double r, int skip_first,
+                       double *mnx, double *mxx, double *mny, double *mxy) {
+    double quantum = PI_GEOS / 2.0 / 16;
+    double total = fabs(start - end);
+    int nseg = (int)(total / quantum + 0.5);
+    double inc = total / nseg;
+    for (int i = skip_first; i < nseg; ++i) {
+        double a = start + (double)(-1 * i) * inc;
+        double x = px + r * cos(a), y = py + r * sin(a);
+        if (x < *mnx) *mnx = x;
+        if (x > *mxx) *mxx = x;
+        if (y < *mny) *mny = y;
+        if (y > *mxy) *mxy = y;
+    }
+}
+
+static void upd(double x, double y, double *mnx, double *mxx, double *mny, double *mxy) {
+    if (x < *mnx) *mnx = x;
+    if (x > *mxx) *mxx = x;
+    if (y < *mny) *mny = y;
+    if (y > *mxy) *mxy = y;
+}
+
+static int bound_crash(double x0, double y0, double x1, double y1, double r, const double *b) {
+    double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
+    if (x0 == x1 && y0 == y1) {
+        for (int i = 0; i < 64; ++i) upd(x0 + r * circ_c[i], y0 + r * circ_s[i], &mnx, &mxx, &mny, &mxy);
+        /* vertex 0 is (x + r, y) exactly; circ_c[0] == 1, circ_s[0] == 0 give the same */
+    } else {
+        double dx = x1 - x0, dy = y1 - y0;
+        double len = sqrt(dx * dx + dy * dy);
+        double ux = 1 * r * dx / len, uy = 1 * r * dy / len;
+        /* left offset (p0 - uy, p0 + ux) (p1 - uy, p1 + ux); right = negated u */
+        upd(x1 - uy, y1 + ux, &mnx, &mxx, &mny, &mxy);      /* L.p1 */
+        upd(x1 + uy, y1 - ux, &mnx, &mxx, &mny, &mxy);      /* R.p1 */
+        upd(x0 + uy, y0 - ux, &mnx, &mxx, &mny, &mxy);      /* R.p0 */
+        upd(x0 - uy, y0 + ux, &mnx, &mxx, &mny, &mxy);      /* L.p0 */
+        double a1 = atan2(dy, dx);
+        fillet_ext(x1, y1, a1 + PI_GEOS / 2.0, a1 - PI_GEOS / 2.0, r, 1, &mnx, &mxx, &mny, &mxy);
+        double a0 = atan2(y0 - y1, x0 - x1);
+        fillet_ext(x0, y0, a0 + PI_GEOS / 2.0, a0 - PI_GEOS / 2.0, r, 1, &mnx, &mxx, &mny, &mxy);
+    }
+    return (mnx <= b[0] && b[0] <= mxx) || (mnx <= b[1] && b[1] <= mxx) ||
+           (mny <= b[2] && b[2] <= mxy) || (mny <= b[3] && b[3] <= mxy);
+}
+
+static int goal_reached(double px, double py, double gx, double gy, double pb) {
+    double dx = gx - px, dy = gy - py;
+    double thr = (pb + 1.0) * apothem;
+    double m = -INFINITY;
+    for (int k = 0; k < 64; ++k) {
+        double v = dx * nrm_c[k] + dy * nrm_s[k];
+        if (v > m) m = v;
+    }
+    return m <= thr;
+}
+
+static int building_hit(double px, double py, double cx, double cy, double pb) {
+    double dx = cx - px, dy = cy - py;
+    if (fabs(dx) > 5.0 + pb || fabs(dy) > 5.0 + pb) return 0;
+    for (int k = 0; k < 32; ++k) {
+        double proj = fabs(dx * nrm_c[k] + dy * nrm_s[k]);
+        double lim = 5.0 * (fabs(nrm_c[k]) + fabs(nrm_s[k])) + pb * apothem;
+        if (proj > lim) return 0;
+    }
+    return 1;
+}
+
+/* Cyrus-Beck entry of segment c->e into the clockwise 64-gon of circumradius r at (px,py) */
+static int ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r, double *tout) {
+    double ddx = ex - cx, ddy = ey - cy;
+    double tlo = 0.0, thi = 1.0;
+    for (int k = 0; k < 64; ++k) {
+        int k1 = (k + 1) & 63;
+        double vx = px + r * circ_c[k], vy = py + r * circ_s[k];
+        double wx = px + r * circ_c[k1], wy = py + r * circ_s[k1];
+        double exx = wx - vx, eyy = wy - vy;
+        double a = exx * (cy - vy) - eyy * (cx - vx);
+        double b = exx * ddy - eyy * ddx;
+        if (b == 0.0) {
+            if (a > 0.0) return 0;
+        } else if (b < 0.0) {
+            double t = -a / b;
+            if (t > tlo) tlo = t;
+        } else {
+            double t = -a / b;
+            if (t < thi) thi = t;
+        }
+        if (tlo > thi) return 0;
+    }
+    *tout = tlo;
+    return 1;
+}
+
+static int ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1, double *dout) {
+    double ddx = ex - cx, ddy = ey - cy;
+    double tx0, tx1, ty0, ty1;
+    if (ddx == 0.0) {
+        if (cx < x0 || cx > x1) return 0;
+        tx0 = -INFINITY; tx1 = INFINITY;
+    } else {
+        double ta = (x0 - cx) / ddx, tb = (x1 - cx) / ddx;
+        if (ta < tb) { tx0 = ta; tx1 = tb; } else { tx0 = tb; tx1 = ta; }
+    }
+    if (ddy == 0.0) {
+        if (cy < y0 || cy > y1) return 0;
+        ty0 = -INFINITY; ty1 = INFINITY;
+    } else {
+        double ta = (y0 - cy) / ddy, tb = (y1 - cy) / ddy;
+        if (ta < tb) { ty0 = ta; ty1 = tb; } else { ty0 = tb; ty1 = ta; }
+    }
+    double tin = tx0 > ty0 ? tx0 : ty0;
+    double tout = tx1 < ty1 ? tx1 : ty1;
+    if (tin > tout || tout < 0.0 || tin > 1.0) return 0;
+    double t = tin >= 0.0 ? tin : tout;
+    if (t > 1.0) return 0;
+    *dout = gdist(cx + t * ddx, cy + t * ddy, cx, cy);
+    return 1;
+}
+
+static int ray_vline(double cx, double cy, double ex, double ey, double lx, double *dout) {
+    if (cx == lx && ex == lx) { *dout = 0.0; return 1; }
+    if ((cx - lx) * (ex - lx) > 0.0) return 0;
+    double t = (lx - cx) / (ex - cx);
+    *dout = gdist(lx, cy + t * (ey - cy), cx, cy);
+    return 1;
+}
+
+static int ray_hline(double cx, double cy, double ex, double ey, double ly, double *dout) {
+    if (cy == ly && ey == ly) { *dout = 0.0; return 1; }
+    if ((cy - ly) * (ey - ly) > 0.0) return 0;
+    double t = (ly - cy) / (ey - cy);
+    *dout = gdist(cx + t * (ex - cx), ly, cx, cy);
+    return 1;
+}
+
+static double radar_obstacles(const oc_cfg *c, double cx, double cy, double ex, double ey, double len) {
+    double mind = len, d;
+    const double *b = c->bound;
+    double gx0 = ceil(b[0] / 10.0) * 10.0, gy0 = ceil(b[2] / 10.0) * 10.0;
+    /* occupied cells whose square can touch the ray: centre within 15 + 5 of c (box) */
+    int i0 = (int)floor((cx - 20.0 - gx0) / 10.0), i1 = (int)ceil((cx + 20.0 - gx0) / 10.0);
+    int j0 = (int)floor((cy - 20.0 - gy0) / 10.0), j1 = (int)ceil((cy + 20.0 - gy0) / 10.0);
+    if (i0 < 0) i0 = 0;
+    if (j0 < 0) j0 = 0;
+    if (i1 > c->gw - 1) i1 = c->gw - 1;
+    if (j1 > c->gh - 1) j1 = c->gh - 1;
+    for (int i = i0; i <= i1; ++i)
+        for (int j = j0; j <= j1; ++j) {
+            if (!c->occ[i * c->gh + j]) continue;
+            double qx = gx0 + 10.0 * i, qy = gy0 + 10.0 * j;
+            if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, &d) && d <= mind) mind = d;
+        }
+    if (ray_vline(cx, cy, ex, ey, b[0], &d) && d < mind) mind = d;
+    if (ray_vline(cx, cy, ex, ey, b[1], &d) && d < mind) mind = d;
+    if (ray_hline(cx, cy, ex, ey, b[2], &d) && d < mind) mind = d;
+    if (ray_hline(cx, cy, ex, ey, b[3], &d) && d < mind) mind = d;
+    return mind;
+}
+
+static double pairwise_sum(const double *a, int n) {
+    if (n < 8) {
+        double s = a[0];
+        for (int i = 1; i < n; ++i) s += a[i];
+        return s;
+    }
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+}
+
+/* ------------------------------------------------------------ tdCPA (util:308-329) */
+static void tdcpa(double ox, double oy, double hx, double hy, double ovx, double ovy, double hvx, double hvy,
+                  double pb, double *tcpa, double *dcpa, int *total) {
+    double rx = -1 * (ox - hx), ry = -1 * (oy - hy);
+    double wx = ovx - hvx, wy = ovy - hvy;
+    double nw = npnorm(wx, wy);
+    double sq = nw * nw;
+    double t, d;
+    if (sq == 0) {
+        t = -10;
+        double nnx = ox + ovx * 1, nny = oy + ovy * 1;
+        double nhx = hx + hvx * 1, nhy = hy + hvy * 1;
+        d = npnorm(nhx - nnx, nhy - nny);
+        if (d < pb + pb) *total += 1;
+    } else {
+        t = fma(ry, wy, rx * wx) / sq;
+        d = npnorm((rx * -1) + (wx * t), (ry * -1) + (wy * t));
+    }
+    if (t <= 1 && t >= 0 && d < pb + pb) *total += 1;
+    *tcpa = t;
+    *dcpa = d;
+}
+
+/* ------------------------------------------------------------ observation (env:837-1493) */
+static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e) {
+    const int N = c->N, K = N - 1, D0 = 6 + 4 * K;
+    const double *b = c->bound;
+    const double XS = (1.0 - (-1.0)) / (b[1] - b[0]), YS = (1.0 - (-1.0)) / (b[3] - b[2]);
+    const double pb = 2.5, vmax = 5.0;
+    for (int i = 0; i < N; ++i) {
+        size_t ai = (size_t)e * N + i;
+        double px = s->pos[2 * ai], py = s->pos[2 * ai + 1];
+        double vx = s->vel[2 * ai], vy = s->vel[2 * ai + 1];
+        float *own = o->own + ai * D0;
+        double npx = -1 + (px - b[0]) * XS, npy = -1 + (py - b[2]) * YS;
+        double gx = s->goal[2 * ai], gy = s->goal[2 * ai + 1];
+        double ngx = 2 * ((gx - b[0]) / (b[1] - b[0])) - 1, ngy = 2 * ((gy - b[2]) / (b[3] - b[2])) - 1;
+        own[0] = (float)npx; own[1] = (float)npy;
+        own[2] = (float)(vx / vmax); own[3] = (float)(vy / vmax);
+        own[4] = (float)(ngx - npx); own[5] = (float)(ngy - npy);
+        int kk = 0, cc = 0, cp = 0;
+        for (int j = 0; j < N; ++j) {
+            if (j == i) continue;
+            size_t aj = (size_t)e * N + j;
+            double qx = s->pos[2 * aj], qy = s->pos[2 * aj + 1];
+            double wx = s->vel[2 * aj], wy = s->vel[2 * aj + 1];
+            double dx = qx - px, dy = qy - py;
+            if (c->compat) {
+                own[6 + 4 * kk] = (float)(-1 + (dx - b[0]) * XS);
+                own[7 + 4 * kk] = (float)(-1 + (dy - b[2]) * YS);
+            } else {
+                own[6 + 4 * kk] = (float)(XS * dx);
+                own[7 + 4 * kk] = (float)(YS * dy);
+            }
+            own[8 + 4 * kk] = (float)(wx / vmax);
+            own[9 + 4 * kk] = (float)(wy / vmax);
+            float *nb = o->nei + (ai * K + kk) * 6;
+            double dxm = b[0] - b[1], dxM = b[1] - b[0], dym = b[2] - b[3], dyM = b[3] - b[2];
+            nb[0] = (float)(2 * ((dx - dxm) / (dxM - dxm)) - 1);
+            nb[1] = (float)(2 * ((dy - dym) / (dyM - dym)) - 1);
+            double g0, g1;
+            if (c->compat) { g0 = wy - qx; g1 = pb - qy; }
+            else { g0 = s->goal[2 * aj] - qx; g1 = s->goal[2 * aj + 1] - qy; }
+            nb[2] = (float)(2 * ((g0 - dxm) / (dxM - dxm)) - 1);
+            nb[3] = (float)(2 * ((g1 - dym) / (dyM - dym)) - 1);
+            nb[4] = (float)(wx / vmax);
+            nb[5] = (float)(wy / vmax);
+            double t, d;
+            tdcpa(qx, qy, px, py, wx, wy, vx, vy, pb, &t, &d, &cc);
+            if (o->tcpa) { o->tcpa[ai * K + kk] = t; o->dcpa[ai * K + kk] = d; }
+            double t2, d2;
+            tdcpa(s->pre_pos[2 * aj], s->pre_pos[2 * aj + 1], s->pre_pos[2 * ai], s->pre_pos[2 * ai + 1],
+                  s->pre_vel[2 * aj], s->pre_vel[2 * aj + 1], s->pre_vel[2 * ai], s->pre_vel[2 * ai + 1], pb, &t2, &d2, &cp);
+            ++kk;
+        }
+        if (o->conf_cur) { o->conf_cur[ai] = cc; o->conf_pre[ai] = cp; }
+        /* radar */
+        for (int r = 0; r < NRAY; ++r) {
+            double ex = px + 15.0 * ray_c[r], ey = py + 15.0 * ray_s[r];
+            double len = gdist(ex, ey, px, py);
+            double dd = len, dob = len;
+            if (c->radar_mode != 1) {
+                double shortest = INFINITY;
+                for (int j = 0; j < N; ++j) {
+                    if (j == i) continue;
+                    size_t aj = (size_t)e * N + j;
+                    double t;
+                    if (!ray_poly_entry(px, py, ex, ey, s->pos[2 * aj], s->pos[2 * aj + 1], pb, &t)) continue;
+                    double ix = px + t * (ex - px), iy = py + t * (ey - py);
+                    double d = gdist(ix, iy, px, py);
+                    if (d < shortest) { shortest = d; dd = d; }
+                }
+            }
+            if (c->radar_mode != 0) dob = radar_obstacles(c, px, py, ex, ey, len);
+            double v = c->radar_mode == 0 ? dd : (c->radar_mode == 1 ? dob : (dd < dob ? dd : dob));
+            o->radar[ai * NRAY + r] = (float)v;
+        }
+    }
+}
+
+/* ------------------------------------------------------------ step (env:2627 + ss_reward) */
+void oc_step(const oc_cfg *c, oc_state *s, const float *act, oc_out *o) {
+    init_tables();
+    const int N = c->N, E = c->E;
+    const double *b = c->bound;
+    const double pb = 2.5, vmax = 5.0, dt = 0.5;
+    double rew[64];
+    for (int e = 0; e < E; ++e) {
+        /* a1 kinematics */
+        for (int i = 0; i < N; ++i) {
+            size_t ai = (size_t)e * N + i;
+            s->pre_pos[2 * ai] = s->pos[2 * ai];
+            s->pre_pos[2 * ai + 1] = s->pos[2 * ai + 1];
+            s->pre_vel[2 * ai] = s->vel[2 * ai];
+            s->pre_vel[2 * ai + 1] = s->vel[2 * ai + 1];
+            double ax = (double)act[2 * ai] * 8, ay = (double)act[2 * ai + 1] * 8;
+            double cvx = s->vel[2 * ai] + ax * dt, cvy = s->vel[2 * ai + 1] + ay * dt;
+            double nh = atan2(cvy, cvx);
+            if (npnorm(cvx, cvy) >= vmax) {
+                s->vel[2 * ai] = vmax * cos(nh);
+                s->vel[2 * ai + 1] = vmax * sin(nh);
+            } else {
+                s->vel[2 * ai] = cvx;
+                s->vel[2 * ai + 1] = cvy;
+            }
+            s->pos[2 * ai] = s->pos[2 * ai] + s->vel[2 * ai] * dt;
+            s->pos[2 * ai + 1] = s->pos[2 * ai + 1] + s->vel[2 * ai + 1] * dt;
+        }
+        observe_env(c, s, o, e);
+        /* ss_reward */
+        uint8_t bbc[4] = {0, 0, 0, 0};
+        int all_goal = 1, any_done = 0, all_reach = 1;
+        const double c_drone = 1 + (2.5 / (10 - 2.5)), m_drone = (0 - 1) / (10 - 2.5);
+        for (int i = 0; i < N; ++i) {
+            size_t ai = (size_t)e * N + i;
+            double px = s->pos[2 * ai], py = s->pos[2 * ai + 1];
+            int ncoll = 0, last_coll = -1, nearest = -1;
+            double shortest = INFINITY, dist[64];
+            int nd = 0;
+            for (int j = 0; j < N; ++j) {
+                if (j == i) continue;
+                size_t aj = (size_t)e * N + j;
+                double d = npnorm(px - s->pos[2 * aj], py - s->pos[2 * aj + 1]);
+                dist[nd++] = d;
+                if (d < shortest) { shortest = d; nearest = j; }
+                if (d <= pb * 2) { ++ncoll; last_coll = j; }
+            }
+            int building = 0;
+            {
+                double gx0 = ceil(b[0] / 10.0) * 10.0, gy0 = ceil(b[2] / 10.0) * 10.0;
+                int ci = (int)floor((px - gx0) / 10.0 + 0.5), cj = (int)floor((py - gy0) / 10.0 + 0.5);
+                for (int ii = ci - 1; ii <= ci + 1 && !building; ++ii)
+                    for (int jj = cj - 1; jj <= cj + 1; ++jj) {
+                        if (ii < 0 || jj < 0 || ii >= c->gw || jj >= c->gh) continue;
+                        if (!c->occ[ii * c->gh + jj]) continue;
+                        if (building_hit(px, py, gx0 + 10.0 * ii, gy0 + 10.0 * jj, pb)) { building = 1; break; }
+                    }
+            }
+            if (building) s->wall[ai] += 1;
+            double gx = s->goal[2 * ai], gy = s->goal[2 * ai + 1];
+            int goal = goal_reached(px, py, gx, gy, pb);
+            int cur = s->wp_cur[ai];
+            const double *w0 = s->wp + ((size_t)ai * c->W + cur) * 2;
+            int wpf = gdist(px, py, w0[0], w0[1]) < 5;
+            double before = npnorm(s->pre_pos[2 * ai] - gx, s->pre_pos[2 * ai + 1] - gy);
+            double after = npnorm(px - gx, py - gy);
+            double dtg = (1 * (before - after)) / 5;
+            double pen = 0;
+            for (int k = 0; k < nd; ++k)
+                if (dist[k] >= 2.5 && dist[k] <= 10) pen = pen + (1 * (m_drone * shortest + c_drone));
+                else pen = pen + 0;
+            int bnd = bound_crash(s->pre_pos[2 * ai], s->pre_pos[2 * ai + 1], px, py, pb, b);
+            uint8_t m = (uint8_t)(bnd | ((ncoll > 0) << 1) | (goal << 2) | (building << 3) | (wpf << 4));
+            int done = 0, cg = 0;
+            double r;
+            if (bnd) { r = ((0.0 - 20) - 0.0) - 0; done = 1; bbc[0] = 1; }
+            else if (ncoll > 0) { r = ((0.0 - 20) - 0.0) - pen; done = 1; bbc[2] = 1; if (last_coll == nearest) bbc[3] = 1; }
+            else if (goal) { r = (0.0 + 20) + 0.0; cg = 1; s->reach[ai] = 1; }
+            else {
+                if (wpf && s->wp_cnt[ai] - cur > 1) s->wp_cur[ai] = cur + 1;
+                r = dtg - pen;
+            }
+            if (cg) m |= 32;
+            rew[i] = r;
+            o->done[ai] = (uint8_t)done;
+            o->mask[ai] = m;
+            any_done |= done;
+            all_goal &= cg;
+            all_reach &= s->reach[ai];
+        }
+        double team = pairwise_sum(rew, N);
+        for (int i = 0; i < N; ++i) o->reward[(size_t)e * N + i] = (float)(c->team_reward ? team : rew[i]);
+        for (int q = 0; q < 4; ++q) o->bbc[4 * e + q] = bbc[q];
+        s->step[e] += 1;
+        o->env_done[e] = (uint8_t)((c->episode_length < s->step[e]) || any_done || all_goal || all_reach);
+    }
+}
+
+/* reset selected envs to the given OD and write their observation (env:199-405) */
+void oc_reset(const oc_cfg *c, oc_state *s, const uint8_t *env_mask, const double *start, const double *wps,
+              const int32_t *wp_cnt, oc_out *o) {
+    init_tables();
+    const int N = c->N;
+    for (int e = 0; e < c->E; ++e) {
+        if (env_mask && !env_mask[e]) continue;
+        for (int i = 0; i < N; ++i) {
+            size_t ai = (size_t)e * N + i;
+            s->pos[2 * ai] = s->pre_pos[2 * ai] = start[2 * ai];
+            s->pos[2 * ai + 1] = s->pre_pos[2 * ai + 1] = start[2 * ai + 1];
+            s->vel[2 * ai] = s->vel[2 * ai + 1] = 0.0;
+            s->pre_vel[2 * ai] = s->pre_vel[2 * ai + 1] = 0.0;
+            int n = wp_cnt[ai];
+            s->wp_cnt[ai] = n;
+            s->wp_cur[ai] = 0;
+            memcpy(s->wp + (size_t)ai * c->W * 2, wps + (size_t)ai * c->W * 2, sizeof(double) * 2 * c->W);
+            s->goal[2 * ai] = wps[((size_t)ai * c->W + n - 1) * 2];
+            s->goal[2 * ai + 1] = wps[((size_t)ai * c->W + n - 1) * 2 + 1];
+            s->reach[ai] = 0;
+            s->wall[ai] = 0;
+        }
+        s->step[e] = 0;
+        observe_env(c, s, o, e);
+    }
+}
+
+/* observation only (no state change) */
+void oc_observe(const oc_cfg *c, oc_state *s, oc_out *o) {
+    init_tables();
+    for (int e = 0; e < c->E; ++e) observe_env(c, s, o, e);
+}
+
+/* building / bound / goal predicate probes for tests */
+int oc_bound_crash(double x0, double y0, double x1, double y1, const double *bound) {
+    init_tables();
+    return bound_crash(x0, y0, x1, y1, 2.5, bound);
+}
+int oc_goal_reached(double px, double py, double gx, double gy) {
+    init_tables();
+    return goal_reached(px, py, gx, gy, 2.5);
+}
+int oc_building_hit(double px, double py, double cx, double cy) {
+    init_tables();
+    return building_hit(px, py, cx, cy, 2.5);
+}

@@ -1,0 +1,324 @@
+"""GEOS (shapely 2.0.1 -> GEOS 3.11) buffer construction and the predicates the
+reference evaluates on those buffers.  TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+The reference builds every shape with shapely's ``buffer`` (quad_segs=16) and then
+asks GEOS ``intersects``/``intersection``/``distance``.  GEOS is not installed here,
+so this module restates
+
+* the *construction* exactly, following GEOS ``OffsetSegmentGenerator``:
+  ``createCircle`` (Point.buffer), ``computeLineBufferCurve`` +
+  ``addLineEndCap``/``addDirectedFillet`` (LineString.buffer with round caps),
+  ``computeOffsetSegment``, and the ``isRedundant`` vertex filter
+  (minimum vertex distance = 1e-6 * distance);
+* the *predicates* as closed forms that are exact in real arithmetic for those
+  convex shapes (used by the batched oracle and by the HIP kernel, same operation
+  order), plus an independent exact-rational formulation (``Fraction``) evaluated
+  on the actual floating-point vertices, used only by tests to cross-check the
+  closed forms.
+
+Reference call sites: ATT/env:1080-1159 (radar), :2172-2175 (capsule, own circle),
+:2243-2250 (building), :2266-2269 (goal), :2507 (bound); OM/env:1100-1141
+(obstacle radar).
+"""
+import math
+from fractions import Fraction
+
+from .consts import MATH_PI, QUAD_SEGS, PB
+
+FILLET_QUANTUM = MATH_PI / 2.0 / QUAD_SEGS      # OffsetSegmentGenerator ctor
+VERTEX_SNAP = 1.0e-6                            # CURVE_VERTEX_SNAP_DISTANCE_FACTOR
+
+
+def _fillet(px, py, start, end, direction, radius):
+    """GEOS ``addDirectedFillet`` (direction -1 == CLOCKWISE)."""
+    total = abs(start - end)
+    nsegs = int(total / FILLET_QUANTUM + 0.5)
+    if nsegs < 1:
+        return []
+    inc = total / nsegs
+    out = []
+    for i in range(nsegs):
+        ang = start + float(direction * i) * inc
+        out.append((px + radius * math.cos(ang), py + radius * math.sin(ang)))
+    return out
+
+
+class _SegList:
+    """GEOS ``OffsetSegmentString`` with its ``isRedundant`` filter."""
+
+    def __init__(self, distance):
+        self.pts = []
+        self.min_dist = distance * VERTEX_SNAP
+
+    def add(self, p):
+        if self.pts:
+            q = self.pts[-1]
+            dx, dy = p[0] - q[0], p[1] - q[1]
+            if math.sqrt(dx * dx + dy * dy) < self.min_dist:
+                return
+        self.pts.append(p)
+
+
+def circle_vertices(px, py, r):
+    """Vertices of ``Point(px, py).buffer(r)`` (GEOS ``createCircle``), ring order, unclosed."""
+    seg = _SegList(r)
+    seg.add((px + r, py))
+    for p in _fillet(px, py, 0.0, 2.0 * MATH_PI, -1, r):
+        seg.add(p)
+    return seg.pts
+
+
+def circle_unit_table():
+    """(cos, sin) of GEOS createCircle angles 0 - i*inc, i = 0..63 (i=0 gives (1, 0))."""
+    total = abs(0.0 - 2.0 * MATH_PI)
+    nsegs = int(total / FILLET_QUANTUM + 0.5)
+    inc = total / nsegs
+    return [(math.cos(0.0 + float(-1 * i) * inc), math.sin(0.0 + float(-1 * i) * inc)) for i in range(nsegs)]
+
+
+def _offset_segment(p0, p1, side, distance):
+    """GEOS ``computeOffsetSegment``: side +1 LEFT, -1 RIGHT."""
+    dx = p1[0] - p0[0]
+    dy = p1[1] - p0[1]
+    ln = math.sqrt(dx * dx + dy * dy)
+    ux = side * distance * dx / ln
+    uy = side * distance * dy / ln
+    return (p0[0] - uy, p0[1] + ux), (p1[0] - uy, p1[1] + ux)
+
+
+def _line_end_cap(seg, p0, p1, distance):
+    """GEOS ``addLineEndCap`` with CAP_ROUND."""
+    _, l1 = _offset_segment(p0, p1, 1, distance)
+    _, r1 = _offset_segment(p0, p1, -1, distance)
+    ang = math.atan2(p1[1] - p0[1], p1[0] - p0[0])
+    seg.add(l1)
+    for p in _fillet(p1[0], p1[1], ang + MATH_PI / 2.0, ang - MATH_PI / 2.0, -1, distance):
+        seg.add(p)
+    seg.add(r1)
+
+
+def capsule_vertices(p0, p1, r):
+    """Vertices of ``LineString([p0, p1]).buffer(r, cap_style='round')`` (ATT/env:2172-2173).
+
+    A zero-length segment collapses to a point and GEOS emits ``createCircle``.
+    """
+    p0 = (float(p0[0]), float(p0[1]))
+    p1 = (float(p1[0]), float(p1[1]))
+    if p0 == p1:
+        return circle_vertices(p0[0], p0[1], r)
+    seg = _SegList(r)
+    # left side: initSideSegments(p0, p1, LEFT) ; addLastSegment -> offset1.p1
+    _, l1 = _offset_segment(p0, p1, 1, r)
+    seg.add(l1)
+    _line_end_cap(seg, p0, p1, r)
+    # right side, traversed backwards, still LEFT
+    _, rr1 = _offset_segment(p1, p0, 1, r)
+    seg.add(rr1)
+    _line_end_cap(seg, p1, p0, r)
+    return seg.pts
+
+
+# ---------------------------------------------------------------------------
+# closed forms (exact in real arithmetic; same operation order as the kernel)
+# ---------------------------------------------------------------------------
+
+def edge_normal_table():
+    """Unit outward normals of the regular 64-gon edges: angle (k + 1/2) * pi/32."""
+    return [(math.cos((k + 0.5) * MATH_PI / 32.0), math.sin((k + 0.5) * MATH_PI / 32.0)) for k in range(64)]
+
+
+APOTHEM_UNIT = math.cos(MATH_PI / 64.0)
+
+
+def goal_reached(px, py, gx, gy):
+    """64-gon(pos, 2.5) intersects 64-gon(goal, 1)   (ATT/env:2266-2269, :2546).
+
+    Both shapes share the vertex angles k*pi/32, so their Minkowski difference is the
+    regular 64-gon of circumradius 3.5 and the test is ``max_k d.n_k <= 3.5 cos(pi/64)``.
+    """
+    dx = gx - px
+    dy = gy - py
+    thr = (PB + 1.0) * APOTHEM_UNIT
+    m = -math.inf
+    for nx, ny in edge_normal_table():
+        v = dx * nx + dy * ny
+        if v > m:
+            m = v
+    return m <= thr
+
+
+def building_hit_cell(px, py, cx, cy, half=5.0):
+    """64-gon(pos, 2.5) intersects the closed square cell centred (cx, cy)  (ATT/env:2243-2250).
+
+    Separating-axis test on the square axes and the 32 distinct 64-gon edge normals.
+    """
+    dx = cx - px
+    dy = cy - py
+    if abs(dx) > half + PB or abs(dy) > half + PB:
+        return False
+    for nx, ny in edge_normal_table()[:32]:
+        proj = abs(dx * nx + dy * ny)
+        lim = half * (abs(nx) + abs(ny)) + PB * APOTHEM_UNIT
+        if proj > lim:
+            return False
+    return True
+
+
+def capsule_extents(p0, p1, r):
+    vs = capsule_vertices(p0, p1, r)
+    xs = [v[0] for v in vs]
+    ys = [v[1] for v in vs]
+    return min(xs), max(xs), min(ys), max(ys)
+
+
+def bound_crash(p0, p1, bound, r=PB):
+    """Any of the 4 infinite bound lines intersects the swept capsule  (ATT/env:2507).
+
+    The capsule is convex, so a line x=c meets it iff min_x <= c <= max_x (GEOS
+    orientation predicates on the float vertices are exact for these axis lines).
+    """
+    mnx, mxx, mny, mxy = capsule_extents(p0, p1, r)
+    return ((mnx <= bound[0] <= mxx) or (mnx <= bound[1] <= mxx)
+            or (mny <= bound[2] <= mxy) or (mny <= bound[3] <= mxy))
+
+
+def ray_polygon_entry(cx, cy, ex, ey, poly):
+    """Parameter t in [0,1] of the first point of segment c->e inside the convex
+    clockwise polygon ``poly`` (Cyrus-Beck), or None.  Same operation order as the kernel."""
+    ddx = ex - cx
+    ddy = ey - cy
+    t_lo, t_hi = 0.0, 1.0
+    n = len(poly)
+    for k in range(n):
+        vx, vy = poly[k]
+        wx, wy = poly[(k + 1) % n]
+        exx = wx - vx
+        eyy = wy - vy
+        a = exx * (cy - vy) - eyy * (cx - vx)
+        b = exx * ddy - eyy * ddx
+        if b == 0.0:
+            if a > 0.0:
+                return None
+        elif b < 0.0:
+            t = -a / b
+            if t > t_lo:
+                t_lo = t
+        else:
+            t = -a / b
+            if t < t_hi:
+                t_hi = t
+        if t_lo > t_hi:
+            return None
+    return t_lo
+
+
+def point_dist(ax, ay, bx, by):
+    """GEOS Coordinate::distance (no FMA)."""
+    dx = ax - bx
+    dy = ay - by
+    return math.sqrt(dx * dx + dy * dy)
+
+
+def ray_square_crossing(cx, cy, ex, ey, x0, x1, y0, y1):
+    """Distance from c to the nearest point of segment(c,e) ∩ boundary(square), or None
+    (OM/env:1117-1126: ``line.intersection(polygon.boundary)`` then ``distance``)."""
+    ddx = ex - cx
+    ddy = ey - cy
+    if ddx == 0.0:
+        if cx < x0 or cx > x1:
+            return None
+        tx0, tx1 = -math.inf, math.inf
+    else:
+        ta = (x0 - cx) / ddx
+        tb = (x1 - cx) / ddx
+        tx0, tx1 = (ta, tb) if ta < tb else (tb, ta)
+    if ddy == 0.0:
+        if cy < y0 or cy > y1:
+            return None
+        ty0, ty1 = -math.inf, math.inf
+    else:
+        ta = (y0 - cy) / ddy
+        tb = (y1 - cy) / ddy
+        ty0, ty1 = (ta, tb) if ta < tb else (tb, ta)
+    t_in = tx0 if tx0 > ty0 else ty0
+    t_out = tx1 if tx1 < ty1 else ty1
+    if t_in > t_out or t_out < 0.0 or t_in > 1.0:
+        return None
+    t = t_in if t_in >= 0.0 else t_out
+    if t > 1.0:
+        return None
+    return point_dist(cx + t * ddx, cy + t * ddy, cx, cy)
+
+
+def ray_vline_crossing(cx, cy, ex, ey, lx):
+    """Distance from c to segment(c,e) ∩ (x = lx) (OM/env:1127-1141), or None."""
+    if cx == lx and ex == lx:
+        return 0.0  # collinear: intersection LineString contains c
+    if (cx - lx) * (ex - lx) > 0.0:
+        return None
+    ddx = ex - cx
+    t = (lx - cx) / ddx
+    return point_dist(lx, cy + t * (ey - cy), cx, cy)
+
+
+def ray_hline_crossing(cx, cy, ex, ey, ly):
+    if cy == ly and ey == ly:
+        return 0.0
+    if (cy - ly) * (ey - ly) > 0.0:
+        return None
+    ddy = ey - cy
+    t = (ly - cy) / ddy
+    return point_dist(cx + t * (ex - cx), ly, cx, cy)
+
+
+# ---------------------------------------------------------------------------
+# independent exact formulations (tests only): rational arithmetic on the
+# actual floating-point vertices GEOS would produce.
+# ---------------------------------------------------------------------------
+
+def _fr(p):
+    return (Fraction(p[0]), Fraction(p[1]))
+
+
+def convex_polys_intersect_exact(A, B):
+    """Closed convex polygons intersect (touching counts) -- exact separating axis test."""
+    A = [_fr(p) for p in A]
+    B = [_fr(p) for p in B]
+    for P in (A, B):
+        n = len(P)
+        for k in range(n):
+            (x0, y0), (x1, y1) = P[k], P[(k + 1) % n]
+            nx, ny = (y1 - y0), -(x1 - x0)
+            pa = [nx * x + ny * y for x, y in A]
+            pb = [nx * x + ny * y for x, y in B]
+            if max(pa) < min(pb) or max(pb) < min(pa):
+                return False
+    return True
+
+
+def segment_convex_entry_exact(c, e, poly):
+    """Exact parameter of the first point of segment c->e inside convex polygon, or None."""
+    cx, cy = _fr(c)
+    ex, ey = _fr(e)
+    P = [_fr(p) for p in poly]
+    # orientation of the ring
+    area2 = sum(P[k][0] * P[(k + 1) % len(P)][1] - P[(k + 1) % len(P)][0] * P[k][1] for k in range(len(P)))
+    sgn = -1 if area2 < 0 else 1   # clockwise rings: interior on the right
+    t_lo, t_hi = Fraction(0), Fraction(1)
+    ddx, ddy = ex - cx, ey - cy
+    for k in range(len(P)):
+        (vx, vy), (wx, wy) = P[k], P[(k + 1) % len(P)]
+        exx, eyy = wx - vx, wy - vy
+        a = sgn * -(exx * (cy - vy) - eyy * (cx - vx))
+        b = sgn * -(exx * ddy - eyy * ddx)
+        # inside  <=>  a + t b <= 0
+        if b == 0:
+            if a > 0:
+                return None
+        elif b < 0:
+            t_lo = max(t_lo, -a / b)
+        else:
+            t_hi = min(t_hi, -a / b)
+        if t_lo > t_hi:
+            return None
+    return t_lo

@@ -1,0 +1,76 @@
+"""Shared helpers for the parity tests (OD drawing via the oracle restatement, padding)."""
+import numpy as np
+
+from oracle import world_ref
+
+W_DEFAULT = 32
+
+
+def draw_env_od(occ, N, rng, pools=None):
+    """One env's OD by the reference rule (ATT/env:251-347), via the oracle restatement."""
+    pools = pools or world_ref.target_pools(occ)
+    starts, goals = [], []
+    for _ in range(N):
+        while True:
+            qs = int(rng.integers(0, 4))
+            qt = int(rng.choice([q for q in range(4) if q != qs]))
+            s = pools[qs][int(rng.integers(0, len(pools[qs])))]
+            if world_ref.start_separated(s, [np.array(p) for p in starts]):
+                break
+        t = pools[qt][int(rng.integers(0, len(pools[qt])))]
+        starts.append(s)
+        goals.append(world_ref.od_waypoints(occ, s, t))
+    return starts, goals
+
+
+def pack_od(od_list, W=W_DEFAULT):
+    """[(starts, goals)] per env -> start (E,N,2), wps (E,N,W,2), cnt (E,N)."""
+    E, N = len(od_list), len(od_list[0][0])
+    st = np.zeros((E, N, 2))
+    wps = np.zeros((E, N, W, 2))
+    cnt = np.zeros((E, N), dtype=np.int32)
+    for e, (s, g) in enumerate(od_list):
+        for i in range(N):
+            st[e, i] = s[i]
+            wps[e, i, :len(g[i])] = g[i]
+            wps[e, i, len(g[i]):] = g[i][-1]
+            cnt[e, i] = len(g[i])
+    return st, wps, cnt
+
+
+def random_od(occ, E, N, seed, W=W_DEFAULT):
+    rng = np.random.default_rng(seed)
+    pools = world_ref.target_pools(occ)
+    return pack_od([draw_env_od(occ, N, rng, pools) for _ in range(E)], W)
+
+
+def mix64(x):
+    """splitmix64 finaliser used by the GPU auto-reset draw (csrc/aac_env.hip ``mix64``)."""
+    M = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & M
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+    return x ^ (x >> 31)
+
+
+def bank_draw(bank_start, n_bank, seed, e, episode, N, pb=2.5):
+    """Python restatement of the auto-reset draw (starts pairwise > 2 pB apart)."""
+    idx = []
+    for a in range(N):
+        k = 0
+        for att in range(4096):
+            key = mix64(mix64(mix64(seed ^ e) ^ episode) ^ (a * 65536 + att))
+            k = key % n_bank
+            s = bank_start[k]
+            ok = True
+            for b in idx:
+                o = bank_start[b]
+                d = np.sqrt(np.fma(s[1] - o[1], s[1] - o[1], (s[0] - o[0]) * (s[0] - o[0]))) if hasattr(np, "fma") \
+                    else np.linalg.norm(s - o)
+                if not d > pb * 2:
+                    ok = False
+                    break
+            if ok:
+                break
+        idx.append(k)
+    return idx
