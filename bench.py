@@ -1,0 +1,290 @@
+"""Benchmark: agent-env-steps/s (whole node) + MADDPG updates/s, one_model_att, 5 agents x 4096 envs.
+
+One timed *step* = one vectorised training iteration of ATT/main:248-447 on every GPU:
+  actor forward + exploration noise for E x N agents      (choose_action, ATT/maddpg:455)
+  fused env step: kinematics, radar, obs, ss_reward, done (env.step + ss_reward, ATT/env:2627/:2105)
+  replay push of E transitions                             (memory.push, ATT/main:400)
+  GPU auto-reset of finished envs from the OD bank         (reset_world, ATT/env:199)
+  one update_myown-equivalent: N=5 gradient iterations at B=1024 + Polyak (ATT/maddpg:219-440)
+value = E_total * N * steps / max-over-ranks wall time.  Inputs are synthetic (seeded map, OD
+bank, random-init networks); the replay is pre-filled to 1e5 transitions before timing.
+
+python bench.py [--gpus N] [--steps K] [--warmup W]        (N > 1: launched by torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 5 agents×4096 envs"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP32_PEAK_TFLOPS = 157.3
+
+
+def env_bytes_per_agent_step(N):
+    """130 + 4 (24 + 10 (N - 1)) algorithmic HBM bytes per agent-env-step."""
+    return 130 + 4 * (24 + 10 * (N - 1))
+
+
+def update_flops(N, D0, B):
+    """(4A + 7C) MACs per sample per gradient iteration, N iterations."""
+    K = N - 1
+    A = N * (D0 * 64 + 18 * 64 + K * 6 * 64 + 64 * 64 + K * 2 * 64 * 64 + 192 * 256 + 256 * 2)
+    C = N * (D0 + 2) * 128 + 128 * N * 256 + 256
+    return 2.0 * (4 * A + 7 * C) * B * N
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    p.add_argument("--agents", type=int, default=5)
+    p.add_argument("--batch", type=int, default=1024)
+    p.add_argument("--memory", type=int, default=100000)
+    p.add_argument("--radar", default="combined", choices=["drones", "obstacles", "combined"])
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "env_step_pmc.json"))
+    return p.parse_args()
+
+
+def setup_dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+class Trainer:
+    """Vectorised ma_main loop on one GPU (shared by bench.py and the examples)."""
+
+    def __init__(self, E, N, B, memory, radar, seed, pg=None):
+        from multi_agent_aac_amd import world
+        from multi_agent_aac_amd.env import BatchedEnv
+        from multi_agent_aac_amd.maddpg import MADDPG
+        self.E, self.N, self.B = E, N, B
+        self.occ = world.synthetic_map(2026)
+        self.bank = world.ODBank(self.occ, n_pairs=65536, seed=2026 + seed, max_wp=32)
+        self.env = BatchedEnv(E, N, self.occ, radar_mode=radar, max_wp=32)
+        self.env.set_od_bank(self.bank, seed=1234 + seed)
+        D0 = 6 + 4 * (N - 1)
+        self.model = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, seed=777, batch_size=B,
+                            memory_length=memory, process_group=pg)
+        self.model.noise_seed = 99 + seed
+        self.replay = self.model.attach_replay(memory, seed=seed)
+        self.cur = self.env.alloc_buffers()
+        self.nxt = self.env.alloc_buffers()
+        self.episode = self.env_episode_view()
+        self.env.auto_reset(None, out=self.cur)      # all envs: first OD draw + initial obs
+        self.env_events = []
+
+    def env_episode_view(self):
+        # per-env episode counter lives in the native handle; a device tensor mirror drives the
+        # noise schedule (env e's own episode index, ATT/maddpg:476-477)
+        return torch.ones(self.E, dtype=torch.int32, device="cuda")
+
+    def step(self, update=True, time_env=False):
+        c, n = self.cur, self.nxt
+        act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
+        if time_env:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        self.env.step(act, out=n)
+        if time_env:
+            ev1.record()
+            self.env_events.append((ev0, ev1))
+        self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
+        self.env.auto_reset(n.env_done, out=n)
+        self.episode.add_(n.env_done.to(torch.int32))
+        self.cur, self.nxt = n, c
+        if update and len(self.replay) > self.B:
+            self.model.update(self.B, use_graph=not NO_GRAPH)
+
+
+NO_GRAPH = False
+
+
+def cpu_baseline(E, N, B, radar, seconds):
+    """The C oracle env step + the torch-CPU learner restatement on the host cores (bounded sample)."""
+    import multiprocessing as mp
+    from oracle import c_oracle, learner_ref  # noqa: F401  (checker / baseline only)
+    cores = len(os.sched_getaffinity(0))
+    procs = min(cores, 16)
+    per = max(1, E // procs)
+    ctx = mp.get_context("spawn")
+    budget = seconds / 2
+    with ctx.Pool(procs) as pool:
+        res = pool.starmap(_cpu_env_worker, [(per, N, radar, budget, w) for w in range(procs)])
+    steps = min(r[0] for r in res)
+    t_env = max(r[1] / r[0] for r in res)             # seconds per env step of the slowest worker
+    env_rate = procs * per * N / t_env
+    torch.set_num_threads(procs)
+    D0 = 6 + 4 * (N - 1)
+    actor, critic = learner_ref.RefActor([D0, 18, 6], 2), learner_ref.RefCritic([D0, 18, 6], N, 2)
+    actor_t, critic_t = learner_ref.RefActor([D0, 18, 6], 2), learner_ref.RefCritic([D0, 18, 6], N, 2)
+    tr = learner_ref.random_transitions(B, N, 0)
+    tr["done"] = tr["done"].float()
+    t0 = time.perf_counter()
+    n_upd, opts = 0, None
+    while time.perf_counter() - t0 < budget or n_upd == 0:
+        _, opts = learner_ref.ref_update(actor, critic, actor_t, critic_t, [tr] * N, opts=opts)
+        n_upd += 1
+    t_upd = (time.perf_counter() - t0) / n_upd
+    t_iter = t_env * (E / (procs * per)) + t_upd
+    return {"value": E * N / t_iter, "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
+            "sample": (f"C oracle env step ({radar} radar) on {procs} processes x {per} envs x {N} agents, "
+                       f"{steps} steps ({env_rate:.3g} agent-env-steps/s env-only) + torch-CPU update_myown "
+                       f"restatement B={B} x {n_upd} ({t_upd * 1e3:.1f} ms each), {procs} threads; "
+                       f"value = {E}x{N} agent-steps / (env step + update) per iteration"),
+            "env_only": env_rate, "update_ms": t_upd * 1e3}
+
+
+def _cpu_env_worker(E, N, radar, budget, wid):
+    sys.path.insert(0, ROOT)
+    from multi_agent_aac_amd import world
+    from oracle import c_oracle
+    occ = world.synthetic_map(2026)
+    bank = world.ODBank(occ, n_pairs=4096, seed=wid, max_wp=32)
+    rng = np.random.default_rng(wid)
+    mode = {"drones": 0, "obstacles": 1, "combined": 2}[radar]
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode)
+    st, wps, cnt = bank.sample_env_od(E, N, rng)
+    co.reset(st, wps, cnt)
+    acts = rng.uniform(-1, 1, size=(8, E, N, 2)).astype(np.float32)
+    t0 = time.perf_counter()
+    steps = 0
+    while time.perf_counter() - t0 < budget or steps < 2:
+        co.step(acts[steps % 8])
+        done = co.env_done.astype(bool)
+        if done.any():
+            co.reset(st, wps, cnt, env_mask=done.astype(np.uint8))
+        steps += 1
+    return steps, time.perf_counter() - t0
+
+
+def env_microbench(E, N, radar, iters=20):
+    """Env-only kernel throughput at large E (the HBM-roofline regime of SURVEY 8(d))."""
+    from multi_agent_aac_amd import world
+    from multi_agent_aac_amd.env import BatchedEnv
+    occ = world.synthetic_map(2026)
+    bank = world.ODBank(occ, n_pairs=65536, seed=5, max_wp=32)
+    env = BatchedEnv(E, N, occ, radar_mode=radar, max_wp=32)
+    env.set_od_bank(bank, seed=3)
+    env.auto_reset(None)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    acts = [torch.rand(E, N, 2, device="cuda", generator=g) * 2 - 1 for _ in range(4)]
+    for i in range(3):
+        env.step(acts[i % 4])
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for i in range(iters):
+        ev[i][0].record()
+        env.step(acts[i % 4])
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    rate = E * N / (ms * 1e-3)
+    gbs = env_bytes_per_agent_step(N) * E * N / (ms * 1e-3) / 1e9
+    return {"envs": E, "agents": N, "kernel_ms": ms, "agent_env_steps_per_s": rate, "achieved_GBs": gbs,
+            "frac": gbs / HBM_PEAK_GBS}
+
+
+def main():
+    global NO_GRAPH
+    a = parse()
+    NO_GRAPH = a.no_graph
+    ws0 = int(os.environ.get("WORLD_SIZE", "1"))
+    cpu = None
+    if ws0 == 1 and not a.no_cpu_baseline:
+        # before any GPU initialisation: the pool's children must not inherit a GPU context
+        cpu = cpu_baseline(a.envs, a.agents, a.batch, a.radar, a.cpu_seconds)
+    ws, rank, local = setup_dist()
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.manual_seed(777 + rank)
+    tr = Trainer(a.envs, a.agents, a.batch, a.memory, a.radar, seed=rank,
+                 pg=dist.group.WORLD if ws > 1 else None)
+    # pre-fill the replay to >= memory transitions (untimed), then capture the update graph
+    while len(tr.replay) < a.memory:
+        tr.step(update=False)
+    for _ in range(a.warmup):
+        tr.step(update=True)
+    barrier(ws)
+    tr.env_events.clear()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.step(update=True, time_env=True)
+    barrier(ws)
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], device="cuda")
+    if ws > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t)
+    env_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in tr.env_events]))
+    E_total = a.envs * ws
+    N = a.agents
+    value = E_total * N * a.steps / dt
+    upd_per_s = a.steps / dt
+    D0 = 6 + 4 * (N - 1)
+    bpa = env_bytes_per_agent_step(N)
+    achieved = bpa * a.envs * N / (env_ms * 1e-3) / 1e9
+    traffic = None
+    tsrc = None
+    if a.traffic and os.path.exists(a.traffic):
+        with open(a.traffic) as f:
+            t = json.load(f)
+        if t.get("envs") == a.envs and t.get("agents") == N and t.get("radar") == a.radar:
+            traffic = t.get("hbm_bytes_per_launch")
+            tsrc = os.path.relpath(a.traffic, ROOT)
+    upd_fl = update_flops(N, D0, a.batch)
+    out = {
+        "metric": METRIC, "value": value, "unit": "agent-env-steps/s", "n_gpus": ws, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64 env state / f32 obs+learner", "data": "synthetic",
+        "config": {"workload": f"one_model_att: {N} agents x {a.envs} envs/GPU, B={a.batch} MADDPG update, "
+                               f"{a.radar} radar", "envs_per_gpu": a.envs, "envs_total": E_total, "agents": N,
+                   "batch": a.batch, "replay": a.memory, "radar": a.radar,
+                   "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
+                   "update_graph": (not a.no_graph) and ws == 1},
+        "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * N,
+        "roofline": {"kernel": "step_kernel (fused env step)", "bound": "hbm", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": tsrc, "bytes_per_agent_step": bpa, "agents_per_launch": a.envs * N,
+                     "avg_launch_ms": env_ms},
+        "update_roofline": {"bound": "mfma", "unit": "TFLOP/s", "flop_per_update": upd_fl,
+                            "achieved": upd_fl * upd_per_s / 1e12, "peak": FP32_PEAK_TFLOPS,
+                            "frac": upd_fl * upd_per_s / 1e12 / FP32_PEAK_TFLOPS, "note": "whole-step rate bound"},
+    }
+    if rank == 0 and ws == 1 and a.env_micro:
+        out["env_microbench"] = env_microbench(a.env_micro, N, a.radar)
+    if rank == 0 and cpu is not None:
+        out["cpu_baseline"] = cpu
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

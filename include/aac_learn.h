@@ -1,0 +1,65 @@
+/* aac_learn.h -- C ABI of the learner-side kernels in libaac_env.so (gfx950).
+ *
+ * They replace the pieces of the reference's MADDPG path that are not plain GEMMs
+ * (SURVEY.md section 8(a) rows a9-a14):
+ *   aac_attn_fwd/bwd     masked single-head attention of ActorNetwork_ATT_TwoPortion
+ *                        (ATT/nets:194-210: mask = nei.mean(-1) != 0, softmax(k.q / 8) over K,
+ *                        masked weights zeroed, v_att = sum alpha v)
+ *   aac_replay_push/...  ReplayMemory (ATT/mem:6-23) as a device ring of fixed-width fp32 rows;
+ *                        sample = uniform without replacement like random.sample (ATT/mem:19)
+ *   aac_adam_flat        torch.optim.Adam step (ATT/maddpg:93-94, :387, :425) on one flat buffer
+ *   aac_polyak_flat      soft_update (ATT/maddpg:18-22) on one flat buffer
+ *   aac_noise_clamp      choose_action exploration: act + randn * var, clamp [-1, 1]
+ *                        (ATT/maddpg:476-500, var schedule :563-570)
+ * Conventions as in aac_env.h: plain device pointers, ``stream`` = hipStream_t as void*, 0 = ok.
+ */
+#ifndef AAC_LEARN_H
+#define AAC_LEARN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AAC_MAX_FIELDS 16
+
+const char *aac_learn_last_error(void);
+
+/* q [R][64]; k, v rows of 64 floats at k + (r*K + j) * kv_stride (same for v); nei [R][K][6]
+ * (mask source, may be NULL = no mask); out rows of 64 at out + r * out_stride; alpha [R][K]. */
+int aac_attn_fwd(const float *q, const float *k, const float *v, int32_t kv_stride, const float *nei, float *out,
+                 int32_t out_stride, float *alpha, int32_t R, int32_t K, void *stream);
+/* dout rows at dout + r * dout_stride; writes dq [R][64], dk/dv rows with kv_stride. */
+int aac_attn_bwd(const float *q, const float *k, const float *v, int32_t kv_stride, const float *alpha,
+                 const float *dout, int32_t dout_stride, float *dq, float *dk, float *dv, int32_t R, int32_t K,
+                 void *stream);
+
+/* One transition = one ring row made of n_fields consecutive fields; field f has widths[f]
+ * elements per transition, source srcs[f] ([E][widths[f]]), dtype[f] 0 = fp32, 1 = uint8.
+ * meta (device int64[2]) = {next write position, current size}; updated on the device. */
+int aac_replay_push(float *ring, int32_t row_width, int64_t capacity, int64_t *meta, int32_t n_fields,
+                    const void *const *srcs, const int32_t *widths, const int32_t *dtypes, int32_t E, void *stream);
+/* B distinct indices uniform in [0, meta[1]) (B <= 4096, meta[1] >= B), deterministic in
+ * (seed, *counter); *counter (device uint64) is advanced by the kernel. */
+int aac_replay_sample(const int64_t *meta, int32_t B, uint64_t seed, uint64_t *counter, int32_t *idx, void *stream);
+/* dsts[f][b][widths[f]] = ring[idx[b]][field f]. */
+int aac_replay_gather(const float *ring, int32_t row_width, const int32_t *idx, int32_t B, int32_t n_fields,
+                      float *const *dsts, const int32_t *widths, void *stream);
+
+/* torch.optim.Adam (no weight decay, no amsgrad); step (device int32) is the step number
+ * AFTER increment, read on the device so the call can be graph-captured. */
+int aac_adam_flat(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr,
+                  float beta1, float beta2, float eps, const int32_t *step, void *stream);
+/* tgt = (1 - tau) * tgt + tau * src */
+int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *stream);
+
+/* act [E*N][2] += (float)(randn * var_e); clamp to [-1, 1]; var_e from episode[e] (device):
+ * var = noise_start + ((0 - noise_start)/(eps_end - 1)) * (ep - 1) if ep <= eps_end else 0. */
+int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, int32_t eps_end, float noise_start,
+                    uint64_t seed, uint64_t *counter, float *noise_out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AAC_LEARN_H */

@@ -1,0 +1,418 @@
+// aac_learn.hip -- gfx950 kernels for the MADDPG learner side (see include/aac_learn.h).
+//
+// attention : one 64-lane wave per row, lane = embedding dim (the reference's 64-wide
+//             attention, ATT/nets:186-189), K <= 32 neighbours held in registers, dot products
+//             by wave butterfly reductions; the mask (nei.mean(-1) != 0) is computed in-kernel.
+// replay    : fixed-width fp32 rows; push = one workgroup per transition, sample = one 1024-thread
+//             workgroup drawing B distinct indices with an LDS hash table (deterministic,
+//             permutation-symmetric => uniform over B-subsets, like random.sample), gather =
+//             one workgroup per sampled row writing field-contiguous batch tensors.
+// adam/polyak: elementwise over one flat fp32 buffer (all parameters of a network).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <string>
+
+#include "../../include/aac_learn.h"
+
+namespace {
+
+constexpr int MAXK = 32;
+constexpr int LEARN_BLOCK = 256;
+
+thread_local std::string l_err;
+
+int lfail(const std::string &m) {
+    l_err = m;
+    return -1;
+}
+
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ inline float wave_sum(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+// ------------------------------------------------------------------------------ attention
+template <int KM>
+__global__ void __launch_bounds__(LEARN_BLOCK) attn_fwd_kernel(const float *__restrict__ q,
+                                                              const float *__restrict__ k,
+                                                              const float *__restrict__ v, int kvs,
+                                                              const float *__restrict__ nei, float *out, int outs,
+                                                              float *alpha, int R, int K) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * (LEARN_BLOCK / 64) + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const float qd = q[(size_t)r * 64 + lane];
+    float s[KM];
+    float mx = -INFINITY;
+    unsigned valid = 0;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        if (j >= K) continue;
+        const float kd = k[((size_t)r * K + j) * kvs + lane];
+        const float sc = wave_sum(qd * kd) / 8.0f;   // score / sqrt(64)
+        bool m = true;
+        if (nei) {
+            const float *nb = nei + ((size_t)r * K + j) * 6;
+            float acc = nb[0];
+            for (int c = 1; c < 6; ++c) acc += nb[c];
+            m = acc != 0.0f;
+        }
+        s[j] = sc;
+        if (m) {
+            valid |= 1u << j;
+            mx = sc > mx ? sc : mx;
+        }
+    }
+    float den = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        if (j >= K) continue;
+        float e = (valid >> j & 1) ? expf(s[j] - mx) : 0.0f;
+        s[j] = e;
+        den += e;
+    }
+    float o = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        if (j >= K) continue;
+        const float a = (valid >> j & 1) ? s[j] / den : 0.0f;
+        o += a * v[((size_t)r * K + j) * kvs + lane];
+        if (lane == j) alpha[(size_t)r * K + j] = a;
+    }
+    out[(size_t)r * outs + lane] = o;
+}
+
+template <int KM>
+__global__ void __launch_bounds__(LEARN_BLOCK) attn_bwd_kernel(const float *__restrict__ q,
+                                                              const float *__restrict__ k,
+                                                              const float *__restrict__ v, int kvs,
+                                                              const float *__restrict__ alpha,
+                                                              const float *__restrict__ dout, int douts, float *dq,
+                                                              float *dk, float *dv, int R, int K) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * (LEARN_BLOCK / 64) + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const float g = dout[(size_t)r * douts + lane];
+    const float qd = q[(size_t)r * 64 + lane];
+    float a[KM], da[KM];
+    float S = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        if (j >= K) continue;
+        a[j] = alpha[(size_t)r * K + j];
+        da[j] = wave_sum(v[((size_t)r * K + j) * kvs + lane] * g);
+        S += a[j] * da[j];
+    }
+    float dqd = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        if (j >= K) continue;
+        const size_t off = ((size_t)r * K + j) * kvs + lane;
+        const float ds = a[j] * (da[j] - S) / 8.0f;
+        dv[off] = a[j] * g;
+        dk[off] = ds * qd;
+        dqd += ds * k[off];
+    }
+    dq[(size_t)r * 64 + lane] = dqd;
+}
+
+// --------------------------------------------------------------------------------- replay
+struct Fields {
+    const void *src[AAC_MAX_FIELDS];
+    float *dst[AAC_MAX_FIELDS];
+    int width[AAC_MAX_FIELDS];
+    int offset[AAC_MAX_FIELDS + 1];
+    int dtype[AAC_MAX_FIELDS];
+    int n;
+};
+
+__global__ void __launch_bounds__(LEARN_BLOCK) push_kernel(float *ring, int rw, int64_t cap, const int64_t *meta,
+                                                          Fields F) {
+    const int e = blockIdx.x;
+    const int64_t row = (meta[0] + e) % cap;
+    float *dst = ring + row * rw;
+    for (int c = threadIdx.x; c < rw; c += LEARN_BLOCK) {
+        int f = 0;
+        while (c >= F.offset[f + 1]) ++f;
+        const int w = F.width[f], cc = c - F.offset[f];
+        float val;
+        if (F.dtype[f] == 1) val = (float)(reinterpret_cast<const uint8_t *>(F.src[f])[(size_t)e * w + cc]);
+        else val = reinterpret_cast<const float *>(F.src[f])[(size_t)e * w + cc];
+        dst[c] = val;
+    }
+}
+
+__global__ void meta_kernel(int64_t *meta, int64_t cap, int E) {
+    meta[0] = (meta[0] + E) % cap;
+    const int64_t s = meta[1] + E;
+    meta[1] = s < cap ? s : cap;
+}
+
+constexpr int TBL = 8192;
+
+__device__ inline int64_t draw(uint64_t seed, uint64_t ctr, int idx, int att, int64_t size) {
+    uint64_t h = mix64(mix64(mix64(seed) ^ ctr) ^ (((uint64_t)idx << 20) | (uint64_t)att));
+    return (int64_t)(h % (uint64_t)size);
+}
+
+__global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B, uint64_t seed, uint64_t *counter,
+                                                     int32_t *out) {
+    __shared__ int keys[TBL];
+    __shared__ int owner[TBL];
+    const int64_t size = meta[1];
+    const uint64_t ctr = *counter;
+    const int nv = (B + 1023) / 1024;
+    int val[4], att[4];
+    for (int u = 0; u < nv; ++u) {
+        const int idx = threadIdx.x + u * 1024;
+        att[u] = 0;
+        val[u] = idx < B ? (int)draw(seed, ctr, idx, 0, size) : -1;
+    }
+    for (int round = 0; round < 64; ++round) {
+        for (int s = threadIdx.x; s < TBL; s += 1024) {
+            keys[s] = -1;
+            owner[s] = INT_MAX;
+        }
+        __syncthreads();
+        for (int u = 0; u < nv; ++u) {
+            const int idx = threadIdx.x + u * 1024;
+            if (idx >= B) continue;
+            int h = (int)(mix64((uint64_t)val[u]) & (TBL - 1));
+            while (true) {
+                int old = atomicCAS(&keys[h], -1, val[u]);
+                if (old == -1 || old == val[u]) {
+                    atomicMin(&owner[h], idx);
+                    break;
+                }
+                h = (h + 1) & (TBL - 1);
+            }
+        }
+        __syncthreads();
+        int redraw = 0;
+        for (int u = 0; u < nv; ++u) {
+            const int idx = threadIdx.x + u * 1024;
+            if (idx >= B) continue;
+            int h = (int)(mix64((uint64_t)val[u]) & (TBL - 1));
+            while (keys[h] != val[u]) h = (h + 1) & (TBL - 1);
+            if (owner[h] != idx) {
+                ++att[u];
+                val[u] = (int)draw(seed, ctr, idx, att[u], size);
+                redraw = 1;
+            }
+        }
+        if (!__syncthreads_or(redraw)) break;
+    }
+    for (int u = 0; u < nv; ++u) {
+        const int idx = threadIdx.x + u * 1024;
+        if (idx < B) out[idx] = val[u];
+    }
+    if (threadIdx.x == 0) *counter = ctr + 1;
+}
+
+__global__ void __launch_bounds__(LEARN_BLOCK) gather_kernel(const float *ring, int rw, const int32_t *idx, Fields F) {
+    const int b = blockIdx.x;
+    const float *src = ring + (int64_t)idx[b] * rw;
+    for (int c = threadIdx.x; c < rw; c += LEARN_BLOCK) {
+        int f = 0;
+        while (c >= F.offset[f + 1]) ++f;
+        const int w = F.width[f];
+        F.dst[f][(size_t)b * w + (c - F.offset[f])] = src[c];
+    }
+}
+
+// ------------------------------------------------------------------------------- optimiser
+__global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2,
+                            float eps, const int32_t *step) {
+    const int t = *step;
+    const double bc1 = 1.0 - pow((double)b1, (double)t);
+    const double bc2 = 1.0 - pow((double)b2, (double)t);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - (double)b1), w2 = (float)(1.0 - (double)b2);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        float mi = m[i];
+        mi = mi + w1 * (gi - mi);               // exp_avg.lerp_(grad, 1 - beta1)
+        float vi = v[i] * b2;                   // exp_avg_sq.mul_(beta2)
+        vi = vi + w2 * (gi * gi);               //   .addcmul_(grad, grad, 1 - beta2)
+        const float den = sqrtf(vi) / bc2s + eps;
+        p[i] = p[i] + (-step_size) * (mi / den);   // param.addcdiv_(exp_avg, denom, -step_size)
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
+__global__ void polyak_kernel(float *tgt, const float *src, int64_t n, float keep, float tau) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float a = keep * tgt[i];
+        const float b = tau * src[i];
+        tgt[i] = a + b;
+    }
+}
+
+// ------------------------------------------------------------------------------ noise
+__global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, int eps_end, float noise_start,
+                             uint64_t seed, uint64_t *counter, float *noise_out) {
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t ctr = *counter;
+    if (row < (int64_t)E * N) {
+        const int e = (int)(row / N);
+        const int ep = episode ? episode[e] : 1;
+        double var;
+        if (ep <= eps_end) {
+            const double slope = (0.0 - (double)noise_start) / (double)(eps_end - 1);
+            var = (double)noise_start + slope * (double)(ep - 1);
+        } else {
+            var = 0.0;
+        }
+        const uint64_t h1 = mix64(mix64(mix64(seed) ^ ctr) ^ (uint64_t)(2 * row));
+        const uint64_t h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
+        const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
+        const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+        const double rr = sqrt(-2.0 * log(u1));
+        const double z0 = rr * cos(6.283185307179586 * u2), z1 = rr * sin(6.283185307179586 * u2);
+        const float n0 = (float)(z0 * var), n1 = (float)(z1 * var);
+        float a0 = act[2 * row] + n0, a1 = act[2 * row + 1] + n1;
+        a0 = fminf(fmaxf(a0, -1.0f), 1.0f);
+        a1 = fminf(fmaxf(a1, -1.0f), 1.0f);
+        act[2 * row] = a0;
+        act[2 * row + 1] = a1;
+        if (noise_out) {
+            noise_out[2 * row] = n0;
+            noise_out[2 * row + 1] = n1;
+        }
+    }
+}
+
+__global__ void counter_kernel(uint64_t *counter) { *counter += 1; }
+
+#define LHIP(x)                                                                                  \
+    do {                                                                                         \
+        hipError_t _e = (x);                                                                     \
+        if (_e != hipSuccess) return lfail(std::string(#x) + ": " + hipGetErrorString(_e));     \
+    } while (0)
+
+int grid_for(int64_t n) {
+    int64_t b = (n + LEARN_BLOCK - 1) / LEARN_BLOCK;
+    return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *aac_learn_last_error(void) { return l_err.c_str(); }
+
+int aac_attn_fwd(const float *q, const float *k, const float *v, int32_t kvs, const float *nei, float *out,
+                 int32_t outs, float *alpha, int32_t R, int32_t K, void *stream) {
+    if (K < 1 || K > MAXK || R < 0) return lfail("attn: need 1 <= K <= 32");
+    if (R == 0) return 0;
+#define FWD(KM) hipLaunchKernelGGL(attn_fwd_kernel<KM>, dim3((R + 3) / 4), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, \
+                                   q, k, v, kvs, nei, out, outs, alpha, R, K)
+    if (K <= 4) FWD(4);
+    else if (K <= 8) FWD(8);
+    else if (K <= 16) FWD(16);
+    else FWD(32);
+#undef FWD
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_attn_bwd(const float *q, const float *k, const float *v, int32_t kvs, const float *alpha, const float *dout,
+                 int32_t douts, float *dq, float *dk, float *dv, int32_t R, int32_t K, void *stream) {
+    if (K < 1 || K > MAXK || R < 0) return lfail("attn: need 1 <= K <= 32");
+    if (R == 0) return 0;
+#define BWD(KM) hipLaunchKernelGGL(attn_bwd_kernel<KM>, dim3((R + 3) / 4), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, \
+                                   q, k, v, kvs, alpha, dout, douts, dq, dk, dv, R, K)
+    if (K <= 4) BWD(4);
+    else if (K <= 8) BWD(8);
+    else if (K <= 16) BWD(16);
+    else BWD(32);
+#undef BWD
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+static int make_fields(Fields &F, int n, const int32_t *widths, int rw) {
+    if (n < 1 || n > AAC_MAX_FIELDS) return lfail("replay: 1..16 fields");
+    F.n = n;
+    F.offset[0] = 0;
+    for (int f = 0; f < n; ++f) {
+        F.width[f] = widths[f];
+        F.offset[f + 1] = F.offset[f] + widths[f];
+    }
+    for (int f = n; f < AAC_MAX_FIELDS; ++f) F.offset[f + 1] = INT_MAX;
+    if (F.offset[n] != rw) return lfail("replay: field widths must sum to row_width");
+    return 0;
+}
+
+int aac_replay_push(float *ring, int32_t rw, int64_t cap, int64_t *meta, int32_t n, const void *const *srcs,
+                    const int32_t *widths, const int32_t *dtypes, int32_t E, void *stream) {
+    Fields F{};
+    if (make_fields(F, n, widths, rw)) return -1;
+    if (E < 1 || E > cap) return lfail("replay: need 1 <= E <= capacity");
+    for (int f = 0; f < n; ++f) {
+        F.src[f] = srcs[f];
+        F.dtype[f] = dtypes ? dtypes[f] : 0;
+    }
+    hipLaunchKernelGGL(push_kernel, dim3(E), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, ring, rw, cap, meta, F);
+    hipLaunchKernelGGL(meta_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, meta, cap, E);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_replay_sample(const int64_t *meta, int32_t B, uint64_t seed, uint64_t *counter, int32_t *idx, void *stream) {
+    if (B < 1 || B > 4096) return lfail("replay: 1 <= B <= 4096");
+    hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, meta, B, seed, counter, idx);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_replay_gather(const float *ring, int32_t rw, const int32_t *idx, int32_t B, int32_t n, float *const *dsts,
+                      const int32_t *widths, void *stream) {
+    Fields F{};
+    if (make_fields(F, n, widths, rw)) return -1;
+    for (int f = 0; f < n; ++f) F.dst[f] = dsts[f];
+    hipLaunchKernelGGL(gather_kernel, dim3(B), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, ring, rw, idx, F);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_adam_flat(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2, float eps,
+                  const int32_t *step, void *stream) {
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, p, g, m, v, n, lr,
+                       b1, b2, eps, step);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *stream) {
+    const float keep = (float)(1.0 - (double)tau);
+    hipLaunchKernelGGL(polyak_kernel, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, tgt, src, n,
+                       keep, tau);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, int32_t eps_end, float noise_start,
+                    uint64_t seed, uint64_t *counter, float *noise_out, void *stream) {
+    const int64_t rows = (int64_t)E * N;
+    hipLaunchKernelGGL(noise_kernel, dim3((unsigned)((rows + LEARN_BLOCK - 1) / LEARN_BLOCK)), dim3(LEARN_BLOCK), 0,
+                       (hipStream_t)stream, act, E, N, episode, eps_end, noise_start, seed, counter, noise_out);
+    hipLaunchKernelGGL(counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,251 @@
+"""MADDPG learner of ``one_model_att`` on the device (ATT/maddpg:31-570).
+
+Batched API (what the bench and the vectorised loop use):
+    act(own, radar, nei, episode)        choose_action for all E envs (actor + noise kernel)
+    push(...)                            replay push of E transitions (one HIP launch)
+    update(B)                            one ``update_myown``-equivalent: N gradient iterations
+                                         (sample B -> critic Adam step -> actor Adam step) then the
+                                         Polyak update, replayed from a captured HIP graph.
+Reference API (drop-in for ma_main, E = 1): ``choose_action``, ``update_myown``, ``memory``,
+``save_model``, ``load_model`` with the reference's signatures and return values.
+
+Canonical contract: D0 = 6 + 4(N-1) (R1), neighbour tensor (K, 6) (R2),
+N-agent critic (R3), the actor always gets [own, radar, nei] (R4).
+"""
+import math
+import os
+import warnings
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from .memory import DeviceReplay, ReplayMemory
+from .networks import ActorNetwork_ATT_TwoPortion, CriticCombine, FlatParams
+
+
+class _Adam:
+    """torch.optim.Adam (defaults, lr from the reference) on a FlatParams buffer."""
+
+    def __init__(self, flat, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.flat, self.lr, self.betas, self.eps = flat, lr, betas, eps
+        self.exp_avg = torch.zeros_like(flat.data)
+        self.exp_avg_sq = torch.zeros_like(flat.data)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=flat.data.device)
+
+    def zero_grad(self):
+        self.flat.zero_grad()
+
+    def step(self):
+        self.step_t.add_(1)
+        ops.adam_flat(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.step_t, self.lr,
+                      self.betas[0], self.betas[1], self.eps)
+
+    def state(self):
+        return [self.exp_avg, self.exp_avg_sq, self.step_t]
+
+
+def _noise_scale(episode, eps_end, start_scale=1, end_scale=0):
+    """get_custom_linear_scaling_factor (ATT/maddpg:563-570)."""
+    if episode <= eps_end:
+        slope = (end_scale - start_scale) / (eps_end - 1)
+        return start_scale + slope * (episode - 1)
+    return end_scale
+
+
+class MADDPG:
+    def __init__(self, actor_dim, critic_dim, dim_act, actor_hidden_state_size=64, gru_history_length=10,
+                 n_agents=5, args=None, cr_lr=1e-3, ac_lr=1e-3, gamma=0.95, tau=0.01,
+                 full_observable_critic_flag=True, device=None, seed=None, memory_length=None, batch_size=None,
+                 process_group=None):
+        self.args = args
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.n_agents = N = int(n_agents)
+        self.n_actions = int(dim_act)
+        self.D0 = 6 + 4 * (N - 1)
+        if actor_dim[0] != self.D0:
+            warnings.warn(f"actor_dim[0]={actor_dim[0]} != 6+4(N-1)={self.D0}; using the env's width (contract R1)")
+        self.n_actor_dim = [self.D0, actor_dim[1], actor_dim[2]]
+        self.n_critic_dim = [self.D0, critic_dim[1], critic_dim[2]]
+        if not full_observable_critic_flag:
+            raise NotImplementedError("one_model_att runs with full_observable_critic_flag=True (ATT/main:77)")
+        if seed is not None:
+            torch.manual_seed(seed)
+        self.actors = ActorNetwork_ATT_TwoPortion(self.n_actor_dim, dim_act).to(self.device)
+        self.critics = CriticCombine(self.n_critic_dim, N, dim_act).to(self.device)
+        self.actors_target = ActorNetwork_ATT_TwoPortion(self.n_actor_dim, dim_act).to(self.device)
+        self.critics_target = CriticCombine(self.n_critic_dim, N, dim_act).to(self.device)
+        self.fa, self.fc = FlatParams(self.actors), FlatParams(self.critics)
+        self.fa_t, self.fc_t = FlatParams(self.actors_target), FlatParams(self.critics_target)
+        self.fa_t.data.copy_(self.fa.data)
+        self.fc_t.data.copy_(self.fc.data)
+        for p in list(self.actors_target.parameters()) + list(self.critics_target.parameters()):
+            p.requires_grad_(False)
+        self.GAMMA, self.tau = float(gamma), float(tau)
+        self.actor_optimizer = _Adam(self.fa, ac_lr)
+        self.critic_optimizer = _Adam(self.fc, cr_lr)
+        mem_len = memory_length or (getattr(args, "memory_length", None) or int(1e5))
+        self.batch_size = batch_size or (getattr(args, "batch_size", None) or 512)
+        self.memory = ReplayMemory(mem_len, device=self.device)
+        self.replay = None
+        self.var = [1.0 for _ in range(N)]
+        self.noise_seed = int(seed or 0) * 7919 + 1
+        self.noise_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self._graph = None
+        self._graph_B = None
+        self.steps_done = 0
+        self.last_stats = None
+
+    # ------------------------------------------------------------------ batched API
+    def attach_replay(self, capacity, seed=0):
+        self.replay = DeviceReplay(capacity, self.n_agents, self.D0, 18, self.device, seed=seed)
+        return self.replay
+
+    @torch.no_grad()
+    def act(self, own, radar, nei, episode=None, noisy=True, eps_end=8000, noise_start=1.0, noise_out=None):
+        """Batched choose_action (ATT/maddpg:455-550): tanh actor + N(0, var^2) noise, clamp."""
+        a = self.actors([own, radar, nei]).contiguous()
+        if noisy:
+            ops.noise_clamp(a, episode, eps_end, noise_start, self.noise_seed, self.noise_counter, noise_out)
+        return a
+
+    def _allreduce(self, flat):
+        if self.world > 1:
+            torch.distributed.all_reduce(flat.grad, group=self.pg)
+            flat.grad.div_(self.world)
+
+    def _iteration(self, rep, B, agent, idx=None):
+        b = rep.sample_batch(B, idx)
+        with torch.no_grad():
+            na = self.actors_target([b["n_own"], b["n_radar"], b["n_nei"]])
+            q_next = self.critics_target([b["n_own"], b["n_radar"]], na).squeeze(-1)
+            done_any = (b["done"] == 1).any(dim=1).to(torch.float32)
+            target = b["rew"][:, agent] + self.GAMMA * q_next * (1 - done_any)
+        q = self.critics([b["s_own"], b["s_radar"]], b["act"])
+        loss_q = F.mse_loss(q, target.unsqueeze(1))
+        self.critic_optimizer.zero_grad()
+        loss_q.backward(inputs=list(self.critics.parameters()))
+        self._allreduce(self.fc)
+        self.critic_optimizer.step()
+        a_pi = self.actors([b["s_own"], b["s_radar"], b["s_nei"]])
+        loss_a = -self.critics([b["s_own"], b["s_radar"]], a_pi).mean()
+        self.actor_optimizer.zero_grad()
+        loss_a.backward(inputs=list(self.actors.parameters()))
+        self._allreduce(self.fa)
+        self.actor_optimizer.step()
+        return loss_q.detach(), loss_a.detach(), q.detach(), target
+
+    def _update_core(self, B, idx_list=None):
+        rep = self.replay if self.replay is not None else self.memory.dev
+        stats = []
+        for agent in range(self.n_agents):
+            stats.append(self._iteration(rep, B, agent, None if idx_list is None else idx_list[agent]))
+        ops.polyak_flat(self.fc_t.data, self.fc.data, self.tau)
+        ops.polyak_flat(self.fa_t.data, self.fa.data, self.tau)
+        return stats
+
+    def _snapshot(self):
+        rep = self.replay if self.replay is not None else self.memory.dev
+        ts = [self.fa.data, self.fc.data, self.fa_t.data, self.fc_t.data, rep.counter]
+        ts += self.actor_optimizer.state() + self.critic_optimizer.state()
+        return ts, [t.clone() for t in ts]
+
+    def capture(self, B, warmup=2):
+        """Capture one update_myown-equivalent into a HIP graph (state restored afterwards)."""
+        if self.world > 1:
+            self._graph = None
+            return None
+        ts, saved = self._snapshot()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._update_core(B)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_stats = self._update_core(B)
+        for t, v in zip(ts, saved):
+            t.copy_(v)
+        self._graph, self._graph_B = g, B
+        return g
+
+    def update(self, B=None, use_graph=True, idx_list=None):
+        """One update_myown-equivalent on the device replay (no host synchronisation)."""
+        B = B or self.batch_size
+        if idx_list is None and use_graph and self.world == 1:
+            if self._graph is None or self._graph_B != B:
+                self.capture(B)
+            self._graph.replay()
+            self.last_stats = self._graph_stats
+        else:
+            self.last_stats = self._update_core(B, idx_list)
+        return self.last_stats
+
+    # ------------------------------------------------------------------ reference API
+    def choose_action(self, state, cur_total_step, cur_episode, step, mini_noise_eps, noise_start_level,
+                      actor_hiddens=None, noisy=True):
+        """ATT/maddpg:455 signature; state = norm_state lists (E = 1)."""
+        N = self.n_agents
+        own = torch.from_numpy(np.stack(state[0])).float().to(self.device).reshape(1, N, -1)
+        grid = torch.from_numpy(np.stack(state[1])).float().to(self.device).reshape(1, N, -1)
+        nei = torch.stack([torch.from_numpy(np.stack(x)).float().reshape(N - 1, 6) for x in state[2]])
+        nei = nei.to(self.device).reshape(1, N, N - 1, 6)
+        for i in range(N):
+            self.var[i] = _noise_scale(cur_episode, mini_noise_eps, noise_start_level)
+        with torch.no_grad():
+            act = self.actors([own, grid, nei])[0]
+        noise_value = np.zeros(2)
+        if noisy:
+            acts = []
+            for i in range(N):
+                noise_value = np.random.randn(2) * self.var[i]
+                a = act[i] + torch.from_numpy(noise_value).float().to(self.device)
+                acts.append(torch.clamp(a, -1.0, 1.0))
+            act = torch.stack(acts)
+        self.steps_done += 1
+        hid = torch.zeros(N, self.n_actions)
+        if actor_hiddens is not None:
+            hid_in = torch.as_tensor(np.asarray(actor_hiddens), dtype=torch.float32)
+        else:
+            hid_in = torch.zeros(N, 64)
+        return act.cpu().numpy(), noise_value, hid_in, hid
+
+    def update_myown(self, i_episode, total_step_count, UPDATE_EVERY, single_eps_critic_cal_record,
+                     transfer_learning=False, wandb=None, full_observable_critic_flag=True):
+        """ATT/maddpg:219 signature and returns; the work is ``update`` on the device ring."""
+        if len(self.memory) <= self.batch_size:
+            return None, None, single_eps_critic_cal_record
+        if i_episode % UPDATE_EVERY != 0:
+            raise NotImplementedError("soft update every call (UPDATE_EVERY=1) as ATT/params:29")
+        stats = self.update(self.batch_size, use_graph=False)
+        c_loss = [s[0] for s in stats]
+        a_loss = [s[1] for s in stats]
+        for s in stats:
+            single_eps_critic_cal_record.append(s)
+        return c_loss, a_loss, single_eps_critic_cal_record
+
+    def save_model(self, episode, file_path):
+        """ATT/maddpg:131-139: actor state_dict only, reference key names."""
+        os.makedirs(file_path, exist_ok=True)
+        torch.save(self.actors.reference_state_dict(), os.path.join(file_path, f"episode_{episode}_actor_net.pth"))
+
+    def load_model(self, filePath):
+        """ATT/maddpg:106-129 (weights_only load)."""
+        for path in filePath:
+            self.actors.load_reference_state_dict(torch.load(path, weights_only=True, map_location="cpu"))
+        self.fa_t.data.copy_(self.fa.data)
+        self.fc_t.data.copy_(self.fc.data)
+
+
+def smoke_check():
+    """One tiny batched update on cuda:0 against the torch-CPU restatement (used by smoke())."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from oracle import learner_ref
+    learner_ref.check_one_update(MADDPG, device="cuda", N=3, B=64, E=32, tol=1e-4)

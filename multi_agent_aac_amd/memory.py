@@ -1,0 +1,115 @@
+"""Replay memory on the device (ATT/mem:6-23 ``ReplayMemory``).
+
+``DeviceReplay`` stores one transition per fixed-width fp32 row
+    [s_own (N*D0) | s_radar (N*18) | s_nei (N*K*6) | a (N*2) | r (N) | done (N) | s'_own | s'_radar | s'_nei]
+(660 floats = 2 640 B at N = 5) in a ring of ``capacity`` rows.  Push is one HIP launch for all E
+transitions of a step; sampling draws B distinct rows uniformly (``random.sample`` semantics) and
+gathers them into field-contiguous batch tensors, all on the device (graph-capturable: the ring
+position / size and the RNG counter live in device memory).
+
+``ReplayMemory`` keeps the reference's ``push(*8 fields)`` / ``sample(B)`` / ``len`` surface for
+an unchanged ``ma_main`` (E = 1); its rows land in the same device ring.
+"""
+from collections import namedtuple
+
+import torch
+
+from . import ops
+
+Experience = namedtuple("Experience", ("states", "actions", "next_states", "rewards", "dones", "history_info",
+                                       "cur_hidden", "next_hidden"))
+
+FIELDS = ("s_own", "s_radar", "s_nei", "act", "rew", "done", "n_own", "n_radar", "n_nei")
+
+
+class DeviceReplay:
+    def __init__(self, capacity, N, D0, R=18, device="cuda", seed=0):
+        self.N, self.D0, self.R, self.K = N, D0, R, N - 1
+        K = self.K
+        self.shapes = [(N, D0), (N, R), (N, K, 6), (N, 2), (N,), (N,), (N, D0), (N, R), (N, K, 6)]
+        self.widths = [int(torch.Size(s).numel()) for s in self.shapes]
+        self.dtypes = [0, 0, 0, 0, 0, 1, 0, 0, 0]
+        self.row_width = sum(self.widths)
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.ring = torch.zeros(self.capacity, self.row_width, dtype=torch.float32, device=self.device)
+        self.meta = torch.zeros(2, dtype=torch.int64, device=self.device)       # [next pos, size]
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)    # sampler RNG counter
+        self.seed = int(seed)
+        self.size = 0          # host mirror of meta[1] (pushes are host-initiated, so no sync needed)
+        self._batch = {}
+
+    def __len__(self):
+        return self.size
+
+    def push_batch(self, s_own, s_radar, s_nei, act, rew, done, n_own, n_radar, n_nei):
+        srcs = [s_own, s_radar, s_nei, act, rew, done, n_own, n_radar, n_nei]
+        E = s_own.shape[0]
+        for t in srcs:
+            assert t.is_contiguous() and t.device == self.device and t.shape[0] == E
+        ops.replay_push(self.ring, self.meta, srcs, self.widths, self.dtypes, E)
+        self.size = min(self.size + E, self.capacity)
+
+    def batch_buffers(self, B):
+        if B not in self._batch:
+            bufs = [torch.empty((B,) + s, dtype=torch.float32, device=self.device) for s in self.shapes]
+            idx = torch.empty(B, dtype=torch.int32, device=self.device)
+            self._batch[B] = (idx, dict(zip(FIELDS, bufs)), bufs)
+        return self._batch[B]
+
+    def sample_batch(self, B, idx=None):
+        """Draw B distinct rows (or use the given device indices) into static batch tensors."""
+        bidx, named, bufs = self.batch_buffers(B)
+        if idx is None:
+            ops.replay_sample(self.meta, B, self.seed, self.counter, bidx)
+        else:
+            bidx.copy_(idx)
+        ops.replay_gather(self.ring, bidx, bufs, self.widths)
+        return named
+
+
+class ReplayMemory:
+    """Reference surface (ATT/mem:6-23) over ``DeviceReplay``; states are the reference's
+    ``[own (N, D0), radar (N, 18), [nei_i (K, 1, 6) or (K, 6)] * N]`` lists."""
+
+    def __init__(self, capacity, device="cuda"):
+        self.capacity = int(capacity)
+        self.device = device
+        self.dev = None
+        self.memory = self       # reference code reads ``len(model.memory)``
+        self.position = 0
+
+    def _ensure(self, states):
+        if self.dev is None:
+            N, D0 = states[0].shape
+            self.dev = DeviceReplay(self.capacity, N, D0, states[1].shape[1], self.device)
+
+    def _obs(self, states):
+        own = torch.as_tensor(states[0], dtype=torch.float32).reshape(1, self.dev.N, self.dev.D0)
+        radar = torch.as_tensor(states[1], dtype=torch.float32).reshape(1, self.dev.N, self.dev.R)
+        nei = torch.stack([torch.as_tensor(x, dtype=torch.float32).reshape(self.dev.K, 6) for x in states[2]])
+        return [t.to(self.dev.device).contiguous() for t in (own, radar, nei.reshape(1, self.dev.N, self.dev.K, 6))]
+
+    def push(self, states, actions, next_states, rewards, dones, history_info=None, cur_hidden=None,
+             next_hidden=None):
+        self._ensure(states)
+        s = self._obs(states)
+        n = self._obs(next_states)
+        d = self.dev.device
+        a = torch.as_tensor(actions, dtype=torch.float32).reshape(1, self.dev.N, 2).to(d).contiguous()
+        r = torch.as_tensor(rewards, dtype=torch.float32).reshape(1, self.dev.N).to(d).contiguous()
+        dn = (torch.as_tensor(dones).reshape(1, self.dev.N) != 0).to(torch.uint8).to(d).contiguous()
+        self.dev.push_batch(s[0], s[1], s[2], a, r, dn, n[0], n[1], n[2])
+        self.position = (self.position + 1) % self.capacity
+
+    def sample(self, batch_size):
+        b = self.dev.sample_batch(batch_size)
+        out = []
+        for i in range(batch_size):
+            st = [b["s_own"][i], b["s_radar"][i], [b["s_nei"][i, k] for k in range(self.dev.N)]]
+            nx = [b["n_own"][i], b["n_radar"][i], [b["n_nei"][i, k] for k in range(self.dev.N)]]
+            out.append(Experience(st, b["act"][i], nx, b["rew"][i], b["done"][i], None, None, None))
+        return out
+
+    def __len__(self):
+        return 0 if self.dev is None else len(self.dev)

@@ -1,0 +1,120 @@
+"""torch bindings of the learner kernels in libaac_env.so (C ABI: include/aac_learn.h).
+
+Every op launches on torch's current stream (so it can be captured in a HIP graph) and raises
+if the native library is missing -- there is no eager-PyTorch fallback.
+"""
+import ctypes
+
+import torch
+
+from . import _native
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+f32 = ctypes.c_float
+u64 = ctypes.c_uint64
+
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        L = _native.lib()
+        L.aac_learn_last_error.restype = ctypes.c_char_p
+        L.aac_attn_fwd.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp]
+        L.aac_attn_bwd.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, i32, i32, vp]
+        L.aac_replay_push.argtypes = [vp, i32, i64, vp, i32, vp, vp, vp, i32, vp]
+        L.aac_replay_sample.argtypes = [vp, i32, u64, vp, vp, vp]
+        L.aac_replay_gather.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp]
+        L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
+        L.aac_polyak_flat.argtypes = [vp, vp, i64, f32, vp]
+        L.aac_noise_clamp.argtypes = [vp, i32, i32, vp, i32, f32, u64, vp, vp, vp]
+        _L = L
+    return _L
+
+
+def _chk(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {lib().aac_learn_last_error().decode(errors='replace')}")
+
+
+def _s():
+    return vp(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t, byte_offset=0):
+    return vp(t.data_ptr() + byte_offset) if t is not None else None
+
+
+# ----------------------------------------------------------------------------- attention
+class _MaskedAttention(torch.autograd.Function):
+    """ATT/nets:194-210 on (R rows, K neighbours, 64 dims); kv = [k | v] rows of 128."""
+
+    @staticmethod
+    def forward(ctx, q, kv, nei):
+        R, K = kv.shape[0], kv.shape[1]
+        q = q.contiguous()
+        kv = kv.contiguous()
+        nei = nei.contiguous()
+        out = torch.empty(R, 64, device=q.device, dtype=torch.float32)
+        alpha = torch.empty(R, K, device=q.device, dtype=torch.float32)
+        _chk(lib().aac_attn_fwd(_p(q), _p(kv), _p(kv, 256), 128, _p(nei), _p(out), 64, _p(alpha), R, K, _s()),
+             "aac_attn_fwd")
+        ctx.save_for_backward(q, kv, alpha)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, kv, alpha = ctx.saved_tensors
+        R, K = kv.shape[0], kv.shape[1]
+        dout = dout.contiguous()
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        _chk(lib().aac_attn_bwd(_p(q), _p(kv), _p(kv, 256), 128, _p(alpha), _p(dout), 64, _p(dq), _p(dkv),
+                                _p(dkv, 256), R, K, _s()), "aac_attn_bwd")
+        return dq, dkv, None
+
+
+def masked_attention(q, kv, nei):
+    """q (R, 64), kv (R, K, 128) = [k | v], nei (R, K, 6) mask source -> v_att (R, 64)."""
+    return _MaskedAttention.apply(q, kv, nei)
+
+
+# ----------------------------------------------------------------------------- optimiser
+def adam_flat(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    _chk(lib().aac_adam_flat(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), lr, beta1, beta2,
+                             eps, _p(step), _s()), "aac_adam_flat")
+
+
+def polyak_flat(target, source, tau):
+    _chk(lib().aac_polyak_flat(_p(target), _p(source), target.numel(), tau, _s()), "aac_polyak_flat")
+
+
+def noise_clamp(act, episode, eps_end, noise_start, seed, counter, noise_out=None):
+    E, N = act.shape[0], act.shape[1]
+    _chk(lib().aac_noise_clamp(_p(act), E, N, _p(episode), eps_end, noise_start, u64(seed), _p(counter),
+                               _p(noise_out), _s()), "aac_noise_clamp")
+
+
+# ----------------------------------------------------------------------------- replay
+def replay_push(ring, meta, srcs, widths, dtypes, E):
+    n = len(srcs)
+    arr = (vp * n)(*[s.data_ptr() for s in srcs])
+    w = (i32 * n)(*widths)
+    d = (i32 * n)(*dtypes)
+    _chk(lib().aac_replay_push(_p(ring), ring.shape[1], ring.shape[0], _p(meta), n, arr, w, d, E, _s()),
+         "aac_replay_push")
+
+
+def replay_sample(meta, B, seed, counter, idx_out):
+    _chk(lib().aac_replay_sample(_p(meta), B, u64(seed), _p(counter), _p(idx_out), _s()), "aac_replay_sample")
+
+
+def replay_gather(ring, idx, dsts, widths):
+    n = len(dsts)
+    arr = (vp * n)(*[t.data_ptr() for t in dsts])
+    w = (i32 * n)(*widths)
+    _chk(lib().aac_replay_gather(_p(ring), ring.shape[1], _p(idx), idx.shape[0], n, arr, w, _s()),
+         "aac_replay_gather")

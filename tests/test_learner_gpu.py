@@ -1,0 +1,172 @@
+"""GPU tests of the learner kernels (attention, replay, Adam, Polyak, noise) and of the full
+device update_myown against the torch-CPU restatement (oracle/learner_ref.py)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import learner_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref_attention(q, k, v, nei):
+    mask = nei.mean(axis=2, keepdim=True).bool()
+    score = torch.bmm(k, q.unsqueeze(2))
+    sm = score.clone()
+    sm[~mask] = float("-inf")
+    alpha = F.softmax(sm / np.sqrt(64), dim=1)
+    am = alpha.clone()
+    am[~mask] = 0
+    return torch.sum(v * am, axis=1)
+
+
+@pytest.mark.parametrize("K", [1, 2, 4, 7, 15])
+def test_attention_fwd_bwd(native_lib, K):
+    from multi_agent_aac_amd import ops
+    torch.manual_seed(K)
+    R = 1000
+    q = torch.randn(R, 64, dtype=torch.float64)
+    kv = torch.randn(R, K, 128, dtype=torch.float64)
+    nei = torch.randn(R, K, 6, dtype=torch.float64)
+    nei[torch.rand(R, K) < 0.3] = 0.0
+    nei[:5] = 0.0                                     # all-masked rows
+    dout = torch.randn(R, 64, dtype=torch.float64)
+    qr, kvr = q.clone().requires_grad_(), kv.clone().requires_grad_()
+    ref = _ref_attention(qr, kvr[..., :64], kvr[..., 64:], nei)
+    ref.backward(dout)
+    qg = q.float().to(DEV).requires_grad_()
+    kvg = kv.float().to(DEV).requires_grad_()
+    out = ops.masked_attention(qg, kvg, nei.float().to(DEV))
+    out.backward(dout.float().to(DEV))
+    assert torch.isfinite(out).all() and torch.isfinite(qg.grad).all() and torch.isfinite(kvg.grad).all()
+    np.testing.assert_allclose(out.detach().cpu().double(), ref.detach(), atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(qg.grad.cpu().double(), qr.grad, atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(kvg.grad.cpu().double(), kvr.grad, atol=2e-5, rtol=1e-5)
+    assert out[:5].abs().max() == 0 and qg.grad[:5].abs().max() == 0
+
+
+def test_replay_push_gather_sample(native_lib):
+    from multi_agent_aac_amd.memory import DeviceReplay
+    N, D0, E, cap = 5, 22, 300, 1000
+    rep = DeviceReplay(cap, N, D0, device=DEV, seed=3)
+    host = []
+    for p in range(5):                      # wraps around the ring (1500 > 1000)
+        tr = learner_ref.random_transitions(E, N, p)
+        rep.push_batch(*[tr[k].to(DEV).contiguous() for k in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
+                                                               "n_own", "n_radar", "n_nei")])
+        host.append(tr)
+    assert len(rep) == cap and int(rep.meta[0]) == 1500 % cap and int(rep.meta[1]) == cap
+    # ring row r holds transition (r - (1500 % cap)) mod cap of the last 1000 pushed
+    allh = {k: torch.cat([h[k] for h in host])[-cap:] for k in host[0]}
+    start = 1500 % cap
+    idx = torch.arange(0, cap, 7, dtype=torch.int32)
+    b = rep.sample_batch(len(idx), idx.to(DEV))
+    src = (idx.long() - start) % cap
+    for k, v in b.items():
+        assert torch.equal(v.cpu(), allh[k][src].to(torch.float32)), k
+    # sampler: distinct, in range, deterministic in (seed, counter), ~uniform
+    counts = np.zeros(cap)
+    c0 = int(rep.counter)
+    for t in range(200):
+        b = rep.sample_batch(512)
+        ids = rep.batch_buffers(512)[0].cpu().numpy()
+        assert len(np.unique(ids)) == 512 and ids.min() >= 0 and ids.max() < cap
+        counts[ids] += 1
+    assert int(rep.counter) == c0 + 200
+    expected = 200 * 512 / cap
+    chi2 = ((counts - expected) ** 2 / expected).sum()
+    assert chi2 < cap + 6 * np.sqrt(2 * cap), chi2
+    rep.counter.fill_(c0)
+    rep.sample_batch(512)
+    first = rep.batch_buffers(512)[0].clone()
+    rep.counter.fill_(c0)
+    rep.sample_batch(512)
+    assert torch.equal(first, rep.batch_buffers(512)[0])
+
+
+def test_adam_polyak_flat(native_lib):
+    from multi_agent_aac_amd import ops
+    torch.manual_seed(0)
+    n = 100003
+    p = torch.randn(n)
+    ref = p.clone().requires_grad_()
+    opt = torch.optim.Adam([ref], lr=1e-3)
+    pd = p.to(DEV)
+    m, v = torch.zeros_like(pd), torch.zeros_like(pd)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for t in range(5):
+        g = torch.randn(n)
+        ref.grad = g.clone()
+        opt.step()
+        step.add_(1)
+        ops.adam_flat(pd, g.to(DEV), m, v, step, 1e-3)
+    np.testing.assert_allclose(pd.cpu(), ref.detach(), atol=1e-6, rtol=1e-6)
+    tgt, src = torch.randn(n), torch.randn(n)
+    want = (1 - 0.01) * tgt + 0.01 * src
+    td = tgt.to(DEV)
+    ops.polyak_flat(td, src.to(DEV), 0.01)
+    np.testing.assert_allclose(td.cpu(), want, atol=1e-7, rtol=1e-6)
+
+
+def test_noise_clamp_schedule(native_lib):
+    from multi_agent_aac_amd import ops
+    E, N = 20000, 5
+    act = torch.zeros(E, N, 2, device=DEV)
+    ep = torch.full((E,), 4001, dtype=torch.int32, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    noise = torch.empty(E, N, 2, device=DEV)
+    ops.noise_clamp(act, ep, 8000, 1.0, 7, ctr, noise)
+    var = 1 + (-1 / 7999) * 4000
+    z = noise.cpu().double() / var
+    assert abs(float(z.mean())) < 0.02 and abs(float(z.std()) - 1) < 0.02
+    assert torch.equal(act.cpu(), noise.cpu().clamp(-1, 1))
+    assert int(ctr) == 1
+    ep.fill_(8001)
+    act.zero_()
+    ops.noise_clamp(act, ep, 8000, 1.0, 7, ctr, noise)
+    assert act.abs().max() == 0
+
+
+@pytest.mark.parametrize("N,B", [(3, 64), (5, 256)])
+def test_update_matches_cpu_restatement(native_lib, N, B):
+    from multi_agent_aac_amd.maddpg import MADDPG
+    assert learner_ref.check_one_update(MADDPG, device=DEV, N=N, B=B, E=128, tol=1e-5, iters=2)
+
+
+def test_graph_replay_equals_eager(native_lib):
+    from multi_agent_aac_amd.maddpg import MADDPG
+    N, B, E = 5, 128, 256
+    ms = []
+    for _ in range(2):
+        m = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=N, device=DEV, seed=1, batch_size=B)
+        rep = m.attach_replay(4 * E, seed=9)
+        for p in range(3):
+            tr = learner_ref.random_transitions(E, N, p)
+            rep.push_batch(*[tr[k].to(DEV).contiguous() for k in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
+                                                                   "n_own", "n_radar", "n_nei")])
+        ms.append(m)
+    for _ in range(3):
+        ms[0].update(B, use_graph=True)
+        ms[1].update(B, use_graph=False)
+    torch.cuda.synchronize()
+    for a, b in ((ms[0].fa.data, ms[1].fa.data), (ms[0].fc.data, ms[1].fc.data), (ms[0].fc_t.data, ms[1].fc_t.data)):
+        np.testing.assert_allclose(a.cpu(), b.cpu(), atol=1e-6, rtol=1e-5)
+
+
+def test_actor_pth_roundtrip(native_lib, tmp_path):
+    from multi_agent_aac_amd.maddpg import MADDPG
+    m = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=5, device=DEV, seed=2)
+    m.save_model(7, str(tmp_path))
+    sd = torch.load(tmp_path / "episode_7_actor_net.pth", weights_only=True)
+    ref = learner_ref.RefActor([22, 18, 6], 2)
+    ref.load_state_dict(sd)                      # reference key names and shapes
+    own, grid = torch.randn(40, 22), torch.rand(40, 18) * 15
+    nei = torch.randn(40, 4, 6)
+    want = ref([own, grid, nei])
+    got = m.actors([own.to(DEV), grid.to(DEV), nei.to(DEV)]).cpu()
+    np.testing.assert_allclose(got.detach(), want.detach(), atol=1e-5)
+    m2 = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=5, device=DEV, seed=3)
+    m2.load_model([str(tmp_path / "episode_7_actor_net.pth")])
+    assert torch.equal(m2.fa.data, m.fa.data)
