@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--memory", type=int, default=100000)
     p.add_argument("--radar", default="combined", choices=["drones", "obstacles", "combined"])
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
@@ -60,13 +61,9 @@ def parse():
     return p.parse_args()
 
 
-def setup_dist():
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if ws > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+def setup_dist(backend):
+    from multi_agent_aac_amd import parallel
+    ws, rank, local, _ = parallel.init_from_env(backend)
     return ws, rank, local
 
 
@@ -220,7 +217,7 @@ def main():
     if ws0 == 1 and not a.no_cpu_baseline:
         # before any GPU initialisation: the pool's children must not inherit a GPU context
         cpu = cpu_baseline(a.envs, a.agents, a.batch, a.radar, a.cpu_seconds)
-    ws, rank, local = setup_dist()
+    ws, rank, local = setup_dist(a.backend)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(777 + rank)
     tr = Trainer(a.envs, a.agents, a.batch, a.memory, a.radar, seed=rank,

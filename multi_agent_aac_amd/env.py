@@ -61,6 +61,8 @@ class BatchedEnv:
         if not torch.cuda.is_available():
             raise RuntimeError("BatchedEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         occ = np.asarray(occ, dtype=np.uint8)
         if occ.ndim == 2:
             occ = occ[None]

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from . import ops
+from . import ops, parallel
 from .memory import DeviceReplay, ReplayMemory
 from .networks import ActorNetwork_ATT_TwoPortion, CriticCombine, FlatParams
 
@@ -61,6 +61,8 @@ class MADDPG:
                  process_group=None):
         self.args = args
         self.device = torch.device(device) if device is not None else torch.device("cuda")
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.n_agents = N = int(n_agents)
         self.n_actions = int(dim_act)
         self.D0 = 6 + 4 * (N - 1)
@@ -114,8 +116,7 @@ class MADDPG:
 
     def _allreduce(self, flat):
         if self.world > 1:
-            torch.distributed.all_reduce(flat.grad, group=self.pg)
-            flat.grad.div_(self.world)
+            parallel.allreduce_mean_(flat.grad, self.pg)
 
     def _iteration(self, rep, B, agent, idx=None):
         b = rep.sample_batch(B, idx)

@@ -32,6 +32,8 @@ class DeviceReplay:
         self.row_width = sum(self.widths)
         self.capacity = int(capacity)
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.ring = torch.zeros(self.capacity, self.row_width, dtype=torch.float32, device=self.device)
         self.meta = torch.zeros(2, dtype=torch.int64, device=self.device)       # [next pos, size]
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)    # sampler RNG counter
