@@ -40,9 +40,11 @@ int aac_attn_bwd(const float *q, const float *k, const float *v, int32_t kv_stri
  * meta (device int64[2]) = {next write position, current size}; updated on the device. */
 int aac_replay_push(float *ring, int32_t row_width, int64_t capacity, int64_t *meta, int32_t n_fields,
                     const void *const *srcs, const int32_t *widths, const int32_t *dtypes, int32_t E, void *stream);
-/* B distinct indices uniform in [0, meta[1]) (B <= 4096, meta[1] >= B), deterministic in
- * (seed, *counter); *counter (device uint64) is advanced by the kernel. */
-int aac_replay_sample(const int64_t *meta, int32_t B, uint64_t seed, uint64_t *counter, int32_t *idx, void *stream);
+/* n_batches independent batches of B distinct indices uniform in [0, meta[1]) (B <= 4096,
+ * meta[1] >= B) into idx[n_batches][B]; deterministic in (seed, *counter); *counter (device
+ * uint64) is advanced by one per call. */
+int aac_replay_sample(const int64_t *meta, int32_t B, int32_t n_batches, uint64_t seed, uint64_t *counter,
+                      int32_t *idx, void *stream);
 /* dsts[f][b][widths[f]] = ring[idx[b]][field f]. */
 int aac_replay_gather(const float *ring, int32_t row_width, const int32_t *idx, int32_t B, int32_t n_fields,
                       float *const *dsts, const int32_t *widths, void *stream);

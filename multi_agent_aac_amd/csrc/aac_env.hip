@@ -231,8 +231,9 @@ __device__ bool ray_hline(double cx, double cy, double ex, double ey, double ly,
 __device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, double cy, double ex, double ey,
                                   double len) {
     double mind = len, d;
-    int i0 = (int)floor((cx - 20.0 - A.gx0) / 10.0), i1 = (int)ceil((cx + 20.0 - A.gx0) / 10.0);
-    int j0 = (int)floor((cy - 20.0 - A.gy0) / 10.0), j1 = (int)ceil((cy + 20.0 - A.gy0) / 10.0);
+    // only cells whose square meets the segment's bounding box can meet the segment
+    int i0 = (int)floor((fmin(cx, ex) - 5.0 - A.gx0) / 10.0), i1 = (int)ceil((fmax(cx, ex) + 5.0 - A.gx0) / 10.0);
+    int j0 = (int)floor((fmin(cy, ey) - 5.0 - A.gy0) / 10.0), j1 = (int)ceil((fmax(cy, ey) + 5.0 - A.gy0) / 10.0);
     i0 = i0 < 0 ? 0 : i0;
     j0 = j0 < 0 ? 0 : j0;
     i1 = i1 > A.gw - 1 ? A.gw - 1 : i1;
@@ -288,17 +289,18 @@ __device__ double pairwise_sum(const double *a, int n) {
     return res;
 }
 
-// LDS image of one workgroup's envs
+// LDS image of one workgroup's envs (A = epb * N agents, <= BLOCK)
 struct Lds {
     double2 pos[BLOCK], vel[BLOCK], ppos[BLOCK], pvel[BLOCK], goal[BLOCK];
     double rew[BLOCK];
-    uint8_t flags[BLOCK];   // bit0 done, bit1 check_goal, bit2 reach (after step), bit3 bound, bit4 drone, bit5 last==nearest
+    uint8_t flags[BLOCK];   // bit0 done, bit1 check_goal, bit2 reach, bit3 bound, bit4 drone, bit5 last==nearest
+    uint8_t active[BLOCK];  // per local env (reset kernel)
     int32_t idx[BLOCK];
     uint8_t occ[MAX_MAP_BYTES];
 };
 
-// observation of agent i of env e (cur_state_norm_state_v3, ATT/env:837-1493)
-__device__ void observe(const Args &A, const Lds &S, int e, int i, int base, const uint8_t *occ) {
+// own + neighbour observation and tdCPA of agent i of env e (ATT/env:1285-1469)
+__device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int base) {
     const int N = A.N, K = A.K;
     const size_t ai = (size_t)e * N + i;
     const double *b = A.bound;
@@ -362,40 +364,45 @@ __device__ void observe(const Args &A, const Lds &S, int e, int i, int base, con
         A.conf_cur[ai] = cc;
         A.conf_pre[ai] = cp;
     }
-    // radar (18 rays from the centre, length radar_len)
-    float *rad = A.radar + ai * NRAY;
-    const double reach2 = (pb + 1e-6) * (pb + 1e-6);
-    for (int r = 0; r < NRAY; ++r) {
-        double ex = px + A.radar_len * c_tab.ray_c[r], ey = py + A.radar_len * c_tab.ray_s[r];
-        double len = gdist(ex, ey, px, py);
-        double dd = len, dob = len;
-        if (A.radar_mode != AAC_RADAR_OBSTACLES) {
-            double shortest = INFINITY;
-            double ddx = ex - px, ddy = ey - py;
-            double inv = 1.0 / (ddx * ddx + ddy * ddy);
-            for (int j = 0; j < N; ++j) {
-                if (j == i) continue;
-                const double2 q = S.pos[base + j];
-                // exact pre-filter: the 64-gon lies inside the circle of radius pb (+1e-15)
-                double wx = q.x - px, wy = q.y - py;
-                double tt = (wx * ddx + wy * ddy) * inv;
-                tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
-                double qx = tt * ddx - wx, qy = tt * ddy - wy;
-                if (qx * qx + qy * qy > reach2) continue;
-                double t;
-                if (!ray_poly_entry(px, py, ex, ey, q.x, q.y, pb, t)) continue;
-                double ix = px + t * (ex - px), iy = py + t * (ey - py);
-                double d = gdist(ix, iy, px, py);
-                if (d < shortest) {
-                    shortest = d;
-                    dd = d;
-                }
+}
+
+// one radar ray r of agent i (ATT/env:1089-1164 drones, OM/env:1089-1141 obstacles)
+__device__ float radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ) {
+    const int N = A.N;
+    const double pb = A.pb;
+    const double2 p = S.pos[base + i];
+    const double px = p.x, py = p.y;
+    const double ex = px + A.radar_len * c_tab.ray_c[r], ey = py + A.radar_len * c_tab.ray_s[r];
+    const double len = gdist(ex, ey, px, py);
+    double dd = len, dob = len;
+    if (A.radar_mode != AAC_RADAR_OBSTACLES) {
+        const double reach2 = (pb + 1e-6) * (pb + 1e-6);
+        double shortest = INFINITY;
+        const double ddx = ex - px, ddy = ey - py;
+        const double inv = 1.0 / (ddx * ddx + ddy * ddy);
+        for (int j = 0; j < N; ++j) {
+            if (j == i) continue;
+            const double2 q = S.pos[base + j];
+            // exact pre-filter: the GEOS 64-gon lies inside the circle of radius pb (+1e-15)
+            double wx = q.x - px, wy = q.y - py;
+            double tt = (wx * ddx + wy * ddy) * inv;
+            tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
+            double qx = tt * ddx - wx, qy = tt * ddy - wy;
+            if (qx * qx + qy * qy > reach2) continue;
+            double t;
+            if (!ray_poly_entry(px, py, ex, ey, q.x, q.y, pb, t)) continue;
+            double ix = px + t * (ex - px), iy = py + t * (ey - py);
+            double d = gdist(ix, iy, px, py);
+            if (d < shortest) {
+                shortest = d;
+                dd = d;
             }
         }
-        if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, px, py, ex, ey, len);
-        double val = A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
-        rad[r] = (float)val;
     }
+    if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, px, py, ex, ey, len);
+    const double val =
+        A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
+    return (float)val;
 }
 
 __device__ inline void load_maps(const Args &A, Lds &S) {
@@ -403,23 +410,43 @@ __device__ inline void load_maps(const Args &A, Lds &S) {
     for (int k = threadIdx.x; k < bytes; k += BLOCK) S.occ[k] = A.occ[k];
 }
 
+// all radar rays of the workgroup's (active) agents: one work item per (agent, ray)
+__device__ inline void radar_phase(const Args &A, const Lds &S, int e0, int nagents, bool check_active) {
+    for (int w = threadIdx.x; w < nagents * NRAY; w += BLOCK) {
+        const int la = w / NRAY, r = w - la * NRAY;
+        const int le = la / A.N, i = la - le * A.N;
+        const int e = e0 + le;
+        if (e >= A.E) continue;
+        if (check_active && !S.active[le]) continue;
+        const uint8_t *occ = S.occ + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
+        A.radar[((size_t)e * A.N + i) * NRAY + r] = radar_ray(A, S, i, r, le * A.N, occ);
+    }
+}
+
 // --------------------------------------------------------------------------------- step
+// Phases: (1) kinematics, one thread per agent; (2) radar, one work item per (agent, ray) over
+// all 256 threads; (3) observation + ss_reward predicates, one thread per agent; (4) team reward
+// and episode termination, one thread per env.
 __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__restrict__ act) {
     __shared__ Lds S;
     const int N = A.N;
-    const int le = threadIdx.x / N, i = threadIdx.x - le * N;
-    const int e = blockIdx.x * A.epb + le;
-    const bool active = (le < A.epb) && (e < A.E);
+    const int nag = A.epb * N;
+    const int e0 = blockIdx.x * A.epb;
+    const int t = threadIdx.x;
+    const int le = t / N, i = t - le * N;
+    const int e = e0 + le;
+    const bool active = (t < nag) && (e < A.E);
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
     load_maps(A, S);
 
     // ---- a1: kinematics (ATT/env:2639-2713)
-    double2 np = make_double2(0.0, 0.0), nv = np, pp = np, pv = np;
+    double2 np = make_double2(0.0, 0.0), pp = np;
     if (active) {
         pp = A.pos[ai];
-        pv = A.vel[ai];
-        float2 a = act[ai];
+        const double2 pv = A.vel[ai];
+        const float2 a = act[ai];
+        double2 nv;
         double ax = (double)a.x * A.acc_max, ay = (double)a.y * A.acc_max;
         double cvx = pv.x + ax * A.dt, cvy = pv.y + ay * A.dt;
         if (npnorm(cvx, cvy) >= A.vmax) {
@@ -433,16 +460,17 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
         A.pre_vel[ai] = pv;
         A.pos[ai] = np;
         A.vel[ai] = nv;
-        S.pos[threadIdx.x] = np;
-        S.vel[threadIdx.x] = nv;
-        S.ppos[threadIdx.x] = pp;
-        S.pvel[threadIdx.x] = pv;
-        S.goal[threadIdx.x] = A.goal[ai];
+        S.pos[t] = np;
+        S.vel[t] = nv;
+        S.ppos[t] = pp;
+        S.pvel[t] = pv;
+        S.goal[t] = A.goal[ai];
     }
     __syncthreads();
+    radar_phase(A, S, e0, nag, false);
     if (active) {
         const uint8_t *occ = S.occ + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
-        observe(A, S, e, i, base, occ);
+        observe_agent(A, S, e, i, base);
 
         // ---- ss_reward (ATT/env:2133-2603)
         const double px = np.x, py = np.y, pb = A.pb;
@@ -484,7 +512,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
                 }
         }
         if (building) A.wall[ai] += 1;
-        const double2 g = S.goal[threadIdx.x];
+        const double2 g = S.goal[t];
         const int goal = goal_reached(px, py, g.x, g.y, pb);
         const int cur = A.wp_cur[ai];
         const double2 w0 = A.wp[(size_t)ai * A.W + cur];
@@ -518,14 +546,14 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
         }
         if (cg) m |= 32;
         fl |= (uint8_t)(done | (cg << 1) | (reach << 2));
-        S.rew[threadIdx.x] = r;
-        S.flags[threadIdx.x] = fl;
+        S.rew[t] = r;
+        S.flags[t] = fl;
         A.done[ai] = (uint8_t)done;
         A.mask[ai] = m;
     }
     __syncthreads();
     if (active) {
-        double team = A.team_reward ? pairwise_sum(&S.rew[base], N) : S.rew[threadIdx.x];
+        double team = A.team_reward ? pairwise_sum(&S.rew[base], N) : S.rew[t];
         A.reward[ai] = (float)team;
         if (i == 0) {
             int any_done = 0, all_goal = 1, all_reach = 1, b0 = 0, b2 = 0, b3 = 0;
@@ -553,10 +581,21 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
 __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     __shared__ Lds S;
     const int N = A.N;
-    const int le = threadIdx.x / N, i = threadIdx.x - le * N;
-    const int e = blockIdx.x * A.epb + le;
-    const bool in_range = (le < A.epb) && (e < A.E);
-    const bool active = in_range && (R.mask == nullptr || R.mask[e] != 0);
+    const int nag = A.epb * N;
+    const int e0 = blockIdx.x * A.epb;
+    const int t = threadIdx.x;
+    // which of this workgroup's envs reset; skip the whole workgroup if none (the common case)
+    if (t < A.epb) {
+        const int e = e0 + t;
+        S.active[t] = (e < A.E) && (R.mask == nullptr || R.mask[e] != 0);
+    }
+    __syncthreads();
+    int any = 0;
+    for (int k = 0; k < A.epb; ++k) any |= S.active[k];
+    if (!any) return;
+    const int le = t / N, i = t - le * N;
+    const int e = e0 + le;
+    const bool active = (t < nag) && (e < A.E) && S.active[le];
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
     load_maps(A, S);
@@ -573,7 +612,10 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
                 bool ok = true;
                 for (int b = 0; b < a; ++b) {
                     double2 o = R.bank_start[S.idx[base + b]];
-                    if (!(npnorm(s.x - o.x, s.y - o.y) > A.pb * 2)) { ok = false; break; }
+                    if (!(npnorm(s.x - o.x, s.y - o.y) > A.pb * 2)) {
+                        ok = false;
+                        break;
+                    }
                 }
                 if (ok) break;
             }
@@ -607,18 +649,15 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         A.reach[ai] = 0;
         A.wall[ai] = 0;
         if (i == 0) A.step[e] = 0;
-        S.pos[threadIdx.x] = st;
-        S.ppos[threadIdx.x] = st;
-        S.vel[threadIdx.x] = z;
-        S.pvel[threadIdx.x] = z;
-        S.goal[threadIdx.x] = A.goal[ai];
+        S.pos[t] = st;
+        S.ppos[t] = st;
+        S.vel[t] = z;
+        S.pvel[t] = z;
+        S.goal[t] = A.goal[ai];
     }
-    __syncthreads();
-    if (active) {
-        int mi = A.map_idx ? A.map_idx[e] : 0;
-        if (R.mode == 0 && R.map_idx) mi = R.map_idx[e];
-        observe(A, S, e, i, base, S.occ + mi * A.gw * A.gh);
-    }
+    __syncthreads();   // map_idx (explicit mode) written above is read by the radar phase below
+    radar_phase(A, S, e0, nag, true);
+    if (active) observe_agent(A, S, e, i, base);
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -748,7 +787,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     h->K = c.N - 1;
     h->D0 = 6 + 4 * h->K;
     h->W = c.max_wp;
-    h->epb = BLOCK / c.N;
+    h->epb = c.N > 24 ? 1 : 24 / c.N;   // ~24 agents x 18 rays of radar work per 256-thread workgroup
     h->blocks = (c.E + h->epb - 1) / h->epb;
     const size_t EN = (size_t)c.E * c.N;
     hipError_t st = hipSuccess;

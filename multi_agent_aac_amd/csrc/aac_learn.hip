@@ -159,15 +159,18 @@ __global__ void meta_kernel(int64_t *meta, int64_t cap, int E) {
     meta[1] = s < cap ? s : cap;
 }
 
+__global__ void counter_kernel(uint64_t *counter) { *counter += 1; }
+
 constexpr int TBL = 8192;
 
 __device__ inline int64_t draw(uint64_t seed, uint64_t ctr, int idx, int att, int64_t size) {
-    uint64_t h = mix64(mix64(mix64(seed) ^ ctr) ^ (((uint64_t)idx << 20) | (uint64_t)att));
+    uint64_t h = mix64(mix64(mix64(seed) ^ ctr) ^ (((uint64_t)blockIdx.x << 44) | ((uint64_t)idx << 20) | (uint64_t)att));
     return (int64_t)(h % (uint64_t)size);
 }
 
-__global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B, uint64_t seed, uint64_t *counter,
-                                                     int32_t *out) {
+__global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B, uint64_t seed,
+                                                     const uint64_t *counter, int32_t *out_all) {
+    int32_t *out = out_all + (size_t)blockIdx.x * B;   // one workgroup per batch
     __shared__ int keys[TBL];
     __shared__ int owner[TBL];
     const int64_t size = meta[1];
@@ -217,7 +220,6 @@ __global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B
         const int idx = threadIdx.x + u * 1024;
         if (idx < B) out[idx] = val[u];
     }
-    if (threadIdx.x == 0) *counter = ctr + 1;
 }
 
 __global__ void __launch_bounds__(LEARN_BLOCK) gather_kernel(const float *ring, int rw, const int32_t *idx, Fields F) {
@@ -295,7 +297,6 @@ __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, i
     }
 }
 
-__global__ void counter_kernel(uint64_t *counter) { *counter += 1; }
 
 #define LHIP(x)                                                                                  \
     do {                                                                                         \
@@ -372,9 +373,12 @@ int aac_replay_push(float *ring, int32_t rw, int64_t cap, int64_t *meta, int32_t
     return 0;
 }
 
-int aac_replay_sample(const int64_t *meta, int32_t B, uint64_t seed, uint64_t *counter, int32_t *idx, void *stream) {
+int aac_replay_sample(const int64_t *meta, int32_t B, int32_t nb, uint64_t seed, uint64_t *counter, int32_t *idx,
+                      void *stream) {
     if (B < 1 || B > 4096) return lfail("replay: 1 <= B <= 4096");
-    hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, meta, B, seed, counter, idx);
+    if (nb < 1) return lfail("replay: n_batches >= 1");
+    hipLaunchKernelGGL(sample_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, meta, B, seed, counter, idx);
+    hipLaunchKernelGGL(counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
     LHIP(hipGetLastError());
     return 0;
 }

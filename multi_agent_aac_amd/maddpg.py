@@ -118,13 +118,19 @@ class MADDPG:
         if self.world > 1:
             parallel.allreduce_mean_(flat.grad, self.pg)
 
-    def _iteration(self, rep, B, agent, idx=None):
-        b = rep.sample_batch(B, idx)
+    def _targets(self, b, B):
+        """y for all N iterations at once.  The target networks only change in the Polyak step
+        after the N iterations (ATT/maddpg:436-438), so evaluating them for the N independently
+        sampled batches in one batched forward is exactly the reference's per-iteration value."""
+        N = self.n_agents
         with torch.no_grad():
             na = self.actors_target([b["n_own"], b["n_radar"], b["n_nei"]])
-            q_next = self.critics_target([b["n_own"], b["n_radar"]], na).squeeze(-1)
+            q_next = self.critics_target([b["n_own"], b["n_radar"]], na).squeeze(-1)      # (N*B,)
             done_any = (b["done"] == 1).any(dim=1).to(torch.float32)
-            target = b["rew"][:, agent] + self.GAMMA * q_next * (1 - done_any)
+            rew = b["rew"].reshape(N, B, N).diagonal(dim1=0, dim2=2).transpose(0, 1)      # r[:, i] of batch i
+            return rew.reshape(-1) + self.GAMMA * q_next * (1 - done_any)
+
+    def _iteration(self, b, target, agent):
         q = self.critics([b["s_own"], b["s_radar"]], b["act"])
         loss_q = F.mse_loss(q, target.unsqueeze(1))
         self.critic_optimizer.zero_grad()
@@ -141,9 +147,14 @@ class MADDPG:
 
     def _update_core(self, B, idx_list=None):
         rep = self.replay if self.replay is not None else self.memory.dev
+        N = self.n_agents
+        idx = None if idx_list is None else torch.cat([i.reshape(-1) for i in idx_list])
+        ball = rep.sample_batch(B, idx, nb=N)           # N independent batches, one launch each
+        target = self._targets(ball, B)
         stats = []
-        for agent in range(self.n_agents):
-            stats.append(self._iteration(rep, B, agent, None if idx_list is None else idx_list[agent]))
+        for agent in range(N):
+            b = {k: v[agent * B:(agent + 1) * B] for k, v in ball.items()}
+            stats.append(self._iteration(b, target[agent * B:(agent + 1) * B], agent))
         ops.polyak_flat(self.fc_t.data, self.fc.data, self.tau)
         ops.polyak_flat(self.fa_t.data, self.fa.data, self.tau)
         return stats

@@ -52,20 +52,22 @@ class DeviceReplay:
         ops.replay_push(self.ring, self.meta, srcs, self.widths, self.dtypes, E)
         self.size = min(self.size + E, self.capacity)
 
-    def batch_buffers(self, B):
-        if B not in self._batch:
-            bufs = [torch.empty((B,) + s, dtype=torch.float32, device=self.device) for s in self.shapes]
-            idx = torch.empty(B, dtype=torch.int32, device=self.device)
-            self._batch[B] = (idx, dict(zip(FIELDS, bufs)), bufs)
-        return self._batch[B]
+    def batch_buffers(self, B, nb=1):
+        key = (B, nb)
+        if key not in self._batch:
+            bufs = [torch.empty((nb * B,) + s, dtype=torch.float32, device=self.device) for s in self.shapes]
+            idx = torch.empty(nb * B, dtype=torch.int32, device=self.device)
+            self._batch[key] = (idx, dict(zip(FIELDS, bufs)), bufs)
+        return self._batch[key]
 
-    def sample_batch(self, B, idx=None):
-        """Draw B distinct rows (or use the given device indices) into static batch tensors."""
-        bidx, named, bufs = self.batch_buffers(B)
+    def sample_batch(self, B, idx=None, nb=1):
+        """Draw ``nb`` independent batches of B distinct rows (or use the given device indices,
+        shape (nb * B,)) into static field-contiguous tensors of leading size nb * B."""
+        bidx, named, bufs = self.batch_buffers(B, nb)
         if idx is None:
             ops.replay_sample(self.meta, B, self.seed, self.counter, bidx)
         else:
-            bidx.copy_(idx)
+            bidx.copy_(idx.reshape(-1))
         ops.replay_gather(self.ring, bidx, bufs, self.widths)
         return named
 

@@ -26,7 +26,7 @@ def lib():
         L.aac_attn_fwd.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp]
         L.aac_attn_bwd.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, i32, i32, vp]
         L.aac_replay_push.argtypes = [vp, i32, i64, vp, i32, vp, vp, vp, i32, vp]
-        L.aac_replay_sample.argtypes = [vp, i32, u64, vp, vp, vp]
+        L.aac_replay_sample.argtypes = [vp, i32, i32, u64, vp, vp, vp]
         L.aac_replay_gather.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp]
         L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
         L.aac_polyak_flat.argtypes = [vp, vp, i64, f32, vp]
@@ -109,7 +109,9 @@ def replay_push(ring, meta, srcs, widths, dtypes, E):
 
 
 def replay_sample(meta, B, seed, counter, idx_out):
-    _chk(lib().aac_replay_sample(_p(meta), B, u64(seed), _p(counter), _p(idx_out), _s()), "aac_replay_sample")
+    """idx_out (n_batches * B,) int32: n_batches independent draws of B distinct rows."""
+    nb = idx_out.numel() // B
+    _chk(lib().aac_replay_sample(_p(meta), B, nb, u64(seed), _p(counter), _p(idx_out), _s()), "aac_replay_sample")
 
 
 def replay_gather(ring, idx, dsts, widths):
