@@ -58,7 +58,7 @@ class MADDPG:
     def __init__(self, actor_dim, critic_dim, dim_act, actor_hidden_state_size=64, gru_history_length=10,
                  n_agents=5, args=None, cr_lr=1e-3, ac_lr=1e-3, gamma=0.95, tau=0.01,
                  full_observable_critic_flag=True, device=None, seed=None, memory_length=None, batch_size=None,
-                 process_group=None):
+                 process_group=None, blas="cublas"):
         self.args = args
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type == "cuda" and self.device.index is None:
@@ -74,6 +74,9 @@ class MADDPG:
             raise NotImplementedError("one_model_att runs with full_observable_critic_flag=True (ATT/main:77)")
         if seed is not None:
             torch.manual_seed(seed)
+        # rocBLAS picks split-K kernels for the reduction-heavy weight-gradient GEMMs
+        # (dW = G^T X over 5k-20k rows); hipBLASLt ran them on 1-6 workgroups (tools/mb_wgrad.py)
+        torch.backends.cuda.preferred_blas_library(blas)
         self.actors = ActorNetwork_ATT_TwoPortion(self.n_actor_dim, dim_act).to(self.device)
         self.critics = CriticCombine(self.n_critic_dim, N, dim_act).to(self.device)
         self.actors_target = ActorNetwork_ATT_TwoPortion(self.n_actor_dim, dim_act).to(self.device)
