@@ -56,6 +56,16 @@ int aac_adam_flat(float *param, const float *grad, float *exp_avg, float *exp_av
 /* tgt = (1 - tau) * tgt + tau * src */
 int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *stream);
 
+/* Fused activation backward + bias gradient of y = act(x W^T + b) (nn.Linear + ReLU/Tanh of
+ * ATT/nets:180-184, ATT/nets:699-701): gm = gy * act'(y) (rows of O at the given strides; gm may
+ * be NULL) and db[o] += sum_m gm[m][o] (db may be NULL; float atomics, caller zeroes db).
+ * act: 0 identity, 1 ReLU, 2 tanh. */
+int aac_act_bgrad(const float *gy, int32_t gy_stride, const float *y, int32_t y_stride, float *gm,
+                  int32_t gm_stride, float *db, int32_t M, int32_t O, int32_t act, void *stream);
+
+/* y[M][O] = act(y + b) in place (bias + activation epilogue of a bias-less GEMM). */
+int aac_bias_act(float *y, const float *b, int64_t M, int32_t O, int32_t act, void *stream);
+
 /* act [E*N][2] += (float)(randn * var_e); clamp to [-1, 1]; var_e from episode[e] (device):
  * var = noise_start + ((0 - noise_start)/(eps_end - 1)) * (ep - 1) if ep <= eps_end else 0. */
 int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, int32_t eps_end, float noise_start,

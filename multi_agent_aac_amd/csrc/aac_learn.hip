@@ -263,6 +263,49 @@ __global__ void polyak_kernel(float *tgt, const float *src, int64_t n, float kee
     }
 }
 
+// --------------------------------------------------------------------- activation backward
+// gm[m][o] = gy[m][o] * act'(y[m][o]);  db[o] += sum_m gm[m][o]
+// act: 0 identity, 1 relu (y > 0), 2 tanh (1 - y^2).  Grid (ceil(O/64), row chunks); each
+// workgroup reduces its rows in LDS and adds one partial per column (float atomics).
+template <int ACT>
+__global__ void __launch_bounds__(LEARN_BLOCK) act_bgrad_kernel(const float *__restrict__ gy, int gys,
+                                                               const float *__restrict__ y, int ys, float *gm,
+                                                               int gms, float *db, int M, int O, int rows_per_wg) {
+    __shared__ float part[4][64];
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int rg = threadIdx.x >> 6;
+    const int m0 = blockIdx.y * rows_per_wg;
+    const int m1 = min(M, m0 + rows_per_wg);
+    float acc = 0.0f;
+    if (col < O) {
+        for (int m = m0 + rg; m < m1; m += 4) {
+            float g = gy[(size_t)m * gys + col];
+            if (ACT == 1) g = y[(size_t)m * ys + col] > 0.0f ? g : 0.0f;
+            if (ACT == 2) {
+                const float t = y[(size_t)m * ys + col];
+                g = g * (1.0f - t * t);
+            }
+            if (gm) gm[(size_t)m * gms + col] = g;
+            acc += g;
+        }
+    }
+    part[rg][threadIdx.x & 63] = acc;
+    __syncthreads();
+    if (rg == 0 && col < O && db) atomicAdd(&db[col], (part[0][threadIdx.x] + part[1][threadIdx.x]) +
+                                                          (part[2][threadIdx.x] + part[3][threadIdx.x]));
+}
+
+// y[m][o] = act(y[m][o] + b[o]) in place
+template <int ACT>
+__global__ void bias_act_kernel(float *y, const float *__restrict__ b, int64_t n, int O) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float v = y[i] + b[i % O];
+        if (ACT == 1) v = v > 0.0f ? v : 0.0f;
+        if (ACT == 2) v = tanhf(v);
+        y[i] = v;
+    }
+}
+
 // ------------------------------------------------------------------------------ noise
 __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, int eps_end, float noise_start,
                              uint64_t seed, uint64_t *counter, float *noise_out) {
@@ -405,6 +448,30 @@ int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *st
     const float keep = (float)(1.0 - (double)tau);
     hipLaunchKernelGGL(polyak_kernel, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, tgt, src, n,
                        keep, tau);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_act_bgrad(const float *gy, int32_t gys, const float *y, int32_t ys, float *gm, int32_t gms, float *db,
+                  int32_t M, int32_t O, int32_t act, void *stream) {
+    if (M <= 0 || O <= 0) return 0;
+    const int rpw = 512;
+    dim3 grid((O + 63) / 64, (M + rpw - 1) / rpw);
+    if (act == 0) hipLaunchKernelGGL(act_bgrad_kernel<0>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
+    else if (act == 1) hipLaunchKernelGGL(act_bgrad_kernel<1>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
+    else if (act == 2) hipLaunchKernelGGL(act_bgrad_kernel<2>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
+    else return lfail("act_bgrad: act must be 0, 1 or 2");
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_bias_act(float *y, const float *b, int64_t M, int32_t O, int32_t act, void *stream) {
+    const int64_t n = M * O;
+    if (n <= 0) return 0;
+    if (act == 0) hipLaunchKernelGGL(bias_act_kernel<0>, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, y, b, n, O);
+    else if (act == 1) hipLaunchKernelGGL(bias_act_kernel<1>, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, y, b, n, O);
+    else if (act == 2) hipLaunchKernelGGL(bias_act_kernel<2>, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, y, b, n, O);
+    else return lfail("bias_act: act must be 0, 1 or 2");
     LHIP(hipGetLastError());
     return 0;
 }

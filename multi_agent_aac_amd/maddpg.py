@@ -137,13 +137,17 @@ class MADDPG:
         q = self.critics([b["s_own"], b["s_radar"]], b["act"])
         loss_q = F.mse_loss(q, target.unsqueeze(1))
         self.critic_optimizer.zero_grad()
-        loss_q.backward(inputs=list(self.critics.parameters()))
+        loss_q.backward()            # fused layers write the critic's grads into its flat buffer
         self._allreduce(self.fc)
         self.critic_optimizer.step()
         a_pi = self.actors([b["s_own"], b["s_radar"], b["s_nei"]])
         loss_a = -self.critics([b["s_own"], b["s_radar"]], a_pi).mean()
         self.actor_optimizer.zero_grad()
-        loss_a.backward(inputs=list(self.actors.parameters()))
+        self.critics.slot.enabled = False    # only d/da flows through the critic here (ATT/maddpg:421-425)
+        try:
+            loss_a.backward()
+        finally:
+            self.critics.slot.enabled = True
         self._allreduce(self.fa)
         self.actor_optimizer.step()
         return loss_q.detach(), loss_a.detach(), q.detach(), target

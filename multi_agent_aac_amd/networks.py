@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .layers import IDENTITY, RELU, TANH, GradSlot, fused_linear, stacked_linear_relu
 from .ops import masked_attention
 
 
@@ -68,6 +69,7 @@ class ActorNetwork_ATT_TwoPortion(nn.Module):
         self.q = nn.Linear(64, 64, bias=False)
         v = nn.Linear(64, 64, bias=False)
         self.kv_weight = nn.Parameter(torch.cat([k.weight.data, v.weight.data], 0))
+        self.slot = GradSlot()
 
     def forward(self, cur_state):
         own, grid, nei = cur_state[0], cur_state[1], cur_state[2]
@@ -76,14 +78,17 @@ class ActorNetwork_ATT_TwoPortion(nn.Module):
         own = _rows(own, (own.shape[-1],))
         grid = _rows(grid, (grid.shape[-1],))
         nei = _rows(nei, (K, nei.shape[-1]))
-        e_o = self.own_fc(own)
-        e_g = self.own_grid(grid)
-        x = self.neigh_fc(nei)
-        q = self.q(e_o)
-        kv = F.linear(x, self.kv_weight)
+        s = self.slot
+        R = own.shape[0]
+        e_o = fused_linear(own, self.own_fc[0].weight, self.own_fc[0].bias, RELU, s)
+        e_g = fused_linear(grid, self.own_grid[0].weight, self.own_grid[0].bias, RELU, s)
+        x = fused_linear(nei.reshape(R * K, -1), self.neigh_fc[0].weight, self.neigh_fc[0].bias, RELU, s)
+        q = fused_linear(e_o, self.q.weight, None, IDENTITY, s)
+        kv = fused_linear(x, self.kv_weight, None, IDENTITY, s).view(R, K, 128)
         v_att = masked_attention(q, kv, nei)
-        h = self.merge_feature(torch.cat((e_o, e_g, v_att), dim=1))
-        out = self.act_out(h)
+        h = fused_linear(torch.cat((e_o, e_g, v_att), dim=1), self.merge_feature[0].weight,
+                         self.merge_feature[0].bias, RELU, s)
+        out = fused_linear(h, self.act_out[0].weight, self.act_out[0].bias, TANH, s)
         return out.reshape(*lead, out.shape[-1])
 
     # .pth compatibility with the reference actor (keys of ATT/nets:180-189)
@@ -120,15 +125,17 @@ class CriticCombine(nn.Module):
         self.enc_b = nn.Parameter(torch.stack([e.bias.data for e in encs]))     # (N, 128)
         self.combine_agents_fea = nn.Sequential(nn.Linear(hidden * n_agents, 256), nn.ReLU())
         self.out_feature_q = nn.Sequential(nn.Linear(256, 1))
+        self.slot = GradSlot()
 
     def forward(self, combine_state, combine_action):
         own = combine_state[0]                       # (B, N, D0)
         if isinstance(combine_action, (list, tuple)):
             combine_action = torch.stack(list(combine_action), 1)
         x = torch.cat((own, combine_action), dim=-1)            # (B, N, D0+2)
-        f = torch.baddbmm(self.enc_b.unsqueeze(1), x.transpose(0, 1), self.enc_w.transpose(1, 2))  # (N, B, 128)
-        f = torch.relu(f).transpose(0, 1).reshape(x.shape[0], -1)
-        return self.out_feature_q(self.combine_agents_fea(f))
+        s = self.slot
+        f = stacked_linear_relu(x, self.enc_w, self.enc_b, s)   # (B, N*128), agent-major features
+        h = fused_linear(f, self.combine_agents_fea[0].weight, self.combine_agents_fea[0].bias, RELU, s)
+        return fused_linear(h, self.out_feature_q[0].weight, self.out_feature_q[0].bias, IDENTITY, s)
 
     def reference_state_dict(self):
         sd = OrderedDict()

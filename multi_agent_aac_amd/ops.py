@@ -31,6 +31,8 @@ def lib():
         L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
         L.aac_polyak_flat.argtypes = [vp, vp, i64, f32, vp]
         L.aac_noise_clamp.argtypes = [vp, i32, i32, vp, i32, f32, u64, vp, vp, vp]
+        L.aac_act_bgrad.argtypes = [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp]
+        L.aac_bias_act.argtypes = [vp, vp, i64, i32, i32, vp]
         _L = L
     return _L
 
@@ -80,6 +82,20 @@ class _MaskedAttention(torch.autograd.Function):
 def masked_attention(q, kv, nei):
     """q (R, 64), kv (R, K, 128) = [k | v], nei (R, K, 6) mask source -> v_att (R, 64)."""
     return _MaskedAttention.apply(q, kv, nei)
+
+
+# ----------------------------------------------------------------------------- layers
+def act_bgrad(gy, y, gm, db, act):
+    """gm = gy * act'(y); db += column sums of gm (see aac_act_bgrad).  Row-major, contiguous."""
+    M, O = gy.shape
+    _chk(lib().aac_act_bgrad(_p(gy), gy.stride(0), _p(y), y.stride(0) if y is not None else 0, _p(gm),
+                             gm.stride(0) if gm is not None else 0, _p(db), M, O, act, _s()), "aac_act_bgrad")
+
+
+def bias_act(y, b, act):
+    """y = act(y + b) in place; y (M, O) contiguous, b (O,)."""
+    M, O = y.shape
+    _chk(lib().aac_bias_act(_p(y), _p(b), M, O, act, _s()), "aac_bias_act")
 
 
 # ----------------------------------------------------------------------------- optimiser
