@@ -269,8 +269,9 @@ __global__ void polyak_kernel(float *tgt, const float *src, int64_t n, float kee
 // workgroup reduces its rows in LDS and adds one partial per column (float atomics).
 template <int ACT>
 __global__ void __launch_bounds__(LEARN_BLOCK) act_bgrad_kernel(const float *__restrict__ gy, int gys,
-                                                               const float *__restrict__ y, int ys, float *gm,
-                                                               int gms, float *db, int M, int O, int rows_per_wg) {
+                                                               const float *__restrict__ y, int ys,
+                                                               float *__restrict__ gm, int gms, float *db, int M, int O,
+                                                               int rows_per_wg) {
     __shared__ float part[4][64];
     const int col = blockIdx.x * 64 + (threadIdx.x & 63);
     const int rg = threadIdx.x >> 6;
@@ -278,6 +279,7 @@ __global__ void __launch_bounds__(LEARN_BLOCK) act_bgrad_kernel(const float *__r
     const int m1 = min(M, m0 + rows_per_wg);
     float acc = 0.0f;
     if (col < O) {
+#pragma unroll 8
         for (int m = m0 + rg; m < m1; m += 4) {
             float g = gy[(size_t)m * gys + col];
             if (ACT == 1) g = y[(size_t)m * ys + col] > 0.0f ? g : 0.0f;
@@ -455,7 +457,7 @@ int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *st
 int aac_act_bgrad(const float *gy, int32_t gys, const float *y, int32_t ys, float *gm, int32_t gms, float *db,
                   int32_t M, int32_t O, int32_t act, void *stream) {
     if (M <= 0 || O <= 0) return 0;
-    const int rpw = 512;
+    const int rpw = 32;   // 8 independent rows per thread; hundreds of workgroups at M = 5k-20k
     dim3 grid((O + 63) / 64, (M + rpw - 1) / rpw);
     if (act == 0) hipLaunchKernelGGL(act_bgrad_kernel<0>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
     else if (act == 1) hipLaunchKernelGGL(act_bgrad_kernel<1>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
