@@ -58,10 +58,12 @@ int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *st
 
 /* Fused activation backward + bias gradient of y = act(x W^T + b) (nn.Linear + ReLU/Tanh of
  * ATT/nets:180-184, ATT/nets:699-701): gm = gy * act'(y) (rows of O at the given strides; gm may
- * be NULL) and db[o] += sum_m gm[m][o] (db may be NULL; float atomics, caller zeroes db).
- * act: 0 identity, 1 ReLU, 2 tanh. */
+ * be NULL) and db[o] = sum_m gm[m][o] (db may be NULL), reduced deterministically in the same
+ * launch through ws (>= ceil(M/32) * O floats) and tickets (>= ceil(O/64) zeroed uint32 that the
+ * kernel leaves zeroed).  act: 0 identity, 1 ReLU, 2 tanh. */
 int aac_act_bgrad(const float *gy, int32_t gy_stride, const float *y, int32_t y_stride, float *gm,
-                  int32_t gm_stride, float *db, int32_t M, int32_t O, int32_t act, void *stream);
+                  int32_t gm_stride, float *db, int32_t M, int32_t O, int32_t act, float *ws, uint32_t *tickets,
+                  void *stream);
 
 /* y[M][O] = act(y + b) in place (bias + activation epilogue of a bias-less GEMM). */
 int aac_bias_act(float *y, const float *b, int64_t M, int32_t O, int32_t act, void *stream);

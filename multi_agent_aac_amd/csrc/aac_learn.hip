@@ -264,16 +264,21 @@ __global__ void polyak_kernel(float *tgt, const float *src, int64_t n, float kee
 }
 
 // --------------------------------------------------------------------- activation backward
-// gm[m][o] = gy[m][o] * act'(y[m][o]);  db[o] += sum_m gm[m][o]
-// act: 0 identity, 1 relu (y > 0), 2 tanh (1 - y^2).  Grid (ceil(O/64), row chunks); each
-// workgroup reduces its rows in LDS and adds one partial per column (float atomics).
+// gm[m][o] = gy[m][o] * act'(y[m][o]);  db[o] = sum_m gm[m][o]   (act: 0 identity, 1 relu, 2 tanh)
+// Grid (ceil(O/64), ceil(M/32)).  Deterministic bias reduction in one launch: every workgroup
+// writes its 64 column partials to ws, takes a ticket; the last workgroup of a column block sums
+// the partials in row-block order (agent-scope release/acquire, MI355X_MICROARCH.md "Valid
+// forms") and resets its ticket, so the kernel is graph-replayable.
 template <int ACT>
 __global__ void __launch_bounds__(LEARN_BLOCK) act_bgrad_kernel(const float *__restrict__ gy, int gys,
                                                                const float *__restrict__ y, int ys,
-                                                               float *__restrict__ gm, int gms, float *db, int M, int O,
-                                                               int rows_per_wg) {
+                                                               float *__restrict__ gm, int gms, float *db, int M,
+                                                               int O, int rows_per_wg, float *ws,
+                                                               unsigned *tickets) {
     __shared__ float part[4][64];
-    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+    __shared__ int s_last;
+    const int lane = threadIdx.x & 63;
+    const int col = blockIdx.x * 64 + lane;
     const int rg = threadIdx.x >> 6;
     const int m0 = blockIdx.y * rows_per_wg;
     const int m1 = min(M, m0 + rows_per_wg);
@@ -291,10 +296,30 @@ __global__ void __launch_bounds__(LEARN_BLOCK) act_bgrad_kernel(const float *__r
             acc += g;
         }
     }
-    part[rg][threadIdx.x & 63] = acc;
+    if (!db) return;
+    part[rg][lane] = acc;
     __syncthreads();
-    if (rg == 0 && col < O && db) atomicAdd(&db[col], (part[0][threadIdx.x] + part[1][threadIdx.x]) +
-                                                          (part[2][threadIdx.x] + part[3][threadIdx.x]));
+    if (rg == 0 && col < O) ws[(size_t)blockIdx.y * O + col] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = atomicAdd(&tickets[blockIdx.x], 1u);
+        s_last = (t == gridDim.y - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float tot = 0.0f;
+    if (col < O)
+        for (int r = rg; r < (int)gridDim.y; r += 4) tot += ws[(size_t)r * O + col];
+    part[rg][lane] = tot;
+    __syncthreads();
+    if (rg == 0 && col < O) db[col] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (threadIdx.x == 0) tickets[blockIdx.x] = 0;
 }
 
 // y[m][o] = act(y[m][o] + b[o]) in place
@@ -455,14 +480,18 @@ int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *st
 }
 
 int aac_act_bgrad(const float *gy, int32_t gys, const float *y, int32_t ys, float *gm, int32_t gms, float *db,
-                  int32_t M, int32_t O, int32_t act, void *stream) {
+                  int32_t M, int32_t O, int32_t act, float *ws, uint32_t *tickets, void *stream) {
     if (M <= 0 || O <= 0) return 0;
     const int rpw = 32;   // 8 independent rows per thread; hundreds of workgroups at M = 5k-20k
     dim3 grid((O + 63) / 64, (M + rpw - 1) / rpw);
-    if (act == 0) hipLaunchKernelGGL(act_bgrad_kernel<0>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
-    else if (act == 1) hipLaunchKernelGGL(act_bgrad_kernel<1>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
-    else if (act == 2) hipLaunchKernelGGL(act_bgrad_kernel<2>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, gm, gms, db, M, O, rpw);
+    if (db && (!ws || !tickets)) return lfail("act_bgrad: db needs ws[ceil(M/32)][O] and tickets[ceil(O/64)]");
+#define ABG(A) hipLaunchKernelGGL(act_bgrad_kernel<A>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, \
+                                  gm, gms, db, M, O, rpw, ws, tickets)
+    if (act == 0) ABG(0);
+    else if (act == 1) ABG(1);
+    else if (act == 2) ABG(2);
     else return lfail("act_bgrad: act must be 0, 1 or 2");
+#undef ABG
     LHIP(hipGetLastError());
     return 0;
 }

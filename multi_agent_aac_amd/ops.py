@@ -31,7 +31,7 @@ def lib():
         L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
         L.aac_polyak_flat.argtypes = [vp, vp, i64, f32, vp]
         L.aac_noise_clamp.argtypes = [vp, i32, i32, vp, i32, f32, u64, vp, vp, vp]
-        L.aac_act_bgrad.argtypes = [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp]
+        L.aac_act_bgrad.argtypes = [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, vp]
         L.aac_bias_act.argtypes = [vp, vp, i64, i32, i32, vp]
         _L = L
     return _L
@@ -85,11 +85,26 @@ def masked_attention(q, kv, nei):
 
 
 # ----------------------------------------------------------------------------- layers
+_tickets = {}
+
+
+def _ticket_buf(dev):
+    t = _tickets.get(dev)
+    if t is None:
+        t = _tickets[dev] = torch.zeros(64, dtype=torch.int32, device=dev)   # kernel keeps it zeroed
+    return t
+
+
 def act_bgrad(gy, y, gm, db, act):
-    """gm = gy * act'(y); db += column sums of gm (see aac_act_bgrad).  Row-major, contiguous."""
+    """gm = gy * act'(y); db = column sums of gm, deterministic (see aac_act_bgrad)."""
     M, O = gy.shape
+    ws = tk = None
+    if db is not None:
+        ws = torch.empty(((M + 31) // 32) * O, dtype=torch.float32, device=gy.device)
+        tk = _ticket_buf(gy.device)
     _chk(lib().aac_act_bgrad(_p(gy), gy.stride(0), _p(y), y.stride(0) if y is not None else 0, _p(gm),
-                             gm.stride(0) if gm is not None else 0, _p(db), M, O, act, _s()), "aac_act_bgrad")
+                             gm.stride(0) if gm is not None else 0, _p(db), M, O, act, _p(ws), _p(tk), _s()),
+         "aac_act_bgrad")
 
 
 def bias_act(y, b, act):
