@@ -314,8 +314,10 @@ __global__ void __launch_bounds__(LEARN_BLOCK) act_bgrad_kernel(const float *__r
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float tot = 0.0f;
-    if (col < O)
+    if (col < O) {
+#pragma unroll 8
         for (int r = rg; r < (int)gridDim.y; r += 4) tot += ws[(size_t)r * O + col];
+    }
     part[rg][lane] = tot;
     __syncthreads();
     if (rg == 0 && col < O) db[col] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
@@ -482,7 +484,7 @@ int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *st
 int aac_act_bgrad(const float *gy, int32_t gys, const float *y, int32_t ys, float *gm, int32_t gms, float *db,
                   int32_t M, int32_t O, int32_t act, float *ws, uint32_t *tickets, void *stream) {
     if (M <= 0 || O <= 0) return 0;
-    const int rpw = 32;   // 8 independent rows per thread; hundreds of workgroups at M = 5k-20k
+    const int rpw = 32;   // 8 rows per thread: larger tiles measured slower (latency-bound rows)
     dim3 grid((O + 63) / 64, (M + rpw - 1) / rpw);
     if (db && (!ws || !tickets)) return lfail("act_bgrad: db needs ws[ceil(M/32)][O] and tickets[ceil(O/64)]");
 #define ABG(A) hipLaunchKernelGGL(act_bgrad_kernel<A>, grid, dim3(LEARN_BLOCK), 0, (hipStream_t)stream, gy, gys, y, ys, \

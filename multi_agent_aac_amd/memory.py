@@ -12,6 +12,7 @@ an unchanged ``ma_main`` (E = 1); its rows land in the same device ring.
 """
 from collections import namedtuple
 
+import numpy as np
 import torch
 
 from . import ops
@@ -83,15 +84,23 @@ class ReplayMemory:
         self.memory = self       # reference code reads ``len(model.memory)``
         self.position = 0
 
+    @staticmethod
+    def _mat(x):
+        """(N, D) tensor from a tensor / array or a list of per-agent rows (ATT/main:363-390)."""
+        if isinstance(x, (list, tuple)):
+            x = np.stack([np.asarray(v.cpu() if torch.is_tensor(v) else v, dtype=np.float32) for v in x])
+        return torch.as_tensor(x, dtype=torch.float32)
+
     def _ensure(self, states):
         if self.dev is None:
-            N, D0 = states[0].shape
-            self.dev = DeviceReplay(self.capacity, N, D0, states[1].shape[1], self.device)
+            N, D0 = self._mat(states[0]).shape
+            self.dev = DeviceReplay(self.capacity, N, D0, self._mat(states[1]).shape[1], self.device)
 
     def _obs(self, states):
-        own = torch.as_tensor(states[0], dtype=torch.float32).reshape(1, self.dev.N, self.dev.D0)
-        radar = torch.as_tensor(states[1], dtype=torch.float32).reshape(1, self.dev.N, self.dev.R)
-        nei = torch.stack([torch.as_tensor(x, dtype=torch.float32).reshape(self.dev.K, 6) for x in states[2]])
+        own = self._mat(states[0]).reshape(1, self.dev.N, self.dev.D0)
+        radar = self._mat(states[1]).reshape(1, self.dev.N, self.dev.R)
+        nei = torch.stack([self._mat([np.asarray(v.cpu() if torch.is_tensor(v) else v).reshape(6) for v in x])
+                           for x in states[2]])
         return [t.to(self.dev.device).contiguous() for t in (own, radar, nei.reshape(1, self.dev.N, self.dev.K, 6))]
 
     def push(self, states, actions, next_states, rewards, dones, history_info=None, cur_hidden=None,
