@@ -117,7 +117,7 @@ class Trainer:
         self.episode.add_(n.env_done.to(torch.int32))
         self.cur, self.nxt = n, c
         if update and len(self.replay) > self.B:
-            self.model.update(self.B, use_graph=not NO_GRAPH)
+            self.model.update(self.B, use_graph=not NO_GRAPH, want_stats=False)
 
 
 NO_GRAPH = False

@@ -1,0 +1,91 @@
+/* aac_fused.h -- C ABI of the fused learner kernels in libaac_env.so (gfx950).
+ *
+ * The MADDPG update of the reference (update_myown, ATT/maddpg:219-440) is a chain of small
+ * nn.Linear forward/backward products over B = 1024 samples x N agents.  On MI355X the cost is
+ * the number of launches, not the FLOPs, so the learner is expressed as ~25 launches per
+ * gradient iteration of two kinds:
+ *
+ *   aac_gemm_batch   up to AAC_GEMM_MAX independent fp32 products in ONE launch (grouped GEMM on
+ *                    v_mfma_f32_16x16x4_f32, one 32x32 tile per wave), each with a fused epilogue
+ *                      C = mact( act( A.B + addend + bias ) )
+ *                    act = ReLU / tanh of the layer (ATT/nets:180-184, :699-701); mact multiplies
+ *                    by the derivative of the layer that produced ``mask`` (relu' or 1 - t^2),
+ *                    i.e. the backward of the activation; ``ones`` appends a virtual column of
+ *                    ones to B so a weight-gradient product dW = G^T X also yields the bias
+ *                    gradient sum_rows G (written to cextra).  Large-K weight-gradient products
+ *                    split K into ``ksplit`` partial copies of C (split_stride apart) that the
+ *                    optimiser kernel sums in fixed order (aac_adam_flat_sum), so no cross-
+ *                    workgroup reduction or fence is needed inside the launch.
+ *   aac_critic_head  the critic's 256 -> 1 output layer per row (one wave per row) fused with
+ *                    the loss gradient: mse (ATT/maddpg:386) / -mean Q (ATT/maddpg:424) / the
+ *                    TD target r + gamma Q'(1 - done_any) (ATT/maddpg:355-370).
+ *
+ * Conventions as in aac_env.h: plain device pointers, ``stream`` = hipStream_t as void*,
+ * 0 = ok, message in aac_fused_last_error().
+ */
+#ifndef AAC_FUSED_H
+#define AAC_FUSED_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AAC_GEMM_MAX 8
+
+/* C[M][N] (row-major, ldc) = epilogue(op(A)[M][K] . op(B)[K][N]).
+ * op(A)[m][k] = ta ? A[k*lda + m] : A[m*lda + k];  op(B)[k][n] = tb ? B[n*ldb + k] : B[k*ldb + n].
+ * ones = 1: column N-1 of op(B) is a virtual column of ones and C column N-1 goes to cextra[m]
+ * (no epilogue on it); the real B / C have N-1 columns.
+ * act: 0 none, 1 relu, 2 tanh.  mact: 0 none, 1 x (mask > 0), 2 x (1 - mask^2); mask[m*ldmask+n].
+ * addend (may be NULL): added before bias.
+ * ksplit <= 1: one pass over K.  ksplit > 1: split s of K writes its partial product to
+ * C + s*split_stride (and cextra + s*split_stride); no addend / bias / act / mact allowed. */
+typedef struct {
+    const float *A, *B;
+    float *C;
+    const float *bias, *addend, *mask;
+    float *cextra;
+    int64_t split_stride;
+    int32_t M, N, K;
+    int32_t lda, ldb, ldc, ldadd, ldmask;
+    int32_t ta, tb, act, mact, ones, ksplit;
+} aac_gemm_prob;
+
+const char *aac_fused_last_error(void);
+
+/* n <= AAC_GEMM_MAX products in one launch. */
+int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream);
+
+/* torch.optim.Adam step (as aac_adam_flat_at) whose gradient is the fixed-order sum of nsplit
+ * partial copies gpart[s*n + i]; grad_out (may be NULL) receives that sum. */
+int aac_adam_flat_sum(float *param, const float *gpart, int32_t nsplit, float *grad_out, float *exp_avg,
+                      float *exp_avg_sq, int64_t n, float lr, float beta1, float beta2, float eps,
+                      const int32_t *step, int32_t step_add, void *stream);
+
+/* out[i] = sum_{s < nsplit} gpart[s*n + i] in split order (before a gradient all-reduce). */
+int aac_sum_partials(float *out, const float *gpart, int32_t nsplit, int64_t n, void *stream);
+
+/* Critic output layer + loss gradient, rows of 256 features h[r*ldh + j]:
+ *   q[r] = h[r] . w + b[0]
+ *   mode 0 (critic loss, mse):  dq = (2/M)(q - y[r])      dh = dq w * (h > 0)
+ *   mode 1 (actor loss, -mean): dq = -(1/M)               dh = dq w * (h > 0)
+ *   mode 2 (TD target):  yout[r] = rew[r*N + r/B] + (gamma q)(1 - any_n(done[r*N + n] == 1))
+ * q, dq, dh, yout may be NULL where unused. */
+int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, const float *b, int32_t mode,
+                    const float *y, const float *rew, const float *done, int32_t B, int32_t N, float gamma, float *q,
+                    float *dq, float *dh, float *yout, void *stream);
+
+/* Replay gather with interleaved destinations: element c of field f of sampled row b goes to
+ * dsts[f][b*(widths[f]/chunks[f])*dstrides[f] + (c/chunks[f])*dstrides[f] + c%chunks[f]]
+ * (chunks = widths, dstrides = widths gives aac_replay_gather).  Lets [own_n | a_n] land as the
+ * critic's (D0 + 2)-wide encoder input rows without a concat. */
+int aac_replay_gather_strided(const float *ring, int32_t row_width, const int32_t *idx, int32_t B, int32_t n_fields,
+                              float *const *dsts, const int32_t *widths, const int32_t *chunks,
+                              const int32_t *dstrides, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AAC_FUSED_H */

@@ -53,6 +53,10 @@ int aac_replay_gather(const float *ring, int32_t row_width, const int32_t *idx, 
  * AFTER increment, read on the device so the call can be graph-captured. */
 int aac_adam_flat(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr,
                   float beta1, float beta2, float eps, const int32_t *step, void *stream);
+/* Same with step number *step + step_add (several optimiser steps per captured update read
+ * one device counter that is advanced once afterwards). */
+int aac_adam_flat_at(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr,
+                     float beta1, float beta2, float eps, const int32_t *step, int32_t step_add, void *stream);
 /* tgt = (1 - tau) * tgt + tau * src */
 int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *stream);
 

@@ -1,0 +1,385 @@
+// aac_fused.hip -- grouped fp32 MFMA GEMM with fused epilogues, the critic head and the
+// interleaving replay gather of the fused MADDPG learner (include/aac_fused.h).
+//
+// GEMM: one 256-thread workgroup per (product, 32x32 output tile, K split).  Each of its four
+// waves accumulates the whole 32x32 tile = 2x2 tiles of v_mfma_f32_16x16x4_f32 (exact f32 fma
+// chains, MI355X_MICROARCH.md "Matrix cores") over every fourth K chunk of 16, loading its MFMA
+// fragments straight from global memory with the next chunk's loads in flight; the four
+// partial tiles are summed through LDS in wave order (one barrier) and each wave runs the
+// epilogue of one 16x16 quadrant.  The short dependent K chains of these small products are
+// what bounds them, so K is cut four ways inside the workgroup before any split across them.
+// Fragment k order is permuted so that lane group g = lane>>4 holds k = 4g..4g+3 of the chunk
+// (the MFMA sums over k, so any order consistent between A and B is the same product): an
+// operand that is contiguous along K with 16-B aligned rows is read as one float4 per fragment
+// pair of k steps, any other as scalars whose 16 lanes cover 64 contiguous bytes.  Products
+// with a large K and a small output (weight gradients) split K into partial copies of C that the
+// optimiser sums (aac_adam_flat_sum), so there is no cross-workgroup reduction in the launch.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/aac_fused.h"
+
+namespace {
+
+thread_local std::string f_err;
+
+int ffail(const std::string &m) {
+    f_err = m;
+    return -1;
+}
+
+#define FHIP(x)                                                                    \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) return ffail(std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int WT = 32;      // output tile edge per wave
+constexpr int KC = 16;      // K chunk
+
+struct GProb {
+    const float *A, *B;
+    float *C;
+    const float *bias, *addend, *mask;
+    float *cextra;
+    int64_t sstride;
+    int M, N, K;
+    int lda, ldb, ldc, ldadd, ldmask;
+    int ta, tb, act, mact, ones, ks;
+    int avec, bvec;            // fragment loads as float4 along K
+    int tiles_n, w_begin;      // first workgroup of this product
+};
+
+struct GBatch {
+    GProb p[AAC_GEMM_MAX];
+    int n, waves;
+};
+
+__device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, int m, int n, float v) {
+    if (m >= P.M || n >= P.N) return;
+    if (P.ones && n == P.N - 1) {
+        cx[m] = v;
+        return;
+    }
+    if (P.addend) v += P.addend[(size_t)m * P.ldadd + n];
+    if (P.bias) v += P.bias[n];
+    if (P.act == 1) v = v > 0.0f ? v : 0.0f;
+    else if (P.act == 2) v = tanhf(v);
+    if (P.mact == 1) v = P.mask[(size_t)m * P.ldmask + n] > 0.0f ? v : 0.0f;
+    else if (P.mact == 2) {
+        const float t = P.mask[(size_t)m * P.ldmask + n];
+        v = v * (1.0f - t * t);
+    }
+    C[(size_t)m * P.ldc + n] = v;
+}
+
+// fragments of one K chunk: f[i][t] = op(X)[row0 + 16 i + lr][kc + 4 lk + t]
+//   A side: row = m, op(A)[m][k];  B side: row = n, op(B)[k][n]
+__device__ __forceinline__ void load_frag(const float *X, int ld, int trans, int vec, int rows, int K, int kc,
+                                          int row0, int lr, int lk, int ones_row, float f[2][4]) {
+    const int k0 = kc + 4 * lk;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = row0 + 16 * i + lr;
+        if (vec) {
+            // K-contiguous rows, ld % 4 == 0, K % 4 == 0, 16-B aligned base
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (r < rows && k0 < K) v = *reinterpret_cast<const float4 *>(X + (size_t)r * ld + k0);
+            f[i][0] = v.x; f[i][1] = v.y; f[i][2] = v.z; f[i][3] = v.w;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int k = k0 + t;
+                float v = 0.0f;
+                if (k < K) {
+                    if (r < rows) v = trans ? X[(size_t)k * ld + r] : X[(size_t)r * ld + k];
+                    else if (r == ones_row) v = 1.0f;
+                }
+                f[i][t] = v;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
+    __shared__ f4 red[4][4][64];       // [wave][quadrant][lane]
+    const int wg = blockIdx.x;
+    int pi = 0;
+    while (pi + 1 < g.n && wg >= g.p[pi + 1].w_begin) ++pi;
+    const GProb &P = g.p[pi];
+    const int local = wg - P.w_begin;
+    const int s = local % P.ks;
+    const int tile = local / P.ks;
+    const int m0 = (tile / P.tiles_n) * WT;
+    const int n0 = (tile % P.tiles_n) * WT;
+    const int w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int nreal = P.N - P.ones;
+    // op(A) rows are m: stored A[m][k] (ta = 0, K-contiguous) or A[k][m] (ta = 1)
+    // op(B) rows are n: stored B[n][k] (tb = 1, K-contiguous) or B[k][n] (tb = 0)
+    const int a_tr = P.ta, b_tr = !P.tb;
+    const int ones_row = P.ones ? nreal : -1;
+
+    // split s of K, and inside it the four waves take every fourth chunk
+    const int nch = (P.K + KC - 1) / KC;
+    const int per = (nch + P.ks - 1) / P.ks;
+    const int c0 = s * per + w;
+    const int c1 = min(nch, s * per + per);
+
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    float a[2][4], b[2][4], an[2][4], bn[2][4];
+    if (c0 < c1) {
+        load_frag(P.A, P.lda, a_tr, P.avec, P.M, P.K, c0 * KC, m0, lr, lk, -1, a);
+        load_frag(P.B, P.ldb, b_tr, P.bvec, nreal, P.K, c0 * KC, n0, lr, lk, ones_row, b);
+    }
+    for (int c = c0; c < c1; c += 4) {
+        const bool more = c + 4 < c1;
+        if (more) {
+            load_frag(P.A, P.lda, a_tr, P.avec, P.M, P.K, (c + 4) * KC, m0, lr, lk, -1, an);
+            load_frag(P.B, P.ldb, b_tr, P.bvec, nreal, P.K, (c + 4) * KC, n0, lr, lk, ones_row, bn);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][t], b[0][t], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][t], b[1][t], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][t], b[0][t], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][t], b[1][t], acc[1][1], 0, 0, 0);
+        }
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    a[i][t] = an[i][t];
+                    b[i][t] = bn[i][t];
+                }
+        }
+    }
+    // reduce the four waves' partial tiles in wave order; wave q finishes quadrant q = (i, j)
+    red[w][0][lane] = acc[0][0];
+    red[w][1][lane] = acc[0][1];
+    red[w][2][lane] = acc[1][0];
+    red[w][3][lane] = acc[1][1];
+    __syncthreads();
+    const f4 v = ((red[0][w][lane] + red[1][w][lane]) + red[2][w][lane]) + red[3][w][lane];
+    const int i = w >> 1, j = w & 1;
+    float *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
+    float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) epilogue(P, C, cx, m0 + i * 16 + lk * 4 + r, n0 + j * 16 + lr, v[r]);
+}
+
+// ------------------------------------------------------------------------------ optimiser
+__global__ void adam_sum_kernel(float *p, const float *gpart, int ns, float *gout, float *m, float *v, int64_t n,
+                                float lr, float b1, float b2, float eps, const int32_t *step, int step_add) {
+    const int t = *step + step_add;
+    const double bc1 = 1.0 - pow((double)b1, (double)t);
+    const double bc2 = 1.0 - pow((double)b2, (double)t);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - (double)b1), w2 = (float)(1.0 - (double)b2);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float gi = gpart[i];
+        for (int s = 1; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
+        if (gout) gout[i] = gi;
+        float mi = m[i];
+        mi = mi + w1 * (gi - mi);               // exp_avg.lerp_(grad, 1 - beta1)
+        float vi = v[i] * b2;                   // exp_avg_sq.mul_(beta2)
+        vi = vi + w2 * (gi * gi);               //   .addcmul_(grad, grad, 1 - beta2)
+        const float den = sqrtf(vi) / bc2s + eps;
+        p[i] = p[i] + (-step_size) * (mi / den);   // param.addcdiv_(exp_avg, denom, -step_size)
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
+__global__ void sum_partials_kernel(float *out, const float *gpart, int ns, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float gi = gpart[i];
+        for (int s = 1; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
+        out[i] = gi;
+    }
+}
+
+// ------------------------------------------------------------------------------ critic head
+__device__ inline float wsum(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+__global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, int ldh, int M,
+                                                   const float *__restrict__ w, const float *__restrict__ b, int mode,
+                                                   const float *__restrict__ y, const float *__restrict__ rew,
+                                                   const float *__restrict__ done, int B, int N, float gamma, float *q,
+                                                   float *dq, float *dh, float *yout) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= M) return;
+    float hv[4], wv[4];
+    float part = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        hv[j] = h[(size_t)r * ldh + lane + 64 * j];
+        wv[j] = w[lane + 64 * j];
+        part = fmaf(hv[j], wv[j], part);
+    }
+    const float qv = wsum(part) + b[0];
+    if (q && lane == 0) q[r] = qv;
+    if (mode == 2) {
+        if (lane == 0) {
+            const int it = r / B;
+            bool any = false;
+            for (int n = 0; n < N; ++n) any |= done[(size_t)r * N + n] == 1.0f;
+            yout[r] = rew[(size_t)r * N + it] + (gamma * qv) * (1.0f - (any ? 1.0f : 0.0f));
+        }
+        return;
+    }
+    const float g = mode == 0 ? (2.0f / (float)M) * (qv - y[r]) : -(1.0f / (float)M);
+    if (dq && lane == 0) dq[r] = g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dh[(size_t)r * 256 + lane + 64 * j] = hv[j] > 0.0f ? g * wv[j] : 0.0f;
+}
+
+// ------------------------------------------------------------------------------ gather
+struct SFields {
+    float *dst[16];
+    int width[16], chunk[16], dstride[16];
+    int offset[17];
+    int n;
+};
+
+__global__ void __launch_bounds__(256) gather_strided_kernel(const float *ring, int rw, const int32_t *idx,
+                                                             SFields F) {
+    const int b = blockIdx.x;
+    const float *src = ring + (int64_t)idx[b] * rw;
+    for (int c = threadIdx.x; c < F.offset[F.n]; c += 256) {
+        int f = 0;
+        while (c >= F.offset[f + 1]) ++f;
+        const int cc = c - F.offset[f];
+        const int ch = F.chunk[f], ds = F.dstride[f];
+        const int64_t row0 = (int64_t)b * (F.width[f] / ch) * ds;
+        F.dst[f][row0 + (int64_t)(cc / ch) * ds + cc % ch] = src[c];
+    }
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int plan(const aac_gemm_prob *in, int n, GBatch &g) {
+    if (n < 1 || n > AAC_GEMM_MAX) return ffail("gemm_batch: 1 <= n <= AAC_GEMM_MAX");
+    g.n = n;
+    int waves = 0;
+    for (int i = 0; i < n; ++i) {
+        const aac_gemm_prob &s = in[i];
+        GProb &d = g.p[i];
+        const std::string who = "gemm_batch product " + std::to_string(i) + ": ";
+        if (s.M <= 0 || s.N <= 0 || s.K <= 0) return ffail(who + "empty product");
+        if (!s.A || !s.B) return ffail(who + "NULL operand");
+        if (s.ones && !s.cextra) return ffail(who + "ones column needs cextra");
+        if (s.N - s.ones > 0 && !s.C) return ffail(who + "NULL C");
+        if (s.mact && !s.mask) return ffail(who + "mact needs mask");
+        if (s.act < 0 || s.act > 2 || s.mact < 0 || s.mact > 2) return ffail(who + "bad act/mact");
+        const int ks = s.ksplit > 1 ? s.ksplit : 1;
+        if (ks > 1 && (s.split_stride <= 0 || s.addend || s.bias || s.act || s.mact))
+            return ffail(who + "ksplit > 1 needs split_stride and a plain epilogue");
+        d.A = s.A; d.B = s.B; d.C = s.C; d.bias = s.bias; d.addend = s.addend; d.mask = s.mask;
+        d.cextra = s.cextra;
+        d.sstride = s.split_stride;
+        d.M = s.M; d.N = s.N; d.K = s.K;
+        d.lda = s.lda; d.ldb = s.ldb; d.ldc = s.ldc; d.ldadd = s.ldadd; d.ldmask = s.ldmask;
+        d.ta = s.ta; d.tb = s.tb; d.act = s.act; d.mact = s.mact; d.ones = s.ones;
+        d.ks = ks;
+        d.avec = !s.ta && s.lda % 4 == 0 && s.K % 4 == 0 && aligned16(s.A);
+        d.bvec = s.tb && !s.ones && s.ldb % 4 == 0 && s.K % 4 == 0 && aligned16(s.B);
+        const int tm = (s.M + WT - 1) / WT, tn = (s.N + WT - 1) / WT;
+        d.tiles_n = tn;
+        d.w_begin = waves;          // in workgroups (one per tile and split)
+        waves += tm * tn * ks;
+    }
+    g.waves = waves;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *aac_fused_last_error(void) { return f_err.c_str(); }
+
+int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
+    GBatch g{};
+    if (plan(probs, n, g)) return -1;
+    hipLaunchKernelGGL(gemm_kernel, dim3(g.waves), dim3(256), 0, (hipStream_t)stream, g);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+static int grid_for(int64_t n) {
+    int64_t b = (n + 255) / 256;
+    return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+int aac_adam_flat_sum(float *p, const float *gpart, int32_t ns, float *gout, float *m, float *v, int64_t n, float lr,
+                      float b1, float b2, float eps, const int32_t *step, int32_t step_add, void *stream) {
+    if (ns < 1) return ffail("adam_flat_sum: nsplit >= 1");
+    hipLaunchKernelGGL(adam_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, gpart, ns, gout, m,
+                       v, n, lr, b1, b2, eps, step, step_add);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_sum_partials(float *out, const float *gpart, int32_t ns, int64_t n, void *stream) {
+    if (ns < 1) return ffail("sum_partials: nsplit >= 1");
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, gpart, ns, n);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, const float *b, int32_t mode,
+                    const float *y, const float *rew, const float *done, int32_t B, int32_t N, float gamma, float *q,
+                    float *dq, float *dh, float *yout, void *stream) {
+    if (M <= 0) return 0;
+    if (mode < 0 || mode > 2) return ffail("critic_head: mode 0, 1 or 2");
+    if (mode == 0 && !y) return ffail("critic_head: mode 0 needs y");
+    if (mode < 2 && !dh) return ffail("critic_head: modes 0/1 need dh");
+    if (mode == 2 && (!rew || !done || !yout || B <= 0 || N <= 0)) return ffail("critic_head: mode 2 needs rew/done/yout");
+    hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, M, w, b, mode, y, rew,
+                       done, B, N, gamma, q, dq, dh, yout);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_replay_gather_strided(const float *ring, int32_t rw, const int32_t *idx, int32_t B, int32_t n,
+                              float *const *dsts, const int32_t *widths, const int32_t *chunks,
+                              const int32_t *dstrides, void *stream) {
+    if (n < 1 || n > 16) return ffail("gather_strided: 1 <= n_fields <= 16");
+    SFields F{};
+    F.n = n;
+    F.offset[0] = 0;
+    for (int f = 0; f < n; ++f) {
+        if (widths[f] <= 0 || chunks[f] <= 0 || widths[f] % chunks[f] || dstrides[f] < chunks[f])
+            return ffail("gather_strided: bad width/chunk/dstride for field " + std::to_string(f));
+        F.dst[f] = dsts[f];
+        F.width[f] = widths[f];
+        F.chunk[f] = chunks[f];
+        F.dstride[f] = dstrides[f];
+        F.offset[f + 1] = F.offset[f] + widths[f];
+    }
+    if (F.offset[n] > rw) return ffail("gather_strided: fields wider than the ring row");
+    if (B <= 0) return 0;
+    hipLaunchKernelGGL(gather_strided_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, ring, rw, idx, F);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

@@ -235,8 +235,8 @@ __global__ void __launch_bounds__(LEARN_BLOCK) gather_kernel(const float *ring, 
 
 // ------------------------------------------------------------------------------- optimiser
 __global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2,
-                            float eps, const int32_t *step) {
-    const int t = *step;
+                            float eps, const int32_t *step, int step_add) {
+    const int t = *step + step_add;
     const double bc1 = 1.0 - pow((double)b1, (double)t);
     const double bc2 = 1.0 - pow((double)b2, (double)t);
     const float step_size = (float)((double)lr / bc1);
@@ -467,8 +467,13 @@ int aac_replay_gather(const float *ring, int32_t rw, const int32_t *idx, int32_t
 
 int aac_adam_flat(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2, float eps,
                   const int32_t *step, void *stream) {
+    return aac_adam_flat_at(p, g, m, v, n, lr, b1, b2, eps, step, 0, stream);
+}
+
+int aac_adam_flat_at(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2,
+                     float eps, const int32_t *step, int32_t step_add, void *stream) {
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, p, g, m, v, n, lr,
-                       b1, b2, eps, step);
+                       b1, b2, eps, step, step_add);
     LHIP(hipGetLastError());
     return 0;
 }

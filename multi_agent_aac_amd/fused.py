@@ -1,0 +1,397 @@
+"""Fused MADDPG learner: ``update_myown`` (ATT/maddpg:219-440) as ~25 HIP launches per gradient
+iteration instead of ~90 autograd kernels.
+
+Every product of the actor / critic forward and backward is an ``aac_gemm_batch`` launch (grouped
+fp32 MFMA GEMM with the activation, activation-derivative, bias-gradient and add epilogues fused,
+include/aac_fused.h); independent products of the same depth share one launch.  The backward is
+written out by hand (no autograd):
+
+critic step (batch i, ATT/maddpg:375-387)        actor step (ATT/maddpg:389-425)
+  f_n = relu(enc_n [own_n, a_n])   (N products)    e_o, e_g, x = relu(...)          (3 products)
+  h   = relu(Wc f)                                 q_att, kv = e_o Wq^T, x Wkv^T    (2)
+  q, dq = 2(q - y)/B, dh = dq Wo * (h > 0)         attention -> v_att  (HIP kernel)
+  dWo|dbo, dWc|dbc, df = dh Wc * (f > 0)  (3)      h_a = relu(Wm [e_o e_g v_att]); a = tanh(Wa h_a)
+  dW_enc_n | db_enc_n                     (N)      critic forward on a (2 + head), dh (dq = -1/B)
+  Adam                                             df; da_n -> dout = da (1 - a^2)   (1 + N)
+                                                   dWa|dba, dh_a                     (2)
+                                                   dWm|dbm, d e_o', d e_g, d v_att   (4)
+                                                   attention backward
+                                                   d e_o, dWq, dWkv, dx              (4)
+                                                   dW_own|db, dW_grid|db, dW_nei|db  (3)
+                                                   Adam
+The TD targets of all N iterations are one batched forward of the target networks (they only
+change in the Polyak step after the loop, ATT/maddpg:436-438), and the N batches are sampled and
+gathered in one launch each.  Weight gradients are written (never accumulated) straight into the
+networks' flat gradient buffers, so there is no zero_grad.
+"""
+import ctypes
+
+import torch
+
+from . import _native, ops
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+f32 = ctypes.c_float
+
+NONE, RELU, TANH = 0, 1, 2
+
+
+class GemmProb(ctypes.Structure):
+    _fields_ = [("A", vp), ("B", vp), ("C", vp), ("bias", vp), ("addend", vp), ("mask", vp), ("cextra", vp),
+                ("split_stride", i64), ("M", i32), ("N", i32), ("K", i32), ("lda", i32), ("ldb", i32), ("ldc", i32), ("ldadd", i32),
+                ("ldmask", i32), ("ta", i32), ("tb", i32), ("act", i32), ("mact", i32), ("ones", i32),
+                ("ksplit", i32)]
+
+
+GEMM_MAX = 8
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        L = _native.lib()
+        L.aac_fused_last_error.restype = ctypes.c_char_p
+        L.aac_gemm_batch.argtypes = [ctypes.POINTER(GemmProb), i32, vp]
+        L.aac_adam_flat_sum.argtypes = [vp, vp, i32, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
+        L.aac_sum_partials.argtypes = [vp, vp, i32, i64, vp]
+        L.aac_critic_head.argtypes = [vp, i32, i32, vp, vp, i32, vp, vp, vp, i32, i32, f32, vp, vp, vp, vp, vp]
+        L.aac_replay_gather_strided.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]
+        L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
+        _L = L
+    return _L
+
+
+def _chk(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {lib().aac_fused_last_error().decode(errors='replace')}")
+
+
+def _stream():
+    return vp(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t, off=0):
+    """Device address of element ``off`` of tensor ``t`` (fp32 / int32 elements)."""
+    return None if t is None else t.data_ptr() + 4 * off
+
+
+def prob(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=NONE, addend=None, ldadd=0, mask=None,
+         ldmask=0, mact=NONE, ones=0, cextra=None, ksplit=1, split_stride=0):
+    """C[M][N] = mact(act(op(A) op(B) + addend + bias)); pointers are ints (see ``ptr``)."""
+    return GemmProb(A, B, C, bias, addend, mask, cextra, split_stride, M, N + ones, K, lda, ldb, ldc, ldadd, ldmask,
+                    ta, tb, act, mact, ones, ksplit)
+
+
+class GemmLaunch:
+    """One aac_gemm_batch launch with a fixed problem list (validated when built)."""
+
+    def __init__(self, probs):
+        assert 1 <= len(probs) <= GEMM_MAX
+        self.n = len(probs)
+        self.arr = (GemmProb * self.n)(*probs)
+
+    def __call__(self):
+        _chk(lib().aac_gemm_batch(self.arr, self.n, _stream()), "aac_gemm_batch")
+
+
+def gemm_launches(probs):
+    """Split a product list into launches of at most GEMM_MAX."""
+    return [GemmLaunch(probs[i:i + GEMM_MAX]) for i in range(0, len(probs), GEMM_MAX)]
+
+
+def critic_head(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0.0, q=None, dq=None, dh=None,
+                yout=None):
+    _chk(lib().aac_critic_head(vp(h), 256, M, vp(w), vp(b), mode, vp(y) if y else None, vp(rew) if rew else None,
+                               vp(done) if done else None, B, N, gamma, vp(q) if q else None,
+                               vp(dq) if dq else None, vp(dh) if dh else None, vp(yout) if yout else None,
+                               _stream()), "aac_critic_head")
+
+
+def gather_strided(ring, idx, dsts, widths, chunks, dstrides):
+    n = len(dsts)
+    arr = (vp * n)(*dsts)
+    w = (i32 * n)(*widths)
+    c = (i32 * n)(*chunks)
+    d = (i32 * n)(*dstrides)
+    _chk(lib().aac_replay_gather_strided(vp(ring.data_ptr()), ring.shape[1], vp(idx.data_ptr()), idx.numel(), n,
+                                         arr, w, c, d, _stream()), "aac_replay_gather_strided")
+
+
+def adam_sum(opt, gpart, nsplit, step_add, grad_out=None):
+    """Adam step whose gradient is the sum of ``nsplit`` partial copies in ``gpart``."""
+    _chk(lib().aac_adam_flat_sum(vp(opt.flat.data.data_ptr()), vp(gpart.data_ptr()), nsplit,
+                                 vp(grad_out.data_ptr()) if grad_out is not None else None,
+                                 vp(opt.exp_avg.data_ptr()), vp(opt.exp_avg_sq.data_ptr()), opt.flat.data.numel(),
+                                 opt.lr, opt.betas[0], opt.betas[1], opt.eps, vp(opt.step_t.data_ptr()), step_add,
+                                 _stream()), "aac_adam_flat_sum")
+
+
+def sum_partials(out, gpart, nsplit):
+    _chk(lib().aac_sum_partials(vp(out.data_ptr()), vp(gpart.data_ptr()), nsplit, out.numel(), _stream()),
+         "aac_sum_partials")
+
+
+def adam_at(opt, step_add):
+    _chk(lib().aac_adam_flat_at(vp(opt.flat.data.data_ptr()), vp(opt.flat.grad.data_ptr()),
+                                vp(opt.exp_avg.data_ptr()), vp(opt.exp_avg_sq.data_ptr()), opt.flat.data.numel(),
+                                opt.lr, opt.betas[0], opt.betas[1], opt.eps, vp(opt.step_t.data_ptr()), step_add,
+                                _stream()), "aac_adam_flat_at")
+
+
+def _attn_fwd(q, kv, nei, out, out_stride, alpha, R, K):
+    L = ops.lib()
+    ops._chk(L.aac_attn_fwd(vp(q), vp(kv), vp(kv + 256), 128, vp(nei), vp(out), out_stride, vp(alpha), R, K,
+                            _stream()), "aac_attn_fwd")
+
+
+def _attn_bwd(q, kv, alpha, dout, dout_stride, dq, dkv, R, K):
+    L = ops.lib()
+    ops._chk(L.aac_attn_bwd(vp(q), vp(kv), vp(kv + 256), 128, vp(alpha), vp(dout), dout_stride, vp(dq), vp(dkv),
+                            vp(dkv + 256), R, K, _stream()), "aac_attn_bwd")
+
+
+# =============================================================================== networks
+def _addr(flat, gbase):
+    """Parameter -> address: its own storage, or the same offset inside another flat buffer."""
+    if gbase is None:
+        return lambda p, o=0: ptr(p, o)
+    base = flat.data.data_ptr()
+    return lambda p, o=0: gbase + (p.data_ptr() - base) + 4 * o
+
+
+class ActorParams:
+    """Device addresses of ActorNetwork_ATT_TwoPortion's weights (or of the same offsets in a
+    gradient-partial buffer when ``gbase`` is given)."""
+
+    def __init__(self, a, flat=None, gbase=None):
+        g = _addr(flat, gbase)
+        self.Wo, self.bo = g(a.own_fc[0].weight), g(a.own_fc[0].bias)
+        self.Wg, self.bg = g(a.own_grid[0].weight), g(a.own_grid[0].bias)
+        self.Wn, self.bn = g(a.neigh_fc[0].weight), g(a.neigh_fc[0].bias)
+        self.Wm, self.bm = g(a.merge_feature[0].weight), g(a.merge_feature[0].bias)
+        self.Wa, self.ba = g(a.act_out[0].weight), g(a.act_out[0].bias)
+        self.Wq, self.Wkv = g(a.q.weight), g(a.kv_weight)
+
+
+class CriticParams:
+    def __init__(self, c, flat=None, gbase=None):
+        g = _addr(flat, gbase)
+        N, H, Din = c.enc_w.shape
+        self.enc_w = [g(c.enc_w, n * H * Din) for n in range(N)]
+        self.enc_b = [g(c.enc_b, n * H) for n in range(N)]
+        self.Wc, self.bc = g(c.combine_agents_fea[0].weight), g(c.combine_agents_fea[0].bias)
+        self.Wq, self.bq = g(c.out_feature_q[0].weight), g(c.out_feature_q[0].bias)
+
+
+class ActorActs:
+    """Activations of one actor forward over R rows (kept for the backward)."""
+
+    def __init__(self, R, K, dev):
+        z = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)   # noqa: E731
+        self.R, self.K = R, K
+        self.cat = z(R, 192)          # [e_o | e_g | v_att]
+        self.xn = z(R * K, 64)
+        self.qa = z(R, 64)
+        self.kv = z(R * K, 128)
+        self.alpha = z(R, max(K, 1))
+        self.ha = z(R, 256)
+
+
+def actor_forward(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
+    """Launch list of ActorNetwork_ATT_TwoPortion.forward (ATT/nets:194-213) over R rows; the
+    tanh actions land at ``out`` with row stride ``ld_out`` (e.g. the critic-input rows)."""
+    c = acts
+    L = []
+    L += gemm_launches([
+        prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
+        prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
+        prob(nei, ap.Wn, ptr(c.xn), R * K, 64, 6, 6, 6, 64, tb=1, bias=ap.bn, act=RELU)])
+    L += gemm_launches([
+        prob(ptr(c.cat), ap.Wq, ptr(c.qa), R, 64, 64, 192, 64, 64, tb=1),
+        prob(ptr(c.xn), ap.Wkv, ptr(c.kv), R * K, 128, 64, 64, 64, 128, tb=1)])
+    L.append(lambda: _attn_fwd(ptr(c.qa), ptr(c.kv), nei, ptr(c.cat, 128), 192, ptr(c.alpha), R, K))
+    L += gemm_launches([prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm,
+                             act=RELU)])
+    L += gemm_launches([prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)])
+    return L
+
+
+def critic_forward(cp, X, rows, N, Din, f, h):
+    """Encoders + combine of CriticCombine (ATT/nets:672-724, R3) over ``rows`` samples whose
+    inputs are the rows X[b][n][:Din] = [own_n | a_n]."""
+    L = gemm_launches([prob(X + 4 * n * Din, cp.enc_w[n], ptr(f, n * 128), rows, 128, Din, N * Din, Din, 128 * N,
+                            tb=1, bias=cp.enc_b[n], act=RELU) for n in range(N)])
+    L += gemm_launches([prob(ptr(f), cp.Wc, ptr(h), rows, 256, 128 * N, 128 * N, 128 * N, 256, tb=1, bias=cp.bc,
+                             act=RELU)])
+    return L
+
+
+class FusedUpdate:
+    """One update_myown-equivalent on a DeviceReplay as a fixed launch list (graph-capturable)."""
+
+    SPLIT_ACTOR = 32     # K splits of the actor weight gradients (K = B*N or B*N*K rows)
+    SPLIT_CRITIC = 8     # K splits of the critic weight gradients (K = B rows)
+
+    def __init__(self, model, replay, B):
+        self.m, self.rep, self.B = model, replay, B
+        N, D0, K = model.n_agents, model.D0, model.n_agents - 1
+        self.N, self.D0, self.K, self.Din = N, D0, K, D0 + 2
+        dev = model.device
+        self.dev = dev
+        nb = N
+        self.nb = nb
+        z = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)   # noqa: E731
+        Bt = nb * B
+        # gathered batches (all N iterations), critic-input rows [own | a] and [own' | a']
+        self.idx = torch.empty(Bt, dtype=torch.int32, device=dev)
+        self.X = z(Bt, N, self.Din)
+        self.Xt = z(Bt, N, self.Din)
+        self.radar, self.nei = z(Bt, N, 18), z(Bt, N, K, 6)
+        self.nradar, self.nnei = z(Bt, N, 18), z(Bt, N, K, 6)
+        self.rew, self.done = z(Bt, N), z(Bt, N)
+        self.y = z(Bt)
+        self.q_c, self.q_a = z(Bt), z(Bt)            # per-iteration Q (stats)
+        # activations / gradients
+        self.acts_t = ActorActs(Bt * N, K, dev)      # target actor over all batches
+        self.acts = ActorActs(B * N, K, dev)
+        self.f_t, self.h_t = z(Bt, 128 * N), z(Bt, 256)
+        self.f, self.h = z(B, 128 * N), z(B, 256)
+        self.dq, self.dh, self.df = z(B), z(B, 256), z(B, 128 * N)
+        R = B * N
+        self.dout, self.dha = z(R, 2), z(R, 256)
+        self.dcat_o, self.dcat_g, self.dv = z(R, 64), z(R, 64), z(R, 64)
+        self.dqa, self.dkv, self.deo, self.dxn = z(R, 64), z(R * K, 128), z(R, 64), z(R * K, 64)
+        # weight-gradient partial copies (summed by the Adam kernel)
+        self.ga = torch.zeros(self.SPLIT_ACTOR, model.fa.numel, device=dev)
+        self.gc = torch.zeros(self.SPLIT_CRITIC, model.fc.numel, device=dev)
+        self._build()
+
+    # ------------------------------------------------------------------ plan
+    def _build(self):
+        m, B, N, D0, K, Din, nb = self.m, self.B, self.N, self.D0, self.K, self.Din, self.nb
+        A, At = ActorParams(m.actors), ActorParams(m.actors_target)
+        C, Ct = CriticParams(m.critics), CriticParams(m.critics_target)
+        rep = self.rep
+        self.pre = []      # sample + gather + targets
+        self.pre.append(lambda: ops.replay_sample(rep.meta, B, rep.seed, rep.counter, self.idx))
+        w = rep.widths
+        dsts = [ptr(self.X), ptr(self.radar), ptr(self.nei), ptr(self.X, D0), ptr(self.rew), ptr(self.done),
+                ptr(self.Xt), ptr(self.nradar), ptr(self.nnei)]
+        chunks = [D0, w[1], w[2], 2, w[4], w[5], D0, w[7], w[8]]
+        strides = [Din, w[1], w[2], Din, w[4], w[5], Din, w[7], w[8]]
+        self.pre.append(lambda: gather_strided(rep.ring, self.idx, dsts, w, chunks, strides))
+        Bt = nb * B
+        self.pre += actor_forward(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar), ptr(self.nnei), Bt * N, K,
+                                  D0, ptr(self.Xt, D0), Din)
+        self.pre += critic_forward(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
+        self.pre.append(lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),
+                                            done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y)))
+        self.iters = [self._iteration(i, A, C) for i in range(N)]
+        self.post = [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau),
+                     lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau),
+                     lambda: m.critic_optimizer.step_t.add_(N),
+                     lambda: m.actor_optimizer.step_t.add_(N)]
+        self.n_launches = len(self.pre) + sum(len(it) for it in self.iters) + len(self.post)
+
+    def _adam(self, opt, flat, gpart, ns, step_add):
+        m = self.m
+        if m.world > 1:     # reduce the partials, all-reduce the gradient, then the plain step
+            return [lambda: sum_partials(flat.grad, gpart, ns), lambda: m._allreduce(flat),
+                    lambda: adam_at(opt, step_add)]
+        return [lambda: adam_sum(opt, gpart, ns, step_add, grad_out=flat.grad)]
+
+    def _iteration(self, i, A, C):
+        m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
+        R = B * N
+        SA, SC = self.SPLIT_ACTOR, self.SPLIT_CRITIC
+        nA, nC = m.fa.numel, m.fc.numel
+        gA = ActorParams(m.actors, m.fa, self.ga.data_ptr())
+        gC = CriticParams(m.critics, m.fc, self.gc.data_ptr())
+        X = ptr(self.X, i * B * N * Din)
+        radar = ptr(self.radar, i * B * N * 18)
+        nei = ptr(self.nei, i * B * N * K * 6)
+        y = ptr(self.y, i * B)
+        f, h, dq, dh, df = self.f, self.h, self.dq, self.dh, self.df
+        L = []
+        # ---------------- critic step (ATT/maddpg:375-387)
+        L += critic_forward(C, X, B, N, Din, f, h)
+        L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh)))
+        L += gemm_launches([
+            prob(ptr(dq), ptr(h), gC.Wq, 1, 256, B, 1, 256, 256, ta=1, ones=1, cextra=gC.bq, ksplit=SC,
+                 split_stride=nC),
+            prob(ptr(dh), ptr(f), gC.Wc, 256, 128 * N, B, 256, 128 * N, 128 * N, ta=1, ones=1, cextra=gC.bc,
+                 ksplit=SC, split_stride=nC),
+            prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f), ldmask=128 * N,
+                 mact=RELU)])
+        L += gemm_launches([prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din,
+                                 Din, ta=1, ones=1, cextra=gC.enc_b[n], ksplit=SC, split_stride=nC)
+                            for n in range(N)])
+        L += self._adam(m.critic_optimizer, m.fc, self.gc, SC, i + 1)
+        # ---------------- actor step (ATT/maddpg:389-425); a_pi overwrites the replay actions in X
+        c = self.acts
+        L += actor_forward(A, c, X, Din, radar, nei, R, K, D0, X + 4 * D0, Din)
+        L += critic_forward(C, X, B, N, Din, f, h)
+        L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 1, q=ptr(self.q_a, i * B), dh=ptr(dh)))
+        L += gemm_launches([prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f),
+                                 ldmask=128 * N, mact=RELU)])
+        # da_n = df_n . W_enc_n[:, D0:D0+2]; dout = da * (1 - a^2)   (rows b*N + n of dout)
+        L += gemm_launches([prob(ptr(df, n * 128), C.enc_w[n] + 4 * D0, ptr(self.dout, 2 * n), B, 2, 128, 128 * N,
+                                 Din, 2 * N, mask=X + 4 * (n * Din + D0), ldmask=N * Din, mact=TANH)
+                            for n in range(N)])
+        L += gemm_launches([
+            prob(ptr(self.dout), ptr(c.ha), gA.Wa, 2, 256, R, 2, 256, 256, ta=1, ones=1, cextra=gA.ba, ksplit=SA,
+                 split_stride=nA),
+            prob(ptr(self.dout), A.Wa, ptr(self.dha), R, 256, 2, 2, 256, 256, mask=ptr(c.ha), ldmask=256,
+                 mact=RELU)])
+        L += gemm_launches([
+            prob(ptr(self.dha), ptr(c.cat), gA.Wm, 256, 192, R, 256, 192, 192, ta=1, ones=1, cextra=gA.bm,
+                 ksplit=SA, split_stride=nA),
+            prob(ptr(self.dha), A.Wm, ptr(self.dcat_o), R, 64, 256, 256, 192, 64),
+            prob(ptr(self.dha), A.Wm + 4 * 64, ptr(self.dcat_g), R, 64, 256, 256, 192, 64, mask=ptr(c.cat, 64),
+                 ldmask=192, mact=RELU),
+            prob(ptr(self.dha), A.Wm + 4 * 128, ptr(self.dv), R, 64, 256, 256, 192, 64)])
+        L.append(lambda: _attn_bwd(ptr(c.qa), ptr(c.kv), ptr(c.alpha), ptr(self.dv), 64, ptr(self.dqa),
+                                   ptr(self.dkv), R, K))
+        L += gemm_launches([
+            prob(ptr(self.dqa), A.Wq, ptr(self.deo), R, 64, 64, 64, 64, 64, addend=ptr(self.dcat_o), ldadd=64,
+                 mask=ptr(c.cat), ldmask=192, mact=RELU),
+            prob(ptr(self.dqa), ptr(c.cat), gA.Wq, 64, 64, R, 64, 192, 64, ta=1, ksplit=SA, split_stride=nA),
+            prob(ptr(self.dkv), ptr(c.xn), gA.Wkv, 128, 64, R * K, 128, 64, 64, ta=1, ksplit=SA, split_stride=nA),
+            prob(ptr(self.dkv), A.Wkv, ptr(self.dxn), R * K, 64, 128, 128, 64, 64, mask=ptr(c.xn), ldmask=64,
+                 mact=RELU)])
+        L += gemm_launches([
+            prob(ptr(self.deo), X, gA.Wo, 64, D0, R, 64, Din, D0, ta=1, ones=1, cextra=gA.bo, ksplit=SA,
+                 split_stride=nA),
+            prob(ptr(self.dcat_g), radar, gA.Wg, 64, 18, R, 64, 18, 18, ta=1, ones=1, cextra=gA.bg, ksplit=SA,
+                 split_stride=nA),
+            prob(ptr(self.dxn), nei, gA.Wn, 64, 6, R * K, 64, 6, 6, ta=1, ones=1, cextra=gA.bn, ksplit=SA,
+                 split_stride=nA)])
+        L += self._adam(m.actor_optimizer, m.fa, self.ga, SA, i + 1)
+        return L
+
+    # ------------------------------------------------------------------ run
+    def run(self, idx=None):
+        if idx is None:
+            self.pre[0]()
+        else:
+            self.idx.copy_(idx.reshape(-1))
+        for op in self.pre[1:]:
+            op()
+        for it in self.iters:
+            for op in it:
+                op()
+        for op in self.post:
+            op()
+
+    def stats(self):
+        """[(loss_q, loss_a, q, target)] per iteration, like MADDPG._iteration."""
+        B = self.B
+        out = []
+        for i in range(self.N):
+            q = self.q_c[i * B:(i + 1) * B].unsqueeze(1)
+            y = self.y[i * B:(i + 1) * B]
+            out.append((((q - y.unsqueeze(1)) ** 2).mean(), -self.q_a[i * B:(i + 1) * B].mean(), q, y))
+        return out

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from . import ops, parallel
+from . import fused, ops, parallel
 from .memory import DeviceReplay, ReplayMemory
 from .networks import ActorNetwork_ATT_TwoPortion, CriticCombine, FlatParams
 
@@ -58,8 +58,9 @@ class MADDPG:
     def __init__(self, actor_dim, critic_dim, dim_act, actor_hidden_state_size=64, gru_history_length=10,
                  n_agents=5, args=None, cr_lr=1e-3, ac_lr=1e-3, gamma=0.95, tau=0.01,
                  full_observable_critic_flag=True, device=None, seed=None, memory_length=None, batch_size=None,
-                 process_group=None, blas="cublas"):
+                 process_group=None, blas="cublas", fused=True):
         self.args = args
+        self.fused = bool(fused)     # fused HIP learner (fused.py); False = autograd over layers.py
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -102,7 +103,8 @@ class MADDPG:
         self._graph = None
         self._graph_B = None
         self.steps_done = 0
-        self.last_stats = None
+        self._last_src = None
+        self._fplans = {}
 
     # ------------------------------------------------------------------ batched API
     def attach_replay(self, capacity, seed=0):
@@ -152,10 +154,21 @@ class MADDPG:
         self.actor_optimizer.step()
         return loss_q.detach(), loss_a.detach(), q.detach(), target
 
+    def _fused_plan(self, B):
+        rep = self.replay if self.replay is not None else self.memory.dev
+        key = (B, id(rep))
+        if key not in self._fplans:
+            self._fplans[key] = fused.FusedUpdate(self, rep, B)
+        return self._fplans[key]
+
     def _update_core(self, B, idx_list=None):
         rep = self.replay if self.replay is not None else self.memory.dev
         N = self.n_agents
         idx = None if idx_list is None else torch.cat([i.reshape(-1) for i in idx_list])
+        if self.fused:
+            fu = self._fused_plan(B)
+            fu.run(idx)
+            return fu
         ball = rep.sample_batch(B, idx, nb=N)           # N independent batches, one launch each
         target = self._targets(ball, B)
         stats = []
@@ -192,17 +205,24 @@ class MADDPG:
         self._graph, self._graph_B = g, B
         return g
 
-    def update(self, B=None, use_graph=True, idx_list=None):
-        """One update_myown-equivalent on the device replay (no host synchronisation)."""
+    def update(self, B=None, use_graph=True, idx_list=None, want_stats=True):
+        """One update_myown-equivalent on the device replay (no host synchronisation).  Returns
+        [(loss_q, loss_a, q, target)] per iteration (computed on demand: ``want_stats=False``
+        launches nothing beyond the update itself)."""
         B = B or self.batch_size
         if idx_list is None and use_graph and self.world == 1:
             if self._graph is None or self._graph_B != B:
                 self.capture(B)
             self._graph.replay()
-            self.last_stats = self._graph_stats
+            self._last_src = self._graph_stats
         else:
-            self.last_stats = self._update_core(B, idx_list)
-        return self.last_stats
+            self._last_src = self._update_core(B, idx_list)
+        return self.last_stats if want_stats else None
+
+    @property
+    def last_stats(self):
+        src = self._last_src
+        return src.stats() if isinstance(src, fused.FusedUpdate) else src
 
     # ------------------------------------------------------------------ reference API
     def choose_action(self, state, cur_total_step, cur_episode, step, mini_noise_eps, noise_start_level,

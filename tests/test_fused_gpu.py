@@ -1,0 +1,194 @@
+"""GPU tests of the fused learner building blocks (include/aac_fused.h) against plain PyTorch
+fp64 references, and of the fused update against the autograd learner and the CPU restatement."""
+import functools
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _op(x, t):
+    return x.t() if t else x
+
+
+CASES = [  # M, N, K, ta, tb, ones, act, mact, addend
+    (5, 3, 7, 0, 0, 0, 0, 0, False),
+    (130, 70, 300, 0, 1, 0, 1, 0, False),
+    (64, 64, 16, 1, 0, 0, 2, 0, True),
+    (1, 256, 1024, 1, 0, 1, 0, 0, False),
+    (256, 193, 5120, 1, 0, 1, 0, 0, False),
+    (1024, 640, 256, 0, 0, 0, 0, 1, False),
+    (5120, 2, 256, 0, 1, 0, 2, 0, False),
+    (5120, 64, 64, 0, 0, 0, 0, 1, True),
+    (97, 129, 33, 1, 1, 0, 0, 2, False),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_gemm_batch_epilogues(native_lib, case):
+    from multi_agent_aac_amd import fused
+    M, N, K, ta, tb, ones, act, mact, add = case
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
+    r = lambda *s: torch.rand(*s, device=DEV, generator=g) * 2 - 1   # noqa: E731
+    A = r(K, M) if ta else r(M, K)
+    B = r(N, K) if tb else r(K, N)
+    bias = r(N) if not ones else None
+    addend = r(M, N) if add else None
+    mask = r(M, N) if mact else None
+    C = torch.full((M, N), 7.0, device=DEV)
+    cextra = torch.zeros(M, device=DEV) if ones else None
+    p = fused.prob(fused.ptr(A), fused.ptr(B), fused.ptr(C), M, N, K, A.shape[1], B.shape[1], N, ta=ta, tb=tb,
+                   bias=fused.ptr(bias), act=act, addend=fused.ptr(addend), ldadd=N, mask=fused.ptr(mask), ldmask=N,
+                   mact=mact, ones=ones, cextra=fused.ptr(cextra))
+    launch = fused.GemmLaunch([p])
+    launch()
+    prod = _op(A.double(), ta) @ _op(B.double(), tb)
+    want = prod.clone()
+    if add:
+        want += addend.double()
+    if bias is not None:
+        want += bias.double()
+    if act == 1:
+        want = want.clamp_min(0)
+    elif act == 2:
+        want = torch.tanh(want)
+    if mact == 1:
+        want = want * (mask > 0)
+    elif mact == 2:
+        want = want * (1 - mask.double() ** 2)
+    tol = 2e-6 * np.sqrt(K) + 1e-6
+    np.testing.assert_allclose(C.cpu().double(), want.cpu(), atol=tol, rtol=1e-5)
+    if ones:
+        np.testing.assert_allclose(cextra.cpu().double(), _op(A.double(), ta).sum(1).cpu(), atol=tol, rtol=1e-5)
+    C2 = torch.zeros_like(C)
+    p2 = fused.prob(fused.ptr(A), fused.ptr(B), fused.ptr(C2), M, N, K, A.shape[1], B.shape[1], N, ta=ta, tb=tb,
+                    bias=fused.ptr(bias), act=act, addend=fused.ptr(addend), ldadd=N, mask=fused.ptr(mask),
+                    ldmask=N, mact=mact, ones=ones, cextra=fused.ptr(cextra))
+    fused.GemmLaunch([p2])()
+    assert torch.equal(C, C2)                    # deterministic
+
+
+def test_gemm_batch_grouped(native_lib):
+    """Several products of different shapes in one launch land where they should."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(0)
+    shapes = [(100, 64, 22), (300, 128, 64), (2, 256, 5000), (64, 6, 9000)]
+    As = [torch.randn(M, K, device=DEV) for M, N, K in shapes]
+    Bs = [torch.randn(K, N, device=DEV) for M, N, K in shapes]
+    Cs = [torch.empty(M, N, device=DEV) for M, N, K in shapes]
+    probs = [fused.prob(fused.ptr(a), fused.ptr(b), fused.ptr(c), M, N, K, K, N, N)
+             for (M, N, K), a, b, c in zip(shapes, As, Bs, Cs)]
+    fused.GemmLaunch(probs)()
+    for (M, N, K), a, b, c in zip(shapes, As, Bs, Cs):
+        np.testing.assert_allclose(c.cpu().double(), (a.double() @ b.double()).cpu(), atol=3e-6 * np.sqrt(K) * 3,
+                                   rtol=1e-5)
+
+
+def test_gemm_split_copies(native_lib):
+    """ksplit > 1 writes per-split partial products that sum to the full product."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(1)
+    M, N, K, S = 64, 23, 5120, 16
+    G = torch.randn(K, M, device=DEV)          # stored rows x outputs, op(A) = G^T
+    X = torch.randn(K, N, device=DEV)
+    stride = M * N + M + 7
+    part = torch.full((S, stride), 3.0, device=DEV)
+    fused.GemmLaunch([fused.prob(fused.ptr(G), fused.ptr(X), fused.ptr(part), M, N, K, M, N, N, ta=1, ones=1,
+                                 cextra=fused.ptr(part, M * N), ksplit=S, split_stride=stride)])()
+    tot = part.double().sum(0)
+    np.testing.assert_allclose(tot[:M * N].reshape(M, N).cpu(), (G.double().t() @ X.double()).cpu(), atol=2e-4)
+    np.testing.assert_allclose(tot[M * N:M * N + M].cpu(), G.double().sum(0).cpu(), atol=2e-4)
+    out = torch.empty(stride, device=DEV)
+    fused.sum_partials(out, part, S)
+    np.testing.assert_allclose(out.cpu().double(), tot.cpu(), atol=1e-4)
+
+
+def test_gemm_rejects_bad_plans(native_lib):
+    from multi_agent_aac_amd import fused
+    for p, msg in ((fused.prob(1, 1, 1, 0, 4, 4, 4, 4, 4), "empty"),
+                   (fused.prob(1, 1, 1, 4, 4, 4, 4, 4, 4, ones=1), "cextra"),
+                   (fused.prob(1, 1, 1, 4, 4, 4, 4, 4, 4, bias=1, ksplit=2, split_stride=64), "plain")):
+        with pytest.raises(RuntimeError, match=msg):
+            fused.GemmLaunch([p])()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_critic_head(native_lib, mode):
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(mode)
+    M, B, N = 3 * 128, 128, 3
+    h = torch.relu(torch.randn(M, 256, device=DEV))
+    w, b = torch.randn(256, device=DEV), torch.randn(1, device=DEV)
+    y = torch.randn(M, device=DEV)
+    rew = torch.randn(M, N, device=DEV)
+    done = (torch.rand(M, N, device=DEV) < 0.2).float()
+    q, dq, dh, yout = (torch.empty(M, device=DEV), torch.empty(M, device=DEV), torch.empty(M, 256, device=DEV),
+                       torch.empty(M, device=DEV))
+    P = fused.ptr
+    fused.critic_head(P(h), M, P(w), P(b), mode, y=P(y), rew=P(rew), done=P(done), B=B, N=N, gamma=0.95, q=P(q),
+                      dq=P(dq), dh=P(dh), yout=P(yout))
+    qr = h.double() @ w.double() + b.double()
+    np.testing.assert_allclose(q.cpu(), qr.cpu(), atol=1e-4, rtol=1e-5)
+    if mode == 2:
+        it = torch.arange(M, device=DEV) // B
+        r = rew[torch.arange(M, device=DEV), it]
+        want = r + 0.95 * q * (1 - (done == 1).any(1).float())
+        np.testing.assert_allclose(yout.cpu(), want.cpu(), atol=1e-5, rtol=1e-5)
+        return
+    g = (2.0 / M) * (q - y) if mode == 0 else torch.full_like(q, -1.0 / M)
+    np.testing.assert_allclose(dq.cpu(), g.cpu(), atol=1e-6, rtol=1e-6)
+    np.testing.assert_allclose(dh.cpu(), (g[:, None] * w[None] * (h > 0)).cpu(), atol=1e-6, rtol=1e-6)
+
+
+def test_gather_strided(native_lib):
+    from multi_agent_aac_amd import fused
+    rw, B = 50, 33
+    ring = torch.arange(200 * rw, dtype=torch.float32, device=DEV).reshape(200, rw)
+    idx = torch.randperm(200, device=DEV)[:B].to(torch.int32)
+    X = torch.full((B, 3, 6), -1.0, device=DEV)
+    rest = torch.empty(B, 50 - 18, device=DEV)
+    fused.gather_strided(ring, idx, [fused.ptr(X), fused.ptr(X, 4), fused.ptr(rest)], [12, 6, 32], [4, 2, 32],
+                         [6, 6, 32])
+    src = ring[idx.long()].cpu()
+    Xc = X.cpu()
+    assert torch.equal(Xc[:, :, :4], src[:, :12].reshape(B, 3, 4))
+    assert torch.equal(Xc[:, :, 4:], src[:, 12:18].reshape(B, 3, 2))
+    assert torch.equal(rest.cpu(), src[:, 18:])
+
+
+@pytest.mark.parametrize("N,B", [(3, 64), (5, 256)])
+def test_autograd_learner_matches_cpu_restatement(native_lib, N, B):
+    """The layer-by-layer autograd learner (fused=False) stays a second, independent GPU path."""
+    from multi_agent_aac_amd.maddpg import MADDPG
+    cls = functools.partial(MADDPG, fused=False)
+    assert learner_ref.check_one_update(cls, device=DEV, N=N, B=B, E=128, tol=1e-5, iters=2)
+
+
+def test_fused_equals_autograd_learner(native_lib):
+    from multi_agent_aac_amd.maddpg import MADDPG
+    N, B, E = 5, 256, 512
+    ms = []
+    for fz in (True, False):
+        m = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=N, device=DEV, seed=4, batch_size=B, fused=fz)
+        rep = m.attach_replay(4 * E, seed=2)
+        for p in range(3):
+            tr = learner_ref.random_transitions(E, N, 10 + p)
+            rep.push_batch(*[tr[k].to(DEV).contiguous() for k in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
+                                                                   "n_own", "n_radar", "n_nei")])
+        ms.append(m)
+    for _ in range(3):
+        sa = ms[0].update(B, use_graph=False)
+        sb = ms[1].update(B, use_graph=False)
+        for (la, aa, qa, ta), (lb, ab, qb, tb) in zip(sa, sb):
+            np.testing.assert_allclose(qa.cpu(), qb.cpu(), atol=1e-5, rtol=1e-5)
+            np.testing.assert_allclose(ta.cpu(), tb.cpu(), atol=1e-5, rtol=1e-5)
+            np.testing.assert_allclose(float(aa), float(ab), atol=1e-5, rtol=1e-5)
+    # 15 Adam steps: a parameter whose gradient sits near zero moves by ~lr * sign(m / sqrt(v)), so
+    # fp32 summation-order differences between the two learners can show at ~1e-5 there
+    for a, b in ((ms[0].fa.data, ms[1].fa.data), (ms[0].fc.data, ms[1].fc.data), (ms[0].fa_t.data, ms[1].fa_t.data)):
+        np.testing.assert_allclose(a.cpu(), b.cpu(), atol=1e-4, rtol=1e-5)
