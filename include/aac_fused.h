@@ -77,6 +77,13 @@ int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, cons
                     const float *y, const float *rew, const float *done, int32_t B, int32_t N, float gamma, float *q,
                     float *dq, float *dh, float *yout, void *stream);
 
+/* Inference form of the actor's neighbour attention (ATT/nets:186-210) for R rows, K <= 32:
+ * x_j = relu(Wn nei_j + bn) computed from the 6-wide rows nei[(r*K + j)*6], scores
+ * x_j . (Wqk e_o) / 8 with Wqk = Wk^T Wq (64x64, precomputed), masked softmax (mask
+ * nei_j.mean() != 0), out[r*ldo + c] = (Wv sum_j a_j x_j)[c]; e_o rows at eo + r*lde. */
+int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *Wn, const float *bn,
+                   const float *Wqk, const float *Wv, float *out, int32_t ldo, int32_t R, int32_t K, void *stream);
+
 /* Replay gather with interleaved destinations: element c of field f of sampled row b goes to
  * dsts[f][b*(widths[f]/chunks[f])*dstrides[f] + (c/chunks[f])*dstrides[f] + c%chunks[f]]
  * (chunks = widths, dstrides = widths gives aac_replay_gather).  Lets [own_n | a_n] land as the

@@ -50,7 +50,8 @@ struct GProb {
     int M, N, K;
     int lda, ldb, ldc, ldadd, ldmask;
     int ta, tb, act, mact, ones, ks;
-    int avec, bvec;            // fragment loads as float4 along K
+    int amode, bmode;          // fragment load modes LV / LS / LT
+    int deep;                  // 4-deep prefetch ring (long chains) or none
     int tiles_n, w_begin;      // first workgroup of this product
 };
 
@@ -77,34 +78,109 @@ __device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, in
     C[(size_t)m * P.ldc + n] = v;
 }
 
-// fragments of one K chunk: f[i][t] = op(X)[row0 + 16 i + lr][kc + 4 lk + t]
-//   A side: row = m, op(A)[m][k];  B side: row = n, op(B)[k][n]
-__device__ __forceinline__ void load_frag(const float *X, int ld, int trans, int vec, int rows, int K, int kc,
-                                          int row0, int lr, int lk, int ones_row, float f[2][4]) {
+// Fragment load modes of an operand whose rows are the MFMA row index (m for A, n for B):
+//   LV  K-contiguous rows, ld % 4 == 0, K % 4 == 0, 16-B aligned: one 16-B load per row
+//   LS  K-contiguous rows, otherwise: four 4-B loads
+//   LT  row-contiguous (stored [k][row]): four 4-B loads, 16 lanes cover 64 contiguous bytes
+// Loads are raw buffer loads; an element outside the operand (row >= rows, k >= K, or a chunk
+// this wave does not own) gets an out-of-range offset and the hardware returns 0, so nothing
+// touches a loaded value before its MFMA and the compiler's vmcnt tracking stays exact across
+// the prefetch ring.  f[i][t] = op(X)[row0 + 16 i + lr][kc + 4 lk + t].
+enum { LV = 0, LS = 1, LT = 2 };
+constexpr int OOB = 0x7ffffff0;     // byte offset past every operand (= num_records)
+
+typedef int i4 __attribute__((ext_vector_type(4)));
+// the LLVM buffer-load intrinsics (the clang b128 builtin lowers to a single dword here)
+__device__ f4 buf_load_x4(i4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ float buf_load_x1(i4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
+
+__device__ __forceinline__ i4 rsrc_of(const float *p) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    i4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+    r.y = __builtin_amdgcn_readfirstlane((int)(a >> 32));     // stride 0
+    r.z = OOB;                                                 // num_records (bytes)
+    r.w = 0x00020000;                                          // gfx9 dword3: 32-bit data format
+    return r;
+}
+
+template <int MODE>
+__device__ __forceinline__ void load_frag(i4 X, int ld, int rows, int K, int kc, int row0,
+                                          int lr, int lk, bool on, float f[2][4]) {
     const int k0 = kc + 4 * lk;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r = row0 + 16 * i + lr;
-        if (vec) {
-            // K-contiguous rows, ld % 4 == 0, K % 4 == 0, 16-B aligned base
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (r < rows && k0 < K) v = *reinterpret_cast<const float4 *>(X + (size_t)r * ld + k0);
-            f[i][0] = v.x; f[i][1] = v.y; f[i][2] = v.z; f[i][3] = v.w;
+        const bool rin = on && r < rows;
+        if (MODE == LV) {
+            const int off = (rin && k0 < K) ? (r * ld + k0) * 4 : OOB;
+            const f4 v = buf_load_x4(X, off, 0, 0);
+            f[i][0] = v.x;
+            f[i][1] = v.y;
+            f[i][2] = v.z;
+            f[i][3] = v.w;
         } else {
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const int k = k0 + t;
-                float v = 0.0f;
-                if (k < K) {
-                    if (r < rows) v = trans ? X[(size_t)k * ld + r] : X[(size_t)r * ld + k];
-                    else if (r == ones_row) v = 1.0f;
-                }
-                f[i][t] = v;
+                const int off = (rin && k < K) ? (MODE == LT ? k * ld + r : r * ld + k) * 4 : OOB;
+                f[i][t] = buf_load_x1(X, off, 0, 0);
             }
         }
     }
 }
 
+// one 32x32 tile over this wave's chunks c0, c0+4, ... < c1 (D-deep register ring: the loads of
+// the next D-1 chunks are in flight while one is multiplied; these chains are latency-bound).
+// The virtual ones row of op(B) (bias gradient) is a constant fragment: extra MFMAs in the one
+// tile column that holds it.
+template <int AM, int BM, int D>
+__device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0, int c1, int lr, int lk,
+                                         f4 acc[2][2]) {
+    const int nreal = P.N - P.ones;
+    const i4 ra = rsrc_of(P.A), rb = rsrc_of(P.B);
+    const bool has_one = P.ones && nreal >= n0 && nreal < n0 + WT;      // wave-uniform
+    float one[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) one[j] = (n0 + 16 * j + lr == nreal) ? 1.0f : 0.0f;
+    float fa[D][2][4], fb[D][2][4];
+    const int nmine = c0 < c1 ? (c1 - c0 + 3) / 4 : 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const bool on = d < nmine;
+        const int kc = (c0 + 4 * d) * KC;
+        load_frag<AM>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
+        load_frag<BM>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
+    }
+    for (int q0 = 0; q0 < nmine; q0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][0][t], fb[d][0][t], acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][0][t], fb[d][1][t], acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][1][t], fb[d][0][t], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][1][t], fb[d][1][t], acc[1][1], 0, 0, 0);
+            }
+            if (has_one) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][i][t], one[j], acc[i][j], 0, 0, 0);
+            }
+            const int qn = q0 + d + D;
+            const bool on = qn < nmine;
+            const int kc = (c0 + 4 * qn) * KC;
+            load_frag<AM>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
+            load_frag<BM>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
+        }
+    }
+}
+
+template <bool DEEP>
 __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     __shared__ f4 red[4][4][64];       // [wave][quadrant][lane]
     const int wg = blockIdx.x;
@@ -119,11 +195,6 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     const int w = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int lr = lane & 15, lk = lane >> 4;
-    const int nreal = P.N - P.ones;
-    // op(A) rows are m: stored A[m][k] (ta = 0, K-contiguous) or A[k][m] (ta = 1)
-    // op(B) rows are n: stored B[n][k] (tb = 1, K-contiguous) or B[k][n] (tb = 0)
-    const int a_tr = P.ta, b_tr = !P.tb;
-    const int ones_row = P.ones ? nreal : -1;
 
     // split s of K, and inside it the four waves take every fourth chunk
     const int nch = (P.K + KC - 1) / KC;
@@ -136,35 +207,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-
-    float a[2][4], b[2][4], an[2][4], bn[2][4];
-    if (c0 < c1) {
-        load_frag(P.A, P.lda, a_tr, P.avec, P.M, P.K, c0 * KC, m0, lr, lk, -1, a);
-        load_frag(P.B, P.ldb, b_tr, P.bvec, nreal, P.K, c0 * KC, n0, lr, lk, ones_row, b);
+    // the deep-ring instantiations need ~120 VGPRs; launches without a long-K product use the
+    // shallow kernel so the large memory-bound products keep their occupancy
+#define TM(a, b)                                                                                   \
+    case (a * 3 + b) * 2 + 0: tile_mma<a, b, 1>(P, m0, n0, c0, c1, lr, lk, acc); break;          \
+    case (a * 3 + b) * 2 + 1: tile_mma<a, b, DEEP ? 4 : 1>(P, m0, n0, c0, c1, lr, lk, acc); break;
+    switch ((P.amode * 3 + P.bmode) * 2 + P.deep) {
+        TM(LV, LV) TM(LV, LS) TM(LV, LT) TM(LS, LV) TM(LS, LS) TM(LS, LT) TM(LT, LV) TM(LT, LS) TM(LT, LT)
     }
-    for (int c = c0; c < c1; c += 4) {
-        const bool more = c + 4 < c1;
-        if (more) {
-            load_frag(P.A, P.lda, a_tr, P.avec, P.M, P.K, (c + 4) * KC, m0, lr, lk, -1, an);
-            load_frag(P.B, P.ldb, b_tr, P.bvec, nreal, P.K, (c + 4) * KC, n0, lr, lk, ones_row, bn);
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][t], b[0][t], acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][t], b[1][t], acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][t], b[0][t], acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][t], b[1][t], acc[1][1], 0, 0, 0);
-        }
-        if (more) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    a[i][t] = an[i][t];
-                    b[i][t] = bn[i][t];
-                }
-        }
-    }
+#undef TM
     // reduce the four waves' partial tiles in wave order; wave q finishes quadrant q = (i, j)
     red[w][0][lane] = acc[0][0];
     red[w][1][lane] = acc[0][1];
@@ -251,6 +302,100 @@ __global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, 
     for (int j = 0; j < 4; ++j) dh[(size_t)r * 256 + lane + 64 * j] = hv[j] > 0.0f ? g * wv[j] : 0.0f;
 }
 
+// ------------------------------------------------------------------------------ attention block
+// Inference form of the actor's neighbour attention (ATT/nets:186-210) for one row per wave
+// iteration, lane = feature:
+//   x_j   = relu(Wn nei_j + bn)                       (neighbour encoder, on the fly from the
+//                                                      6-wide rows: no [rows*K][64] tensor)
+//   s_j   = (Wk x_j) . (Wq e_o) / 8 = x_j . (Wqk e_o) / 8,   Wqk = Wk^T Wq (precomputed)
+//   a     = softmax over the valid j (nei_j.mean() != 0), 0 for the masked ones
+//   v_att = sum_j a_j (Wv x_j) = Wv (sum_j a_j x_j)  (no [rows*K][128] k|v tensor)
+// Each wave keeps row ``lane`` of Wqk and of Wv in registers; the vector being multiplied is
+// broadcast from a 64-float LDS slot of the wave.
+template <int KM>
+__global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict__ eo, int lde,
+                                                         const float *__restrict__ nei,
+                                                         const float *__restrict__ Wn,
+                                                         const float *__restrict__ bn,
+                                                         const float *__restrict__ Wqk,
+                                                         const float *__restrict__ Wv, float *out, int ldo, int R,
+                                                         int K) {
+    __shared__ f4 buf4[4][16];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    float *buf = reinterpret_cast<float *>(buf4[wv]);
+    float wq[64], wvr[64], wn[6];
+#pragma unroll
+    for (int o = 0; o < 64; o += 4) {
+        const f4 a = *reinterpret_cast<const f4 *>(Wqk + lane * 64 + o);
+        const f4 b = *reinterpret_cast<const f4 *>(Wv + lane * 64 + o);
+        wq[o] = a.x; wq[o + 1] = a.y; wq[o + 2] = a.z; wq[o + 3] = a.w;
+        wvr[o] = b.x; wvr[o + 1] = b.y; wvr[o + 2] = b.z; wvr[o + 3] = b.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) wn[i] = Wn[lane * 6 + i];
+    const float bnl = bn[lane];
+    const int nwaves = gridDim.x * 4;
+    for (int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv); r < R; r += nwaves) {
+        buf[lane] = eo[(size_t)r * lde + lane];
+        float qk = 0.0f;
+#pragma unroll
+        for (int o = 0; o < 64; o += 4) {
+            const f4 e = buf4[wv][o >> 2];
+            qk = fmaf(wq[o], e.x, qk);
+            qk = fmaf(wq[o + 1], e.y, qk);
+            qk = fmaf(wq[o + 2], e.z, qk);
+            qk = fmaf(wq[o + 3], e.w, qk);
+        }
+        float x[KM], sc[KM];
+        float mx = -INFINITY;
+        unsigned valid = 0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            const float *nb = nei + ((size_t)r * K + j) * 6;
+            float h = bnl;
+            float sum = nb[0];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) h = fmaf(wn[i], nb[i], h);
+#pragma unroll
+            for (int i = 1; i < 6; ++i) sum += nb[i];
+            x[j] = h > 0.0f ? h : 0.0f;
+            sc[j] = wsum(x[j] * qk) / 8.0f;
+            if (sum != 0.0f) {
+                valid |= 1u << j;
+                mx = sc[j] > mx ? sc[j] : mx;
+            }
+        }
+        float den = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            const float e = (valid >> j & 1) ? expf(sc[j] - mx) : 0.0f;
+            sc[j] = e;
+            den += e;
+        }
+        float xb = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            const float a = (valid >> j & 1) ? sc[j] / den : 0.0f;
+            xb = fmaf(a, x[j], xb);
+        }
+        buf[lane] = xb;
+        float v = 0.0f;
+#pragma unroll
+        for (int o = 0; o < 64; o += 4) {
+            const f4 e = buf4[wv][o >> 2];
+            v = fmaf(wvr[o], e.x, v);
+            v = fmaf(wvr[o + 1], e.y, v);
+            v = fmaf(wvr[o + 2], e.z, v);
+            v = fmaf(wvr[o + 3], e.w, v);
+        }
+        out[(size_t)r * ldo + lane] = v;
+    }
+}
+
 // ------------------------------------------------------------------------------ gather
 struct SFields {
     float *dst[16];
@@ -299,8 +444,14 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         d.lda = s.lda; d.ldb = s.ldb; d.ldc = s.ldc; d.ldadd = s.ldadd; d.ldmask = s.ldmask;
         d.ta = s.ta; d.tb = s.tb; d.act = s.act; d.mact = s.mact; d.ones = s.ones;
         d.ks = ks;
-        d.avec = !s.ta && s.lda % 4 == 0 && s.K % 4 == 0 && aligned16(s.A);
-        d.bvec = s.tb && !s.ones && s.ldb % 4 == 0 && s.K % 4 == 0 && aligned16(s.B);
+        // op(A) rows (m) are K-contiguous unless ta; op(B) rows (n) are K-contiguous iff tb
+        d.amode = s.ta ? LT : (s.lda % 4 == 0 && s.K % 4 == 0 && aligned16(s.A) ? LV : LS);
+        d.bmode = !s.tb ? LT : (!s.ones && s.ldb % 4 == 0 && s.K % 4 == 0 && aligned16(s.B) ? LV : LS);
+        {
+            const int nch = (s.K + KC - 1) / KC;
+            const int per = (nch + ks - 1) / ks;
+            d.deep = (per + 3) / 4 > 2;       // > 2 chunks per wave: prefetch ring
+        }
         const int tm = (s.M + WT - 1) / WT, tn = (s.N + WT - 1) / WT;
         d.tiles_n = tn;
         d.w_begin = waves;          // in workgroups (one per tile and split)
@@ -319,7 +470,10 @@ const char *aac_fused_last_error(void) { return f_err.c_str(); }
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
     GBatch g{};
     if (plan(probs, n, g)) return -1;
-    hipLaunchKernelGGL(gemm_kernel, dim3(g.waves), dim3(256), 0, (hipStream_t)stream, g);
+    bool deep = false;
+    for (int i = 0; i < g.n; ++i) deep |= g.p[i].deep != 0;
+    if (deep) hipLaunchKernelGGL(gemm_kernel<true>, dim3(g.waves), dim3(256), 0, (hipStream_t)stream, g);
+    else hipLaunchKernelGGL(gemm_kernel<false>, dim3(g.waves), dim3(256), 0, (hipStream_t)stream, g);
     FHIP(hipGetLastError());
     return 0;
 }
@@ -355,6 +509,22 @@ int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, cons
     if (mode == 2 && (!rew || !done || !yout || B <= 0 || N <= 0)) return ffail("critic_head: mode 2 needs rew/done/yout");
     hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, M, w, b, mode, y, rew,
                        done, B, N, gamma, q, dq, dh, yout);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *Wn, const float *bn,
+                   const float *Wqk, const float *Wv, float *out, int32_t ldo, int32_t R, int32_t K, void *stream) {
+    if (R <= 0) return 0;
+    if (K < 1 || K > 32) return ffail("attn_block: 1 <= K <= 32");
+    int waves = (R + 3) / 4 < 1024 ? (R + 3) / 4 : 1024;
+    waves = waves < 1 ? 1 : waves;
+    const dim3 grid(waves), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (K <= 4) hipLaunchKernelGGL(attn_block_kernel<4>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
+    else if (K <= 8) hipLaunchKernelGGL(attn_block_kernel<8>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
+    else if (K <= 16) hipLaunchKernelGGL(attn_block_kernel<16>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
+    else hipLaunchKernelGGL(attn_block_kernel<32>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
     FHIP(hipGetLastError());
     return 0;
 }

@@ -59,6 +59,7 @@ def lib():
         L.aac_sum_partials.argtypes = [vp, vp, i32, i64, vp]
         L.aac_critic_head.argtypes = [vp, i32, i32, vp, vp, i32, vp, vp, vp, i32, i32, f32, vp, vp, vp, vp, vp]
         L.aac_replay_gather_strided.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]
+        L.aac_attn_block.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
         L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         _L = L
     return _L
@@ -141,6 +142,11 @@ def adam_at(opt, step_add):
                                 _stream()), "aac_adam_flat_at")
 
 
+def attn_block(eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K):
+    _chk(lib().aac_attn_block(vp(eo), lde, vp(nei), vp(Wn), vp(bn), vp(Wqk), vp(Wv), vp(out), ldo, R, K, _stream()),
+         "aac_attn_block")
+
+
 def _attn_fwd(q, kv, nei, out, out_stride, alpha, R, K):
     L = ops.lib()
     ops._chk(L.aac_attn_fwd(vp(q), vp(kv), vp(kv + 256), 128, vp(nei), vp(out), out_stride, vp(alpha), R, K,
@@ -219,6 +225,32 @@ def actor_forward(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
     return L
 
 
+class ActorInferActs:
+    """Buffers of the inference (no-backward) actor forward over R rows."""
+
+    def __init__(self, R, dev):
+        self.R = R
+        self.cat = torch.empty(R, 192, dtype=torch.float32, device=dev)
+        self.ha = torch.empty(R, 256, dtype=torch.float32, device=dev)
+        self.wqk = torch.empty(64, 64, dtype=torch.float32, device=dev)
+
+
+def actor_forward_infer(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
+    """Inference launch list of ActorNetwork_ATT_TwoPortion.forward: the own / radar encoders and
+    Wqk = Wk^T Wq in one grouped launch, the fused attention block (aac_attn_block), merge, out."""
+    c = acts
+    L = gemm_launches([
+        prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
+        prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
+        prob(ap.Wkv, ap.Wq, ptr(c.wqk), 64, 64, 64, 64, 64, 64, ta=1)])           # Wk^T Wq
+    L.append(lambda: attn_block(ptr(c.cat), 192, nei, ap.Wn, ap.bn, ptr(c.wqk), ap.Wkv + 4 * 64 * 64,
+                                ptr(c.cat, 128), 192, R, K))
+    L += gemm_launches([prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm,
+                             act=RELU)])
+    L += gemm_launches([prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)])
+    return L
+
+
 def critic_forward(cp, X, rows, N, Din, f, h):
     """Encoders + combine of CriticCombine (ATT/nets:672-724, R3) over ``rows`` samples whose
     inputs are the rows X[b][n][:Din] = [own_n | a_n]."""
@@ -227,6 +259,32 @@ def critic_forward(cp, X, rows, N, Din, f, h):
     L += gemm_launches([prob(ptr(f), cp.Wc, ptr(h), rows, 256, 128 * N, 128 * N, 128 * N, 256, tb=1, bias=cp.bc,
                              act=RELU)])
     return L
+
+
+class ActorInfer:
+    """Batched choose_action forward (ATT/maddpg:455-550) of one actor over E*N rows, as a cached
+    launch list per input buffer set."""
+
+    def __init__(self, actor, N, D0, dev):
+        self.ap = ActorParams(actor)
+        self.N, self.D0, self.K, self.dev = N, D0, N - 1, dev
+        self.plans = {}
+
+    def __call__(self, own, radar, nei):
+        R = own.numel() // self.D0
+        key = (own.data_ptr(), radar.data_ptr(), nei.data_ptr(), R)
+        if key not in self.plans:
+            for t in (own, radar, nei):
+                assert t.is_contiguous() and t.device == self.dev and t.dtype == torch.float32
+            acts = ActorInferActs(R, self.dev)
+            out = torch.empty(R, 2, dtype=torch.float32, device=self.dev)
+            L = actor_forward_infer(self.ap, acts, ptr(own), self.D0, ptr(radar), ptr(nei), R, self.K, self.D0,
+                                    ptr(out), 2)
+            self.plans[key] = (L, acts, out, (own, radar, nei))
+        L, _, out, _ = self.plans[key]
+        for op in L:
+            op()
+        return out
 
 
 class FusedUpdate:
@@ -255,7 +313,7 @@ class FusedUpdate:
         self.y = z(Bt)
         self.q_c, self.q_a = z(Bt), z(Bt)            # per-iteration Q (stats)
         # activations / gradients
-        self.acts_t = ActorActs(Bt * N, K, dev)      # target actor over all batches
+        self.acts_t = ActorInferActs(Bt * N, dev)    # target actor over all batches
         self.acts = ActorActs(B * N, K, dev)
         self.f_t, self.h_t = z(Bt, 128 * N), z(Bt, 256)
         self.f, self.h = z(B, 128 * N), z(B, 256)
@@ -284,8 +342,8 @@ class FusedUpdate:
         strides = [Din, w[1], w[2], Din, w[4], w[5], Din, w[7], w[8]]
         self.pre.append(lambda: gather_strided(rep.ring, self.idx, dsts, w, chunks, strides))
         Bt = nb * B
-        self.pre += actor_forward(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar), ptr(self.nnei), Bt * N, K,
-                                  D0, ptr(self.Xt, D0), Din)
+        self.pre += actor_forward_infer(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar), ptr(self.nnei),
+                                        Bt * N, K, D0, ptr(self.Xt, D0), Din)
         self.pre += critic_forward(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
         self.pre.append(lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),
                                             done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y)))

@@ -105,6 +105,7 @@ class MADDPG:
         self.steps_done = 0
         self._last_src = None
         self._fplans = {}
+        self._infer = None
 
     # ------------------------------------------------------------------ batched API
     def attach_replay(self, capacity, seed=0):
@@ -114,7 +115,12 @@ class MADDPG:
     @torch.no_grad()
     def act(self, own, radar, nei, episode=None, noisy=True, eps_end=8000, noise_start=1.0, noise_out=None):
         """Batched choose_action (ATT/maddpg:455-550): tanh actor + N(0, var^2) noise, clamp."""
-        a = self.actors([own, radar, nei]).contiguous()
+        if self.fused:
+            if self._infer is None:
+                self._infer = fused.ActorInfer(self.actors, self.n_agents, self.D0, self.device)
+            a = self._infer(own, radar, nei).view(*own.shape[:-1], 2)
+        else:
+            a = self.actors([own, radar, nei]).contiguous()
         if noisy:
             ops.noise_clamp(a, episode, eps_end, noise_start, self.noise_seed, self.noise_counter, noise_out)
         return a

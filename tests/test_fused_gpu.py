@@ -192,3 +192,48 @@ def test_fused_equals_autograd_learner(native_lib):
     # fp32 summation-order differences between the two learners can show at ~1e-5 there
     for a, b in ((ms[0].fa.data, ms[1].fa.data), (ms[0].fc.data, ms[1].fc.data), (ms[0].fa_t.data, ms[1].fa_t.data)):
         np.testing.assert_allclose(a.cpu(), b.cpu(), atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("K", [1, 4, 7, 15])
+def test_attn_block_matches_reference_attention(native_lib, K):
+    """Fused inference attention (x_j on the fly, Wqk = Wk^T Wq, v_att = Wv sum a_j x_j) against
+    the reference's k / v projections and masked softmax (ATT/nets:186-210), fp64."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(K)
+    R = 777
+    eo = torch.relu(torch.randn(R, 64, device=DEV))
+    nei = torch.randn(R, K, 6, device=DEV)
+    nei[::5, 0] = 0.0                          # masked neighbours
+    nei[3] = 0.0                               # an all-masked row
+    Wn, bn = torch.randn(64, 6, device=DEV) * 0.4, torch.randn(64, device=DEV) * 0.1
+    Wq, Wk, Wv = (torch.randn(64, 64, device=DEV) * 0.125 for _ in range(3))
+    kv = torch.cat([Wk, Wv], 0).contiguous()
+    wqk = (Wk.t() @ Wq).contiguous()
+    out = torch.full((R, 64), 9.0, device=DEV)
+    P = fused.ptr
+    fused.attn_block(P(eo), 64, P(nei), P(Wn), P(bn), P(wqk), P(kv, 64 * 64), P(out), 64, R, K)
+    d = lambda t: t.double().cpu()   # noqa: E731
+    x = torch.relu(d(nei) @ d(Wn).t() + d(bn))
+    q = d(eo) @ d(Wq).t()
+    k, v = x @ d(Wk).t(), x @ d(Wv).t()
+    score = torch.einsum("rkc,rc->rk", k, q) / 8.0
+    mask = d(nei).mean(-1) != 0
+    score[~mask] = float("-inf")
+    a = torch.softmax(score, dim=1)
+    a[~mask] = 0.0
+    a = torch.nan_to_num(a)
+    want = torch.einsum("rk,rkc->rc", a, v)
+    np.testing.assert_allclose(out.cpu().double(), want, atol=2e-5, rtol=1e-5)
+
+
+def test_fused_act_matches_actor_module(native_lib):
+    from multi_agent_aac_amd.maddpg import MADDPG
+    m = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=5, device=DEV, seed=3)
+    torch.manual_seed(5)
+    E = 300
+    own, radar = torch.randn(E, 5, 22, device=DEV), torch.rand(E, 5, 18, device=DEV) * 15
+    nei = torch.randn(E, 5, 4, 6, device=DEV)
+    nei[::7, :, 1] = 0.0
+    got = m.act(own, radar, nei, noisy=False).clone()
+    want = m.actors([own, radar, nei])
+    np.testing.assert_allclose(got.cpu(), want.detach().cpu(), atol=1e-5, rtol=1e-5)
