@@ -86,11 +86,12 @@ int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *
 
 /* Replay gather with interleaved destinations: element c of field f of sampled row b goes to
  * dsts[f][b*(widths[f]/chunks[f])*dstrides[f] + (c/chunks[f])*dstrides[f] + c%chunks[f]]
- * (chunks = widths, dstrides = widths gives aac_replay_gather).  Lets [own_n | a_n] land as the
- * critic's (D0 + 2)-wide encoder input rows without a concat. */
+ * (chunks = widths, dstrides = widths gives aac_replay_gather), and to the same place in
+ * dsts2[f] when dsts2 and dsts2[f] are not NULL.  Lets [own_n | a_n] land as the critic's
+ * (D0 + 2)-wide encoder input rows without a concat. */
 int aac_replay_gather_strided(const float *ring, int32_t row_width, const int32_t *idx, int32_t B, int32_t n_fields,
-                              float *const *dsts, const int32_t *widths, const int32_t *chunks,
-                              const int32_t *dstrides, void *stream);
+                              float *const *dsts, float *const *dsts2, const int32_t *widths,
+                              const int32_t *chunks, const int32_t *dstrides, void *stream);
 
 #ifdef __cplusplus
 }

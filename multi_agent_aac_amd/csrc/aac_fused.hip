@@ -52,6 +52,7 @@ struct GProb {
     int ta, tb, act, mact, ones, ks;
     int amode, bmode;          // fragment load modes LV / LS / LT
     int deep;                  // 4-deep prefetch ring (long chains) or none
+    int wide;                  // one tile per wave, four adjacent tiles per workgroup
     int tiles_n, w_begin;      // first workgroup of this product
 };
 
@@ -135,8 +136,8 @@ __device__ __forceinline__ void load_frag(i4 X, int ld, int rows, int K, int kc,
 // The virtual ones row of op(B) (bias gradient) is a constant fragment: extra MFMAs in the one
 // tile column that holds it.
 template <int AM, int BM, int D>
-__device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0, int c1, int lr, int lk,
-                                         f4 acc[2][2]) {
+__device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0, int c1, int cstep, int lr,
+                                         int lk, f4 acc[2][2]) {
     const int nreal = P.N - P.ones;
     const i4 ra = rsrc_of(P.A), rb = rsrc_of(P.B);
     const bool has_one = P.ones && nreal >= n0 && nreal < n0 + WT;      // wave-uniform
@@ -144,11 +145,11 @@ __device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0,
 #pragma unroll
     for (int j = 0; j < 2; ++j) one[j] = (n0 + 16 * j + lr == nreal) ? 1.0f : 0.0f;
     float fa[D][2][4], fb[D][2][4];
-    const int nmine = c0 < c1 ? (c1 - c0 + 3) / 4 : 0;
+    const int nmine = c0 < c1 ? (c1 - c0 + cstep - 1) / cstep : 0;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const bool on = d < nmine;
-        const int kc = (c0 + 4 * d) * KC;
+        const int kc = (c0 + cstep * d) * KC;
         load_frag<AM>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
         load_frag<BM>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
     }
@@ -173,7 +174,7 @@ __device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0,
             }
             const int qn = q0 + d + D;
             const bool on = qn < nmine;
-            const int kc = (c0 + 4 * qn) * KC;
+            const int kc = (c0 + cstep * qn) * KC;
             load_frag<AM>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
             load_frag<BM>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
         }
@@ -189,18 +190,32 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     const GProb &P = g.p[pi];
     const int local = wg - P.w_begin;
     const int s = local % P.ks;
-    const int tile = local / P.ks;
-    const int m0 = (tile / P.tiles_n) * WT;
-    const int n0 = (tile % P.tiles_n) * WT;
     const int w = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int lr = lane & 15, lk = lane >> 4;
-
-    // split s of K, and inside it the four waves take every fourth chunk
     const int nch = (P.K + KC - 1) / KC;
     const int per = (nch + P.ks - 1) / P.ks;
-    const int c0 = s * per + w;
-    const int c1 = min(nch, s * per + per);
+    int m0, n0, c0, c1, cstep;
+    if (P.wide) {
+        // wide: the four waves take four adjacent 32x32 tiles of one 32-row block (A rows shared
+        // through L1), each over the whole K range of the split
+        const int grp = local / P.ks;
+        const int gpr = (P.tiles_n + 3) / 4;
+        const int tn = (grp % gpr) * 4 + w;
+        if (tn >= P.tiles_n) return;
+        m0 = (grp / gpr) * WT;
+        n0 = tn * WT;
+        c0 = s * per;
+        cstep = 1;
+    } else {
+        // the four waves share one tile and take every fourth chunk of the split
+        const int tile = local / P.ks;
+        m0 = (tile / P.tiles_n) * WT;
+        n0 = (tile % P.tiles_n) * WT;
+        c0 = s * per + w;
+        cstep = 4;
+    }
+    c1 = min(nch, s * per + per);
 
     f4 acc[2][2];
 #pragma unroll
@@ -209,13 +224,25 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
         for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
     // the deep-ring instantiations need ~120 VGPRs; launches without a long-K product use the
     // shallow kernel so the large memory-bound products keep their occupancy
-#define TM(a, b)                                                                                   \
-    case (a * 3 + b) * 2 + 0: tile_mma<a, b, 1>(P, m0, n0, c0, c1, lr, lk, acc); break;          \
-    case (a * 3 + b) * 2 + 1: tile_mma<a, b, DEEP ? 4 : 1>(P, m0, n0, c0, c1, lr, lk, acc); break;
+#define TM(a, b)                                                                                            \
+    case (a * 3 + b) * 2 + 0: tile_mma<a, b, 1>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;             \
+    case (a * 3 + b) * 2 + 1: tile_mma<a, b, DEEP ? 4 : 1>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;
     switch ((P.amode * 3 + P.bmode) * 2 + P.deep) {
         TM(LV, LV) TM(LV, LS) TM(LV, LT) TM(LS, LV) TM(LS, LS) TM(LS, LT) TM(LT, LV) TM(LT, LS) TM(LT, LT)
     }
 #undef TM
+    float *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
+    float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
+    if (P.wide) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    epilogue(P, C, cx, m0 + i * 16 + lk * 4 + r, n0 + j * 16 + lr, acc[i][j][r]);
+        return;
+    }
     // reduce the four waves' partial tiles in wave order; wave q finishes quadrant q = (i, j)
     red[w][0][lane] = acc[0][0];
     red[w][1][lane] = acc[0][1];
@@ -224,8 +251,6 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     __syncthreads();
     const f4 v = ((red[0][w][lane] + red[1][w][lane]) + red[2][w][lane]) + red[3][w][lane];
     const int i = w >> 1, j = w & 1;
-    float *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
-    float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
 #pragma unroll
     for (int r = 0; r < 4; ++r) epilogue(P, C, cx, m0 + i * 16 + lk * 4 + r, n0 + j * 16 + lr, v[r]);
 }
@@ -399,6 +424,7 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
 // ------------------------------------------------------------------------------ gather
 struct SFields {
     float *dst[16];
+    float *dst2[16];
     int width[16], chunk[16], dstride[16];
     int offset[17];
     int n;
@@ -414,7 +440,10 @@ __global__ void __launch_bounds__(256) gather_strided_kernel(const float *ring, 
         const int cc = c - F.offset[f];
         const int ch = F.chunk[f], ds = F.dstride[f];
         const int64_t row0 = (int64_t)b * (F.width[f] / ch) * ds;
-        F.dst[f][row0 + (int64_t)(cc / ch) * ds + cc % ch] = src[c];
+        const int64_t o = row0 + (int64_t)(cc / ch) * ds + cc % ch;
+        const float v = src[c];
+        F.dst[f][o] = v;
+        if (F.dst2[f]) F.dst2[f][o] = v;
     }
 }
 
@@ -447,15 +476,18 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         // op(A) rows (m) are K-contiguous unless ta; op(B) rows (n) are K-contiguous iff tb
         d.amode = s.ta ? LT : (s.lda % 4 == 0 && s.K % 4 == 0 && aligned16(s.A) ? LV : LS);
         d.bmode = !s.tb ? LT : (!s.ones && s.ldb % 4 == 0 && s.K % 4 == 0 && aligned16(s.B) ? LV : LS);
+        const int tm = (s.M + WT - 1) / WT, tn = (s.N + WT - 1) / WT;
+        d.tiles_n = tn;
+        // large products (>= 2048 tiles) need no K cut inside a workgroup: one tile per wave
+        d.wide = ks == 1 && tm * tn >= 2048;
         {
             const int nch = (s.K + KC - 1) / KC;
             const int per = (nch + ks - 1) / ks;
-            d.deep = (per + 3) / 4 > 2;       // > 2 chunks per wave: prefetch ring
+            const int chain = d.wide ? per : (per + 3) / 4;      // chunks per wave
+            d.deep = chain > 2;
         }
-        const int tm = (s.M + WT - 1) / WT, tn = (s.N + WT - 1) / WT;
-        d.tiles_n = tn;
-        d.w_begin = waves;          // in workgroups (one per tile and split)
-        waves += tm * tn * ks;
+        d.w_begin = waves;          // in workgroups
+        waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
     }
     g.waves = waves;
     return 0;
@@ -530,8 +562,8 @@ int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *
 }
 
 int aac_replay_gather_strided(const float *ring, int32_t rw, const int32_t *idx, int32_t B, int32_t n,
-                              float *const *dsts, const int32_t *widths, const int32_t *chunks,
-                              const int32_t *dstrides, void *stream) {
+                              float *const *dsts, float *const *dsts2, const int32_t *widths,
+                              const int32_t *chunks, const int32_t *dstrides, void *stream) {
     if (n < 1 || n > 16) return ffail("gather_strided: 1 <= n_fields <= 16");
     SFields F{};
     F.n = n;
@@ -540,6 +572,7 @@ int aac_replay_gather_strided(const float *ring, int32_t rw, const int32_t *idx,
         if (widths[f] <= 0 || chunks[f] <= 0 || widths[f] % chunks[f] || dstrides[f] < chunks[f])
             return ffail("gather_strided: bad width/chunk/dstride for field " + std::to_string(f));
         F.dst[f] = dsts[f];
+        F.dst2[f] = dsts2 ? dsts2[f] : nullptr;
         F.width[f] = widths[f];
         F.chunk[f] = chunks[f];
         F.dstride[f] = dstrides[f];

@@ -58,7 +58,7 @@ def lib():
         L.aac_adam_flat_sum.argtypes = [vp, vp, i32, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         L.aac_sum_partials.argtypes = [vp, vp, i32, i64, vp]
         L.aac_critic_head.argtypes = [vp, i32, i32, vp, vp, i32, vp, vp, vp, i32, i32, f32, vp, vp, vp, vp, vp]
-        L.aac_replay_gather_strided.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]
+        L.aac_replay_gather_strided.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp]
         L.aac_attn_block.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
         L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         _L = L
@@ -111,14 +111,15 @@ def critic_head(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0
                                _stream()), "aac_critic_head")
 
 
-def gather_strided(ring, idx, dsts, widths, chunks, dstrides):
+def gather_strided(ring, idx, dsts, widths, chunks, dstrides, dsts2=None):
     n = len(dsts)
     arr = (vp * n)(*dsts)
+    arr2 = (vp * n)(*dsts2) if dsts2 is not None else None
     w = (i32 * n)(*widths)
     c = (i32 * n)(*chunks)
     d = (i32 * n)(*dstrides)
     _chk(lib().aac_replay_gather_strided(vp(ring.data_ptr()), ring.shape[1], vp(idx.data_ptr()), idx.numel(), n,
-                                         arr, w, c, d, _stream()), "aac_replay_gather_strided")
+                                         arr, arr2, w, c, d, _stream()), "aac_replay_gather_strided")
 
 
 def adam_sum(opt, gpart, nsplit, step_add, grad_out=None):
@@ -206,23 +207,27 @@ class ActorActs:
         self.ha = z(R, 256)
 
 
-def actor_forward(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
-    """Launch list of ActorNetwork_ATT_TwoPortion.forward (ATT/nets:194-213) over R rows; the
-    tanh actions land at ``out`` with row stride ``ld_out`` (e.g. the critic-input rows)."""
+def actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
+    """ActorNetwork_ATT_TwoPortion.forward (ATT/nets:194-213) over R rows as dependent stages
+    [encoders, q|kv, attention (callable), merge, out]; GEMM stages are product lists so they
+    can share launches with independent work.  The tanh actions land at ``out`` (row stride
+    ``ld_out``, e.g. the critic-input rows)."""
     c = acts
-    L = []
-    L += gemm_launches([
-        prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
-        prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
-        prob(nei, ap.Wn, ptr(c.xn), R * K, 64, 6, 6, 6, 64, tb=1, bias=ap.bn, act=RELU)])
-    L += gemm_launches([
-        prob(ptr(c.cat), ap.Wq, ptr(c.qa), R, 64, 64, 192, 64, 64, tb=1),
-        prob(ptr(c.xn), ap.Wkv, ptr(c.kv), R * K, 128, 64, 64, 64, 128, tb=1)])
-    L.append(lambda: _attn_fwd(ptr(c.qa), ptr(c.kv), nei, ptr(c.cat, 128), 192, ptr(c.alpha), R, K))
-    L += gemm_launches([prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm,
-                             act=RELU)])
-    L += gemm_launches([prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)])
-    return L
+    enc = [prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
+           prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
+           prob(nei, ap.Wn, ptr(c.xn), R * K, 64, 6, 6, 6, 64, tb=1, bias=ap.bn, act=RELU)]
+    qkv = [prob(ptr(c.cat), ap.Wq, ptr(c.qa), R, 64, 64, 192, 64, 64, tb=1),
+           prob(ptr(c.xn), ap.Wkv, ptr(c.kv), R * K, 128, 64, 64, 64, 128, tb=1)]
+    attn = lambda: _attn_fwd(ptr(c.qa), ptr(c.kv), nei, ptr(c.cat, 128), 192, ptr(c.alpha), R, K)  # noqa: E731
+    merge = [prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm, act=RELU)]
+    outp = [prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)]
+    return enc, qkv, attn, merge, outp
+
+
+def actor_forward(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
+    """Launch list of the training actor forward (activations kept for the backward)."""
+    enc, qkv, attn, merge, outp = actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
+    return gemm_launches(enc) + gemm_launches(qkv) + [attn] + gemm_launches(merge) + gemm_launches(outp)
 
 
 class ActorInferActs:
@@ -251,14 +256,18 @@ def actor_forward_infer(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out
     return L
 
 
-def critic_forward(cp, X, rows, N, Din, f, h):
+def critic_forward_stages(cp, X, rows, N, Din, f, h):
     """Encoders + combine of CriticCombine (ATT/nets:672-724, R3) over ``rows`` samples whose
-    inputs are the rows X[b][n][:Din] = [own_n | a_n]."""
-    L = gemm_launches([prob(X + 4 * n * Din, cp.enc_w[n], ptr(f, n * 128), rows, 128, Din, N * Din, Din, 128 * N,
-                            tb=1, bias=cp.enc_b[n], act=RELU) for n in range(N)])
-    L += gemm_launches([prob(ptr(f), cp.Wc, ptr(h), rows, 256, 128 * N, 128 * N, 128 * N, 256, tb=1, bias=cp.bc,
-                             act=RELU)])
-    return L
+    inputs are the rows X[b][n][:Din] = [own_n | a_n], as two product lists."""
+    enc = [prob(X + 4 * n * Din, cp.enc_w[n], ptr(f, n * 128), rows, 128, Din, N * Din, Din, 128 * N, tb=1,
+                bias=cp.enc_b[n], act=RELU) for n in range(N)]
+    comb = [prob(ptr(f), cp.Wc, ptr(h), rows, 256, 128 * N, 128 * N, 128 * N, 256, tb=1, bias=cp.bc, act=RELU)]
+    return enc, comb
+
+
+def critic_forward(cp, X, rows, N, Din, f, h):
+    enc, comb = critic_forward_stages(cp, X, rows, N, Din, f, h)
+    return gemm_launches(enc) + gemm_launches(comb)
 
 
 class ActorInfer:
@@ -305,8 +314,9 @@ class FusedUpdate:
         Bt = nb * B
         # gathered batches (all N iterations), critic-input rows [own | a] and [own' | a']
         self.idx = torch.empty(Bt, dtype=torch.int32, device=dev)
-        self.X = z(Bt, N, self.Din)
-        self.Xt = z(Bt, N, self.Din)
+        self.X = z(Bt, N, self.Din)      # [own | replay action]   (critic step)
+        self.X2 = z(Bt, N, self.Din)     # [own | policy action]   (actor step)
+        self.Xt = z(Bt, N, self.Din)     # [own' | target action]  (TD target)
         self.radar, self.nei = z(Bt, N, 18), z(Bt, N, K, 6)
         self.nradar, self.nnei = z(Bt, N, 18), z(Bt, N, K, 6)
         self.rew, self.done = z(Bt, N), z(Bt, N)
@@ -340,7 +350,8 @@ class FusedUpdate:
                 ptr(self.Xt), ptr(self.nradar), ptr(self.nnei)]
         chunks = [D0, w[1], w[2], 2, w[4], w[5], D0, w[7], w[8]]
         strides = [Din, w[1], w[2], Din, w[4], w[5], Din, w[7], w[8]]
-        self.pre.append(lambda: gather_strided(rep.ring, self.idx, dsts, w, chunks, strides))
+        dsts2 = [ptr(self.X2)] + [None] * 8
+        self.pre.append(lambda: gather_strided(rep.ring, self.idx, dsts, w, chunks, strides, dsts2=dsts2))
         Bt = nb * B
         self.pre += actor_forward_infer(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar), ptr(self.nnei),
                                         Bt * N, K, D0, ptr(self.Xt, D0), Din)
@@ -369,28 +380,37 @@ class FusedUpdate:
         gA = ActorParams(m.actors, m.fa, self.ga.data_ptr())
         gC = CriticParams(m.critics, m.fc, self.gc.data_ptr())
         X = ptr(self.X, i * B * N * Din)
+        X2 = ptr(self.X2, i * B * N * Din)
         radar = ptr(self.radar, i * B * N * 18)
         nei = ptr(self.nei, i * B * N * K * 6)
         y = ptr(self.y, i * B)
         f, h, dq, dh, df = self.f, self.h, self.dq, self.dh, self.df
+        c = self.acts
         L = []
+        # The actor forward of this iteration (ATT/maddpg:389-392) depends only on the actor
+        # weights, which change after the critic step, so its products share the critic step's
+        # launches; the policy actions land in X2 (own columns gathered there too).
+        a_enc, a_qkv, a_attn, a_merge, a_out = actor_forward_stages(A, c, X2, Din, radar, nei, R, K, D0, X2 + 4 * D0,
+                                                                    Din)
+        c_enc, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
         # ---------------- critic step (ATT/maddpg:375-387)
-        L += critic_forward(C, X, B, N, Din, f, h)
+        L += gemm_launches(c_enc + a_enc)
+        L += gemm_launches(c_comb + a_qkv)
         L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh)))
+        L.append(a_attn)
         L += gemm_launches([
             prob(ptr(dq), ptr(h), gC.Wq, 1, 256, B, 1, 256, 256, ta=1, ones=1, cextra=gC.bq, ksplit=SC,
                  split_stride=nC),
             prob(ptr(dh), ptr(f), gC.Wc, 256, 128 * N, B, 256, 128 * N, 128 * N, ta=1, ones=1, cextra=gC.bc,
                  ksplit=SC, split_stride=nC),
             prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f), ldmask=128 * N,
-                 mact=RELU)])
+                 mact=RELU)] + a_merge)
         L += gemm_launches([prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din,
                                  Din, ta=1, ones=1, cextra=gC.enc_b[n], ksplit=SC, split_stride=nC)
-                            for n in range(N)])
+                            for n in range(N)] + a_out)
         L += self._adam(m.critic_optimizer, m.fc, self.gc, SC, i + 1)
-        # ---------------- actor step (ATT/maddpg:389-425); a_pi overwrites the replay actions in X
-        c = self.acts
-        L += actor_forward(A, c, X, Din, radar, nei, R, K, D0, X + 4 * D0, Din)
+        # ---------------- actor step (ATT/maddpg:389-425): critic on the policy actions
+        X = X2
         L += critic_forward(C, X, B, N, Din, f, h)
         L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 1, q=ptr(self.q_a, i * B), dh=ptr(dh)))
         L += gemm_launches([prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f),

@@ -151,11 +151,14 @@ def test_gather_strided(native_lib):
     ring = torch.arange(200 * rw, dtype=torch.float32, device=DEV).reshape(200, rw)
     idx = torch.randperm(200, device=DEV)[:B].to(torch.int32)
     X = torch.full((B, 3, 6), -1.0, device=DEV)
+    X2 = torch.full((B, 3, 6), -2.0, device=DEV)
     rest = torch.empty(B, 50 - 18, device=DEV)
     fused.gather_strided(ring, idx, [fused.ptr(X), fused.ptr(X, 4), fused.ptr(rest)], [12, 6, 32], [4, 2, 32],
-                         [6, 6, 32])
+                         [6, 6, 32], dsts2=[fused.ptr(X2), None, None])
     src = ring[idx.long()].cpu()
     Xc = X.cpu()
+    assert torch.equal(X2.cpu()[:, :, :4], src[:, :12].reshape(B, 3, 4))
+    assert (X2.cpu()[:, :, 4:] == -2.0).all()
     assert torch.equal(Xc[:, :, :4], src[:, :12].reshape(B, 3, 4))
     assert torch.equal(Xc[:, :, 4:], src[:, 12:18].reshape(B, 3, 2))
     assert torch.equal(rest.cpu(), src[:, 18:])
