@@ -42,6 +42,26 @@ def update_flops(N, D0, B):
     return 2.0 * (4 * A + 7 * C) * B * N
 
 
+def gemm_roofline(model, B, updates=4):
+    """Roofline of the dominant kernel, the grouped fp32 MFMA GEMM (gemm_kernel) of the fused
+    learner: algorithmic FLOPs of each launch / its HIP-event duration, over ``updates`` eager
+    update_myown-equivalents run right after the timed region (same launches as the captured
+    graph; the rocprof kernel stats under profiles/ give the same per-launch durations)."""
+    fu = model._fused_plan(B)
+    rec = []
+    for _ in range(updates):
+        rec += fu.run_timed()
+    torch.cuda.synchronize()
+    flops = sum(r[0] for r in rec)
+    ms = sum(r[1].elapsed_time(r[2]) for r in rec)
+    n = len(rec)
+    achieved = flops / (ms * 1e-3) / 1e12
+    return {"kernel": "gemm_kernel (grouped fp32 MFMA GEMM of the fused learner)", "bound": "mfma",
+            "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+            "flop_per_launch": flops / n, "avg_launch_ms": ms / n, "launches_per_update": n // updates,
+            "gemm_ms_per_update": ms / updates}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -58,6 +78,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "env_step_pmc.json"))
+    p.add_argument("--gemm-traffic", default=os.path.join(ROOT, "profiles", "gemm_pmc.json"))
     return p.parse_args()
 
 
@@ -265,14 +286,26 @@ def main():
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
                    "update_graph": (not a.no_graph) and ws == 1},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * N,
-        "roofline": {"kernel": "step_kernel (fused env step)", "bound": "hbm", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": tsrc, "bytes_per_agent_step": bpa, "agents_per_launch": a.envs * N,
-                     "avg_launch_ms": env_ms},
+        "env_roofline": {"kernel": "step_kernel (fused env step)", "bound": "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": tsrc, "bytes_per_agent_step": bpa, "agents_per_launch": a.envs * N,
+                         "avg_launch_ms": env_ms},
         "update_roofline": {"bound": "mfma", "unit": "TFLOP/s", "flop_per_update": upd_fl,
                             "achieved": upd_fl * upd_per_s / 1e12, "peak": FP32_PEAK_TFLOPS,
                             "frac": upd_fl * upd_per_s / 1e12 / FP32_PEAK_TFLOPS, "note": "whole-step rate bound"},
     }
+    if tr.model.fused:
+        rf = gemm_roofline(tr.model, a.batch)
+        rf["traffic"] = None
+        if a.gemm_traffic and os.path.exists(a.gemm_traffic):
+            with open(a.gemm_traffic) as f:
+                t = json.load(f)
+            if t.get("envs") == a.envs and t.get("agents") == N and t.get("batch") == a.batch:
+                rf["traffic"] = t.get("hbm_bytes_per_launch")
+                rf["traffic_source"] = os.path.relpath(a.gemm_traffic, ROOT)
+        out["roofline"] = rf
+    else:
+        out["roofline"] = out["env_roofline"]
     if rank == 0 and ws == 1 and a.env_micro:
         out["env_microbench"] = env_microbench(a.env_micro, N, a.radar)
     if rank == 0 and cpu is not None:

@@ -93,6 +93,8 @@ class GemmLaunch:
         assert 1 <= len(probs) <= GEMM_MAX
         self.n = len(probs)
         self.arr = (GemmProb * self.n)(*probs)
+        # algorithmic FLOPs (2 M N K per product; the virtual ones column is the bias gradient)
+        self.flops = sum(2.0 * p.M * p.N * p.K for p in probs)
 
     def __call__(self):
         _chk(lib().aac_gemm_batch(self.arr, self.n, _stream()), "aac_gemm_batch")
@@ -451,6 +453,9 @@ class FusedUpdate:
         return L
 
     # ------------------------------------------------------------------ run
+    def ops(self):
+        return self.pre + [op for it in self.iters for op in it] + self.post
+
     def run(self, idx=None):
         if idx is None:
             self.pre[0]()
@@ -463,6 +468,21 @@ class FusedUpdate:
                 op()
         for op in self.post:
             op()
+
+    def run_timed(self):
+        """One eager update with a HIP event pair around every GEMM launch (on the launching
+        stream); returns [(algorithmic FLOPs, event pair)] for the grouped-GEMM roofline."""
+        rec = []
+        for op in self.ops():
+            if isinstance(op, GemmLaunch):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                op()
+                e1.record()
+                rec.append((op.flops, e0, e1))
+            else:
+                op()
+        return rec
 
     def stats(self):
         """[(loss_q, loss_a, q, target)] per iteration, like MADDPG._iteration."""
