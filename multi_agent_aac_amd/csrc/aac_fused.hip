@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/aac_fused.h"
@@ -181,7 +182,7 @@ __device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0,
     }
 }
 
-template <bool DEEP>
+template <int DEPTH>
 __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     __shared__ f4 red[4][4][64];       // [wave][quadrant][lane]
     const int wg = blockIdx.x;
@@ -226,7 +227,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     // shallow kernel so the large memory-bound products keep their occupancy
 #define TM(a, b)                                                                                            \
     case (a * 3 + b) * 2 + 0: tile_mma<a, b, 1>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;             \
-    case (a * 3 + b) * 2 + 1: tile_mma<a, b, DEEP ? 4 : 1>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;
+    case (a * 3 + b) * 2 + 1: tile_mma<a, b, DEPTH>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;
     switch ((P.amode * 3 + P.bmode) * 2 + P.deep) {
         TM(LV, LV) TM(LV, LS) TM(LV, LT) TM(LS, LV) TM(LS, LS) TM(LS, LT) TM(LT, LV) TM(LT, LS) TM(LT, LT)
     }
@@ -449,6 +450,16 @@ __global__ void __launch_bounds__(256) gather_strided_kernel(const float *ring, 
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// tuning knobs (environment, read once): prefetch-ring depth 1..4 for long K chains, and the
+// tile count from which a product runs one tile per wave
+int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+const int g_depth = env_int("AAC_GEMM_DEPTH", 2);
+const int g_deep_tiles = env_int("AAC_GEMM_DEEP_TILES", 1024);
+const int g_wide_tiles = env_int("AAC_GEMM_WIDE_TILES", 2048);
+
 int plan(const aac_gemm_prob *in, int n, GBatch &g) {
     if (n < 1 || n > AAC_GEMM_MAX) return ffail("gemm_batch: 1 <= n <= AAC_GEMM_MAX");
     g.n = n;
@@ -479,12 +490,14 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         const int tm = (s.M + WT - 1) / WT, tn = (s.N + WT - 1) / WT;
         d.tiles_n = tn;
         // large products (>= 2048 tiles) need no K cut inside a workgroup: one tile per wave
-        d.wide = ks == 1 && tm * tn >= 2048;
+        d.wide = ks == 1 && tm * tn >= g_wide_tiles;
         {
             const int nch = (s.K + KC - 1) / KC;
             const int per = (nch + ks - 1) / ks;
             const int chain = d.wide ? per : (per + 3) / 4;      // chunks per wave
-            d.deep = chain > 2;
+            // measured (tools/mb_gemm.py): the prefetch ring only pays on large products; elsewhere
+            // the occupancy of the ring-free kernel hides more latency
+            d.deep = g_depth > 1 && chain > 2 && tm * tn >= g_deep_tiles;
         }
         d.w_begin = waves;          // in workgroups
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
@@ -504,8 +517,12 @@ int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
     if (plan(probs, n, g)) return -1;
     bool deep = false;
     for (int i = 0; i < g.n; ++i) deep |= g.p[i].deep != 0;
-    if (deep) hipLaunchKernelGGL(gemm_kernel<true>, dim3(g.waves), dim3(256), 0, (hipStream_t)stream, g);
-    else hipLaunchKernelGGL(gemm_kernel<false>, dim3(g.waves), dim3(256), 0, (hipStream_t)stream, g);
+    const dim3 grid(g.waves), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (!deep) hipLaunchKernelGGL(gemm_kernel<1>, grid, block, 0, st, g);
+    else if (g_depth == 2) hipLaunchKernelGGL(gemm_kernel<2>, grid, block, 0, st, g);
+    else if (g_depth == 3) hipLaunchKernelGGL(gemm_kernel<3>, grid, block, 0, st, g);
+    else hipLaunchKernelGGL(gemm_kernel<4>, grid, block, 0, st, g);
     FHIP(hipGetLastError());
     return 0;
 }
