@@ -12,7 +12,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libaac_env.so")
+# AAC_LIB: load another build of the same library (kernel experiments); default = the in-tree build
+LIB_PATH = os.environ.get("AAC_LIB") or os.path.join(_HERE, "libaac_env.so")
 
 EXPORTS = (
     "aac_env_create", "aac_env_destroy", "aac_last_error", "aac_env_reset", "aac_env_step",

@@ -34,6 +34,7 @@ struct Tab {
     double ray_c[NRAY], ray_s[NRAY]; // cos/sin(math.radians(20 r))
     double apothem;                  // cos(pi/64)
     double quantum;                  // GEOS filletAngleQuantum = pi/2/16
+    double cos_quantum;              // cos(quantum): bound on a fillet arc's reach along an axis
 };
 
 __constant__ Tab c_tab;
@@ -109,6 +110,24 @@ __device__ bool bound_crash(const Args &A, double x0, double y0, double x1, doub
     const double m = r + 1e-6;
     double lx = fmin(x0, x1), hx = fmax(x0, x1), ly = fmin(y0, y1), hy = fmax(y0, y1);
     if (lx - m > b[0] && hx + m < b[1] && ly - m > b[2] && hy + m < b[3]) return false;
+    // Certain bands: every capsule vertex is within r of an endpoint, and the arc around the
+    // extreme endpoint has a vertex within half a fillet step (<= quantum) of each axis
+    // direction, so min x lies in [lx - r, lx - r cos(quantum)] (likewise the other sides).  A
+    // line outside [min, max] of those bands is decided without building the capsule.
+    {
+        const double lo = r + 1e-9, hi = r * c_tab.cos_quantum - 1e-9;
+        const double mn_lo[2] = {lx - lo, ly - lo}, mn_hi[2] = {lx - hi, ly - hi};
+        const double mx_lo[2] = {hx + hi, hy + hi}, mx_hi[2] = {hx + lo, hy + lo};
+        bool certain = true;
+        for (int q = 0; q < 4; ++q) {
+            const int ax = q >> 1;
+            const double v = b[q];
+            if (v < mn_lo[ax] || v > mx_hi[ax]) continue;                  // certainly outside
+            if (v >= mn_hi[ax] && v <= mx_lo[ax]) return true;             // certainly inside
+            certain = false;
+        }
+        if (certain) return false;
+    }
     double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
     if (x0 == x1 && y0 == y1) {
         for (int i = 0; i < 64; ++i) upd(x0 + r * c_tab.circ_c[i], y0 + r * c_tab.circ_s[i], mnx, mxx, mny, mxy);
@@ -133,6 +152,10 @@ __device__ bool bound_crash(const Args &A, double x0, double y0, double x1, doub
 __device__ bool goal_reached(double px, double py, double gx, double gy, double pb) {
     double dx = gx - px, dy = gy - py;
     double thr = (pb + 1.0) * c_tab.apothem;
+    // max_k d.n_k lies in [|d| cos(pi/64), |d|]: outside the band the answer is certain
+    const double dist = sqrt(dx * dx + dy * dy);
+    if (dist > (pb + 1.0) * (1.0 + 1e-12) + 1e-12) return false;
+    if (dist < thr * (1.0 - 1e-12) - 1e-12) return true;
     double m = -INFINITY;
 #pragma unroll 8
     for (int k = 0; k < 64; ++k) {
@@ -146,6 +169,14 @@ __device__ bool goal_reached(double px, double py, double gx, double gy, double 
 __device__ bool building_hit(double px, double py, double cx, double cy, double pb) {
     double dx = cx - px, dy = cy - py;
     if (fabs(dx) > 5.0 + pb || fabs(dy) > 5.0 + pb) return false;
+    // the 64-gon lies between its inscribed (pb cos(pi/64)) and circumscribed (pb) circles:
+    // away from that band the distance to the square decides
+    {
+        const double ox = fmax(fabs(dx) - 5.0, 0.0), oy = fmax(fabs(dy) - 5.0, 0.0);
+        const double dist = sqrt(ox * ox + oy * oy);
+        if (dist > pb * (1.0 + 1e-12) + 1e-12) return false;
+        if (dist < pb * c_tab.apothem * (1.0 - 1e-12) - 1e-12) return true;
+    }
     for (int k = 0; k < 32; ++k) {
         double proj = fabs(dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k]);
         double lim = 5.0 * (fabs(c_tab.nrm_c[k]) + fabs(c_tab.nrm_s[k])) + pb * c_tab.apothem;
@@ -155,8 +186,8 @@ __device__ bool building_hit(double px, double py, double cx, double cy, double 
 }
 
 // Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p
-__device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
-                               double &tout) {
+__device__ bool ray_poly_entry_full(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                    double &tout) {
     double ddx = ex - cx, ddy = ey - cy;
     double tlo = 0.0, thi = 1.0;
     double vx = px + r * c_tab.circ_c[0], vy = py + r * c_tab.circ_s[0];
@@ -179,6 +210,51 @@ __device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, doubl
         vx = wx;
         vy = wy;
     }
+    tout = tlo;
+    return true;
+}
+
+// Same result from a window of edges.  When the line crosses the inscribed circle (not near
+// tangency) and c lies outside the circumscribed circle, the entry is the maximum of -a/b over
+// the entering edges and every entering edge other than the one(s) holding the entry point
+// gives a smaller value; that edge lies within half an edge of the ray's entry angle on the
+// circumscribed circle, so the maximum over the six edges around it is the same number (same
+// vertices, same arithmetic) as over all 64.  The exit lies beyond the entry, so the segment
+// meets the polygon iff that maximum is <= 1.  Anything else takes the full clip.
+__device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
+                               double &tout) {
+    const double ddx = ex - cx, ddy = ey - cy;
+    const double L2 = ddx * ddx + ddy * ddy;
+    const double wx = px - cx, wy = py - cy;
+    const double w2 = wx * wx + wy * wy;
+    const double L = sqrt(L2);
+    const double s0 = (wx * ddx + wy * ddy) / L;                   // along the ray
+    const double h = fabs(wx * ddy - wy * ddx) / L;               // distance of p to the line
+    const double ap = r * c_tab.apothem;
+    if (!(h < ap * (1.0 - 1e-9)) || !(w2 > r * r * (1.0 + 1e-9)) || !(s0 > 0.0))
+        return ray_poly_entry_full(cx, cy, ex, ey, px, py, r, tout);
+    const double tc = (s0 - sqrt(r * r - h * h)) / L;              // circumscribed-circle entry
+    const float phi = atan2f((float)(cy + tc * ddy - py), (float)(cx + tc * ddx - px));
+    // vertex angles are -i 2pi/64: nearest vertex index
+    int i0 = (int)lrintf(-phi * (64.0f / 6.28318530717958647f));
+    double tlo = 0.0;
+    bool any = false;
+#pragma unroll
+    for (int dk = -3; dk <= 2; ++dk) {
+        const int k = (i0 + dk) & 63, k1 = (k + 1) & 63;
+        const double vx = px + r * c_tab.circ_c[k], vy = py + r * c_tab.circ_s[k];
+        const double qx = px + r * c_tab.circ_c[k1], qy = py + r * c_tab.circ_s[k1];
+        const double exx = qx - vx, eyy = qy - vy;
+        const double a = exx * (cy - vy) - eyy * (cx - vx);
+        const double b = exx * ddy - eyy * ddx;
+        if (b < 0.0) {
+            const double t = -a / b;
+            tlo = t > tlo ? t : tlo;
+            any = true;
+        }
+    }
+    if (!any) return ray_poly_entry_full(cx, cy, ex, ey, px, py, r, tout);
+    if (tlo > 1.0) return false;
     tout = tlo;
     return true;
 }
@@ -467,8 +543,14 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
         S.goal[t] = A.goal[ai];
     }
     __syncthreads();
+#ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
     radar_phase(A, S, e0, nag, false);
+#endif
+#ifdef AAC_DBG_SKIP_AGENT
+    if (false) {
+#else
     if (active) {
+#endif
         const uint8_t *occ = S.occ + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
         observe_agent(A, S, e, i, base);
 
@@ -707,6 +789,7 @@ static void fill_tables(Tab &t) {
         t.ray_s[r] = std::sin(rad);
     }
     t.apothem = std::cos(PI_GEOS / 64.0);
+    t.cos_quantum = std::cos(quantum);
     t.quantum = quantum;
 }
 

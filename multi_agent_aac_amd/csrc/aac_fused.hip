@@ -336,8 +336,10 @@ __global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, 
 //   s_j   = (Wk x_j) . (Wq e_o) / 8 = x_j . (Wqk e_o) / 8,   Wqk = Wk^T Wq (precomputed)
 //   a     = softmax over the valid j (nei_j.mean() != 0), 0 for the masked ones
 //   v_att = sum_j a_j (Wv x_j) = Wv (sum_j a_j x_j)  (no [rows*K][128] k|v tensor)
-// Each wave keeps row ``lane`` of Wqk and of Wv in registers; the vector being multiplied is
-// broadcast from a 64-float LDS slot of the wave.
+// The workgroup stages Wqk and Wv in LDS once ([row][68]: lane c reads row c with 16-B loads,
+// conflict-free) and its four waves walk the rows; the vector being multiplied is broadcast
+// from a 64-float LDS slot of the wave.
+constexpr int WS = 68;
 template <int KM>
 __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict__ eo, int lde,
                                                          const float *__restrict__ nei,
@@ -346,32 +348,35 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
                                                          const float *__restrict__ Wqk,
                                                          const float *__restrict__ Wv, float *out, int ldo, int R,
                                                          int K) {
+    __shared__ f4 wq4[64 * WS / 4], wv4[64 * WS / 4];
     __shared__ f4 buf4[4][16];
+    float *wqs = reinterpret_cast<float *>(wq4), *wvs = reinterpret_cast<float *>(wv4);
+    for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+        const int row = e >> 4, c4 = (e & 15) * 4;
+        *reinterpret_cast<f4 *>(wqs + row * WS + c4) = *reinterpret_cast<const f4 *>(Wqk + row * 64 + c4);
+        *reinterpret_cast<f4 *>(wvs + row * WS + c4) = *reinterpret_cast<const f4 *>(Wv + row * 64 + c4);
+    }
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     float *buf = reinterpret_cast<float *>(buf4[wv]);
-    float wq[64], wvr[64], wn[6];
-#pragma unroll
-    for (int o = 0; o < 64; o += 4) {
-        const f4 a = *reinterpret_cast<const f4 *>(Wqk + lane * 64 + o);
-        const f4 b = *reinterpret_cast<const f4 *>(Wv + lane * 64 + o);
-        wq[o] = a.x; wq[o + 1] = a.y; wq[o + 2] = a.z; wq[o + 3] = a.w;
-        wvr[o] = b.x; wvr[o + 1] = b.y; wvr[o + 2] = b.z; wvr[o + 3] = b.w;
-    }
+    float wn[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) wn[i] = Wn[lane * 6 + i];
     const float bnl = bn[lane];
+    const f4 *wqr = reinterpret_cast<const f4 *>(wqs + lane * WS);
+    const f4 *wvr = reinterpret_cast<const f4 *>(wvs + lane * WS);
     const int nwaves = gridDim.x * 4;
     for (int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv); r < R; r += nwaves) {
         buf[lane] = eo[(size_t)r * lde + lane];
         float qk = 0.0f;
 #pragma unroll
-        for (int o = 0; o < 64; o += 4) {
-            const f4 e = buf4[wv][o >> 2];
-            qk = fmaf(wq[o], e.x, qk);
-            qk = fmaf(wq[o + 1], e.y, qk);
-            qk = fmaf(wq[o + 2], e.z, qk);
-            qk = fmaf(wq[o + 3], e.w, qk);
+        for (int o4 = 0; o4 < 16; ++o4) {
+            const f4 e = buf4[wv][o4], w = wqr[o4];
+            qk = fmaf(w.x, e.x, qk);
+            qk = fmaf(w.y, e.y, qk);
+            qk = fmaf(w.z, e.z, qk);
+            qk = fmaf(w.w, e.w, qk);
         }
         float x[KM], sc[KM];
         float mx = -INFINITY;
@@ -411,12 +416,12 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
         buf[lane] = xb;
         float v = 0.0f;
 #pragma unroll
-        for (int o = 0; o < 64; o += 4) {
-            const f4 e = buf4[wv][o >> 2];
-            v = fmaf(wvr[o], e.x, v);
-            v = fmaf(wvr[o + 1], e.y, v);
-            v = fmaf(wvr[o + 2], e.z, v);
-            v = fmaf(wvr[o + 3], e.w, v);
+        for (int o4 = 0; o4 < 16; ++o4) {
+            const f4 e = buf4[wv][o4], w = wvr[o4];
+            v = fmaf(w.x, e.x, v);
+            v = fmaf(w.y, e.y, v);
+            v = fmaf(w.z, e.z, v);
+            v = fmaf(w.w, e.w, v);
         }
         out[(size_t)r * ldo + lane] = v;
     }
@@ -566,9 +571,10 @@ int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *
                    const float *Wqk, const float *Wv, float *out, int32_t ldo, int32_t R, int32_t K, void *stream) {
     if (R <= 0) return 0;
     if (K < 1 || K > 32) return ffail("attn_block: 1 <= K <= 32");
-    int waves = (R + 3) / 4 < 1024 ? (R + 3) / 4 : 1024;
-    waves = waves < 1 ? 1 : waves;
-    const dim3 grid(waves), block(256);
+    // ~16 rows per wave: the 34 KB weight staging per workgroup stays small next to the rows
+    int wgs = (R + 63) / 64;
+    wgs = wgs < 1 ? 1 : (wgs > 2048 ? 2048 : wgs);
+    const dim3 grid(wgs), block(256);
     hipStream_t st = (hipStream_t)stream;
     if (K <= 4) hipLaunchKernelGGL(attn_block_kernel<4>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
     else if (K <= 8) hipLaunchKernelGGL(attn_block_kernel<8>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
