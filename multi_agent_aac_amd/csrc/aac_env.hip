@@ -314,10 +314,18 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, 
     j0 = j0 < 0 ? 0 : j0;
     i1 = i1 > A.gw - 1 ? A.gw - 1 : i1;
     j1 = j1 > A.gh - 1 ? A.gh - 1 : j1;
+    // a square can only meet the segment if its centre is within its circumradius 5 sqrt(2) of
+    // the segment's line and of its extent along the line (exact: the slab test decides the rest)
+    const double ddx = ex - cx, ddy = ey - cy;
+    const double L = sqrt(ddx * ddx + ddy * ddy);
+    const double reach = 5.0 * 1.4142135623730951 * (1.0 + 1e-9) * L;   // scaled by L: no division
     for (int i = i0; i <= i1; ++i)
         for (int j = j0; j <= j1; ++j) {
             if (!occ[i * A.gh + j]) continue;
             double qx = A.gx0 + 10.0 * i, qy = A.gy0 + 10.0 * j;
+            const double wx = qx - cx, wy = qy - cy;
+            const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
+            if (fabs(cr) > reach || al < -reach || al > L * L + reach) continue;
             if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
         }
     if (ray_vline(cx, cy, ex, ey, A.bound[0], d) && d < mind) mind = d;
