@@ -689,27 +689,43 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
     load_maps(A, S);
-    if (R.mode == 1 && active && i == 0) {
-        // draw N OD entries; starts pairwise > 2 pB apart (ATT/env:258-268)
-        int ep = R.episode[e] + 1;
-        R.episode[e] = ep;
-        for (int a = 0; a < N; ++a) {
-            int idx = 0;
-            for (int att = 0; att < 4096; ++att) {
-                uint64_t key = mix64(mix64(mix64(R.seed ^ (uint64_t)e) ^ (uint64_t)ep) ^ ((uint64_t)a * 65536ull + att));
-                idx = (int)(key % (uint64_t)R.bank_n);
-                double2 s = R.bank_start[idx];
-                bool ok = true;
-                for (int b = 0; b < a; ++b) {
-                    double2 o = R.bank_start[S.idx[base + b]];
-                    if (!(npnorm(s.x - o.x, s.y - o.y) > A.pb * 2)) {
-                        ok = false;
-                        break;
+    if (R.mode == 1) {
+        // draw N OD entries; starts pairwise > 2 pB apart (ATT/env:258-268).  One wave per
+        // resetting env: the 64 lanes test 64 consecutive attempts of agent a at once and the
+        // lowest valid attempt wins, i.e. exactly the sequential rule (first valid attempt, else
+        // the last of 4096).
+        const int lane = t & 63, wv = t >> 6;
+        for (int lq = wv; lq < A.epb; lq += BLOCK / 64) {
+            const int eq = e0 + lq;
+            if (eq >= A.E || !S.active[lq]) continue;
+            const int ep = R.episode[eq] + 1;
+            const int bq = lq * N;
+            for (int a = 0; a < N; ++a) {
+                int chosen = -1, last = 0;
+                for (int att0 = 0; att0 < 4096 && chosen < 0; att0 += 64) {
+                    const int att = att0 + lane;
+                    const uint64_t key =
+                        mix64(mix64(mix64(R.seed ^ (uint64_t)eq) ^ (uint64_t)ep) ^ ((uint64_t)a * 65536ull + att));
+                    const int idx = (int)(key % (uint64_t)R.bank_n);
+                    const double2 sp = R.bank_start[idx];
+                    bool ok = true;
+                    for (int b = 0; b < a; ++b) {
+                        const double2 o = S.ppos[bq + b];
+                        if (!(npnorm(sp.x - o.x, sp.y - o.y) > A.pb * 2)) ok = false;
                     }
+                    const unsigned long long m = __ballot(ok);
+                    if (m) chosen = __shfl(idx, __ffsll((long long)m) - 1, 64);
+                    last = __shfl(idx, 63, 64);
                 }
-                if (ok) break;
+                const int pick = chosen >= 0 ? chosen : last;
+                if (lane == 0) {
+                    S.idx[bq + a] = pick;
+                    S.ppos[bq + a] = R.bank_start[pick];      // scratch: chosen starts
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             }
-            S.idx[base + a] = idx;
+            if (lane == 0) R.episode[eq] = ep;
         }
     }
     __syncthreads();
