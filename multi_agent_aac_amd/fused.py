@@ -25,6 +25,7 @@ gathered in one launch each.  Weight gradients are written (never accumulated) s
 networks' flat gradient buffers, so there is no zero_grad.
 """
 import ctypes
+import os
 
 import torch
 
@@ -301,8 +302,10 @@ class ActorInfer:
 class FusedUpdate:
     """One update_myown-equivalent on a DeviceReplay as a fixed launch list (graph-capturable)."""
 
-    SPLIT_ACTOR = 32     # K splits of the actor weight gradients (K = B*N or B*N*K rows)
-    SPLIT_CRITIC = 8     # K splits of the critic weight gradients (K = B rows)
+    # K splits of the weight gradients (partial copies summed by the Adam kernel); actor K = B*N
+    # or B*N*K rows, critic K = B rows.  AAC_SPLIT_ACTOR / AAC_SPLIT_CRITIC override (tuning).
+    SPLIT_ACTOR = int(os.environ.get("AAC_SPLIT_ACTOR", "32"))
+    SPLIT_CRITIC = int(os.environ.get("AAC_SPLIT_CRITIC", "8"))
 
     def __init__(self, model, replay, B):
         self.m, self.rep, self.B = model, replay, B
