@@ -284,7 +284,8 @@ def main():
                                f"{a.radar} radar", "envs_per_gpu": a.envs, "envs_total": E_total, "agents": N,
                    "batch": a.batch, "replay": a.memory, "radar": a.radar,
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
-                   "update_graph": (not a.no_graph) and ws == 1},
+                   "update_graph": (not a.no_graph) and (ws == 1 or tr.model.fused),
+                   "graph_segments": "one per update" if ws == 1 else "cut at each gradient all-reduce"},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * N,
         "env_roofline": {"kernel": "step_kernel (fused env step)", "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

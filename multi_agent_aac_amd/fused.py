@@ -87,6 +87,16 @@ def prob(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=NONE, adden
                     ta, tb, act, mact, ones, ksplit)
 
 
+class Collective:
+    """A cross-rank exchange in a launch list (the gradient all-reduce): the graph is cut there."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self):
+        self.fn()
+
+
 class GemmLaunch:
     """One aac_gemm_batch launch with a fixed problem list (validated when built)."""
 
@@ -373,7 +383,7 @@ class FusedUpdate:
     def _adam(self, opt, flat, gpart, ns, step_add):
         m = self.m
         if m.world > 1:     # reduce the partials, all-reduce the gradient, then the plain step
-            return [lambda: sum_partials(flat.grad, gpart, ns), lambda: m._allreduce(flat),
+            return [lambda: sum_partials(flat.grad, gpart, ns), Collective(lambda: m._allreduce(flat)),
                     lambda: adam_at(opt, step_add)]
         return [lambda: adam_sum(opt, gpart, ns, step_add, grad_out=flat.grad)]
 
@@ -471,6 +481,20 @@ class FusedUpdate:
                 op()
         for op in self.post:
             op()
+
+    def segments(self):
+        """The launch list cut at the collectives: ([segment ops], [collective]) with
+        len(segments) == len(collectives) + 1."""
+        segs, colls, cur = [], [], []
+        for op in self.ops():
+            if isinstance(op, Collective):
+                segs.append(cur)
+                colls.append(op)
+                cur = []
+            else:
+                cur.append(op)
+        segs.append(cur)
+        return segs, colls
 
     def run_timed(self):
         """One eager update with a HIP event pair around every GEMM launch (on the launching

@@ -192,8 +192,12 @@ class MADDPG:
         return ts, [t.clone() for t in ts]
 
     def capture(self, B, warmup=2):
-        """Capture one update_myown-equivalent into a HIP graph (state restored afterwards)."""
-        if self.world > 1:
+        """Capture one update_myown-equivalent into HIP graphs (state restored afterwards).
+
+        world == 1: one graph.  world > 1 (fused learner): one graph per segment between the
+        gradient all-reduces; the collectives are issued between the replays (RCCL enqueues them
+        on its own stream, ordered against the current stream), so no collective is captured."""
+        if self.world > 1 and not self.fused:
             self._graph = None
             return None
         ts, saved = self._snapshot()
@@ -203,23 +207,47 @@ class MADDPG:
             for _ in range(warmup):
                 self._update_core(B)
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._graph_stats = self._update_core(B)
+        if self.world > 1:
+            fu = self._fused_plan(B)
+            segs, colls = fu.segments()
+            graphs = []
+            for seg in segs:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for op in seg:
+                        op()
+                graphs.append(g)
+            self._graph = (graphs, colls)
+            self._graph_stats = fu
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_stats = self._update_core(B)
+            self._graph = g
         for t, v in zip(ts, saved):
             t.copy_(v)
-        self._graph, self._graph_B = g, B
-        return g
+        self._graph_B = B
+        return self._graph
+
+    def _replay(self):
+        if isinstance(self._graph, tuple):
+            graphs, colls = self._graph
+            for k, g in enumerate(graphs):
+                g.replay()
+                if k < len(colls):
+                    colls[k]()
+        else:
+            self._graph.replay()
 
     def update(self, B=None, use_graph=True, idx_list=None, want_stats=True):
         """One update_myown-equivalent on the device replay (no host synchronisation).  Returns
         [(loss_q, loss_a, q, target)] per iteration (computed on demand: ``want_stats=False``
         launches nothing beyond the update itself)."""
         B = B or self.batch_size
-        if idx_list is None and use_graph and self.world == 1:
+        if idx_list is None and use_graph and (self.world == 1 or self.fused):
             if self._graph is None or self._graph_B != B:
                 self.capture(B)
-            self._graph.replay()
+            self._replay()
             self._last_src = self._graph_stats
         else:
             self._last_src = self._update_core(B, idx_list)
