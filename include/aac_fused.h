@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AAC_GEMM_MAX 8
+#define AAC_GEMM_MAX 12
 
 /* C[M][N] (row-major, ldc) = epilogue(op(A)[M][K] . op(B)[K][N]).
  * op(A)[m][k] = ta ? A[k*lda + m] : A[m*lda + k];  op(B)[k][n] = tb ? B[n*ldb + k] : B[k*ldb + n].
@@ -76,6 +76,29 @@ int aac_sum_partials(float *out, const float *gpart, int32_t nsplit, int64_t n, 
 int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, const float *b, int32_t mode,
                     const float *y, const float *rew, const float *done, int32_t B, int32_t N, float gamma, float *q,
                     float *dq, float *dh, float *yout, void *stream);
+
+/* Backward of the critic's action inputs into the actor's output layer, one row r = b*N + n per
+ * actor row (R = B*N): da_j = df[b][n*128 .. +128] . W_enc_n[:, d0 + j] (wenc = N stacked
+ * [128][din] encoder weights), dout[r][j] = da_j (1 - a_j^2) with a_j = X[(b*N + n)*din + d0 + j],
+ * dha[r][c] = (dout_0 wa[c] + dout_1 wa[256 + c]) * (ha[r][c] > 0), ha / dha rows of 256. */
+int aac_actor_out_bwd(const float *df, int32_t ldf, const float *wenc, int32_t din, int32_t d0, const float *X,
+                      const float *wa, const float *ha, int32_t N, int32_t R, float *dout, float *dha, void *stream);
+
+/* Training form of the actor's neighbour attention (ATT/nets:186-210) over R rows of K neighbour
+ * features xn[(r*K + j)*64] (mask from nei rows, nei_j.mean() != 0), e_o rows eo + r*lde:
+ * q = Wq e_o, qk = Wk^T q, alpha = masked softmax(x_j . qk / 8), xb = sum alpha_j x_j,
+ * vout[r*ldv + c] = (Wv xb)[c]; q, qk, xb [R][64] and alpha [R][K] are kept for the backward.
+ * Wq, Wk, Wv: the 64x64 q / k / v weights (row-major, nn.Linear layout). */
+int aac_attn_train_fwd(const float *eo, int32_t lde, const float *xn, const float *nei, const float *Wq,
+                       const float *Wk, const float *Wv, float *q, float *qk, float *alpha, float *xb, float *vout,
+                       int32_t ldv, int32_t R, int32_t K, void *stream);
+/* Its backward from dv (= d v_att, rows dv + r*lddv): dxn = d x_j * (x_j > 0) [R*K][64],
+ * dqk, dq [R][64], deo = (dcat_o + Wq^T dq) * (e_o > 0) [R][64] (dcat_o rows + r*ldd: the
+ * merge layer's gradient into e_o). */
+int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const float *alpha, const float *qk,
+                       const float *eo, int32_t lde, const float *dcat_o, int32_t ldd, const float *Wq, const float *Wk,
+                       const float *Wv, float *dxn, float *dqk, float *dq, float *deo, int32_t R, int32_t K,
+                       void *stream);
 
 /* Inference form of the actor's neighbour attention (ATT/nets:186-210) for R rows, K <= 32:
  * x_j = relu(Wn nei_j + bn) computed from the 6-wide rows nei[(r*K + j)*6], scores

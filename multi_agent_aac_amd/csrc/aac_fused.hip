@@ -64,6 +64,9 @@ struct GBatch {
 
 __device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, int m, int n, float v) {
     if (m >= P.M || n >= P.N) return;
+#ifdef AAC_DBG_NO_STORE      // timing probes only (tools/gemm_probe.sh): keep the value live, store ~never
+    if (v != 1234.5678f) return;
+#endif
     if (P.ones && n == P.N - 1) {
         cx[m] = v;
         return;
@@ -110,6 +113,13 @@ template <int MODE>
 __device__ __forceinline__ void load_frag(i4 X, int ld, int rows, int K, int kc, int row0,
                                           int lr, int lk, bool on, float f[2][4]) {
     const int k0 = kc + 4 * lk;
+#ifdef AAC_DBG_NO_LOAD       // timing probes only: fragments from registers
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) f[i][t] = (float)(k0 + t + i) * 1e-3f;
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r = row0 + 16 * i + lr;
@@ -289,11 +299,22 @@ __global__ void sum_partials_kernel(float *out, const float *gpart, int ns, int6
 }
 
 // ------------------------------------------------------------------------------ critic head
-__device__ inline float wsum(float x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
+// wave-wide sum by DPP (rocPRIM's gfx9 pattern): xor 1, xor 2, row_ror 4, row_ror 8 leave each
+// row's sum in every lane of the row, row_bcast 15 / 31 fold the rows into lane 63, which is
+// broadcast with readlane.  No LDS round trips (ds_swizzle / bpermute) in the chain.
+#define DPP_STEP(x, ctrl)                                                                                  \
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), ctrl, 0xf, 0xf, \
+                                                               false))
+__device__ __forceinline__ float wsum(float x) {
+    DPP_STEP(x, 0xb1);   // quad_perm [1,0,3,2]
+    DPP_STEP(x, 0x4e);   // quad_perm [2,3,0,1]
+    DPP_STEP(x, 0x124);  // row_ror:4
+    DPP_STEP(x, 0x128);  // row_ror:8
+    DPP_STEP(x, 0x142);  // row_bcast:15
+    DPP_STEP(x, 0x143);  // row_bcast:31
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
+#undef DPP_STEP
 
 __global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, int ldh, int M,
                                                    const float *__restrict__ w, const float *__restrict__ b, int mode,
@@ -326,6 +347,47 @@ __global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, 
     if (dq && lane == 0) dq[r] = g;
 #pragma unroll
     for (int j = 0; j < 4; ++j) dh[(size_t)r * 256 + lane + 64 * j] = hv[j] > 0.0f ? g * wv[j] : 0.0f;
+}
+
+// ------------------------------------------------------------------------------ actor output backward
+// Gradient through the critic's action inputs into the actor's tanh output layer, one wave per
+// actor row r = b*N + n (ATT/maddpg:421-425 backward):
+//   da_j   = sum_k df[b][n*128 + k] W_enc_n[k][D0 + j]       (d loss / d a_j via encoder n)
+//   dout_j = da_j (1 - a_j^2)                                 (tanh, ATT/nets:184)
+//   dh_a   = (dout_0 Wa[0] + dout_1 Wa[1]) * (h_a > 0)         (act_out + merge ReLU)
+__global__ void __launch_bounds__(256) actor_out_bwd_kernel(const float *__restrict__ df, int ldf,
+                                                            const float *__restrict__ wenc, int din, int d0,
+                                                            const float *__restrict__ X, const float *__restrict__ wa,
+                                                            const float *__restrict__ ha, int N, int R, float *dout,
+                                                            float *dha) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= R) return;
+    const int b = r / N, n = r - b * N;
+    const float *dfr = df + (size_t)b * ldf + n * 128;
+    const float *w = wenc + (size_t)n * 128 * din + d0;
+    float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int k = lane + 64 * q;
+        const float g = dfr[k];
+        p0 = fmaf(g, w[k * din], p0);
+        p1 = fmaf(g, w[k * din + 1], p1);
+    }
+    const float da0 = wsum(p0), da1 = wsum(p1);
+    const float *a = X + ((size_t)b * N + n) * din + d0;
+    const float a0 = a[0], a1 = a[1];
+    const float o0 = da0 * (1.0f - a0 * a0), o1 = da1 * (1.0f - a1 * a1);
+    if (lane == 0) {
+        dout[(size_t)r * 2] = o0;
+        dout[(size_t)r * 2 + 1] = o1;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int c = lane + 64 * q;
+        const float v = o0 * wa[c] + o1 * wa[256 + c];
+        dha[(size_t)r * 256 + c] = ha[(size_t)r * 256 + c] > 0.0f ? v : 0.0f;
+    }
 }
 
 // ------------------------------------------------------------------------------ attention block
@@ -424,6 +486,202 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
             v = fmaf(w.w, e.w, v);
         }
         out[(size_t)r * ldo + lane] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------ training attention
+// Training form of the same attention (ATT/nets:186-210), one row per wave iteration, lane =
+// feature, with every 64x64 projection done in-kernel from LDS-staged weights:
+//   forward   q = Wq e_o, qk = Wk^T q, a = masked softmax(x_j . qk / 8), xb = sum a_j x_j,
+//             v_att = Wv xb                              (saves q, qk, a, xb for the backward)
+//   backward  dxb = Wv^T dv; da_j = x_j . dxb; S = sum a_j da_j; ds_j = a_j (da_j - S) / 8;
+//             dqk = sum ds_j x_j; dx_j = (a_j dxb + ds_j qk) * (x_j > 0)   (-> dW_n via GEMM);
+//             dq = Wk dqk; de_o = (dcat_o + Wq^T dq) * (e_o > 0)
+// (k_j.q = x_j.(Wk^T q) and sum a_j v_j = Wv sum a_j x_j), so the [rows*K][128] k|v tensor and
+// its three GEMMs (forward, dW_kv, dx) are never formed; the weight gradients dWv = dv^T xb,
+// dWk = q^T dqk, dWq = dq^T e_o are GEMM products of the saved rows.
+__device__ __forceinline__ void stage_w(float *dst, const float *src, bool transpose) {
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        dst[(transpose ? c : r) * WS + (transpose ? r : c)] = src[e];
+    }
+}
+
+__device__ __forceinline__ float matvec_row(const float *w, const f4 *x4, int lane) {
+    const f4 *wr = reinterpret_cast<const f4 *>(w + lane * WS);
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;     // four independent chains
+#pragma unroll
+    for (int o4 = 0; o4 < 16; ++o4) {
+        const f4 a = wr[o4], b = x4[o4];
+        a0 = fmaf(a.x, b.x, a0);
+        a1 = fmaf(a.y, b.y, a1);
+        a2 = fmaf(a.z, b.z, a2);
+        a3 = fmaf(a.w, b.w, a3);
+    }
+    return (a0 + a1) + (a2 + a3);
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256) attn_train_fwd_kernel(const float *__restrict__ eo, int lde,
+                                                             const float *__restrict__ xn,
+                                                             const float *__restrict__ nei,
+                                                             const float *__restrict__ Wq, const float *__restrict__ Wk,
+                                                             const float *__restrict__ Wv, float *__restrict__ q_out,
+                                                             float *__restrict__ qk_out, float *__restrict__ alpha,
+                                                             float *__restrict__ xb_out, float *__restrict__ vout,
+                                                             int ldv, int R, int K) {
+    __shared__ f4 w4[3][64 * WS / 4];
+    __shared__ f4 buf4[4][16];
+    float *wq = reinterpret_cast<float *>(w4[0]), *wkt = reinterpret_cast<float *>(w4[1]),
+          *wv = reinterpret_cast<float *>(w4[2]);
+    stage_w(wq, Wq, false);
+    stage_w(wkt, Wk, true);
+    stage_w(wv, Wv, false);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wvi = threadIdx.x >> 6;
+    float *buf = reinterpret_cast<float *>(buf4[wvi]);
+    const int nwaves = gridDim.x * 4;
+    int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wvi);
+    // software pipeline over the wave's rows: the next row's e_o / x_j / mask are loaded while
+    // the current row is computed
+    float e_n = 0.0f, x_n[KM], m_n[KM];
+    auto fetch = [&](int rr) {
+        e_n = eo[(size_t)rr * lde + lane];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            x_n[j] = xn[((size_t)rr * K + j) * 64 + lane];
+            const float *nb = nei + ((size_t)rr * K + j) * 6;
+            float sum = nb[0];
+#pragma unroll
+            for (int i = 1; i < 6; ++i) sum += nb[i];
+            m_n[j] = sum;
+        }
+    };
+    if (r < R) fetch(r);
+    for (; r < R; r += nwaves) {
+        // keep the weight rows in LDS (re-read per row) instead of 192 hoisted VGPRs: occupancy
+        asm volatile("" ::: "memory");
+        float x[KM], msum[KM];
+        const float ev = e_n;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            x[j] = x_n[j];
+            msum[j] = m_n[j];
+        }
+        if (r + nwaves < R) fetch(r + nwaves);
+        buf[lane] = ev;
+        const float qv = matvec_row(wq, buf4[wvi], lane);
+        q_out[(size_t)r * 64 + lane] = qv;
+        buf[lane] = qv;
+        const float qk = matvec_row(wkt, buf4[wvi], lane);
+        qk_out[(size_t)r * 64 + lane] = qk;
+        float sc[KM];
+        float mx = -INFINITY;
+        unsigned valid = 0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            sc[j] = wsum(x[j] * qk) / 8.0f;
+            if (msum[j] != 0.0f) {
+                valid |= 1u << j;
+                mx = sc[j] > mx ? sc[j] : mx;
+            }
+        }
+        float den = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            const float e = (valid >> j & 1) ? expf(sc[j] - mx) : 0.0f;
+            sc[j] = e;
+            den += e;
+        }
+        float xb = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            const float a = (valid >> j & 1) ? sc[j] / den : 0.0f;
+            xb = fmaf(a, x[j], xb);
+            if (lane == j) alpha[(size_t)r * K + j] = a;
+        }
+        xb_out[(size_t)r * 64 + lane] = xb;
+        buf[lane] = xb;
+        vout[(size_t)r * ldv + lane] = matvec_row(wv, buf4[wvi], lane);
+    }
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256) attn_train_bwd_kernel(const float *__restrict__ dv, int lddv,
+                                                             const float *__restrict__ xn,
+                                                             const float *__restrict__ alpha,
+                                                             const float *__restrict__ qk_in,
+                                                             const float *__restrict__ eo, int lde,
+                                                             const float *__restrict__ dcat_o, int ldd,
+                                                             const float *__restrict__ Wq, const float *__restrict__ Wk,
+                                                             const float *__restrict__ Wv, float *__restrict__ dxn,
+                                                             float *__restrict__ dqk_out, float *__restrict__ dq_out,
+                                                             float *__restrict__ deo_out, int R, int K) {
+    __shared__ f4 w4[3][64 * WS / 4];
+    __shared__ f4 buf4[4][16];
+    float *wvt = reinterpret_cast<float *>(w4[0]), *wk = reinterpret_cast<float *>(w4[1]),
+          *wqt = reinterpret_cast<float *>(w4[2]);
+    stage_w(wvt, Wv, true);
+    stage_w(wk, Wk, false);
+    stage_w(wqt, Wq, true);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wvi = threadIdx.x >> 6;
+    float *buf = reinterpret_cast<float *>(buf4[wvi]);
+    const int nwaves = gridDim.x * 4;
+    int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wvi);
+    float dv_n = 0.0f, qk_n = 0.0f, e_n = 0.0f, dc_n = 0.0f, x_n[KM], a_n[KM];
+    auto fetch = [&](int rr) {
+        dv_n = dv[(size_t)rr * lddv + lane];
+        qk_n = qk_in[(size_t)rr * 64 + lane];
+        e_n = eo[(size_t)rr * lde + lane];
+        dc_n = dcat_o[(size_t)rr * ldd + lane];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            x_n[j] = xn[((size_t)rr * K + j) * 64 + lane];
+            a_n[j] = alpha[(size_t)rr * K + j];
+        }
+    };
+    if (r < R) fetch(r);
+    for (; r < R; r += nwaves) {
+        asm volatile("" ::: "memory");     // weight rows stay in LDS (see the forward)
+        const float dvv = dv_n, qk = qk_n, e = e_n, dc = dc_n;
+        float x[KM], a[KM], da[KM];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            x[j] = x_n[j];
+            a[j] = a_n[j];
+        }
+        if (r + nwaves < R) fetch(r + nwaves);
+        buf[lane] = dvv;
+        const float dxb = matvec_row(wvt, buf4[wvi], lane);
+        float S = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            da[j] = wsum(x[j] * dxb);
+            S += a[j] * da[j];
+        }
+        float dqk = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+            const float ds = a[j] * (da[j] - S) / 8.0f;
+            const float g = a[j] * dxb + ds * qk;
+            dxn[((size_t)r * K + j) * 64 + lane] = x[j] > 0.0f ? g : 0.0f;
+            dqk = fmaf(ds, x[j], dqk);
+        }
+        dqk_out[(size_t)r * 64 + lane] = dqk;
+        buf[lane] = dqk;
+        const float dq = matvec_row(wk, buf4[wvi], lane);
+        dq_out[(size_t)r * 64 + lane] = dq;
+        buf[lane] = dq;
+        const float t = matvec_row(wqt, buf4[wvi], lane);
+        deo_out[(size_t)r * 64 + lane] = e > 0.0f ? dc + t : 0.0f;
     }
 }
 
@@ -563,6 +821,58 @@ int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, cons
     if (mode == 2 && (!rew || !done || !yout || B <= 0 || N <= 0)) return ffail("critic_head: mode 2 needs rew/done/yout");
     hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, M, w, b, mode, y, rew,
                        done, B, N, gamma, q, dq, dh, yout);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_actor_out_bwd(const float *df, int32_t ldf, const float *wenc, int32_t din, int32_t d0, const float *X,
+                      const float *wa, const float *ha, int32_t N, int32_t R, float *dout, float *dha, void *stream) {
+    if (R <= 0) return 0;
+    if (N <= 0 || din < d0 + 2) return ffail("actor_out_bwd: need N > 0 and din >= d0 + 2");
+    hipLaunchKernelGGL(actor_out_bwd_kernel, dim3((R + 3) / 4), dim3(256), 0, (hipStream_t)stream, df, ldf, wenc,
+                       din, d0, X, wa, ha, N, R, dout, dha);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+static int attn_grid(int R) {
+    int wgs = (R + 15) / 16;          // ~4 rows per wave
+    return wgs < 1 ? 1 : (wgs > 2048 ? 2048 : wgs);
+}
+
+int aac_attn_train_fwd(const float *eo, int32_t lde, const float *xn, const float *nei, const float *Wq,
+                       const float *Wk, const float *Wv, float *q, float *qk, float *alpha, float *xb, float *vout,
+                       int32_t ldv, int32_t R, int32_t K, void *stream) {
+    if (R <= 0) return 0;
+    if (K < 1 || K > 32) return ffail("attn_train_fwd: 1 <= K <= 32");
+    const dim3 grid(attn_grid(R)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+#define ATF(KM) hipLaunchKernelGGL(attn_train_fwd_kernel<KM>, grid, block, 0, st, eo, lde, xn, nei, Wq, Wk, Wv, q, qk, \
+                                   alpha, xb, vout, ldv, R, K)
+    if (K <= 4) ATF(4);
+    else if (K <= 8) ATF(8);
+    else if (K <= 16) ATF(16);
+    else ATF(32);
+#undef ATF
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const float *alpha, const float *qk,
+                       const float *eo, int32_t lde, const float *dcat_o, int32_t ldd, const float *Wq, const float *Wk,
+                       const float *Wv, float *dxn, float *dqk, float *dq, float *deo, int32_t R, int32_t K,
+                       void *stream) {
+    if (R <= 0) return 0;
+    if (K < 1 || K > 32) return ffail("attn_train_bwd: 1 <= K <= 32");
+    const dim3 grid(attn_grid(R)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+#define ATB(KM) hipLaunchKernelGGL(attn_train_bwd_kernel<KM>, grid, block, 0, st, dv, lddv, xn, alpha, qk, eo, lde, \
+                                   dcat_o, ldd, Wq, Wk, Wv, dxn, dqk, dq, deo, R, K)
+    if (K <= 4) ATB(4);
+    else if (K <= 8) ATB(8);
+    else if (K <= 16) ATB(16);
+    else ATB(32);
+#undef ATB
     FHIP(hipGetLastError());
     return 0;
 }

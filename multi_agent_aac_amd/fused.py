@@ -8,16 +8,13 @@ written out by hand (no autograd):
 
 critic step (batch i, ATT/maddpg:375-387)        actor step (ATT/maddpg:389-425)
   f_n = relu(enc_n [own_n, a_n])   (N products)    e_o, e_g, x = relu(...)          (3 products)
-  h   = relu(Wc f)                                 q_att, kv = e_o Wq^T, x Wkv^T    (2)
-  q, dq = 2(q - y)/B, dh = dq Wo * (h > 0)         attention -> v_att  (HIP kernel)
-  dWo|dbo, dWc|dbc, df = dh Wc * (f > 0)  (3)      h_a = relu(Wm [e_o e_g v_att]); a = tanh(Wa h_a)
-  dW_enc_n | db_enc_n                     (N)      critic forward on a (2 + head), dh (dq = -1/B)
-  Adam                                             df; da_n -> dout = da (1 - a^2)   (1 + N)
-                                                   dWa|dba, dh_a                     (2)
-                                                   dWm|dbm, d e_o', d e_g, d v_att   (4)
-                                                   attention backward
-                                                   d e_o, dWq, dWkv, dx              (4)
-                                                   dW_own|db, dW_grid|db, dW_nei|db  (3)
+  h   = relu(Wc f)                                 attention: q, Wk^T q, softmax, Wv sum a x (kernel)
+  q, dq = 2(q - y)/B, dh = dq Wo * (h > 0)         h_a = relu(Wm [e_o e_g v_att]); a = tanh(Wa h_a)
+  dWo|dbo, dWc|dbc, df = dh Wc * (f > 0)  (3)      critic forward on a (2 + head), dh (dq = -1/B)
+  dW_enc_n | db_enc_n                     (N)      df; dout = (df W_enc[:, a]) (1 - a^2), dh_a (kernel)
+  Adam                                             dWa|dba, dWm|dbm, d e_o', d e_g, d v_att  (5)
+                                                   attention backward -> dx, dqk, dq, d e_o (kernel)
+                                                   dWv, dWk, dWq, dW_nei|db, dW_own|db, dW_grid|db (6)
                                                    Adam
 The TD targets of all N iterations are one batched forward of the target networks (they only
 change in the Polyak step after the loop, ATT/maddpg:436-438), and the N batches are sampled and
@@ -61,6 +58,10 @@ def lib():
         L.aac_critic_head.argtypes = [vp, i32, i32, vp, vp, i32, vp, vp, vp, i32, i32, f32, vp, vp, vp, vp, vp]
         L.aac_replay_gather_strided.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp]
         L.aac_attn_block.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
+        L.aac_actor_out_bwd.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp]
+        L.aac_attn_train_fwd.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
+        L.aac_attn_train_bwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, i32, i32,
+                                         vp]
         L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         _L = L
     return _L
@@ -156,21 +157,25 @@ def adam_at(opt, step_add):
                                 _stream()), "aac_adam_flat_at")
 
 
+def actor_out_bwd(df, ldf, wenc, din, d0, X, wa, ha, N, R, dout, dha):
+    _chk(lib().aac_actor_out_bwd(vp(df), ldf, vp(wenc), din, d0, vp(X), vp(wa), vp(ha), N, R, vp(dout), vp(dha),
+                                 _stream()), "aac_actor_out_bwd")
+
+
+def attn_train_fwd(eo, lde, xn, nei, Wq, Wk, Wv, q, qk, alpha, xb, vout, ldv, R, K):
+    _chk(lib().aac_attn_train_fwd(vp(eo), lde, vp(xn), vp(nei), vp(Wq), vp(Wk), vp(Wv), vp(q), vp(qk), vp(alpha),
+                                  vp(xb), vp(vout), ldv, R, K, _stream()), "aac_attn_train_fwd")
+
+
+def attn_train_bwd(dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq, Wk, Wv, dxn, dqk, dq, deo, R, K):
+    _chk(lib().aac_attn_train_bwd(vp(dv), lddv, vp(xn), vp(alpha), vp(qk), vp(eo), lde, vp(dcat_o), ldd, vp(Wq),
+                                  vp(Wk), vp(Wv), vp(dxn), vp(dqk), vp(dq), vp(deo), R, K, _stream()),
+         "aac_attn_train_bwd")
+
+
 def attn_block(eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K):
     _chk(lib().aac_attn_block(vp(eo), lde, vp(nei), vp(Wn), vp(bn), vp(Wqk), vp(Wv), vp(out), ldo, R, K, _stream()),
          "aac_attn_block")
-
-
-def _attn_fwd(q, kv, nei, out, out_stride, alpha, R, K):
-    L = ops.lib()
-    ops._chk(L.aac_attn_fwd(vp(q), vp(kv), vp(kv + 256), 128, vp(nei), vp(out), out_stride, vp(alpha), R, K,
-                            _stream()), "aac_attn_fwd")
-
-
-def _attn_bwd(q, kv, alpha, dout, dout_stride, dq, dkv, R, K):
-    L = ops.lib()
-    ops._chk(L.aac_attn_bwd(vp(q), vp(kv), vp(kv + 256), 128, vp(alpha), vp(dout), dout_stride, vp(dq), vp(dkv),
-                            vp(dkv + 256), R, K, _stream()), "aac_attn_bwd")
 
 
 # =============================================================================== networks
@@ -213,34 +218,34 @@ class ActorActs:
         z = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)   # noqa: E731
         self.R, self.K = R, K
         self.cat = z(R, 192)          # [e_o | e_g | v_att]
-        self.xn = z(R * K, 64)
-        self.qa = z(R, 64)
-        self.kv = z(R * K, 128)
+        self.xn = z(R * K, 64)        # neighbour features x_j
+        self.qa = z(R, 64)            # q = Wq e_o
+        self.qk = z(R, 64)            # Wk^T q
+        self.xb = z(R, 64)            # sum_j alpha_j x_j
         self.alpha = z(R, max(K, 1))
         self.ha = z(R, 256)
 
 
 def actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
     """ActorNetwork_ATT_TwoPortion.forward (ATT/nets:194-213) over R rows as dependent stages
-    [encoders, q|kv, attention (callable), merge, out]; GEMM stages are product lists so they
-    can share launches with independent work.  The tanh actions land at ``out`` (row stride
-    ``ld_out``, e.g. the critic-input rows)."""
+    [encoders, attention (callable, aac_attn_train_fwd: q, Wk^T q, masked softmax, Wv sum a x),
+    merge, out]; GEMM stages are product lists so they can share launches with independent
+    work.  The tanh actions land at ``out`` (row stride ``ld_out``, e.g. the critic-input rows)."""
     c = acts
     enc = [prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
            prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
            prob(nei, ap.Wn, ptr(c.xn), R * K, 64, 6, 6, 6, 64, tb=1, bias=ap.bn, act=RELU)]
-    qkv = [prob(ptr(c.cat), ap.Wq, ptr(c.qa), R, 64, 64, 192, 64, 64, tb=1),
-           prob(ptr(c.xn), ap.Wkv, ptr(c.kv), R * K, 128, 64, 64, 64, 128, tb=1)]
-    attn = lambda: _attn_fwd(ptr(c.qa), ptr(c.kv), nei, ptr(c.cat, 128), 192, ptr(c.alpha), R, K)  # noqa: E731
+    attn = lambda: attn_train_fwd(ptr(c.cat), 192, ptr(c.xn), nei, ap.Wq, ap.Wkv, ap.Wkv + 4 * 64 * 64,  # noqa: E731
+                                  ptr(c.qa), ptr(c.qk), ptr(c.alpha), ptr(c.xb), ptr(c.cat, 128), 192, R, K)
     merge = [prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm, act=RELU)]
     outp = [prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)]
-    return enc, qkv, attn, merge, outp
+    return enc, attn, merge, outp
 
 
 def actor_forward(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
     """Launch list of the training actor forward (activations kept for the backward)."""
-    enc, qkv, attn, merge, outp = actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
-    return gemm_launches(enc) + gemm_launches(qkv) + [attn] + gemm_launches(merge) + gemm_launches(outp)
+    enc, attn, merge, outp = actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
+    return gemm_launches(enc) + [attn] + gemm_launches(merge) + gemm_launches(outp)
 
 
 class ActorInferActs:
@@ -346,7 +351,7 @@ class FusedUpdate:
         R = B * N
         self.dout, self.dha = z(R, 2), z(R, 256)
         self.dcat_o, self.dcat_g, self.dv = z(R, 64), z(R, 64), z(R, 64)
-        self.dqa, self.dkv, self.deo, self.dxn = z(R, 64), z(R * K, 128), z(R, 64), z(R * K, 64)
+        self.dqa, self.dqk, self.deo, self.dxn = z(R, 64), z(R, 64), z(R, 64), z(R * K, 64)
         # weight-gradient partial copies (summed by the Adam kernel)
         self.ga = torch.zeros(self.SPLIT_ACTOR, model.fa.numel, device=dev)
         self.gc = torch.zeros(self.SPLIT_CRITIC, model.fc.numel, device=dev)
@@ -405,14 +410,13 @@ class FusedUpdate:
         # The actor forward of this iteration (ATT/maddpg:389-392) depends only on the actor
         # weights, which change after the critic step, so its products share the critic step's
         # launches; the policy actions land in X2 (own columns gathered there too).
-        a_enc, a_qkv, a_attn, a_merge, a_out = actor_forward_stages(A, c, X2, Din, radar, nei, R, K, D0, X2 + 4 * D0,
-                                                                    Din)
+        a_enc, a_attn, a_merge, a_out = actor_forward_stages(A, c, X2, Din, radar, nei, R, K, D0, X2 + 4 * D0, Din)
         c_enc, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
         # ---------------- critic step (ATT/maddpg:375-387)
         L += gemm_launches(c_enc + a_enc)
-        L += gemm_launches(c_comb + a_qkv)
-        L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh)))
         L.append(a_attn)
+        L += gemm_launches(c_comb)
+        L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh)))
         L += gemm_launches([
             prob(ptr(dq), ptr(h), gC.Wq, 1, 256, B, 1, 256, 256, ta=1, ones=1, cextra=gC.bq, ksplit=SC,
                  split_stride=nC),
@@ -430,37 +434,31 @@ class FusedUpdate:
         L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 1, q=ptr(self.q_a, i * B), dh=ptr(dh)))
         L += gemm_launches([prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f),
                                  ldmask=128 * N, mact=RELU)])
-        # da_n = df_n . W_enc_n[:, D0:D0+2]; dout = da * (1 - a^2)   (rows b*N + n of dout)
-        L += gemm_launches([prob(ptr(df, n * 128), C.enc_w[n] + 4 * D0, ptr(self.dout, 2 * n), B, 2, 128, 128 * N,
-                                 Din, 2 * N, mask=X + 4 * (n * Din + D0), ldmask=N * Din, mact=TANH)
-                            for n in range(N)])
+        # da_n = df_n . W_enc_n[:, D0:D0+2]; dout = da * (1 - a^2); dh_a = (dout Wa) * (h_a > 0)
+        L.append(lambda: actor_out_bwd(ptr(df), 128 * N, C.enc_w[0], Din, D0, X, A.Wa, ptr(c.ha), N, R,
+                                       ptr(self.dout), ptr(self.dha)))
         L += gemm_launches([
             prob(ptr(self.dout), ptr(c.ha), gA.Wa, 2, 256, R, 2, 256, 256, ta=1, ones=1, cextra=gA.ba, ksplit=SA,
                  split_stride=nA),
-            prob(ptr(self.dout), A.Wa, ptr(self.dha), R, 256, 2, 2, 256, 256, mask=ptr(c.ha), ldmask=256,
-                 mact=RELU)])
-        L += gemm_launches([
             prob(ptr(self.dha), ptr(c.cat), gA.Wm, 256, 192, R, 256, 192, 192, ta=1, ones=1, cextra=gA.bm,
                  ksplit=SA, split_stride=nA),
             prob(ptr(self.dha), A.Wm, ptr(self.dcat_o), R, 64, 256, 256, 192, 64),
             prob(ptr(self.dha), A.Wm + 4 * 64, ptr(self.dcat_g), R, 64, 256, 256, 192, 64, mask=ptr(c.cat, 64),
                  ldmask=192, mact=RELU),
             prob(ptr(self.dha), A.Wm + 4 * 128, ptr(self.dv), R, 64, 256, 256, 192, 64)])
-        L.append(lambda: _attn_bwd(ptr(c.qa), ptr(c.kv), ptr(c.alpha), ptr(self.dv), 64, ptr(self.dqa),
-                                   ptr(self.dkv), R, K))
+        L.append(lambda: attn_train_bwd(ptr(self.dv), 64, ptr(c.xn), ptr(c.alpha), ptr(c.qk), ptr(c.cat), 192,
+                                        ptr(self.dcat_o), 64, A.Wq, A.Wkv, A.Wkv + 4 * 64 * 64, ptr(self.dxn),
+                                        ptr(self.dqk), ptr(self.dqa), ptr(self.deo), R, K))
         L += gemm_launches([
-            prob(ptr(self.dqa), A.Wq, ptr(self.deo), R, 64, 64, 64, 64, 64, addend=ptr(self.dcat_o), ldadd=64,
-                 mask=ptr(c.cat), ldmask=192, mact=RELU),
+            prob(ptr(self.dv), ptr(c.xb), gA.Wkv + 4 * 64 * 64, 64, 64, R, 64, 64, 64, ta=1, ksplit=SA,
+                 split_stride=nA),                                                         # dWv
+            prob(ptr(c.qa), ptr(self.dqk), gA.Wkv, 64, 64, R, 64, 64, 64, ta=1, ksplit=SA, split_stride=nA),  # dWk
             prob(ptr(self.dqa), ptr(c.cat), gA.Wq, 64, 64, R, 64, 192, 64, ta=1, ksplit=SA, split_stride=nA),
-            prob(ptr(self.dkv), ptr(c.xn), gA.Wkv, 128, 64, R * K, 128, 64, 64, ta=1, ksplit=SA, split_stride=nA),
-            prob(ptr(self.dkv), A.Wkv, ptr(self.dxn), R * K, 64, 128, 128, 64, 64, mask=ptr(c.xn), ldmask=64,
-                 mact=RELU)])
-        L += gemm_launches([
+            prob(ptr(self.dxn), nei, gA.Wn, 64, 6, R * K, 64, 6, 6, ta=1, ones=1, cextra=gA.bn, ksplit=SA,
+                 split_stride=nA),
             prob(ptr(self.deo), X, gA.Wo, 64, D0, R, 64, Din, D0, ta=1, ones=1, cextra=gA.bo, ksplit=SA,
                  split_stride=nA),
             prob(ptr(self.dcat_g), radar, gA.Wg, 64, 18, R, 64, 18, 18, ta=1, ones=1, cextra=gA.bg, ksplit=SA,
-                 split_stride=nA),
-            prob(ptr(self.dxn), nei, gA.Wn, 64, 6, R * K, 64, 6, 6, ta=1, ones=1, cextra=gA.bn, ksplit=SA,
                  split_stride=nA)])
         L += self._adam(m.actor_optimizer, m.fa, self.ga, SA, i + 1)
         return L

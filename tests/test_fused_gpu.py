@@ -240,3 +240,48 @@ def test_fused_act_matches_actor_module(native_lib):
     got = m.act(own, radar, nei, noisy=False).clone()
     want = m.actors([own, radar, nei])
     np.testing.assert_allclose(got.cpu(), want.detach().cpu(), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("K", [1, 4, 7])
+def test_attn_train_fwd_bwd_matches_autograd(native_lib, K):
+    """Training attention kernels (in-kernel q / k / v projections) against fp64 autograd of the
+    reference form (ATT/nets:186-210): v_att, and the gradients into x_j, q and e_o."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(10 + K)
+    R = 600
+    eo = torch.relu(torch.randn(R, 64, device=DEV))
+    x = torch.relu(torch.randn(R, K, 64, device=DEV))
+    nei = torch.randn(R, K, 6, device=DEV)
+    nei[::4, 0] = 0.0
+    nei[7] = 0.0
+    Wq, Wk, Wv = (torch.randn(64, 64, device=DEV) * 0.125 for _ in range(3))
+    kv = torch.cat([Wk, Wv], 0).contiguous()
+    cat = torch.zeros(R, 192, device=DEV)
+    cat[:, :64] = eo
+    z = lambda *s: torch.empty(*s, device=DEV)   # noqa: E731
+    q, qk, alpha, xb = z(R, 64), z(R, 64), z(R, K), z(R, 64)
+    P = fused.ptr
+    fused.attn_train_fwd(P(cat), 192, P(x), P(nei), P(Wq), P(kv), P(kv, 64 * 64), P(q), P(qk), P(alpha), P(xb),
+                         P(cat, 128), 192, R, K)
+    dv, dcat_o = torch.randn(R, 64, device=DEV), torch.randn(R, 64, device=DEV)
+    dxn, dqk, dq, deo = z(R * K, 64), z(R, 64), z(R, 64), z(R, 64)
+    fused.attn_train_bwd(P(dv), 64, P(x), P(alpha), P(qk), P(cat), 192, P(dcat_o), 64, P(Wq), P(kv), P(kv, 64 * 64),
+                         P(dxn), P(dqk), P(dq), P(deo), R, K)
+    d = lambda t: t.double().cpu()   # noqa: E731
+    eo_r = d(eo).requires_grad_()
+    x_r = d(x).requires_grad_()
+    q_r = eo_r @ d(Wq).t()
+    q_r.retain_grad()
+    k_r, v_r = x_r @ d(Wk).t(), x_r @ d(Wv).t()
+    score = torch.einsum("rkc,rc->rk", k_r, q_r) / 8.0
+    mask = d(nei).mean(-1) != 0
+    score = score.masked_fill(~mask, float("-inf"))
+    a = torch.nan_to_num(torch.softmax(score, dim=1)).masked_fill(~mask, 0.0)
+    v_att = torch.einsum("rk,rkc->rc", a, v_r)
+    ((v_att * d(dv)).sum() + (eo_r * d(dcat_o)).sum()).backward()
+    np.testing.assert_allclose(cat[:, 128:].cpu().double(), v_att.detach(), atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(alpha.cpu().double(), a.detach(), atol=1e-6)
+    np.testing.assert_allclose(q.cpu().double(), q_r.detach(), atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(dxn.cpu().double().reshape(R, K, 64), x_r.grad * (d(x) > 0), atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(dq.cpu().double(), q_r.grad, atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(deo.cpu().double(), eo_r.grad * (d(eo) > 0), atol=2e-5, rtol=1e-5)
