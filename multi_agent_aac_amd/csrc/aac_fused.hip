@@ -402,14 +402,28 @@ __global__ void __launch_bounds__(256) actor_out_bwd_kernel(const float *__restr
 // conflict-free) and its four waves walk the rows; the vector being multiplied is broadcast
 // from a 64-float LDS slot of the wave.
 constexpr int WS = 68;
+__device__ __forceinline__ float matvec_row(const float *w, const f4 *x4, int lane) {
+    const f4 *wr = reinterpret_cast<const f4 *>(w + lane * WS);
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;     // four independent chains
+#pragma unroll
+    for (int o4 = 0; o4 < 16; ++o4) {
+        const f4 a = wr[o4], b = x4[o4];
+        a0 = fmaf(a.x, b.x, a0);
+        a1 = fmaf(a.y, b.y, a1);
+        a2 = fmaf(a.z, b.z, a2);
+        a3 = fmaf(a.w, b.w, a3);
+    }
+    return (a0 + a1) + (a2 + a3);
+}
+
 template <int KM>
 __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict__ eo, int lde,
                                                          const float *__restrict__ nei,
                                                          const float *__restrict__ Wn,
                                                          const float *__restrict__ bn,
                                                          const float *__restrict__ Wqk,
-                                                         const float *__restrict__ Wv, float *out, int ldo, int R,
-                                                         int K) {
+                                                         const float *__restrict__ Wv, float *__restrict__ out, int ldo,
+                                                         int R, int K) {
     __shared__ f4 wq4[64 * WS / 4], wv4[64 * WS / 4];
     __shared__ f4 buf4[4][16];
     float *wqs = reinterpret_cast<float *>(wq4), *wvs = reinterpret_cast<float *>(wv4);
@@ -426,33 +440,42 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
 #pragma unroll
     for (int i = 0; i < 6; ++i) wn[i] = Wn[lane * 6 + i];
     const float bnl = bn[lane];
-    const f4 *wqr = reinterpret_cast<const f4 *>(wqs + lane * WS);
-    const f4 *wvr = reinterpret_cast<const f4 *>(wvs + lane * WS);
     const int nwaves = gridDim.x * 4;
-    for (int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv); r < R; r += nwaves) {
-        buf[lane] = eo[(size_t)r * lde + lane];
-        float qk = 0.0f;
+    int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+    // software pipeline: the next row's e_o and neighbour rows load while this row is computed
+    float e_n = 0.0f, nb_n[KM][6];
+    auto fetch = [&](int rr) {
+        e_n = eo[(size_t)rr * lde + lane];
 #pragma unroll
-        for (int o4 = 0; o4 < 16; ++o4) {
-            const f4 e = buf4[wv][o4], w = wqr[o4];
-            qk = fmaf(w.x, e.x, qk);
-            qk = fmaf(w.y, e.y, qk);
-            qk = fmaf(w.z, e.z, qk);
-            qk = fmaf(w.w, e.w, qk);
+        for (int j = 0; j < KM; ++j) {
+            if (j >= K) continue;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) nb_n[j][i] = nei[((size_t)rr * K + j) * 6 + i];
         }
+    };
+    if (r < R) fetch(r);
+    for (; r < R; r += nwaves) {
+        float nb[KM][6];
+        const float ev = e_n;
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) nb[j][i] = nb_n[j][i];
+        if (r + nwaves < R) fetch(r + nwaves);
+        buf[lane] = ev;
+        const float qk = matvec_row(wqs, buf4[wv], lane);
         float x[KM], sc[KM];
         float mx = -INFINITY;
         unsigned valid = 0;
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
             if (j >= K) continue;
-            const float *nb = nei + ((size_t)r * K + j) * 6;
             float h = bnl;
-            float sum = nb[0];
+            float sum = nb[j][0];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) h = fmaf(wn[i], nb[i], h);
+            for (int i = 0; i < 6; ++i) h = fmaf(wn[i], nb[j][i], h);
 #pragma unroll
-            for (int i = 1; i < 6; ++i) sum += nb[i];
+            for (int i = 1; i < 6; ++i) sum += nb[j][i];
             x[j] = h > 0.0f ? h : 0.0f;
             sc[j] = wsum(x[j] * qk) / 8.0f;
             if (sum != 0.0f) {
@@ -476,16 +499,7 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
             xb = fmaf(a, x[j], xb);
         }
         buf[lane] = xb;
-        float v = 0.0f;
-#pragma unroll
-        for (int o4 = 0; o4 < 16; ++o4) {
-            const f4 e = buf4[wv][o4], w = wvr[o4];
-            v = fmaf(w.x, e.x, v);
-            v = fmaf(w.y, e.y, v);
-            v = fmaf(w.z, e.z, v);
-            v = fmaf(w.w, e.w, v);
-        }
-        out[(size_t)r * ldo + lane] = v;
+        out[(size_t)r * ldo + lane] = matvec_row(wvs, buf4[wv], lane);
     }
 }
 
@@ -505,20 +519,6 @@ __device__ __forceinline__ void stage_w(float *dst, const float *src, bool trans
         const int r = e >> 6, c = e & 63;
         dst[(transpose ? c : r) * WS + (transpose ? r : c)] = src[e];
     }
-}
-
-__device__ __forceinline__ float matvec_row(const float *w, const f4 *x4, int lane) {
-    const f4 *wr = reinterpret_cast<const f4 *>(w + lane * WS);
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;     // four independent chains
-#pragma unroll
-    for (int o4 = 0; o4 < 16; ++o4) {
-        const f4 a = wr[o4], b = x4[o4];
-        a0 = fmaf(a.x, b.x, a0);
-        a1 = fmaf(a.y, b.y, a1);
-        a2 = fmaf(a.z, b.z, a2);
-        a3 = fmaf(a.w, b.w, a3);
-    }
-    return (a0 + a1) + (a2 + a3);
 }
 
 template <int KM>
