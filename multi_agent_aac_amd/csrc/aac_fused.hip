@@ -16,7 +16,9 @@
 // optimiser sums (aac_adam_flat_sum), so there is no cross-workgroup reduction in the launch.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -51,7 +53,7 @@ struct GProb {
     int M, N, K;
     int lda, ldb, ldc, ldadd, ldmask;
     int ta, tb, act, mact, ones, ks;
-    int amode, bmode;          // fragment load modes LV / LS / LT
+    int amode, bmode;          // fragment load modes LV / LS / LT / LW
     int deep;                  // 4-deep prefetch ring (long chains) or none
     int wide;                  // one tile per wave, four adjacent tiles per workgroup
     int tiles_n, w_begin;      // first workgroup of this product
@@ -87,17 +89,23 @@ __device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, in
 //   LV  K-contiguous rows, ld % 4 == 0, K % 4 == 0, 16-B aligned: one 16-B load per row
 //   LS  K-contiguous rows, otherwise: four 4-B loads
 //   LT  row-contiguous (stored [k][row]): four 4-B loads, 16 lanes cover 64 contiguous bytes
+//   LW  row-contiguous, rows % T == 0, ld % T == 0, 4T-B aligned: lane lr loads the T consecutive
+//       rows T*lr .. T*lr + T-1 at one k with one 4T-B load (16 lanes cover 16T*4 contiguous
+//       bytes, whole lines), so 16x16 block i holds the rows T*lr + i: the tile's rows are
+//       permuted and the epilogue undoes it
 // Loads are raw buffer loads; an element outside the operand (row >= rows, k >= K, or a chunk
 // this wave does not own) gets an out-of-range offset and the hardware returns 0, so nothing
 // touches a loaded value before its MFMA and the compiler's vmcnt tracking stays exact across
 // the prefetch ring.  f[i][t] = op(X)[row0 + 16 i + lr][kc + 4 lk + t].
-enum { LV = 0, LS = 1, LT = 2 };
+enum { LV = 0, LS = 1, LT = 2, LW = 3 };
 constexpr int OOB = 0x7ffffff0;     // byte offset past every operand (= num_records)
 
 typedef int i4 __attribute__((ext_vector_type(4)));
 // the LLVM buffer-load intrinsics (the clang b128 builtin lowers to a single dword here)
 __device__ f4 buf_load_x4(i4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 __device__ float buf_load_x1(i4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ f2 buf_load_x2(i4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2f32");
 
 __device__ __forceinline__ i4 rsrc_of(const float *p) {
     const uint64_t a = reinterpret_cast<uint64_t>(p);
@@ -109,19 +117,40 @@ __device__ __forceinline__ i4 rsrc_of(const float *p) {
     return r;
 }
 
-template <int MODE>
+template <int MODE, int T>
 __device__ __forceinline__ void load_frag(i4 X, int ld, int rows, int K, int kc, int row0,
-                                          int lr, int lk, bool on, float f[2][4]) {
+                                          int lr, int lk, bool on, float f[T][4]) {
     const int k0 = kc + 4 * lk;
 #ifdef AAC_DBG_NO_LOAD       // timing probes only: fragments from registers
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < T; ++i)
 #pragma unroll
         for (int t = 0; t < 4; ++t) f[i][t] = (float)(k0 + t + i) * 1e-3f;
     return;
 #endif
+    if (MODE == LW) {
+        const int r = row0 + T * lr;
+        const bool rin = on && r < rows;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+        for (int t = 0; t < 4; ++t) {
+            const int k = k0 + t;
+            const int off = (rin && k < K) ? (k * ld + r) * 4 : OOB;
+            if (T == 4) {
+                const f4 v = buf_load_x4(X, off, 0, 0);
+                f[0][t] = v.x;
+                f[1 % T][t] = v.y;
+                f[2 % T][t] = v.z;
+                f[3 % T][t] = v.w;
+            } else {
+                const f2 v = buf_load_x2(X, off, 0, 0);
+                f[0][t] = v.x;
+                f[1 % T][t] = v.y;
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
         const int r = row0 + 16 * i + lr;
         const bool rin = on && r < rows;
         if (MODE == LV) {
@@ -142,128 +171,148 @@ __device__ __forceinline__ void load_frag(i4 X, int ld, int rows, int K, int kc,
     }
 }
 
-// one 32x32 tile over this wave's chunks c0, c0+4, ... < c1 (D-deep register ring: the loads of
-// the next D-1 chunks are in flight while one is multiplied; these chains are latency-bound).
-// The virtual ones row of op(B) (bias gradient) is a constant fragment: extra MFMAs in the one
-// tile column that holds it.
-template <int AM, int BM, int D>
+// one (16T)x(16T) tile over this wave's chunks c0, c0+cstep, ... < c1 (D-deep register ring: the
+// loads of the next D-1 chunks are in flight while one is multiplied; these chains are
+// latency-bound).  The virtual ones row of op(B) (bias gradient) is a constant fragment: extra
+// MFMAs in the one tile column that holds it.
+template <int AM, int BM, int D, int T>
 __device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0, int c1, int cstep, int lr,
-                                         int lk, f4 acc[2][2]) {
+                                         int lk, f4 acc[T][T]) {
     const int nreal = P.N - P.ones;
     const i4 ra = rsrc_of(P.A), rb = rsrc_of(P.B);
-    const bool has_one = P.ones && nreal >= n0 && nreal < n0 + WT;      // wave-uniform
-    float one[2];
+    const bool has_one = P.ones && nreal >= n0 && nreal < n0 + 16 * T;      // wave-uniform
+    float one[T];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) one[j] = (n0 + 16 * j + lr == nreal) ? 1.0f : 0.0f;
-    float fa[D][2][4], fb[D][2][4];
+    for (int j = 0; j < T; ++j) one[j] = ((BM == LW ? n0 + T * lr + j : n0 + 16 * j + lr) == nreal) ? 1.0f : 0.0f;
+    float fa[D][T][4], fb[D][T][4];
     const int nmine = c0 < c1 ? (c1 - c0 + cstep - 1) / cstep : 0;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const bool on = d < nmine;
         const int kc = (c0 + cstep * d) * KC;
-        load_frag<AM>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
-        load_frag<BM>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
+        load_frag<AM, T>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
+        load_frag<BM, T>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
     }
     for (int q0 = 0; q0 < nmine; q0 += D) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][0][t], fb[d][0][t], acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][0][t], fb[d][1][t], acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][1][t], fb[d][0][t], acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][1][t], fb[d][1][t], acc[1][1], 0, 0, 0);
-            }
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int i = 0; i < T; ++i)
+#pragma unroll
+                    for (int j = 0; j < T; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][i][t], fb[d][j][t], acc[i][j], 0, 0, 0);
             if (has_one) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int i = 0; i < T; ++i)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j)
+                        for (int j = 0; j < T; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[d][i][t], one[j], acc[i][j], 0, 0, 0);
             }
             const int qn = q0 + d + D;
             const bool on = qn < nmine;
             const int kc = (c0 + cstep * qn) * KC;
-            load_frag<AM>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
-            load_frag<BM>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
+            load_frag<AM, T>(ra, P.lda, P.M, P.K, kc, m0, lr, lk, on, fa[d]);
+            load_frag<BM, T>(rb, P.ldb, nreal, P.K, kc, n0, lr, lk, on, fb[d]);
+            // keep the refill issued here: left to itself the scheduler sinks it below the next
+            // stage's wait, and the ring holds one chunk in flight instead of D
+            if (D > 1) __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
 
-template <int DEPTH>
-__global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
-    __shared__ f4 red[4][4][64];       // [wave][quadrant][lane]
-    const int wg = blockIdx.x;
-    int pi = 0;
-    while (pi + 1 < g.n && wg >= g.p[pi + 1].w_begin) ++pi;
-    const GProb &P = g.p[pi];
-    const int local = wg - P.w_begin;
+// One workgroup's share of product P with (16T)x(16T) wave tiles.
+template <int T, int DEPTH>
+__device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4][64]) {
+    constexpr int TW = 16 * T;
     const int s = local % P.ks;
     const int w = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int nch = (P.K + KC - 1) / KC;
     const int per = (nch + P.ks - 1) / P.ks;
-    int m0, n0, c0, c1, cstep;
+    int m0, n0, c0, cstep;
     if (P.wide) {
-        // wide: the four waves take four adjacent 32x32 tiles of one 32-row block (A rows shared
-        // through L1), each over the whole K range of the split
+        // wide: the four waves take four adjacent tiles of one row block (A rows shared through
+        // L1), each over the whole K range of the split
         const int grp = local / P.ks;
         const int gpr = (P.tiles_n + 3) / 4;
         const int tn = (grp % gpr) * 4 + w;
         if (tn >= P.tiles_n) return;
-        m0 = (grp / gpr) * WT;
-        n0 = tn * WT;
+        m0 = (grp / gpr) * TW;
+        n0 = tn * TW;
         c0 = s * per;
         cstep = 1;
     } else {
         // the four waves share one tile and take every fourth chunk of the split
         const int tile = local / P.ks;
-        m0 = (tile / P.tiles_n) * WT;
-        n0 = (tile % P.tiles_n) * WT;
+        m0 = (tile / P.tiles_n) * TW;
+        n0 = (tile % P.tiles_n) * TW;
         c0 = s * per + w;
         cstep = 4;
     }
-    c1 = min(nch, s * per + per);
+    const int c1 = min(nch, s * per + per);
 
-    f4 acc[2][2];
+    f4 acc[T][T];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < T; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    // the deep-ring instantiations need ~120 VGPRs; launches without a long-K product use the
+        for (int j = 0; j < T; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    // the deep-ring instantiations need more VGPRs; launches without a long-K product use the
     // shallow kernel so the large memory-bound products keep their occupancy
 #define TM(a, b)                                                                                            \
-    case (a * 3 + b) * 2 + 0: tile_mma<a, b, 1>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;             \
-    case (a * 3 + b) * 2 + 1: tile_mma<a, b, DEPTH>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;
-    switch ((P.amode * 3 + P.bmode) * 2 + P.deep) {
-        TM(LV, LV) TM(LV, LS) TM(LV, LT) TM(LS, LV) TM(LS, LS) TM(LS, LT) TM(LT, LV) TM(LT, LS) TM(LT, LT)
+    case (a * 4 + b) * 2 + 0: tile_mma<a, b, 1, T>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;          \
+    case (a * 4 + b) * 2 + 1: tile_mma<a, b, DEPTH, T>(P, m0, n0, c0, c1, cstep, lr, lk, acc); break;
+    switch ((P.amode * 4 + P.bmode) * 2 + P.deep) {
+        TM(LV, LV) TM(LV, LS) TM(LV, LT) TM(LV, LW) TM(LS, LV) TM(LS, LS) TM(LS, LT) TM(LS, LW)
+        TM(LT, LV) TM(LT, LS) TM(LT, LT) TM(LT, LW) TM(LW, LV) TM(LW, LS) TM(LW, LT) TM(LW, LW)
     }
 #undef TM
     float *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
     float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
+    // output row / column of element (block, position) of the tile (LW operands permute them)
+    const bool pa = P.amode == LW, pb = P.bmode == LW;
+    auto row_of = [&](int i, int rho) { return pa ? m0 + T * rho + i : m0 + 16 * i + rho; };
+    auto col_of = [&](int j, int c) { return pb ? n0 + T * c + j : n0 + 16 * j + c; };
     if (P.wide) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < T; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < T; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    epilogue(P, C, cx, m0 + i * 16 + lk * 4 + r, n0 + j * 16 + lr, acc[i][j][r]);
+                    epilogue(P, C, cx, row_of(i, lk * 4 + r), col_of(j, lr), acc[i][j][r]);
         return;
     }
-    // reduce the four waves' partial tiles in wave order; wave q finishes quadrant q = (i, j)
-    red[w][0][lane] = acc[0][0];
-    red[w][1][lane] = acc[0][1];
-    red[w][2][lane] = acc[1][0];
-    red[w][3][lane] = acc[1][1];
-    __syncthreads();
-    const f4 v = ((red[0][w][lane] + red[1][w][lane]) + red[2][w][lane]) + red[3][w][lane];
-    const int i = w >> 1, j = w & 1;
+    // reduce the four waves' partial tiles in wave order, four 16x16 blocks per round; in round
+    // r wave q finishes block 4r + q
 #pragma unroll
-    for (int r = 0; r < 4; ++r) epilogue(P, C, cx, m0 + i * 16 + lk * 4 + r, n0 + j * 16 + lr, v[r]);
+    for (int r0 = 0; r0 < T * T; r0 += 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[w][q][lane] = acc[(r0 + q) / T][(r0 + q) % T];
+        __syncthreads();
+        const f4 v = ((red[0][w][lane] + red[1][w][lane]) + red[2][w][lane]) + red[3][w][lane];
+        const int i = (r0 + w) / T, j = (r0 + w) % T;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) epilogue(P, C, cx, row_of(i, lk * 4 + r), col_of(j, lr), v[r]);
+        if (r0 + 4 < T * T) __syncthreads();
+    }
+}
+
+template <int DEPTH>
+__global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
+    __shared__ f4 red[4][4][64];       // [wave][block of the round][lane]
+#ifdef AAC_DBG_EMPTY                   // timing probes only: the launch floor of this grid
+    if (g.n > 0) return;
+#endif
+    const int wg = blockIdx.x;
+    int pi = 0;
+    while (pi + 1 < g.n && wg >= g.p[pi + 1].w_begin) ++pi;
+    const GProb &P = g.p[pi];
+    gemm_tile<2, DEPTH>(P, wg - P.w_begin, red);
 }
 
 // ------------------------------------------------------------------------------ optimiser
@@ -719,9 +768,11 @@ int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
     return v ? atoi(v) : dflt;
 }
-const int g_depth = env_int("AAC_GEMM_DEPTH", 2);
+const int g_depth = std::min(2, std::max(1, env_int("AAC_GEMM_DEPTH", 2)));
 const int g_deep_tiles = env_int("AAC_GEMM_DEEP_TILES", 1024);
 const int g_wide_tiles = env_int("AAC_GEMM_WIDE_TILES", 2048);
+const int g_lw = env_int("AAC_GEMM_LW", 1);                  // row-contiguous operands by 4T-B loads
+int g_dump = env_int("AAC_GEMM_DUMP", 0);      // print the plans of the first g_dump launches
 
 int plan(const aac_gemm_prob *in, int n, GBatch &g) {
     if (n < 1 || n > AAC_GEMM_MAX) return ffail("gemm_batch: 1 <= n <= AAC_GEMM_MAX");
@@ -747,12 +798,21 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         d.lda = s.lda; d.ldb = s.ldb; d.ldc = s.ldc; d.ldadd = s.ldadd; d.ldmask = s.ldmask;
         d.ta = s.ta; d.tb = s.tb; d.act = s.act; d.mact = s.mact; d.ones = s.ones;
         d.ks = ks;
-        // op(A) rows (m) are K-contiguous unless ta; op(B) rows (n) are K-contiguous iff tb
-        d.amode = s.ta ? LT : (s.lda % 4 == 0 && s.K % 4 == 0 && aligned16(s.A) ? LV : LS);
-        d.bmode = !s.tb ? LT : (!s.ones && s.ldb % 4 == 0 && s.K % 4 == 0 && aligned16(s.B) ? LV : LS);
+        // 32x32 wave tiles (T = 2 blocks of 16 per edge); 64x64 ones measured slower on every
+        // learner launch (fewer waves per SIMD to hide the load latency)
+        constexpr int T = 2;
+        // op(A) rows (m) are K-contiguous unless ta; op(B) rows (n) are K-contiguous iff tb; a
+        // row-contiguous operand is read T rows per lane (LW) where its shape allows
+        auto lw_ok = [&](const float *X, int ld, int rows) {
+            return g_lw && ld % T == 0 && rows % T == 0 && (reinterpret_cast<uintptr_t>(X) & (4 * T - 1)) == 0;
+        };
+        d.amode = s.ta ? (lw_ok(s.A, s.lda, s.M) ? LW : LT)
+                       : (s.lda % 4 == 0 && s.K % 4 == 0 && aligned16(s.A) ? LV : LS);
+        d.bmode = !s.tb ? (lw_ok(s.B, s.ldb, s.N - s.ones) ? LW : LT)
+                        : (!s.ones && s.ldb % 4 == 0 && s.K % 4 == 0 && aligned16(s.B) ? LV : LS);
         const int tm = (s.M + WT - 1) / WT, tn = (s.N + WT - 1) / WT;
         d.tiles_n = tn;
-        // large products (>= 2048 tiles) need no K cut inside a workgroup: one tile per wave
+        // large products need no K cut inside a workgroup: one tile per wave
         d.wide = ks == 1 && tm * tn >= g_wide_tiles;
         {
             const int nch = (s.K + KC - 1) / KC;
@@ -766,6 +826,16 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
     }
     g.waves = waves;
+    if (g_dump > 0) {
+        --g_dump;
+        fprintf(stderr, "gemm_batch n=%d wg=%d\n", n, waves);
+        for (int i = 0; i < n; ++i) {
+            const GProb &d = g.p[i];
+            fprintf(stderr, "  M=%d N=%d K=%d ta=%d tb=%d ones=%d ks=%d amode=%d bmode=%d wide=%d deep=%d act=%d mact=%d add=%d\n",
+                    d.M, d.N, d.K, d.ta, d.tb, d.ones, d.ks, d.amode, d.bmode, d.wide, d.deep, d.act, d.mact,
+                    d.addend != nullptr);
+        }
+    }
     return 0;
 }
 
@@ -782,10 +852,8 @@ int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
     for (int i = 0; i < g.n; ++i) deep |= g.p[i].deep != 0;
     const dim3 grid(g.waves), block(256);
     hipStream_t st = (hipStream_t)stream;
-    if (!deep) hipLaunchKernelGGL(gemm_kernel<1>, grid, block, 0, st, g);
-    else if (g_depth == 2) hipLaunchKernelGGL(gemm_kernel<2>, grid, block, 0, st, g);
-    else if (g_depth == 3) hipLaunchKernelGGL(gemm_kernel<3>, grid, block, 0, st, g);
-    else hipLaunchKernelGGL(gemm_kernel<4>, grid, block, 0, st, g);
+    if (deep && g_depth == 2) hipLaunchKernelGGL(gemm_kernel<2>, grid, block, 0, st, g);
+    else hipLaunchKernelGGL(gemm_kernel<1>, grid, block, 0, st, g);
     FHIP(hipGetLastError());
     return 0;
 }
