@@ -10,6 +10,11 @@ value = E_total * N * steps / max-over-ranks wall time.  Inputs are synthetic (s
 bank, random-init networks); the replay is pre-filled to 1e5 transitions before timing.
 
 python bench.py [--gpus N] [--steps K] [--warmup W]        (N > 1: launched by torch.distributed.run)
+
+``--model gru`` measures config 4 instead (randomOD_gru_radar): the
+same vectorised loop with the GRU-actor MADDPG of MADDPG_ownENV_randomOD_Wgru_radar (one GRU actor
+and one GRU critic per agent, hidden states carried per agent, zeroed when an episode ends, and
+stored in the replay), 8 agents, B = 512 (its argparse default).  The default line is config 3.
 """
 import argparse
 import json
@@ -25,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 5 agents×4096 envs"
+METRIC_GRU = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 8 agents×4096 envs, GRU actor"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3
 
@@ -42,15 +48,32 @@ def update_flops(N, D0, B):
     return 2.0 * (4 * A + 7 * C) * B * N
 
 
+def run_timed(ops):
+    """Run a launch list eagerly with a HIP event pair around every grouped-GEMM launch (on the
+    launching stream); [(algorithmic FLOPs, event pair)]."""
+    from multi_agent_aac_amd.fused import GemmLaunch
+    rec = []
+    for op in ops:
+        if isinstance(op, GemmLaunch):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            op()
+            e1.record()
+            rec.append((op.flops, e0, e1))
+        else:
+            op()
+    return rec
+
+
 def gemm_roofline(model, B, updates=4):
     """Roofline of the dominant kernel, the grouped fp32 MFMA GEMM (gemm_kernel) of the fused
     learner: algorithmic FLOPs of each launch / its HIP-event duration, over ``updates`` eager
     update_myown-equivalents run right after the timed region (same launches as the captured
     graph; the rocprof kernel stats under profiles/ give the same per-launch durations)."""
-    fu = model._fused_plan(B)
+    fu = model._fused_plan(B) if hasattr(model, "_fused_plan") else model._plan(B)
     rec = []
     for _ in range(updates):
-        rec += fu.run_timed()
+        rec += run_timed(fu.ops())
     torch.cuda.synchronize()
     flops = sum(r[0] for r in rec)
     ms = sum(r[1].elapsed_time(r[2]) for r in rec)
@@ -65,11 +88,13 @@ def gemm_roofline(model, B, updates=4):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--model", default="att", choices=["att", "gru"],
+                   help="att: config 3 (default); gru: config 4, GRU actor (defaults 8 agents, B=512)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    p.add_argument("--agents", type=int, default=5)
-    p.add_argument("--batch", type=int, default=1024)
+    p.add_argument("--agents", type=int, default=None, help="default 5 (att) / 8 (gru)")
+    p.add_argument("--batch", type=int, default=None, help="default 1024 (att) / 512 (gru)")
     p.add_argument("--memory", type=int, default=100000)
     p.add_argument("--radar", default="combined", choices=["drones", "obstacles", "combined"])
     p.add_argument("--no-graph", action="store_true")
@@ -79,7 +104,12 @@ def parse():
     p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "env_step_pmc.json"))
     p.add_argument("--gemm-traffic", default=os.path.join(ROOT, "profiles", "gemm_pmc.json"))
-    return p.parse_args()
+    a = p.parse_args()
+    if a.agents is None:
+        a.agents = 8 if a.model == "gru" else 5
+    if a.batch is None:
+        a.batch = 512 if a.model == "gru" else 1024
+    return a
 
 
 def setup_dist(backend):
@@ -97,18 +127,26 @@ def barrier(ws):
 class Trainer:
     """Vectorised ma_main loop on one GPU (shared by bench.py and the examples)."""
 
-    def __init__(self, E, N, B, memory, radar, seed, pg=None):
+    def __init__(self, E, N, B, memory, radar, seed, pg=None, model="att"):
         from multi_agent_aac_amd import world
         from multi_agent_aac_amd.env import BatchedEnv
         from multi_agent_aac_amd.maddpg import MADDPG
         self.E, self.N, self.B = E, N, B
+        self.gru = model == "gru"
         self.occ = world.synthetic_map(2026)
         self.bank = world.ODBank(self.occ, n_pairs=65536, seed=2026 + seed, max_wp=32)
         self.env = BatchedEnv(E, N, self.occ, radar_mode=radar, max_wp=32)
         self.env.set_od_bank(self.bank, seed=1234 + seed)
         D0 = 6 + 4 * (N - 1)
-        self.model = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, seed=777, batch_size=B,
-                            memory_length=memory, process_group=pg)
+        if self.gru:
+            from multi_agent_aac_amd import gru
+            # WGRU/ma_main:380-389: actor_dim = critic_dim = [6, 18, 6], 64 hidden units
+            self.model = gru.MADDPG([6, 18, 6], [6, 18, 6], 2, 64, 10, n_agents=N, seed=777, batch_size=B,
+                                    memory_length=memory, process_group=pg)
+            self.h = torch.zeros(E, N, 64, device="cuda")
+        else:
+            self.model = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, seed=777, batch_size=B,
+                                memory_length=memory, process_group=pg)
         self.model.noise_seed = 99 + seed
         self.replay = self.model.attach_replay(memory, seed=seed)
         self.cur = self.env.alloc_buffers()
@@ -124,7 +162,10 @@ class Trainer:
 
     def step(self, update=True, time_env=False):
         c, n = self.cur, self.nxt
-        act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
+        if self.gru:
+            act, hn = self.model.act(c.own, c.radar, self.h, self.episode, noisy=True)
+        else:
+            act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
         if time_env:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
@@ -133,7 +174,13 @@ class Trainer:
         if time_env:
             ev1.record()
             self.env_events.append((ev0, ev1))
-        self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
+        if self.gru:     # rows keep (cur_hidden, next_hidden) as WGRU/ma_main:636
+            self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, self.h, hn)
+            self.h.copy_(hn)
+            from multi_agent_aac_amd import gru
+            gru.reset_hidden(self.h, n.env_done)     # a new episode starts from zeros (WGRU/ma_main:476-478)
+        else:
+            self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
         self.env.auto_reset(n.env_done, out=n)
         self.episode.add_(n.env_done.to(torch.int32))
         self.cur, self.nxt = n, c
@@ -144,7 +191,7 @@ class Trainer:
 NO_GRAPH = False
 
 
-def cpu_baseline(E, N, B, radar, seconds):
+def cpu_baseline(E, N, B, radar, seconds, model="att"):
     """The C oracle env step + the torch-CPU learner restatement on the host cores (bounded sample)."""
     import multiprocessing as mp
     from oracle import c_oracle, learner_ref  # noqa: F401  (checker / baseline only)
@@ -160,14 +207,25 @@ def cpu_baseline(E, N, B, radar, seconds):
     env_rate = procs * per * N / t_env
     torch.set_num_threads(procs)
     D0 = 6 + 4 * (N - 1)
-    actor, critic = learner_ref.RefActor([D0, 18, 6], 2), learner_ref.RefCritic([D0, 18, 6], N, 2)
-    actor_t, critic_t = learner_ref.RefActor([D0, 18, 6], 2), learner_ref.RefCritic([D0, 18, 6], N, 2)
-    tr = learner_ref.random_transitions(B, N, 0)
-    tr["done"] = tr["done"].float()
+    if model == "gru":
+        from oracle import gru_ref
+        import copy
+        acts = [gru_ref.RefGRUActor([6, 18, 6], 2) for _ in range(N)]
+        crits = [gru_ref.RefGRUCritic([6, 18, 6], 2) for _ in range(N)]
+        acts_t, crits_t = copy.deepcopy(acts), copy.deepcopy(crits)
+        tr = gru_ref.random_gru_transitions(B, N, 0)
+        tr["done"] = tr["done"].float()
+        step = lambda o: gru_ref.ref_gru_update(acts, crits, acts_t, crits_t, tr, 6, opts=o)[1]  # noqa: E731
+    else:
+        actor, critic = learner_ref.RefActor([D0, 18, 6], 2), learner_ref.RefCritic([D0, 18, 6], N, 2)
+        actor_t, critic_t = learner_ref.RefActor([D0, 18, 6], 2), learner_ref.RefCritic([D0, 18, 6], N, 2)
+        tr = learner_ref.random_transitions(B, N, 0)
+        tr["done"] = tr["done"].float()
+        step = lambda o: learner_ref.ref_update(actor, critic, actor_t, critic_t, [tr] * N, opts=o)[1]  # noqa: E731
     t0 = time.perf_counter()
     n_upd, opts = 0, None
     while time.perf_counter() - t0 < budget or n_upd == 0:
-        _, opts = learner_ref.ref_update(actor, critic, actor_t, critic_t, [tr] * N, opts=opts)
+        opts = step(opts)
         n_upd += 1
     t_upd = (time.perf_counter() - t0) / n_upd
     t_iter = t_env * (E / (procs * per)) + t_upd
@@ -237,12 +295,12 @@ def main():
     cpu = None
     if ws0 == 1 and not a.no_cpu_baseline:
         # before any GPU initialisation: the pool's children must not inherit a GPU context
-        cpu = cpu_baseline(a.envs, a.agents, a.batch, a.radar, a.cpu_seconds)
+        cpu = cpu_baseline(a.envs, a.agents, a.batch, a.radar, a.cpu_seconds, model=a.model)
     ws, rank, local = setup_dist(a.backend)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(777 + rank)
     tr = Trainer(a.envs, a.agents, a.batch, a.memory, a.radar, seed=rank,
-                 pg=dist.group.WORLD if ws > 1 else None)
+                 pg=dist.group.WORLD if ws > 1 else None, model=a.model)
     # pre-fill the replay to >= memory transitions (untimed), then capture the update graph
     while len(tr.replay) < a.memory:
         tr.step(update=False)
@@ -275,18 +333,24 @@ def main():
         if t.get("envs") == a.envs and t.get("agents") == N and t.get("radar") == a.radar:
             traffic = t.get("hbm_bytes_per_launch")
             tsrc = os.path.relpath(a.traffic, ROOT)
-    upd_fl = update_flops(N, D0, a.batch)
+    if tr.gru:      # algorithmic GEMM FLOPs of the plan's launches (2 M N K per product)
+        from multi_agent_aac_amd.fused import GemmLaunch
+        upd_fl = sum(op.flops for op in tr.model._plan(a.batch).ops() if isinstance(op, GemmLaunch))
+        workload = f"randomOD_gru_radar: {N} agents x {a.envs} envs/GPU, GRU actor, B={a.batch} MADDPG update, " \
+                   f"{a.radar} radar"
+    else:
+        upd_fl = update_flops(N, D0, a.batch)
+        workload = f"one_model_att: {N} agents x {a.envs} envs/GPU, B={a.batch} MADDPG update, {a.radar} radar"
     out = {
-        "metric": METRIC, "value": value, "unit": "agent-env-steps/s", "n_gpus": ws, "steps": a.steps,
+        "metric": METRIC_GRU if tr.gru else METRIC, "value": value, "unit": "agent-env-steps/s", "n_gpus": ws, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64 env state / f32 obs+learner", "data": "synthetic",
-        "config": {"workload": f"one_model_att: {N} agents x {a.envs} envs/GPU, B={a.batch} MADDPG update, "
-                               f"{a.radar} radar", "envs_per_gpu": a.envs, "envs_total": E_total, "agents": N,
+        "config": {"workload": workload, "envs_per_gpu": a.envs, "envs_total": E_total, "agents": N,
                    "batch": a.batch, "replay": a.memory, "radar": a.radar,
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
                    "update_graph": (not a.no_graph) and (ws == 1 or tr.model.fused),
                    "graph_segments": "one per update" if ws == 1 else "cut at each gradient all-reduce"},
-        "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * N,
+        "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if tr.gru else N),
         "env_roofline": {"kernel": "step_kernel (fused env step)", "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": tsrc, "bytes_per_agent_step": bpa, "agents_per_launch": a.envs * N,
@@ -295,13 +359,14 @@ def main():
                             "achieved": upd_fl * upd_per_s / 1e12, "peak": FP32_PEAK_TFLOPS,
                             "frac": upd_fl * upd_per_s / 1e12 / FP32_PEAK_TFLOPS, "note": "whole-step rate bound"},
     }
-    if tr.model.fused:
+    if tr.gru or tr.model.fused:
         rf = gemm_roofline(tr.model, a.batch)
         rf["traffic"] = None
         if a.gemm_traffic and os.path.exists(a.gemm_traffic):
             with open(a.gemm_traffic) as f:
                 t = json.load(f)
-            if t.get("envs") == a.envs and t.get("agents") == N and t.get("batch") == a.batch:
+            if t.get("envs") == a.envs and t.get("agents") == N and t.get("batch") == a.batch and \
+                    t.get("model", "att") == a.model:
                 rf["traffic"] = t.get("hbm_bytes_per_launch")
                 rf["traffic_source"] = os.path.relpath(a.gemm_traffic, ROOT)
         out["roofline"] = rf

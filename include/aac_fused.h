@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AAC_GEMM_MAX 12
+#define AAC_GEMM_MAX 16
 
 /* C[M][N] (row-major, ldc) = epilogue(op(A)[M][K] . op(B)[K][N]).
  * op(A)[m][k] = ta ? A[k*lda + m] : A[m*lda + k];  op(B)[k][n] = tb ? B[n*ldb + k] : B[k*ldb + n].

@@ -73,9 +73,11 @@ int aac_act_bgrad(const float *gy, int32_t gy_stride, const float *y, int32_t y_
 int aac_bias_act(float *y, const float *b, int64_t M, int32_t O, int32_t act, void *stream);
 
 /* act [E*N][2] += (float)(randn * var_e); clamp to [-1, 1]; var_e from episode[e] (device):
- * var = noise_start + ((0 - noise_start)/(eps_end - 1)) * (ep - 1) if ep <= eps_end else 0. */
+ * var = noise_start + ((noise_end - noise_start)/(eps_end - 1)) * (ep - 1) if ep <= eps_end else
+ * noise_end (get_custom_linear_scaling_factor: end_scale 0 in ATT/maddpg:563-570, 0.03 in
+ * MADDPG_ownENV_randomOD_Wgru_radar/maddpg_agent_randomOD_Wgru_radar.py:432-439). */
 int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, int32_t eps_end, float noise_start,
-                    uint64_t seed, uint64_t *counter, float *noise_out, void *stream);
+                    float noise_end, uint64_t seed, uint64_t *counter, float *noise_out, void *stream);
 
 #ifdef __cplusplus
 }

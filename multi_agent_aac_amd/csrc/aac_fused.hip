@@ -23,6 +23,7 @@
 #include <string>
 
 #include "../../include/aac_fused.h"
+#include "aac_wave.h"
 
 namespace {
 
@@ -348,22 +349,8 @@ __global__ void sum_partials_kernel(float *out, const float *gpart, int ns, int6
 }
 
 // ------------------------------------------------------------------------------ critic head
-// wave-wide sum by DPP (rocPRIM's gfx9 pattern): xor 1, xor 2, row_ror 4, row_ror 8 leave each
-// row's sum in every lane of the row, row_bcast 15 / 31 fold the rows into lane 63, which is
-// broadcast with readlane.  No LDS round trips (ds_swizzle / bpermute) in the chain.
-#define DPP_STEP(x, ctrl)                                                                                  \
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), ctrl, 0xf, 0xf, \
-                                                               false))
-__device__ __forceinline__ float wsum(float x) {
-    DPP_STEP(x, 0xb1);   // quad_perm [1,0,3,2]
-    DPP_STEP(x, 0x4e);   // quad_perm [2,3,0,1]
-    DPP_STEP(x, 0x124);  // row_ror:4
-    DPP_STEP(x, 0x128);  // row_ror:8
-    DPP_STEP(x, 0x142);  // row_bcast:15
-    DPP_STEP(x, 0x143);  // row_bcast:31
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
-}
-#undef DPP_STEP
+using aacw::wsum;
+
 
 __global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, int ldh, int M,
                                                    const float *__restrict__ w, const float *__restrict__ b, int mode,

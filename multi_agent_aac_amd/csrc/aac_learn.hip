@@ -173,7 +173,9 @@ __global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B
     int32_t *out = out_all + (size_t)blockIdx.x * B;   // one workgroup per batch
     __shared__ int keys[TBL];
     __shared__ int owner[TBL];
-    const int64_t size = meta[1];
+    // an empty ring still yields in-range rows (row 0): the host refuses to sample fewer rows than
+    // B (DeviceReplay.sample_batch / the learners' plans), this only keeps a bad call in bounds
+    const int64_t size = meta[1] > 0 ? meta[1] : 1;
     const uint64_t ctr = *counter;
     const int nv = (B + 1023) / 1024;
     int val[4], att[4];
@@ -337,7 +339,7 @@ __global__ void bias_act_kernel(float *y, const float *__restrict__ b, int64_t n
 
 // ------------------------------------------------------------------------------ noise
 __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, int eps_end, float noise_start,
-                             uint64_t seed, uint64_t *counter, float *noise_out) {
+                             float noise_end, uint64_t seed, uint64_t *counter, float *noise_out) {
     const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t ctr = *counter;
     if (row < (int64_t)E * N) {
@@ -345,10 +347,10 @@ __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, i
         const int ep = episode ? episode[e] : 1;
         double var;
         if (ep <= eps_end) {
-            const double slope = (0.0 - (double)noise_start) / (double)(eps_end - 1);
+            const double slope = ((double)noise_end - (double)noise_start) / (double)(eps_end - 1);
             var = (double)noise_start + slope * (double)(ep - 1);
         } else {
-            var = 0.0;
+            var = (double)noise_end;
         }
         const uint64_t h1 = mix64(mix64(mix64(seed) ^ ctr) ^ (uint64_t)(2 * row));
         const uint64_t h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
@@ -515,10 +517,11 @@ int aac_bias_act(float *y, const float *b, int64_t M, int32_t O, int32_t act, vo
 }
 
 int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, int32_t eps_end, float noise_start,
-                    uint64_t seed, uint64_t *counter, float *noise_out, void *stream) {
+                    float noise_end, uint64_t seed, uint64_t *counter, float *noise_out, void *stream) {
     const int64_t rows = (int64_t)E * N;
     hipLaunchKernelGGL(noise_kernel, dim3((unsigned)((rows + LEARN_BLOCK - 1) / LEARN_BLOCK)), dim3(LEARN_BLOCK), 0,
-                       (hipStream_t)stream, act, E, N, episode, eps_end, noise_start, seed, counter, noise_out);
+                       (hipStream_t)stream, act, E, N, episode, eps_end, noise_start, noise_end, seed, counter,
+                       noise_out);
     hipLaunchKernelGGL(counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
     LHIP(hipGetLastError());
     return 0;

@@ -43,7 +43,7 @@ class GemmProb(ctypes.Structure):
                 ("ksplit", i32)]
 
 
-GEMM_MAX = 8
+GEMM_MAX = 16
 _L = None
 
 

@@ -160,19 +160,22 @@ class MADDPG:
         self.actor_optimizer.step()
         return loss_q.detach(), loss_a.detach(), q.detach(), target
 
-    def _fused_plan(self, B):
-        rep = self.replay if self.replay is not None else self.memory.dev
+    def _fused_plan(self, B, rep=None):
+        if rep is None:
+            rep = self.replay if self.replay is not None else self.memory.dev
         key = (B, id(rep))
         if key not in self._fplans:
             self._fplans[key] = fused.FusedUpdate(self, rep, B)
         return self._fplans[key]
 
-    def _update_core(self, B, idx_list=None):
-        rep = self.replay if self.replay is not None else self.memory.dev
+    def _update_core(self, B, idx_list=None, rep=None):
+        if rep is None:
+            rep = self.replay if self.replay is not None else self.memory.dev
         N = self.n_agents
         idx = None if idx_list is None else torch.cat([i.reshape(-1) for i in idx_list])
         if self.fused:
-            fu = self._fused_plan(B)
+            rep.check_sample(B)
+            fu = self._fused_plan(B, rep)
             fu.run(idx)
             return fu
         ball = rep.sample_batch(B, idx, nb=N)           # N independent batches, one launch each
@@ -239,12 +242,17 @@ class MADDPG:
         else:
             self._graph.replay()
 
-    def update(self, B=None, use_graph=True, idx_list=None, want_stats=True):
+    def update(self, B=None, use_graph=True, idx_list=None, want_stats=True, replay=None):
         """One update_myown-equivalent on the device replay (no host synchronisation).  Returns
         [(loss_q, loss_a, q, target)] per iteration (computed on demand: ``want_stats=False``
-        launches nothing beyond the update itself)."""
+        launches nothing beyond the update itself).  ``replay`` defaults to the attached batched
+        replay, else the reference-API memory."""
         B = B or self.batch_size
+        if replay is not None:
+            self._last_src = self._update_core(B, idx_list, replay)
+            return self.last_stats if want_stats else None
         if idx_list is None and use_graph and (self.world == 1 or self.fused):
+            (self.replay if self.replay is not None else self.memory.dev).check_sample(B)
             if self._graph is None or self._graph_B != B:
                 self.capture(B)
             self._replay()
@@ -294,7 +302,7 @@ class MADDPG:
             return None, None, single_eps_critic_cal_record
         if i_episode % UPDATE_EVERY != 0:
             raise NotImplementedError("soft update every call (UPDATE_EVERY=1) as ATT/params:29")
-        stats = self.update(self.batch_size, use_graph=False)
+        stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev)
         c_loss = [s[0] for s in stats]
         a_loss = [s[1] for s in stats]
         for s in stats:

@@ -30,7 +30,7 @@ def lib():
         L.aac_replay_gather.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp]
         L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
         L.aac_polyak_flat.argtypes = [vp, vp, i64, f32, vp]
-        L.aac_noise_clamp.argtypes = [vp, i32, i32, vp, i32, f32, u64, vp, vp, vp]
+        L.aac_noise_clamp.argtypes = [vp, i32, i32, vp, i32, f32, f32, u64, vp, vp, vp]
         L.aac_act_bgrad.argtypes = [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, vp]
         L.aac_bias_act.argtypes = [vp, vp, i64, i32, i32, vp]
         _L = L
@@ -123,9 +123,9 @@ def polyak_flat(target, source, tau):
     _chk(lib().aac_polyak_flat(_p(target), _p(source), target.numel(), tau, _s()), "aac_polyak_flat")
 
 
-def noise_clamp(act, episode, eps_end, noise_start, seed, counter, noise_out=None):
+def noise_clamp(act, episode, eps_end, noise_start, seed, counter, noise_out=None, noise_end=0.0):
     E, N = act.shape[0], act.shape[1]
-    _chk(lib().aac_noise_clamp(_p(act), E, N, _p(episode), eps_end, noise_start, u64(seed), _p(counter),
+    _chk(lib().aac_noise_clamp(_p(act), E, N, _p(episode), eps_end, noise_start, noise_end, u64(seed), _p(counter),
                                _p(noise_out), _s()), "aac_noise_clamp")
 
 

@@ -7,6 +7,7 @@ import os
 from fractions import Fraction
 
 import numpy as np
+import torch
 import pytest
 
 from oracle import c_oracle, env_ref, geos, world_ref
@@ -253,3 +254,51 @@ def test_map_fixture(occ):
     assert np.array_equal(world.synthetic_map(2026), occ)
     pools = world.target_pools(occ)
     assert [len(p) for p in pools] == [len(p) for p in world_ref.target_pools(occ)]
+
+
+def test_gru_oracle_cell_and_update_cpu():
+    """The GRU-actor restatement (oracle/gru_ref.py): GRUCell gates in torch's order and one
+    update of all agents runs; the per-agent loop equals the reference's (WGRU/maddpg:242-310)."""
+    from oracle import gru_ref
+    torch.manual_seed(0)
+    a = gru_ref.RefGRUActor([6, 18, 6], 2)
+    x, h = torch.randn(5, 128), torch.randn(5, 64)
+    c = a.gru_cell
+    gi, gh = x @ c.weight_ih.t() + c.bias_ih, h @ c.weight_hh.t() + c.bias_hh
+    r = torch.sigmoid(gi[:, :64] + gh[:, :64])
+    z = torch.sigmoid(gi[:, 64:128] + gh[:, 64:128])
+    n = torch.tanh(gi[:, 128:] + r * gh[:, 128:])
+    torch.testing.assert_close(c(x, h), (h - n) * z + n, atol=1e-6, rtol=1e-6)
+    N, B = 2, 16
+    tr = gru_ref.random_gru_transitions(B, N, 1)
+    tr["done"] = tr["done"].float()
+    acts = [gru_ref.RefGRUActor([6, 18, 6], 2) for _ in range(N)]
+    crits = [gru_ref.RefGRUCritic([6, 18, 6], 2) for _ in range(N)]
+    import copy
+    at, ct = copy.deepcopy(acts), copy.deepcopy(crits)
+    before = [p.clone() for p in acts[0].parameters()]
+    stats, _ = gru_ref.ref_gru_update(acts, crits, at, ct, tr, 6)
+    assert len(stats) == N and all(np.isfinite(s[0]) for s in stats)
+    assert any(not torch.equal(p, q) for p, q in zip(before, acts[0].parameters()))
+
+
+def test_mpe_oracle_cpu():
+    """The simple_spread restatement (oracle/mpe_ref.py): contact forces are equal and opposite
+    (momentum changes only by the action forces), every agent's reward includes its own
+    'collision' (-1), the float32 action scaling, and the observation layout."""
+    from oracle import mpe_ref
+    rng = np.random.default_rng(0)
+    pos, vel, lmk = rng.uniform(-1, 1, (3, 2)), rng.normal(0, 1, (3, 2)), rng.uniform(-1, 1, (3, 2))
+    pos[1] = pos[0] + [0.2, 0.0]            # in contact
+    act = rng.uniform(-1, 1, (3, 2)).astype(np.float32)
+    p2, v2 = mpe_ref.step(pos, vel, lmk, act)
+    u5 = (act * np.float32(5)).astype(np.float64)
+    np.testing.assert_allclose((v2 - vel * 0.75).sum(0), u5.sum(0) * 0.1, atol=1e-12)
+    r = mpe_ref.reward(p2, lmk)
+    assert np.all(r <= -1.0)
+    far = np.array([[5.0, 5.0], [-5.0, 5.0], [0.0, -5.0]])
+    assert np.allclose(mpe_ref.reward(far, far) , -1.0)      # landmarks on the agents, no contact
+    o = mpe_ref.observe(p2, v2, lmk)
+    assert o.shape == (3, 18)
+    np.testing.assert_allclose(o[1, 10:12], p2[0] - p2[1])
+    assert np.all(o[:, 14:] == 0)
