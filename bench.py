@@ -349,7 +349,7 @@ def main():
                    "batch": a.batch, "replay": a.memory, "radar": a.radar,
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
                    "update_graph": (not a.no_graph) and (ws == 1 or tr.model.fused),
-                   "graph_segments": "one per update" if ws == 1 else "cut at each gradient all-reduce"},
+                   "graph_segments": "one per update" if ws == 1 else "cut at each of the N+1 gradient all-reduces"},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if tr.gru else N),
         "env_roofline": {"kernel": "step_kernel (fused env step)", "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

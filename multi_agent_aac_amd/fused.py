@@ -348,6 +348,11 @@ class FusedUpdate:
         self.f_t, self.h_t = z(Bt, 128 * N), z(Bt, 256)
         self.f, self.h = z(B, 128 * N), z(B, 256)
         self.dq, self.dh, self.df = z(B), z(B, 256), z(B, 128 * N)
+        # critic-step activation sets [f, h, dq, dh, df]: [0] is shared with the actor step; world > 1
+        # runs the critic step of iteration i+1 beside the actor step of i, in set [1]
+        self.cbuf = [(self.f, self.h, self.dq, self.dh, self.df)]
+        if model.world > 1:
+            self.cbuf.append((z(B, 128 * N), z(B, 256), z(B), z(B, 256), z(B, 128 * N)))
         R = B * N
         self.dout, self.dha = z(R, 2), z(R, 256)
         self.dcat_o, self.dcat_g, self.dv = z(R, 64), z(R, 64), z(R, 64)
@@ -378,7 +383,14 @@ class FusedUpdate:
         self.pre += critic_forward(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
         self.pre.append(lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),
                                             done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y)))
-        self.iters = [self._iteration(i, A, C) for i in range(N)]
+        if m.world > 1:
+            self.iters = self._pipelined(A, C)
+        else:
+            self.iters = [self._critic_step(i, A, C, self.cbuf[0], fuse_actor_fwd=True)
+                          + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, i + 1)
+                          + self._actor_step(i, A, C)
+                          + self._adam(m.actor_optimizer, m.fa, self.ga, self.SPLIT_ACTOR, i + 1)
+                          for i in range(N)]
         self.post = [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau),
                      lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau),
                      lambda: m.critic_optimizer.step_t.add_(N),
@@ -386,35 +398,71 @@ class FusedUpdate:
         self.n_launches = len(self.pre) + sum(len(it) for it in self.iters) + len(self.post)
 
     def _adam(self, opt, flat, gpart, ns, step_add):
-        m = self.m
-        if m.world > 1:     # reduce the partials, all-reduce the gradient, then the plain step
-            return [lambda: sum_partials(flat.grad, gpart, ns), Collective(lambda: m._allreduce(flat)),
-                    lambda: adam_at(opt, step_add)]
+        """world == 1: the Adam step sums the split-K partial copies itself."""
         return [lambda: adam_sum(opt, gpart, ns, step_add, grad_out=flat.grad)]
 
-    def _iteration(self, i, A, C):
-        m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
-        R = B * N
+    def _pipelined(self, A, C):
+        """world > 1: one gradient all-reduce per ``update_myown`` iteration boundary instead of two.
+
+        The critic step of iteration i+1 reads the critic weights after critic Adam step i (and
+        the fixed targets), exactly what the actor step of iteration i reads, and neither reads
+        the other's result: so the two are computed in the same segment (separate activation
+        buffers) and their gradients -- contiguous in the shared gradient buffer
+        (MADDPG._share_grads) -- are averaged by ONE collective.  N + 1 all-reduces per update
+        (6 at N = 5) instead of 2N; the arithmetic of every product is unchanged, so the result
+        is bit-identical to the per-step order (tests/test_parallel_gpu.py)."""
+        m, N = self.m, self.N
         SA, SC = self.SPLIT_ACTOR, self.SPLIT_CRITIC
-        nA, nC = m.fa.numel, m.fc.numel
-        gA = ActorParams(m.actors, m.fa, self.ga.data_ptr())
+        copt, aopt = m.critic_optimizer, m.actor_optimizer
+        red_c = lambda: sum_partials(m.fc.grad, self.gc, SC)      # noqa: E731
+        red_a = lambda: sum_partials(m.fa.grad, self.ga, SA)      # noqa: E731
+        L = self._critic_step(0, A, C, self.cbuf[0], fuse_actor_fwd=False)
+        L += [red_c, Collective(lambda: m._allreduce_grads(critic=True, actor=False)), lambda: adam_at(copt, 1)]
+        segs = [L]
+        for i in range(N):
+            L = self._actor_fwd_launches(i, A) + self._actor_step(i, A, C)
+            if i + 1 < N:
+                L += self._critic_step(i + 1, A, C, self.cbuf[1], fuse_actor_fwd=False)
+                L += [red_a, red_c, Collective(lambda: m._allreduce_grads(critic=True, actor=True)),
+                      lambda i=i: adam_at(copt, i + 2), lambda i=i: adam_at(aopt, i + 1)]
+            else:
+                L += [red_a, Collective(lambda: m._allreduce_grads(critic=False, actor=True)),
+                      lambda i=i: adam_at(aopt, i + 1)]
+            segs.append(L)
+        return segs
+
+    def _batch_ptrs(self, i):
+        B, N, D0, K, Din = self.B, self.N, self.D0, self.K, self.Din
+        return (ptr(self.X, i * B * N * Din), ptr(self.X2, i * B * N * Din), ptr(self.radar, i * B * N * 18),
+                ptr(self.nei, i * B * N * K * 6), ptr(self.y, i * B))
+
+    def _actor_fwd_stages(self, i, A):
+        B, N, D0, K, Din = self.B, self.N, self.D0, self.K, self.Din
+        _, X2, radar, nei, _ = self._batch_ptrs(i)
+        return actor_forward_stages(A, self.acts, X2, Din, radar, nei, B * N, K, D0, X2 + 4 * D0, Din)
+
+    def _actor_fwd_launches(self, i, A):
+        a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+        return gemm_launches(a_enc) + [a_attn] + gemm_launches(a_merge) + gemm_launches(a_out)
+
+    def _critic_step(self, i, A, C, cb, fuse_actor_fwd):
+        """Critic step of iteration i (ATT/maddpg:375-387) up to its weight-gradient partials.
+        With ``fuse_actor_fwd`` the actor forward of the same iteration (ATT/maddpg:389-392) --
+        which depends only on the actor weights, changed after the critic step -- shares the
+        critic step's launches; the policy actions land in X2 (own columns gathered there too)."""
+        m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
+        SC, nC = self.SPLIT_CRITIC, m.fc.numel
         gC = CriticParams(m.critics, m.fc, self.gc.data_ptr())
-        X = ptr(self.X, i * B * N * Din)
-        X2 = ptr(self.X2, i * B * N * Din)
-        radar = ptr(self.radar, i * B * N * 18)
-        nei = ptr(self.nei, i * B * N * K * 6)
-        y = ptr(self.y, i * B)
-        f, h, dq, dh, df = self.f, self.h, self.dq, self.dh, self.df
-        c = self.acts
-        L = []
-        # The actor forward of this iteration (ATT/maddpg:389-392) depends only on the actor
-        # weights, which change after the critic step, so its products share the critic step's
-        # launches; the policy actions land in X2 (own columns gathered there too).
-        a_enc, a_attn, a_merge, a_out = actor_forward_stages(A, c, X2, Din, radar, nei, R, K, D0, X2 + 4 * D0, Din)
+        X, _, _, _, y = self._batch_ptrs(i)
+        f, h, dq, dh, df = cb
+        if fuse_actor_fwd:
+            a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+        else:
+            a_enc, a_attn, a_merge, a_out = [], None, [], []
         c_enc, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
-        # ---------------- critic step (ATT/maddpg:375-387)
-        L += gemm_launches(c_enc + a_enc)
-        L.append(a_attn)
+        L = gemm_launches(c_enc + a_enc)
+        if a_attn is not None:
+            L.append(a_attn)
         L += gemm_launches(c_comb)
         L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh)))
         L += gemm_launches([
@@ -427,10 +475,19 @@ class FusedUpdate:
         L += gemm_launches([prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din,
                                  Din, ta=1, ones=1, cextra=gC.enc_b[n], ksplit=SC, split_stride=nC)
                             for n in range(N)] + a_out)
-        L += self._adam(m.critic_optimizer, m.fc, self.gc, SC, i + 1)
-        # ---------------- actor step (ATT/maddpg:389-425): critic on the policy actions
-        X = X2
-        L += critic_forward(C, X, B, N, Din, f, h)
+        return L
+
+    def _actor_step(self, i, A, C):
+        """Actor step of iteration i (ATT/maddpg:389-425) after its forward, up to the weight-
+        gradient partials: critic on the policy actions, backward into the actor."""
+        m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
+        R = B * N
+        SA, nA = self.SPLIT_ACTOR, m.fa.numel
+        gA = ActorParams(m.actors, m.fa, self.ga.data_ptr())
+        _, X, radar, nei, _ = self._batch_ptrs(i)
+        f, h, dq, dh, df = self.cbuf[0]
+        c = self.acts
+        L = critic_forward(C, X, B, N, Din, f, h)
         L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 1, q=ptr(self.q_a, i * B), dh=ptr(dh)))
         L += gemm_launches([prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f),
                                  ldmask=128 * N, mact=RELU)])
@@ -460,7 +517,6 @@ class FusedUpdate:
                  split_stride=nA),
             prob(ptr(self.dcat_g), radar, gA.Wg, 64, 18, R, 64, 18, 18, ta=1, ones=1, cextra=gA.bg, ksplit=SA,
                  split_stride=nA)])
-        L += self._adam(m.actor_optimizer, m.fa, self.ga, SA, i + 1)
         return L
 
     # ------------------------------------------------------------------ run

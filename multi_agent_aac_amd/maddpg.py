@@ -100,6 +100,9 @@ class MADDPG:
         self.noise_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.grads = None
+        if self.world > 1:
+            self._share_grads()
         self._graph = None
         self._graph_B = None
         self.steps_done = 0
@@ -128,6 +131,22 @@ class MADDPG:
     def _allreduce(self, flat):
         if self.world > 1:
             parallel.allreduce_mean_(flat.grad, self.pg)
+
+    def _share_grads(self):
+        """world > 1: the critic's and the actor's flat gradients become the two halves of one
+        buffer [critic | actor], so the fused learner averages both with one collective."""
+        nc, na = self.fc.numel, self.fa.numel
+        self.grads = torch.zeros(nc + na, dtype=torch.float32, device=self.device)
+        for flat, g in ((self.fc, self.grads[:nc]), (self.fa, self.grads[nc:])):
+            flat.grad = g
+            for p, off, k in flat.slices:
+                p.grad = g[off:off + k].view_as(p)
+
+    def _allreduce_grads(self, critic, actor):
+        """Mean over the ranks of the critic and / or actor gradient (one collective)."""
+        nc = self.fc.numel
+        t = self.grads if (critic and actor) else (self.grads[:nc] if critic else self.grads[nc:])
+        parallel.allreduce_mean_(t, self.pg)
 
     def _targets(self, b, B):
         """y for all N iterations at once.  The target networks only change in the Polyak step

@@ -1,5 +1,5 @@
 """Two ranks on the one GPU of the test box (gloo backend, world_size 2): the multi-rank fused
-update -- one captured graph per segment between the gradient all-reduces -- must give exactly
+update -- one captured graph per segment between the gradient all-reduces, the critic step of iteration i+1 beside the actor step of i -- must give exactly
 the single-process result when both ranks hold the same data (the mean of two identical
 gradients is the gradient)."""
 import os
@@ -69,5 +69,5 @@ def test_segmented_graph_update_two_ranks(native_lib):
         assert p.exitcode == 0
     for r in range(2):
         res = out[r]
-        assert res["segmented"] and res["n_segments"] == 11       # 2 all-reduces per iteration, N = 5
+        assert res["segmented"] and res["n_segments"] == 7        # N + 1 all-reduces per update, N = 5
         assert res["actor_equal"] and res["critic_equal"] and res["target_equal"], res
