@@ -21,25 +21,12 @@
 #include <string>
 
 #include "../../include/aac_env.h"
+#include "aac_geom.h"
 
-#define NRAY 18
 #define BLOCK 256
 #define MAX_MAP_BYTES 8192
 
 namespace {
-
-struct Tab {
-    double circ_c[64], circ_s[64];   // GEOS createCircle unit vectors, angle 0 - i*inc
-    double nrm_c[64], nrm_s[64];     // 64-gon edge normals, angle (k + 1/2) pi/32
-    double ray_c[NRAY], ray_s[NRAY]; // cos/sin(math.radians(20 r))
-    double apothem;                  // cos(pi/64)
-    double quantum;                  // GEOS filletAngleQuantum = pi/2/16
-    double cos_quantum;              // cos(quantum): bound on a fillet arc's reach along an axis
-};
-
-__constant__ Tab c_tab;
-
-constexpr double PI_GEOS = 3.14159265358979323846;
 
 struct Args {
     int E, N, K, D0, W, radar_mode, compat, team_reward, episode_length, gw, gh, n_maps, epb;
@@ -70,99 +57,14 @@ struct ResetArgs {
     int32_t *episode;         // [E] per-env episode counter (bank mode)
 };
 
-__host__ __device__ inline uint64_t mix64(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
+// LineString([p0,p1]).buffer(pB) meets one of the 4 infinite bound lines (ATT/env:2507)
+__device__ inline bool bound_crash(const Args &A, double x0, double y0, double x1, double y1) {
+    return capsule_crash(A.pb, A.bound, x0, y0, x1, y1);
 }
 
-__device__ inline double npnorm(double x, double y) { return sqrt(__builtin_fma(y, y, x * x)); }
-__device__ inline double gdist(double ax, double ay, double bx, double by) {
-    double dx = ax - bx, dy = ay - by;
-    return sqrt(dx * dx + dy * dy);
-}
-
-// ------------------------------------------------------------------ GEOS-shape predicates
-__device__ inline void upd(double x, double y, double &mnx, double &mxx, double &mny, double &mxy) {
-    mnx = x < mnx ? x : mnx;
-    mxx = x > mxx ? x : mxx;
-    mny = y < mny ? y : mny;
-    mxy = y > mxy ? y : mxy;
-}
-
-__device__ void fillet_ext(double px, double py, double start, double end, double r, double &mnx, double &mxx,
-                           double &mny, double &mxy) {
-    double total = fabs(start - end);
-    int nseg = (int)(total / c_tab.quantum + 0.5);
-    double inc = total / nseg;
-    for (int i = 1; i < nseg; ++i) {  // i = 0 is redundant with the offset point (GEOS isRedundant)
-        double a = start + (double)(-1 * i) * inc;
-        upd(px + r * cos(a), py + r * sin(a), mnx, mxx, mny, mxy);
-    }
-}
-
-// LineString([p0,p1]).buffer(r) meets one of the 4 infinite bound lines (ATT/env:2507)
-__device__ bool bound_crash(const Args &A, double x0, double y0, double x1, double y1) {
-    const double r = A.pb;
-    const double *b = A.bound;
-    // every capsule vertex lies within r (1 + 1e-15) of p0 or p1: cheap exact pre-filter
-    const double m = r + 1e-6;
-    double lx = fmin(x0, x1), hx = fmax(x0, x1), ly = fmin(y0, y1), hy = fmax(y0, y1);
-    if (lx - m > b[0] && hx + m < b[1] && ly - m > b[2] && hy + m < b[3]) return false;
-    // Certain bands: every capsule vertex is within r of an endpoint, and the arc around the
-    // extreme endpoint has a vertex within half a fillet step (<= quantum) of each axis
-    // direction, so min x lies in [lx - r, lx - r cos(quantum)] (likewise the other sides).  A
-    // line outside [min, max] of those bands is decided without building the capsule.
-    {
-        const double lo = r + 1e-9, hi = r * c_tab.cos_quantum - 1e-9;
-        const double mn_lo[2] = {lx - lo, ly - lo}, mn_hi[2] = {lx - hi, ly - hi};
-        const double mx_lo[2] = {hx + hi, hy + hi}, mx_hi[2] = {hx + lo, hy + lo};
-        bool certain = true;
-        for (int q = 0; q < 4; ++q) {
-            const int ax = q >> 1;
-            const double v = b[q];
-            if (v < mn_lo[ax] || v > mx_hi[ax]) continue;                  // certainly outside
-            if (v >= mn_hi[ax] && v <= mx_lo[ax]) return true;             // certainly inside
-            certain = false;
-        }
-        if (certain) return false;
-    }
-    double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
-    if (x0 == x1 && y0 == y1) {
-        for (int i = 0; i < 64; ++i) upd(x0 + r * c_tab.circ_c[i], y0 + r * c_tab.circ_s[i], mnx, mxx, mny, mxy);
-    } else {
-        double dx = x1 - x0, dy = y1 - y0;
-        double len = sqrt(dx * dx + dy * dy);
-        double ux = 1 * r * dx / len, uy = 1 * r * dy / len;
-        upd(x1 - uy, y1 + ux, mnx, mxx, mny, mxy);
-        upd(x1 + uy, y1 - ux, mnx, mxx, mny, mxy);
-        upd(x0 + uy, y0 - ux, mnx, mxx, mny, mxy);
-        upd(x0 - uy, y0 + ux, mnx, mxx, mny, mxy);
-        double a1 = atan2(dy, dx);
-        fillet_ext(x1, y1, a1 + PI_GEOS / 2.0, a1 - PI_GEOS / 2.0, r, mnx, mxx, mny, mxy);
-        double a0 = atan2(y0 - y1, x0 - x1);
-        fillet_ext(x0, y0, a0 + PI_GEOS / 2.0, a0 - PI_GEOS / 2.0, r, mnx, mxx, mny, mxy);
-    }
-    return (mnx <= b[0] && b[0] <= mxx) || (mnx <= b[1] && b[1] <= mxx) || (mny <= b[2] && b[2] <= mxy) ||
-           (mny <= b[3] && b[3] <= mxy);
-}
-
-// 64-gon(pos, pB) meets 64-gon(goal, 1): Minkowski closed form (ATT/env:2266-2269)
-__device__ bool goal_reached(double px, double py, double gx, double gy, double pb) {
-    double dx = gx - px, dy = gy - py;
-    double thr = (pb + 1.0) * c_tab.apothem;
-    // max_k d.n_k lies in [|d| cos(pi/64), |d|]: outside the band the answer is certain
-    const double dist = sqrt(dx * dx + dy * dy);
-    if (dist > (pb + 1.0) * (1.0 + 1e-12) + 1e-12) return false;
-    if (dist < thr * (1.0 - 1e-12) - 1e-12) return true;
-    double m = -INFINITY;
-#pragma unroll 8
-    for (int k = 0; k < 64; ++k) {
-        double v = dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k];
-        m = v > m ? v : m;
-    }
-    return m <= thr;
+// 64-gon(pos, pB) meets 64-gon(goal, 1) (ATT/env:2266-2269)
+__device__ inline bool goal_reached(double px, double py, double gx, double gy, double pb) {
+    return gons_meet(gx - px, gy - py, pb + 1.0, false);
 }
 
 // 64-gon(pos, pB) meets the closed square cell (ATT/env:2243-2250): separating axes
@@ -182,125 +84,6 @@ __device__ bool building_hit(double px, double py, double cx, double cy, double 
         double lim = 5.0 * (fabs(c_tab.nrm_c[k]) + fabs(c_tab.nrm_s[k])) + pb * c_tab.apothem;
         if (proj > lim) return false;
     }
-    return true;
-}
-
-// Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p
-__device__ bool ray_poly_entry_full(double cx, double cy, double ex, double ey, double px, double py, double r,
-                                    double &tout) {
-    double ddx = ex - cx, ddy = ey - cy;
-    double tlo = 0.0, thi = 1.0;
-    double vx = px + r * c_tab.circ_c[0], vy = py + r * c_tab.circ_s[0];
-    for (int k = 0; k < 64; ++k) {
-        int k1 = (k + 1) & 63;
-        double wx = px + r * c_tab.circ_c[k1], wy = py + r * c_tab.circ_s[k1];
-        double exx = wx - vx, eyy = wy - vy;
-        double a = exx * (cy - vy) - eyy * (cx - vx);
-        double b = exx * ddy - eyy * ddx;
-        if (b == 0.0) {
-            if (a > 0.0) return false;
-        } else if (b < 0.0) {
-            double t = -a / b;
-            tlo = t > tlo ? t : tlo;
-        } else {
-            double t = -a / b;
-            thi = t < thi ? t : thi;
-        }
-        if (tlo > thi) return false;
-        vx = wx;
-        vy = wy;
-    }
-    tout = tlo;
-    return true;
-}
-
-// Same result from a window of edges.  When the line crosses the inscribed circle (not near
-// tangency) and c lies outside the circumscribed circle, the entry is the maximum of -a/b over
-// the entering edges and every entering edge other than the one(s) holding the entry point
-// gives a smaller value; that edge lies within half an edge of the ray's entry angle on the
-// circumscribed circle, so the maximum over the six edges around it is the same number (same
-// vertices, same arithmetic) as over all 64.  The exit lies beyond the entry, so the segment
-// meets the polygon iff that maximum is <= 1.  Anything else takes the full clip.
-__device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
-                               double &tout) {
-    const double ddx = ex - cx, ddy = ey - cy;
-    const double L2 = ddx * ddx + ddy * ddy;
-    const double wx = px - cx, wy = py - cy;
-    const double w2 = wx * wx + wy * wy;
-    const double L = sqrt(L2);
-    const double s0 = (wx * ddx + wy * ddy) / L;                   // along the ray
-    const double h = fabs(wx * ddy - wy * ddx) / L;               // distance of p to the line
-    const double ap = r * c_tab.apothem;
-    if (!(h < ap * (1.0 - 1e-9)) || !(w2 > r * r * (1.0 + 1e-9)) || !(s0 > 0.0))
-        return ray_poly_entry_full(cx, cy, ex, ey, px, py, r, tout);
-    const double tc = (s0 - sqrt(r * r - h * h)) / L;              // circumscribed-circle entry
-    const float phi = atan2f((float)(cy + tc * ddy - py), (float)(cx + tc * ddx - px));
-    // vertex angles are -i 2pi/64: nearest vertex index
-    int i0 = (int)lrintf(-phi * (64.0f / 6.28318530717958647f));
-    double tlo = 0.0;
-    bool any = false;
-#pragma unroll
-    for (int dk = -3; dk <= 2; ++dk) {
-        const int k = (i0 + dk) & 63, k1 = (k + 1) & 63;
-        const double vx = px + r * c_tab.circ_c[k], vy = py + r * c_tab.circ_s[k];
-        const double qx = px + r * c_tab.circ_c[k1], qy = py + r * c_tab.circ_s[k1];
-        const double exx = qx - vx, eyy = qy - vy;
-        const double a = exx * (cy - vy) - eyy * (cx - vx);
-        const double b = exx * ddy - eyy * ddx;
-        if (b < 0.0) {
-            const double t = -a / b;
-            tlo = t > tlo ? t : tlo;
-            any = true;
-        }
-    }
-    if (!any) return ray_poly_entry_full(cx, cy, ex, ey, px, py, r, tout);
-    if (tlo > 1.0) return false;
-    tout = tlo;
-    return true;
-}
-
-__device__ bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1,
-                           double &dout) {
-    double ddx = ex - cx, ddy = ey - cy;
-    double tx0, tx1, ty0, ty1;
-    if (ddx == 0.0) {
-        if (cx < x0 || cx > x1) return false;
-        tx0 = -INFINITY;
-        tx1 = INFINITY;
-    } else {
-        double ta = (x0 - cx) / ddx, tb = (x1 - cx) / ddx;
-        if (ta < tb) { tx0 = ta; tx1 = tb; } else { tx0 = tb; tx1 = ta; }
-    }
-    if (ddy == 0.0) {
-        if (cy < y0 || cy > y1) return false;
-        ty0 = -INFINITY;
-        ty1 = INFINITY;
-    } else {
-        double ta = (y0 - cy) / ddy, tb = (y1 - cy) / ddy;
-        if (ta < tb) { ty0 = ta; ty1 = tb; } else { ty0 = tb; ty1 = ta; }
-    }
-    double tin = tx0 > ty0 ? tx0 : ty0;
-    double tout = tx1 < ty1 ? tx1 : ty1;
-    if (tin > tout || tout < 0.0 || tin > 1.0) return false;
-    double t = tin >= 0.0 ? tin : tout;
-    if (t > 1.0) return false;
-    dout = gdist(cx + t * ddx, cy + t * ddy, cx, cy);
-    return true;
-}
-
-__device__ bool ray_vline(double cx, double cy, double ex, double ey, double lx, double &dout) {
-    if (cx == lx && ex == lx) { dout = 0.0; return true; }
-    if ((cx - lx) * (ex - lx) > 0.0) return false;
-    double t = (lx - cx) / (ex - cx);
-    dout = gdist(lx, cy + t * (ey - cy), cx, cy);
-    return true;
-}
-
-__device__ bool ray_hline(double cx, double cy, double ex, double ey, double ly, double &dout) {
-    if (cy == ly && ey == ly) { dout = 0.0; return true; }
-    if ((cy - ly) * (ey - ly) > 0.0) return false;
-    double t = (ly - cy) / (ey - cy);
-    dout = gdist(cx + t * (ex - cx), ly, cx, cy);
     return true;
 }
 
@@ -333,44 +116,6 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, 
     if (ray_hline(cx, cy, ex, ey, A.bound[2], d) && d < mind) mind = d;
     if (ray_hline(cx, cy, ex, ey, A.bound[3], d) && d < mind) mind = d;
     return mind;
-}
-
-__device__ void tdcpa(double ox, double oy, double hx, double hy, double ovx, double ovy, double hvx, double hvy,
-                      double pb, double &tcpa, double &dcpa, int &total) {
-    double rx = -1 * (ox - hx), ry = -1 * (oy - hy);
-    double wx = ovx - hvx, wy = ovy - hvy;
-    double nw = npnorm(wx, wy);
-    double sq = nw * nw;
-    double t, d;
-    if (sq == 0) {
-        t = -10;
-        double nnx = ox + ovx * 1, nny = oy + ovy * 1;
-        double nhx = hx + hvx * 1, nhy = hy + hvy * 1;
-        d = npnorm(nhx - nnx, nhy - nny);
-        if (d < pb + pb) total += 1;
-    } else {
-        t = __builtin_fma(ry, wy, rx * wx) / sq;
-        d = npnorm((rx * -1) + (wx * t), (ry * -1) + (wy * t));
-    }
-    if (t <= 1 && t >= 0 && d < pb + pb) total += 1;
-    tcpa = t;
-    dcpa = d;
-}
-
-__device__ double pairwise_sum(const double *a, int n) {
-    if (n < 8) {
-        double s = a[0];
-        for (int i = 1; i < n; ++i) s += a[i];
-        return s;
-    }
-    double r[8];
-    for (int j = 0; j < 8; ++j) r[j] = a[j];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8)
-        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res += a[i];
-    return res;
 }
 
 // LDS image of one workgroup's envs (A = epb * N agents, <= BLOCK)
@@ -794,28 +539,6 @@ struct aac_env {
     int32_t bank_n;
     uint64_t bank_seed;
 };
-
-static void fill_tables(Tab &t) {
-    const double quantum = PI_GEOS / 2.0 / 16;
-    const double total = std::fabs(0.0 - 2.0 * PI_GEOS);
-    const int nseg = (int)(total / quantum + 0.5);
-    const double inc = total / nseg;
-    for (int i = 0; i < 64; ++i) {
-        double a = 0.0 + (double)(-1 * i) * inc;
-        t.circ_c[i] = std::cos(a);
-        t.circ_s[i] = std::sin(a);
-        t.nrm_c[i] = std::cos((i + 0.5) * PI_GEOS / 32.0);
-        t.nrm_s[i] = std::sin((i + 0.5) * PI_GEOS / 32.0);
-    }
-    for (int r = 0; r < NRAY; ++r) {
-        double rad = (double)(20 * r) * (PI_GEOS / 180.0);
-        t.ray_c[r] = std::cos(rad);
-        t.ray_s[r] = std::sin(rad);
-    }
-    t.apothem = std::cos(PI_GEOS / 64.0);
-    t.cos_quantum = std::cos(quantum);
-    t.quantum = quantum;
-}
 
 static Args make_args(const aac_env *h, const aac_step_out *o) {
     Args A;
