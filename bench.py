@@ -14,7 +14,11 @@ python bench.py [--gpus N] [--steps K] [--warmup W]        (N > 1: launched by t
 ``--model gru`` measures config 4 instead (randomOD_gru_radar): the
 same vectorised loop with the GRU-actor MADDPG of MADDPG_ownENV_randomOD_Wgru_radar (one GRU actor
 and one GRU critic per agent, hidden states carried per agent, zeroed when an episode ends, and
-stored in the replay), 8 agents, B = 512 (its argparse default).  The default line is config 3.
+stored in the replay), 8 agents, B = 512 (its argparse default).  ``--model uam`` measures config 5
+(MADDPG_ownENV_randomOD_radar_N_model_use_tdCPA_forV2_changeskin_UAM): the UAM
+env kernel (clouds, go-around aircraft, runway, sorted neighbours) with its float64 shared actor /
+single critic learner, 16 aircraft x 8192 envs, one gradient iteration per update at B = 512, one
+replay row per aircraft.  The default line is config 3.
 """
 import argparse
 import json
@@ -31,13 +35,32 @@ sys.path.insert(0, ROOT)
 
 METRIC = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 5 agents×4096 envs"
 METRIC_GRU = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 8 agents×4096 envs, GRU actor"
+METRIC_UAM = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 16 agents×8192 envs, UAM"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3
+FP64_PEAK_TFLOPS = 78.6    # AMD MI355X spec sheet, dense FP64 vector / matrix (the guide lists no FP64 row)
 
 
 def env_bytes_per_agent_step(N):
     """130 + 4 (24 + 10 (N - 1)) algorithmic HBM bytes per agent-env-step."""
     return 130 + 4 * (24 + 10 * (N - 1))
+
+
+def uam_bytes_per_agent_step(N):
+    """Algorithmic HBM bytes of one UAM agent-env-step (aac_uam.hip): read
+    pos, vel, action, goal, start (5 x 16), heading (8), reach (1), top2 (2) = 91; write pos, vel,
+    pre_pos, pre_vel (64), heading (8), reach (1), top2 (2) = 75; float64 observations own 7, radar
+    18, neighbours 5 (N - 1); reward 8, done 1, mask 1."""
+    return 91 + 75 + 8 * (7 + 18 + 5 * (N - 1)) + 10
+
+
+def uam_update_flops(B):
+    """2 M N K over the UAM learner's products per update_myown (one gradient iteration at B rows):
+    target actor + target critic forward, critic forward + backward (3x), actor forward, critic
+    forward on the policy action + backward to the action, actor backward."""
+    A = 7 * 64 + 18 * 64 + 128 * 128 + 128 * 2
+    C = 9 * 64 + 18 * 64 + 128 * 256 + 256
+    return 2.0 * B * (A + C + 3 * C + A + 3 * C + 3 * A)
 
 
 def update_flops(N, D0, B):
@@ -88,14 +111,15 @@ def gemm_roofline(model, B, updates=4):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--model", default="att", choices=["att", "gru"],
-                   help="att: config 3 (default); gru: config 4, GRU actor (defaults 8 agents, B=512)")
+    p.add_argument("--model", default="att", choices=["att", "gru", "uam"],
+                   help="att: config 3 (default); gru: config 4, GRU actor (defaults 8 agents, B=512); "
+                        "uam: config 5 (16 aircraft x 8192 envs, B=512)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096; uam 8192)")
     p.add_argument("--agents", type=int, default=None, help="default 5 (att) / 8 (gru)")
     p.add_argument("--batch", type=int, default=None, help="default 1024 (att) / 512 (gru)")
-    p.add_argument("--memory", type=int, default=100000)
+    p.add_argument("--memory", type=int, default=None, help="replay rows (default 1e5; uam 2^20)")
     p.add_argument("--radar", default="combined", choices=["drones", "obstacles", "combined"])
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
@@ -106,9 +130,13 @@ def parse():
     p.add_argument("--gemm-traffic", default=os.path.join(ROOT, "profiles", "gemm_pmc.json"))
     a = p.parse_args()
     if a.agents is None:
-        a.agents = 8 if a.model == "gru" else 5
+        a.agents = {"gru": 8, "uam": 16}.get(a.model, 5)
     if a.batch is None:
-        a.batch = 512 if a.model == "gru" else 1024
+        a.batch = 1024 if a.model == "att" else 512
+    if a.envs is None:
+        a.envs = 8192 if a.model == "uam" else 4096
+    if a.memory is None:
+        a.memory = (1 << 20) if a.model == "uam" else 100000
     return a
 
 
@@ -191,9 +219,104 @@ class Trainer:
 NO_GRAPH = False
 
 
+class UamTrainer:
+    """Vectorised UAM/main:361-640 loop on one GPU: actor + noise, env step, one replay row per
+    aircraft, GPU auto-reset from the episode bank, one update_myown (one gradient iteration)."""
+
+    def __init__(self, E, N, B, memory, seed, pg=None):
+        from multi_agent_aac_amd import uam, uam_learner
+        self.E, self.N, self.B = E, N, B
+        self.gru = False
+        self.env = uam.BatchedUAM(E, N, neighbours=True)
+        self.env.set_bank(uam.build_bank(16384, N, seed=2026 + seed), seed=1234 + seed)
+        # UAM/main:159-165: actor_dim = critic_dim = [7, (N-1)*5, 18, 6]
+        dims = [7, (N - 1) * 5, 18, 6]
+        self.model = uam_learner.MADDPG(dims, dims, 2, n_agents=N, seed=777, batch_size=B, memory_length=memory,
+                                        process_group=pg)
+        self.replay = self.model.attach_replay(memory, seed=seed)
+        self.cur = self.env.alloc_buffers()
+        self.nxt = self.env.alloc_buffers()
+        self.episode = torch.ones(E, dtype=torch.int32, device="cuda")
+        self.env.auto_reset(None, out=self.cur)
+        self.env_events = []
+
+    def step(self, update=True, time_env=False):
+        c, n = self.cur, self.nxt
+        act = self.model.act(c.own, c.radar, self.episode, noisy=True)
+        if time_env:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        self.env.step(act, out=n)
+        if time_env:
+            ev1.record()
+            self.env_events.append((ev0, ev1))
+        self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
+        self.env.auto_reset(n.env_done, out=n)
+        self.episode.add_(n.env_done.to(torch.int32))
+        self.cur, self.nxt = n, c
+        if update and len(self.replay) > self.B:
+            self.model.update(self.B, use_graph=not NO_GRAPH)
+
+
+def cpu_baseline_uam(E, N, B, seconds):
+    """UAM: the reference-shaped scalar oracle env step (oracle/uam_ref.py) on the host cores plus the
+    CPU float64 update_myown restatement (bounded sample)."""
+    import multiprocessing as mp
+    from oracle import uam_learner_ref as R
+    cores = len(os.sched_getaffinity(0))
+    procs = min(cores, 16)
+    ctx = mp.get_context("spawn")
+    budget = seconds / 2
+    with ctx.Pool(procs) as pool:
+        res = pool.starmap(_cpu_uam_worker, [(N, budget, w) for w in range(procs)])
+    steps = sum(r[0] for r in res)
+    env_rate = sum(r[0] / r[1] for r in res) * N                 # agent-env-steps/s over all workers
+    torch.set_num_threads(procs)
+    a, c = R.RefActor().double(), R.RefCritic().double()
+    at, ct = R.RefActor().double(), R.RefCritic().double()
+    oa, oc = torch.optim.Adam(a.parameters(), lr=1e-4), torch.optim.Adam(c.parameters(), lr=1e-4)
+    g = torch.Generator().manual_seed(0)
+    b = {k: torch.rand(B, w, generator=g, dtype=torch.float64) for k, w in
+         (("own", 7), ("radar", 18), ("act", 2), ("n_own", 7), ("n_radar", 18))}
+    b["rew"], b["done"] = torch.rand(B, generator=g, dtype=torch.float64), torch.zeros(B, dtype=torch.float64)
+    t0 = time.perf_counter()
+    n_upd = 0
+    while time.perf_counter() - t0 < budget or n_upd == 0:
+        R.ref_update(a, c, at, ct, oa, oc, b)
+        n_upd += 1
+    t_upd = (time.perf_counter() - t0) / n_upd
+    t_iter = E * N / env_rate + t_upd
+    return {"value": E * N / t_iter, "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
+            "sample": (f"reference-shaped scalar UAM env oracle on {procs} processes x 1 env x {N} aircraft, "
+                       f"{steps} env steps ({env_rate:.3g} agent-env-steps/s env-only) + CPU float64 "
+                       f"update_myown restatement B={B} x {n_upd} ({t_upd * 1e3:.2f} ms each), {procs} threads; "
+                       f"value = {E}x{N} agent-steps / (env step + update) per iteration"),
+            "env_only": env_rate, "update_ms": t_upd * 1e3}
+
+
+def _cpu_uam_worker(N, budget, wid):
+    import random as _random
+    sys.path.insert(0, ROOT)
+    from oracle import uam_ref as U
+    py, npr = _random.Random(wid), np.random.RandomState(wid)
+    env = U.UAMEnv(N)
+    env.reset(*U.sample_episode(N, py, npr))
+    rng = np.random.default_rng(wid)
+    t0 = time.perf_counter()
+    steps = 0
+    while time.perf_counter() - t0 < budget or steps < 2:
+        *_, over = env.full_step(rng.uniform(-1, 1, (N, 2)))
+        if over:
+            env.reset(*U.sample_episode(N, py, npr))
+        steps += 1
+    return steps, time.perf_counter() - t0
+
+
 def cpu_baseline(E, N, B, radar, seconds, model="att"):
     """The C oracle env step + the torch-CPU learner restatement on the host cores (bounded sample)."""
     import multiprocessing as mp
+    if model == "uam":
+        return cpu_baseline_uam(E, N, B, seconds)
     from oracle import c_oracle, learner_ref  # noqa: F401  (checker / baseline only)
     cores = len(os.sched_getaffinity(0))
     procs = min(cores, 16)
@@ -287,6 +410,30 @@ def env_microbench(E, N, radar, iters=20):
             "frac": gbs / HBM_PEAK_GBS}
 
 
+def uam_env_microbench(E, N, iters=10):
+    """UAM env-only kernel throughput at large E."""
+    from multi_agent_aac_amd import uam
+    env = uam.BatchedUAM(E, N)
+    env.set_bank(uam.build_bank(8192, N, seed=5), seed=3)
+    env.auto_reset(None)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    acts = [torch.rand(E, N, 2, device="cuda", generator=g, dtype=torch.float64) * 2 - 1 for _ in range(4)]
+    for i in range(3):
+        env.step(acts[i % 4])
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for i in range(iters):
+        ev[i][0].record()
+        env.step(acts[i % 4])
+        ev[i][1].record()
+        env.auto_reset(env.bufs.env_done)
+    torch.cuda.synchronize()
+    ms = float(np.mean([x.elapsed_time(y) for x, y in ev]))
+    gbs = uam_bytes_per_agent_step(N) * E * N / (ms * 1e-3) / 1e9
+    return {"envs": E, "agents": N, "kernel_ms": ms, "agent_env_steps_per_s": E * N / (ms * 1e-3),
+            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
+
+
 def main():
     global NO_GRAPH
     a = parse()
@@ -299,10 +446,13 @@ def main():
     ws, rank, local = setup_dist(a.backend)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(777 + rank)
-    tr = Trainer(a.envs, a.agents, a.batch, a.memory, a.radar, seed=rank,
-                 pg=dist.group.WORLD if ws > 1 else None, model=a.model)
+    pg = dist.group.WORLD if ws > 1 else None
+    if a.model == "uam":
+        tr = UamTrainer(a.envs, a.agents, a.batch, a.memory, seed=rank, pg=pg)
+    else:
+        tr = Trainer(a.envs, a.agents, a.batch, a.memory, a.radar, seed=rank, pg=pg, model=a.model)
     # pre-fill the replay to >= memory transitions (untimed), then capture the update graph
-    while len(tr.replay) < a.memory:
+    while len(tr.replay) < min(a.memory, 100000):
         tr.step(update=False)
     for _ in range(a.warmup):
         tr.step(update=True)
@@ -322,18 +472,24 @@ def main():
     N = a.agents
     value = E_total * N * a.steps / dt
     upd_per_s = a.steps / dt
+    uam = a.model == "uam"
     D0 = 6 + 4 * (N - 1)
-    bpa = env_bytes_per_agent_step(N)
+    bpa = uam_bytes_per_agent_step(N) if uam else env_bytes_per_agent_step(N)
     achieved = bpa * a.envs * N / (env_ms * 1e-3) / 1e9
     traffic = None
     tsrc = None
-    if a.traffic and os.path.exists(a.traffic):
-        with open(a.traffic) as f:
+    tpath = os.path.join(ROOT, "profiles", "uam_env_pmc.json") if uam else a.traffic
+    if tpath and os.path.exists(tpath):
+        with open(tpath) as f:
             t = json.load(f)
-        if t.get("envs") == a.envs and t.get("agents") == N and t.get("radar") == a.radar:
+        if t.get("envs") == a.envs and t.get("agents") == N and (uam or t.get("radar") == a.radar):
             traffic = t.get("hbm_bytes_per_launch")
-            tsrc = os.path.relpath(a.traffic, ROOT)
-    if tr.gru:      # algorithmic GEMM FLOPs of the plan's launches (2 M N K per product)
+            tsrc = os.path.relpath(tpath, ROOT)
+    if uam:
+        upd_fl = uam_update_flops(a.batch)
+        workload = (f"tdCPA_forV2_changeskin_UAM: {N} aircraft x {a.envs} envs/GPU, drifting cloud + go-around "
+                    f"aircraft, float64 shared actor / single critic, B={a.batch}, 1 gradient iteration per update")
+    elif tr.gru:      # algorithmic GEMM FLOPs of the plan's launches (2 M N K per product)
         from multi_agent_aac_amd.fused import GemmLaunch
         upd_fl = sum(op.flops for op in tr.model._plan(a.batch).ops() if isinstance(op, GemmLaunch))
         workload = f"randomOD_gru_radar: {N} agents x {a.envs} envs/GPU, GRU actor, B={a.batch} MADDPG update, " \
@@ -341,25 +497,30 @@ def main():
     else:
         upd_fl = update_flops(N, D0, a.batch)
         workload = f"one_model_att: {N} agents x {a.envs} envs/GPU, B={a.batch} MADDPG update, {a.radar} radar"
+    peak = FP64_PEAK_TFLOPS if uam else FP32_PEAK_TFLOPS
     out = {
-        "metric": METRIC_GRU if tr.gru else METRIC, "value": value, "unit": "agent-env-steps/s", "n_gpus": ws, "steps": a.steps,
+        "metric": METRIC_UAM if uam else (METRIC_GRU if tr.gru else METRIC), "value": value,
+        "unit": "agent-env-steps/s", "n_gpus": ws, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64 env state / f32 obs+learner", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f64 env + f64 learner" if uam else "f64 env state / f32 obs+learner",
+        "data": "synthetic",
         "config": {"workload": workload, "envs_per_gpu": a.envs, "envs_total": E_total, "agents": N,
-                   "batch": a.batch, "replay": a.memory, "radar": a.radar,
+                   "batch": a.batch, "replay": a.memory, "radar": "runway+bound+clouds+aircraft" if uam else a.radar,
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
-                   "update_graph": (not a.no_graph) and (ws == 1 or tr.model.fused),
-                   "graph_segments": "one per update" if ws == 1 else "cut at each of the N+1 gradient all-reduces"},
-        "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if tr.gru else N),
-        "env_roofline": {"kernel": "step_kernel (fused env step)", "bound": "hbm", "achieved": achieved,
+                   "update_graph": (not a.no_graph) and (ws == 1 or (not uam and tr.model.fused)),
+                   "graph_segments": "one per update" if ws == 1 else (
+                       "eager (per-module all-reduce)" if uam else "cut at each of the N+1 gradient all-reduces")},
+        "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if (tr.gru or uam) else N),
+        "env_roofline": {"kernel": "uam_step_kernel (fused UAM env step)" if uam else "step_kernel (fused env step)",
+                         "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": tsrc, "bytes_per_agent_step": bpa, "agents_per_launch": a.envs * N,
                          "avg_launch_ms": env_ms},
         "update_roofline": {"bound": "mfma", "unit": "TFLOP/s", "flop_per_update": upd_fl,
-                            "achieved": upd_fl * upd_per_s / 1e12, "peak": FP32_PEAK_TFLOPS,
-                            "frac": upd_fl * upd_per_s / 1e12 / FP32_PEAK_TFLOPS, "note": "whole-step rate bound"},
+                            "achieved": upd_fl * upd_per_s / 1e12, "peak": peak,
+                            "frac": upd_fl * upd_per_s / 1e12 / peak, "note": "whole-step rate bound"},
     }
-    if tr.gru or tr.model.fused:
+    if not uam and (tr.gru or tr.model.fused):
         rf = gemm_roofline(tr.model, a.batch)
         rf["traffic"] = None
         if a.gemm_traffic and os.path.exists(a.gemm_traffic):
@@ -373,7 +534,7 @@ def main():
     else:
         out["roofline"] = out["env_roofline"]
     if rank == 0 and ws == 1 and a.env_micro:
-        out["env_microbench"] = env_microbench(a.env_micro, N, a.radar)
+        out["env_microbench"] = uam_env_microbench(1 << 16, N) if uam else env_microbench(a.env_micro, N, a.radar)
     if rank == 0 and cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

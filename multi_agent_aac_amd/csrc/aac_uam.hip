@@ -100,6 +100,10 @@ __device__ bool ray_gon_boundary(double cx, double cy, double ex, double ey, dou
         const double qx = tt * ddx - wx, qy = tt * ddy - wy;
         if (qx * qx + qy * qy > (r + 1e-6) * (r + 1e-6)) return false;
     }
+    {   // c outside the circumscribed circle: the boundary point is the entry (aac_geom.h window clip)
+        const double wx = px - cx, wy = py - cy;
+        if (wx * wx + wy * wy > r * r * (1.0 + 1e-9)) return ray_poly_entry(cx, cy, ex, ey, px, py, r, tout);
+    }
     double tin = -INFINITY, tex = INFINITY;
     double vx = px + r * c_tab.circ_c[0], vy = py + r * c_tab.circ_s[0];
     for (int k = 0; k < 64; ++k) {
@@ -167,21 +171,31 @@ __device__ bool gon_rect_overlap(double dx, double dy, double hx, double hy, dou
 }
 
 // ------------------------------------------------------------------------------ phases
+// pairwise np.linalg.norm distances of the workgroup's aircraft, row la = [d(la, base + j)]_j
+// (dynamic LDS, epb * N * N doubles); npnorm is symmetric in the sign of the difference
+extern __shared__ double s_dist[];
+
+__device__ void dist_row(const UArgs &A, const Lds &S, int la, int base) {
+    const double2 p = S.pos[la];
+    double *row = s_dist + (size_t)la * A.N;
+    for (int j = 0; j < A.N; ++j) {
+        const double2 q = S.pos[base + j];
+        row[j] = npnorm(q.x - p.x, q.y - p.y);
+    }
+}
+
 // (2) neighbour order of aircraft la: get_current_agent_nei(queue=True) is a stable sort by
 // np.linalg.norm distance, i.e. rank_j = #{k : d_k < d_j or (d_k == d_j and k < j)}
-__device__ void order_phase(const UArgs &A, Lds &S, int la, int base, int i) {
+__device__ void order_phase(const UArgs &A, Lds &S, int la, int i) {
     const int N = A.N;
-    const double2 p = S.pos[la];
+    const double *row = s_dist + (size_t)la * N;
     for (int j = 0; j < N; ++j) {
         if (j == i) continue;
-        const double2 q = S.pos[base + j];
-        const double dj = npnorm(q.x - p.x, q.y - p.y);
+        const double dj = row[j];
         int rank = 0;
         for (int k = 0; k < N; ++k) {
-            if (k == i || k == j) continue;
-            const double2 w = S.pos[base + k];
-            const double dk = npnorm(w.x - p.x, w.y - p.y);
-            rank += (dk < dj) || (dk == dj && k < j);
+            const double dk = row[k];
+            rank += (k != i && k != j) && ((dk < dj) || (dk == dj && k < j));
         }
         S.order[la][rank] = (uint8_t)j;
     }
@@ -379,7 +393,9 @@ __global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 
         S.reach[t] = reach;
     }
     __syncthreads();
-    if (active) order_phase(A, S, t, base, i);
+    if (active) dist_row(A, S, t, base);
+    __syncthreads();
+    if (active) order_phase(A, S, t, i);
     __syncthreads();
     radar_phase(A, S, e0, nag);
     __syncthreads();
@@ -398,10 +414,10 @@ __global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 
         const int me = S.reach[t];
         int ncoll = 0, nearest = -1, last = -1, prev_two = 0;
         double shortest = INFINITY;
+        const double *drow = s_dist + (size_t)t * N;
         for (int k = 0; k < K; ++k) {
             const int j = S.order[t][k];
-            const double2 q = S.pos[base + j];
-            const double d = npnorm(px - q.x, py - q.y);
+            const double d = drow[j];
             if (d < shortest) {
                 shortest = d;
                 nearest = j;
@@ -578,7 +594,9 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
         lds_agent(S, t, st, v, st, v, g, hd);
     }
     __syncthreads();
-    if (active) order_phase(A, S, t, base, i);
+    if (active) dist_row(A, S, t, base);
+    __syncthreads();
+    if (active) order_phase(A, S, t, i);
     __syncthreads();
     radar_phase(A, S, e0, nag);
     __syncthreads();
@@ -689,6 +707,8 @@ struct aac_uam {
     int32_t bank_n;
     uint64_t bank_seed;
 };
+
+static size_t dist_bytes(const aac_uam *h) { return sizeof(double) * (size_t)h->epb * h->cfg.N * h->cfg.N; }
 
 static UArgs make_uargs(const aac_uam *h, const aac_uam_out *o) {
     UArgs A;
@@ -803,7 +823,7 @@ int aac_uam_step(aac_uam *h, const double *actions, const aac_uam_out *o, void *
     if (rc) return rc;
     if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return ufail(AAC_E_INVALID, "step outputs");
     UArgs A = make_uargs(h, o);
-    hipLaunchKernelGGL(uam_step_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A,
+    hipLaunchKernelGGL(uam_step_kernel, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A,
                        reinterpret_cast<const double2 *>(actions));
     UCHK(hipGetLastError());
     return AAC_OK;
@@ -813,7 +833,7 @@ static int launch_reset(aac_uam *h, const UReset &R, const aac_uam_out *o, void 
     int rc = check_uout(o);
     if (rc) return rc;
     UArgs A = make_uargs(h, o);
-    hipLaunchKernelGGL(uam_reset_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A, R);
+    hipLaunchKernelGGL(uam_reset_kernel, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A, R);
     UCHK(hipGetLastError());
     return AAC_OK;
 }

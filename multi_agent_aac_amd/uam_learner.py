@@ -1,0 +1,360 @@
+"""The UAM variant's learner on the device, in float64.
+
+UAM/ = MADDPG_ownENV_randomOD_radar_N_model_use_tdCPA_forV2_changeskin_UAM.  With the default flags of
+UAM/main:60-100 (full_observable_critic_flag = use_GRU_flag = use_*_wRadar = False) the learner is
+ONE shared ``ActorNetwork_TwoPortion`` and ONE shared ``critic_single_TwoPortion`` (UAM/maddpg:45-104),
+both converted to float64 (UAM/maddpg:148-180), trained on per-aircraft transitions
+(UAM/main:582-603): each ``update_myown`` (UAM/maddpg:304-595) is ONE gradient iteration
+(var_iteration = 1) -- sample B transitions, TD target ``r + 0.95 Q'(s', pi'(s')) (1 - done)`` with the
+aircraft's own done, MSE critic Adam step, ``-mean Q(s, pi(s))`` actor Adam step (lr 1e-4 both,
+UAM/main:245-246) -- then the Polyak update (tau 0.01).
+
+Canonical contract: the two networks read [own (7), radar (18)]
+(UAM/maddpg:445-554), so their second encoder is 18 wide; the reference declares
+``actor_dim[1] = (N-1)*5`` for it, which cannot run (R1).
+
+Batched API: ``act`` (choose_action for E x N aircraft + noise), ``UamReplay.push_batch`` (E x N
+transitions per env step into a device fp64 ring), ``update`` (one update_myown, replayed from a
+captured HIP graph).  Reference API (drop-in for UAM/main, E = 1): ``choose_action``,
+``update_myown``, ``memory.push/sample/len``, ``save_model``, ``load_model``.
+
+Compute: torch fp64 GEMMs (hipBLASLt / rocBLAS drive the fp64 MFMA) and fused elementwise kernels;
+the sampler is the replay kernel of aac_learn.hip (``aac_replay_sample``).  Nothing runs on the CPU.
+"""
+import copy
+import os
+from collections import namedtuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+
+F64 = torch.float64
+ROW = 7 + 18 + 2 + 1 + 1 + 7 + 18           # [own | radar | a | r | done | own' | radar']
+SLICES = {"own": (0, 7), "radar": (7, 25), "act": (25, 27), "rew": (27, 28), "done": (28, 29),
+          "n_own": (29, 36), "n_radar": (36, 54)}
+Experience = namedtuple("Experience", ("states_obs", "states_nei", "states_grid", "actions", "next_states_obs",
+                                       "next_states_nei", "next_states_grid", "rewards", "dones", "history_info",
+                                       "cur_hidden", "next_hidden"))
+
+
+class ActorNetwork_TwoPortion(nn.Module):
+    """UAM/nets:167-190: relu(own_fc(own)) | relu(own_grid(radar)) -> relu(merge) -> tanh(act_out)."""
+
+    def __init__(self, actor_dim, n_actions):
+        super().__init__()
+        self.own_fc = nn.Sequential(nn.Linear(actor_dim[0], 64), nn.ReLU())
+        self.own_grid = nn.Sequential(nn.Linear(actor_dim[2], 64), nn.ReLU())   # radar width (R1)
+        self.merge_feature = nn.Sequential(nn.Linear(64 + 64, 128), nn.ReLU())
+        self.act_out = nn.Sequential(nn.Linear(128, n_actions), nn.Tanh())
+
+    def forward(self, cur_state):
+        x = torch.cat((self.own_fc(cur_state[0]), self.own_grid(cur_state[1])), dim=1)
+        return self.act_out(self.merge_feature(x))
+
+
+class critic_single_TwoPortion(nn.Module):
+    """UAM/nets:692-720: relu(SA_fc([own, a])) | relu(SA_grid(radar)) -> relu(256) -> q."""
+
+    def __init__(self, critic_obs, n_agents, n_actions, single_history=None, hidden_state_size=None):
+        super().__init__()
+        self.SA_fc = nn.Sequential(nn.Linear(critic_obs[0] + n_actions, 64), nn.ReLU())
+        self.SA_grid = nn.Sequential(nn.Linear(critic_obs[2], 64), nn.ReLU())    # radar width (R1)
+        self.merge_fc_grid = nn.Sequential(nn.Linear(64 + 64, 256), nn.ReLU())
+        self.out_feature_q = nn.Sequential(nn.Linear(256, 1))
+
+    def forward(self, single_state, single_action):
+        x = torch.cat((self.SA_fc(torch.cat((single_state[0], single_action), dim=1)), self.SA_grid(single_state[1])),
+                      dim=1)
+        return self.out_feature_q(self.merge_fc_grid(x))
+
+
+def noise_scale(episode, eps_end, start_scale=1, end_scale=0):
+    """get_custom_linear_scaling_factor (UAM/maddpg:1399-1406), elementwise on a device tensor."""
+    slope = (end_scale - start_scale) / (eps_end - 1)
+    ep = episode.to(F64)
+    return torch.where(ep <= eps_end, start_scale + slope * (ep - 1), torch.full_like(ep, float(end_scale)))
+
+
+class UamReplay:
+    """Device ring of fp64 transition rows [own | radar | a | r | done | own' | radar'] (54 doubles).
+    The reference stores one Experience per aircraft (UAM/main:582-603) and the learner reads only
+    these fields (the neighbour rows, history and hidden states are unused with the default
+    flags).  ``meta`` = [next position, size] lives on the device for the sampler kernel."""
+
+    def __init__(self, capacity, device="cuda", seed=0):
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.ring = torch.zeros(self.capacity, ROW, dtype=F64, device=self.device)
+        self.meta = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.seed = int(seed)
+        self.pos = 0
+        self.size = 0
+
+    def __len__(self):
+        return self.size
+
+    def push_batch(self, own, radar, act, rew, done, n_own, n_radar):
+        """E x N transitions (leading dims flattened) in one row-assembly launch per ring segment."""
+        cols = [own.reshape(-1, 7), radar.reshape(-1, 18), act.reshape(-1, 2), rew.reshape(-1, 1),
+                done.reshape(-1, 1), n_own.reshape(-1, 7), n_radar.reshape(-1, 18)]
+        M = cols[0].shape[0]
+        if M > self.capacity:
+            raise ValueError("one push larger than the replay capacity")
+        cols = [c if c.dtype == F64 else c.to(F64) for c in cols]
+        p = self.pos
+        first = min(M, self.capacity - p)
+        torch.cat([c[:first] for c in cols], dim=1, out=self.ring[p:p + first])
+        if first < M:
+            torch.cat([c[first:] for c in cols], dim=1, out=self.ring[:M - first])
+        self.pos = (p + M) % self.capacity
+        self.size = min(self.size + M, self.capacity)
+        self.meta[0] = self.pos          # device-side copies of the host counters (no sync)
+        self.meta[1] = self.size
+
+    def fields(self, rows):
+        return {k: rows[:, a:b] for k, (a, b) in SLICES.items()}
+
+
+class UamReplayMemory:
+    """ReplayMemory surface of UAM/memory:8-23: ``push(*12 fields)`` per aircraft, ``sample``, ``len``."""
+
+    def __init__(self, capacity, device="cuda", seed=0):
+        self.dev = UamReplay(capacity, device, seed)
+        self.memory = self
+        self.position = 0
+
+    def push(self, states_obs, states_nei, states_grid, actions, next_states_obs, next_states_nei, next_states_grid,
+             rewards, dones, history_info=None, cur_hidden=None, next_hidden=None):
+        d = self.dev.device
+        t = lambda x, n: torch.as_tensor(np.asarray(x.cpu() if torch.is_tensor(x) else x, dtype=np.float64)  # noqa: E731
+                                         ).reshape(1, n).to(d)
+        self.dev.push_batch(t(states_obs, 7), t(states_grid, 18), t(actions, 2), t(rewards, 1), t(dones, 1),
+                            t(next_states_obs, 7), t(next_states_grid, 18))
+        self.position = self.dev.pos
+
+    def sample(self, batch_size):
+        idx = torch.empty(batch_size, dtype=torch.int32, device=self.dev.device)
+        ops.replay_sample(self.dev.meta, batch_size, self.dev.seed, self.dev.counter, idx)
+        f = self.dev.fields(self.dev.ring.index_select(0, idx.long()))
+        return [Experience(f["own"][i], None, f["radar"][i], f["act"][i], f["n_own"][i], None, f["n_radar"][i],
+                           f["rew"][i, 0], f["done"][i, 0], None, None, None) for i in range(batch_size)]
+
+    def __len__(self):
+        return len(self.dev)
+
+
+def _init_adam_state(opt):
+    """Device-side Adam state before the first step (so a graph can be captured from step 1) with a
+    float64 step counter: capturable Adam computes its bias corrections from this tensor, and the
+    default float32 counter would round 1 - 0.999**t to 7 digits in a float64 learner."""
+    for group in opt.param_groups:
+        for p in group["params"]:
+            opt.state[p] = {"step": torch.zeros((), dtype=F64, device=p.device),
+                            "exp_avg": torch.zeros_like(p, memory_format=torch.preserve_format),
+                            "exp_avg_sq": torch.zeros_like(p, memory_format=torch.preserve_format)}
+
+
+class MADDPG:
+    """UAM/maddpg:35-181 with the default flags (shared actor + shared single critic, float64)."""
+
+    def __init__(self, actor_dim, critic_dim, dim_act, actor_hidden_state_size=64, gru_history_length=10,
+                 n_agents=5, args=None, cr_lr=1e-4, ac_lr=1e-4, gamma=0.95, tau=0.01,
+                 full_observable_critic_flag=False, use_GRU_flag=False, use_single_portion_selfATT=False,
+                 use_selfATT_with_radar=False, use_allNeigh_wRadar=False, own_obs_only=False, normalizer=None,
+                 use_nearestN_neigh_wRadar=False, device=None, seed=None, memory_length=None, batch_size=None,
+                 process_group=None):
+        if full_observable_critic_flag or use_GRU_flag or use_single_portion_selfATT or use_selfATT_with_radar \
+                or use_allNeigh_wRadar or use_nearestN_neigh_wRadar:
+            raise NotImplementedError("UAM learner: the default flags of UAM/main:60-100 only")
+        self.args = args
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        if seed is not None:
+            torch.manual_seed(seed)
+        self.n_agents, self.n_actions = int(n_agents), int(dim_act)
+        self.n_actor_dim, self.n_critic_dim = list(actor_dim), list(critic_dim)
+        self.actors = ActorNetwork_TwoPortion(actor_dim, dim_act).to(self.device, F64)
+        self.critics = critic_single_TwoPortion(critic_dim, n_agents, dim_act).to(self.device, F64)
+        self.actors_target = copy.deepcopy(self.actors)
+        self.critics_target = copy.deepcopy(self.critics)
+        for p in list(self.actors_target.parameters()) + list(self.critics_target.parameters()):
+            p.requires_grad_(False)
+        self.GAMMA, self.tau = float(gamma), float(tau)
+        cap = self.device.type == "cuda"
+        self.critic_optimizer = torch.optim.Adam(self.critics.parameters(), lr=cr_lr, capturable=cap, foreach=True)
+        self.actor_optimizer = torch.optim.Adam(self.actors.parameters(), lr=ac_lr, capturable=cap, foreach=True)
+        if cap:
+            for opt in (self.critic_optimizer, self.actor_optimizer):
+                _init_adam_state(opt)
+        mem_len = memory_length or (getattr(args, "memory_length", None) or int(1e5))
+        self.batch_size = batch_size or (getattr(args, "batch_size", None) or 512)
+        self.memory = UamReplayMemory(mem_len, self.device, seed=int(seed or 0))
+        self.replay = None
+        self.var = [1.0 for _ in range(self.n_agents)]
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.steps_done = 0
+        self._graph = None
+        self._graph_B = None
+        self._static = {}
+        self._noise_gen = torch.Generator(device=self.device)
+        self._noise_gen.manual_seed(int(seed or 0) * 7919 + 1)
+
+    # ------------------------------------------------------------------ batched API
+    def attach_replay(self, capacity, seed=0):
+        self.replay = UamReplay(capacity, self.device, seed)
+        return self.replay
+
+    @torch.no_grad()
+    def act(self, own, radar, episode, noisy=True, eps_end=10000, noise_start=1.0):
+        """choose_action (UAM/maddpg:597-676) for every aircraft: tanh actor + N(0, var^2) noise with
+        var from each env's own episode counter, clamped to [-1, 1].  own (E, N, 7), radar (E, N, 18)."""
+        E, N = own.shape[0], own.shape[1]
+        a = self.actors([own.reshape(-1, 7), radar.reshape(-1, 18)]).view(E, N, 2)
+        if noisy:
+            var = noise_scale(episode, eps_end, noise_start).view(E, 1, 1)
+            z = torch.randn(a.shape, dtype=F64, device=a.device, generator=self._noise_gen)
+            a = torch.clamp(a + z * var, -1.0, 1.0)
+        return a
+
+    def _soft_update(self):
+        """soft_update (UAM/maddpg:21-25): target = target (1 - tau) + source tau."""
+        for tgt, src in ((self.critics_target, self.critics), (self.actors_target, self.actors)):
+            tp, sp = list(tgt.parameters()), [p.detach() for p in src.parameters()]
+            torch._foreach_mul_(tp, 1.0 - self.tau)
+            torch._foreach_add_(tp, torch._foreach_mul(sp, self.tau))
+
+    def _allreduce_grads(self, module):
+        if self.world > 1:
+            from . import parallel
+            grads = [p.grad for p in module.parameters()]
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            parallel.allreduce_mean_(flat, self.pg)
+            torch._foreach_copy_(grads, [t.view_as(g) for t, g in zip(flat.split([g.numel() for g in grads]), grads)])
+
+    def _core(self, rows):
+        """One update_myown gradient iteration on sampled rows (UAM/maddpg:330-512) + soft update."""
+        f = {k: rows[:, a:b] for k, (a, b) in SLICES.items()}
+        s, s2 = [f["own"], f["radar"]], [f["n_own"], f["n_radar"]]
+        with torch.no_grad():
+            na = self.actors_target(s2)
+            q_next = self.critics_target(s2, na).squeeze()
+            target = (f["rew"][:, 0] + self.GAMMA * q_next * (1 - f["done"][:, 0])).unsqueeze(1)
+        q = self.critics(s, f["act"])
+        loss_q = nn.MSELoss()(q, target.detach())
+        self.critic_optimizer.zero_grad(set_to_none=False)
+        loss_q.backward()
+        self._allreduce_grads(self.critics)
+        self.critic_optimizer.step()
+        loss_a = -self.critics(s, self.actors(s)).mean()
+        self.actor_optimizer.zero_grad(set_to_none=False)
+        loss_a.backward()
+        self._allreduce_grads(self.actors)
+        self.actor_optimizer.step()
+        self._soft_update()
+        return loss_q.detach(), loss_a.detach()
+
+    def _buffers(self, rep, B):
+        key = (id(rep), B)
+        if key not in self._static:
+            self._static[key] = (torch.empty(B, dtype=torch.int32, device=self.device),
+                                 torch.empty(B, ROW, dtype=F64, device=self.device))
+        return self._static[key]
+
+    def _sampled_core(self, rep, B, idx=None):
+        bidx, rows = self._buffers(rep, B)
+        if idx is None:
+            ops.replay_sample(rep.meta, B, rep.seed, rep.counter, bidx)
+        else:
+            bidx.copy_(idx.reshape(-1))
+        torch.index_select(rep.ring, 0, bidx.long(), out=rows)
+        return self._core(rows)
+
+    def _init_grads(self):
+        for m in (self.actors, self.critics):
+            for p in m.parameters():
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+
+    def capture(self, B, rep):
+        """Capture one update (sample -> gather -> critic step -> actor step -> soft update) into a HIP
+        graph; the state is restored afterwards so capture has no side effect."""
+        self._init_grads()
+        snap = [t.clone() for t in self._state_tensors(rep)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._sampled_core(rep, B)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_out = self._sampled_core(rep, B)
+        for t, v in zip(self._state_tensors(rep), snap):
+            t.copy_(v)
+        self._graph, self._graph_B, self._graph_rep = g, B, id(rep)
+        return g
+
+    def _state_tensors(self, rep):
+        ts = [p.data for m in (self.actors, self.critics, self.actors_target, self.critics_target)
+              for p in m.parameters()]
+        for opt in (self.actor_optimizer, self.critic_optimizer):
+            for st in opt.state.values():
+                ts += [v for v in st.values() if torch.is_tensor(v)]
+        return ts + [rep.counter]
+
+    def update(self, B=None, use_graph=True, idx=None, replay=None):
+        """One update_myown-equivalent; returns (loss_q, loss_a) device scalars."""
+        B = B or self.batch_size
+        rep = replay if replay is not None else (self.replay if self.replay is not None else self.memory.dev)
+        if len(rep) < B:
+            raise ValueError(f"replay holds {len(rep)} transitions, cannot sample {B} distinct rows")
+        if idx is None and use_graph and self.device.type == "cuda" and self.world == 1:
+            if self._graph is None or self._graph_B != B or self._graph_rep != id(rep):
+                self.capture(B, rep)
+            self._graph.replay()
+            return self._graph_out
+        return self._sampled_core(rep, B, idx)
+
+    # ------------------------------------------------------------------ reference API
+    def choose_action(self, state, cur_total_step, cur_episode, step, mini_noise_eps, noise_start_level,
+                      actor_hiddens=None, use_allNeigh_wRadar=False, use_selfATT_with_radar=False, own_obs_only=False,
+                      use_nearestN_neigh_wRadar=False, noisy=True, use_GRU_flag=False):
+        """UAM/maddpg:597-676 (E = 1): returns (actions (N, 2) float64, noise, hiddens, act_hn)."""
+        N = self.n_agents
+        own = torch.as_tensor(np.stack(state[0]), dtype=F64, device=self.device).view(1, N, 7)
+        radar = torch.as_tensor(np.stack(state[2]), dtype=F64, device=self.device).view(1, N, 18)
+        for i in range(N):
+            self.var[i] = float(noise_scale(torch.tensor([cur_episode]), mini_noise_eps, noise_start_level)[0])
+        ep = torch.full((1,), int(cur_episode), dtype=torch.int32, device=self.device)
+        a = self.act(own, radar, ep, noisy=noisy, eps_end=mini_noise_eps, noise_start=noise_start_level)
+        self.steps_done += 1
+        return a[0].cpu().numpy(), np.zeros(2), actor_hiddens, torch.zeros(N, self.n_actions)
+
+    def update_myown(self, i_episode, total_step_count, UPDATE_EVERY, single_eps_critic_cal_record,
+                     transfer_learning=False, use_allNeigh_wRadar=False, use_selfATT_with_radar=False,
+                     use_nearestN_neigh_wRadar=False, wandb=None, full_observable_critic_flag=False,
+                     use_GRU_flag=False):
+        """UAM/maddpg:304-595: guard len(memory) <= batch_size, one gradient iteration, soft update."""
+        if len(self.memory) <= self.batch_size:
+            return None, None, single_eps_critic_cal_record
+        lq, la = self.update(self.batch_size, use_graph=False, replay=self.memory.dev)
+        return [lq], [la], single_eps_critic_cal_record
+
+    def save_model(self, episode, file_path):
+        os.makedirs(file_path, exist_ok=True)
+        sd = {k: v.detach().cpu() for k, v in self.actors.state_dict().items()}
+        torch.save(sd, os.path.join(file_path, "episode_" + str(episode) + "_actor_net.pth"))
+
+    def load_model(self, filePath, full_observable_critic_flag=False):
+        for path in filePath:
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+            self.actors.load_state_dict({k: v.to(F64) for k, v in sd.items()})
+        self.actors_target.load_state_dict(self.actors.state_dict())
+        self.critics_target.load_state_dict(self.critics.state_dict())
+        self._graph = None

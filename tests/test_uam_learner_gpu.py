@@ -1,0 +1,105 @@
+"""GPU tests of the UAM learner (multi_agent_aac_amd/uam_learner.py)
+against the CPU float64 restatement oracle/uam_learner_ref.py: identical weights and sampled rows,
+parameters after two update_myown calls within 1e-10; graph replay equal to eager; the batched
+act / replay; the reference method surface."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import uam_learner_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(seed=1, B=64):
+    from multi_agent_aac_amd import uam_learner as L
+    m = L.MADDPG([7, 20, 18, 6], [7, 20, 18, 6], 2, n_agents=5, device=DEV, seed=seed, batch_size=B,
+                 memory_length=4096)
+    rep = m.attach_replay(4096, seed=3)
+    g = torch.Generator().manual_seed(seed)
+    E, N = 64, 5
+    for _ in range(4):
+        rnd = lambda *s: torch.rand(*s, generator=g, dtype=torch.float64) * 2 - 1   # noqa: E731
+        rep.push_batch(rnd(E, N, 7).to(DEV), rnd(E, N, 18).abs().mul(5).to(DEV), rnd(E, N, 2).to(DEV),
+                       rnd(E, N).mul(50).to(DEV), (rnd(E, N) > 0.8).double().to(DEV), rnd(E, N, 7).to(DEV),
+                       rnd(E, N, 18).abs().mul(5).to(DEV))
+    return m, rep
+
+
+def _ref_from(m):
+    a, c = R.RefActor().double(), R.RefCritic().double()
+    a.load_state_dict({k: v.cpu() for k, v in m.actors.state_dict().items()})
+    c.load_state_dict({k: v.cpu() for k, v in m.critics.state_dict().items()})
+    return a, c, copy.deepcopy(a), copy.deepcopy(c)
+
+
+def test_update_matches_cpu_restatement(native_lib):
+    from multi_agent_aac_amd import uam_learner as L
+    m, rep = _model()
+    a, c, at, ct = _ref_from(m)
+    oa = torch.optim.Adam(a.parameters(), lr=1e-4)
+    oc = torch.optim.Adam(c.parameters(), lr=1e-4)
+    rng = np.random.default_rng(0)
+    for it in range(2):
+        idx = torch.as_tensor(rng.choice(len(rep), 64, replace=False), dtype=torch.int32, device=DEV)
+        lq, la = m.update(64, idx=idx)
+        rows = rep.ring[idx.long()].cpu()
+        b = {k: rows[:, s:e] for k, (s, e) in L.SLICES.items()}
+        b["rew"], b["done"] = b["rew"][:, 0], b["done"][:, 0]
+        rq, ra = R.ref_update(a, c, at, ct, oa, oc, b)
+        assert abs(float(lq) - rq) < 1e-10 and abs(float(la) - ra) < 1e-10
+    for mine, ref in ((m.actors, a), (m.critics, c), (m.actors_target, at), (m.critics_target, ct)):
+        for (k, p), (_, q) in zip(mine.state_dict().items(), ref.state_dict().items()):
+            np.testing.assert_allclose(p.cpu().numpy(), q.numpy(), rtol=0, atol=1e-10, err_msg=k)
+
+
+def test_graph_replay_equals_eager(native_lib):
+    m1, rep1 = _model(seed=4)
+    m2, rep2 = _model(seed=4)
+    for _ in range(3):
+        m1.update(64, use_graph=True)
+        m2.update(64, use_graph=False)
+    torch.cuda.synchronize()
+    for p, q in zip(list(m1.actors.parameters()) + list(m1.critics_target.parameters()),
+                    list(m2.actors.parameters()) + list(m2.critics_target.parameters())):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), q.detach().cpu().numpy(), rtol=0, atol=1e-14)
+
+
+def test_act_and_noise_schedule(native_lib):
+    m, _ = _model()
+    own = torch.rand(32, 5, 7, dtype=torch.float64, device=DEV)
+    radar = torch.rand(32, 5, 18, dtype=torch.float64, device=DEV) * 5
+    ep = torch.ones(32, dtype=torch.int32, device=DEV)
+    a0 = m.act(own, radar, ep, noisy=False)
+    ref = m.actors([own.view(-1, 7), radar.view(-1, 18)]).view(32, 5, 2)
+    assert torch.equal(a0, ref) and a0.dtype == torch.float64
+    ep[:] = 20000       # past eps_end = 10000: var = 0, no noise (UAM/maddpg:1399-1406)
+    assert torch.equal(m.act(own, radar, ep, noisy=True), torch.clamp(ref, -1, 1))
+    ep[:] = 1
+    an = m.act(own, radar, ep, noisy=True)
+    assert an.abs().max() <= 1 and not torch.equal(an, a0)
+
+
+def test_reference_surface(native_lib, tmp_path):
+    from multi_agent_aac_amd import uam_learner as L
+    m = L.MADDPG([7, 20, 18, 6], [7, 20, 18, 6], 2, n_agents=3, device=DEV, seed=2, batch_size=8, memory_length=64)
+    st = [[np.random.rand(7) for _ in range(3)], [np.random.rand(20) for _ in range(3)],
+          [np.random.rand(18) for _ in range(3)]]
+    act, noise, _, _ = m.choose_action(st, 1, 1, 1, 10000, 1, None)
+    assert act.shape == (3, 2) and act.dtype == np.float64
+    assert m.update_myown(1, 1, 1, []) == (None, None, [])
+    for _ in range(4):
+        for i in range(3):
+            m.memory.push(st[0][i], st[1][i], st[2][i], act[i], st[0][i], st[1][i], st[2][i], 1.0, 0, None, None, None)
+    assert len(m.memory) == 12
+    cl, al, rec = m.update_myown(1, 1, 1, [])
+    assert len(cl) == 1 and np.isfinite(float(cl[0]))
+    assert len(m.memory.sample(8)) == 8
+    m.save_model(3, str(tmp_path))
+    m2 = L.MADDPG([7, 20, 18, 6], [7, 20, 18, 6], 2, n_agents=3, device=DEV, seed=9)
+    m2.load_model([str(tmp_path / "episode_3_actor_net.pth")])
+    for p, q in zip(m.actors.parameters(), m2.actors.parameters()):
+        assert torch.equal(p, q)
