@@ -35,6 +35,14 @@ def _model(pg, N, B, E):
 
 
 def _worker(rank, ws, port, q):
+    try:
+        _work(rank, ws, port, q)
+    except BaseException as e:      # report instead of leaving the peer blocked in a collective
+        q.put((rank, {"error": repr(e)}))
+        raise
+
+
+def _work(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws), RANK=str(rank),
                       LOCAL_RANK="0")
     import torch.distributed as dist
@@ -63,7 +71,9 @@ def test_segmented_graph_update_two_ranks(native_lib):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=300) for _ in procs)
+    out = dict(q.get(timeout=150) for _ in procs)
+    for r in range(2):
+        assert "error" not in out[r], out[r]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
