@@ -317,8 +317,25 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
 }
 
 // ------------------------------------------------------------------------------ optimiser
-__global__ void adam_sum_kernel(float *p, const float *gpart, int ns, float *gout, float *m, float *v, int64_t n,
-                                float lr, float b1, float b2, float eps, const int32_t *step, int step_add) {
+// sum of the ns split-K partial copies of element i, in copy order (so the result does not depend
+// on how the loads are batched): eight independent loads in flight per step instead of a
+// dependent chain of ns
+__device__ __forceinline__ float sum_copies(const float *__restrict__ gpart, int ns, int64_t n, int64_t i) {
+    float gi = gpart[i];
+    int s = 1;
+    for (; s + 8 <= ns; s += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = gpart[(int64_t)(s + u) * n + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) gi += v[u];
+    }
+    for (; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
+    return gi;
+}
+
+__global__ void adam_sum_kernel(float *p, const float *__restrict__ gpart, int ns, float *gout, float *m, float *v,
+                                int64_t n, float lr, float b1, float b2, float eps, const int32_t *step, int step_add) {
     const int t = *step + step_add;
     const double bc1 = 1.0 - pow((double)b1, (double)t);
     const double bc2 = 1.0 - pow((double)b2, (double)t);
@@ -326,8 +343,7 @@ __global__ void adam_sum_kernel(float *p, const float *gpart, int ns, float *gou
     const float bc2s = (float)sqrt(bc2);
     const float w1 = (float)(1.0 - (double)b1), w2 = (float)(1.0 - (double)b2);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        float gi = gpart[i];
-        for (int s = 1; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
+        const float gi = sum_copies(gpart, ns, n, i);
         if (gout) gout[i] = gi;
         float mi = m[i];
         mi = mi + w1 * (gi - mi);               // exp_avg.lerp_(grad, 1 - beta1)
@@ -340,12 +356,9 @@ __global__ void adam_sum_kernel(float *p, const float *gpart, int ns, float *gou
     }
 }
 
-__global__ void sum_partials_kernel(float *out, const float *gpart, int ns, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        float gi = gpart[i];
-        for (int s = 1; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
-        out[i] = gi;
-    }
+__global__ void sum_partials_kernel(float *out, const float *__restrict__ gpart, int ns, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = sum_copies(gpart, ns, n, i);
 }
 
 // ------------------------------------------------------------------------------ critic head

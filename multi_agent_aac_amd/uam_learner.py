@@ -148,12 +148,13 @@ class UamReplayMemory:
 
 
 def _init_adam_state(opt):
-    """Device-side Adam state before the first step (so a graph can be captured from step 1) with a
-    float64 step counter: capturable Adam computes its bias corrections from this tensor, and the
-    default float32 counter would round 1 - 0.999**t to 7 digits in a float64 learner."""
+    """Device-side Adam state before the first step, so a graph can be captured from step 1.  The
+    fused kernel keeps a float32 step counter (integers are exact in it) and computes the bias
+    corrections 1 - beta^t in float64 for float64 parameters (the non-fused capturable path would
+    round them to float32: 7 digits)."""
     for group in opt.param_groups:
         for p in group["params"]:
-            opt.state[p] = {"step": torch.zeros((), dtype=F64, device=p.device),
+            opt.state[p] = {"step": torch.zeros((), dtype=torch.float32, device=p.device),
                             "exp_avg": torch.zeros_like(p, memory_format=torch.preserve_format),
                             "exp_avg_sq": torch.zeros_like(p, memory_format=torch.preserve_format)}
 
@@ -186,8 +187,10 @@ class MADDPG:
             p.requires_grad_(False)
         self.GAMMA, self.tau = float(gamma), float(tau)
         cap = self.device.type == "cuda"
-        self.critic_optimizer = torch.optim.Adam(self.critics.parameters(), lr=cr_lr, capturable=cap, foreach=True)
-        self.actor_optimizer = torch.optim.Adam(self.actors.parameters(), lr=ac_lr, capturable=cap, foreach=True)
+        # fused Adam: one kernel per optimizer step (capturable on the device)
+        kw = dict(capturable=True, fused=True) if cap else dict(foreach=False)
+        self.critic_optimizer = torch.optim.Adam(self.critics.parameters(), lr=cr_lr, **kw)
+        self.actor_optimizer = torch.optim.Adam(self.actors.parameters(), lr=ac_lr, **kw)
         if cap:
             for opt in (self.critic_optimizer, self.actor_optimizer):
                 _init_adam_state(opt)
@@ -223,11 +226,10 @@ class MADDPG:
         return a
 
     def _soft_update(self):
-        """soft_update (UAM/maddpg:21-25): target = target (1 - tau) + source tau."""
+        """soft_update (UAM/maddpg:21-25): target <- target (1 - tau) + source tau, one foreach
+        kernel per network (lerp: target + tau (source - target), the same value to rounding)."""
         for tgt, src in ((self.critics_target, self.critics), (self.actors_target, self.actors)):
-            tp, sp = list(tgt.parameters()), [p.detach() for p in src.parameters()]
-            torch._foreach_mul_(tp, 1.0 - self.tau)
-            torch._foreach_add_(tp, torch._foreach_mul(sp, self.tau))
+            torch._foreach_lerp_(list(tgt.parameters()), [p.detach() for p in src.parameters()], self.tau)
 
     def _allreduce_grads(self, module):
         if self.world > 1:
@@ -247,13 +249,21 @@ class MADDPG:
             target = (f["rew"][:, 0] + self.GAMMA * q_next * (1 - f["done"][:, 0])).unsqueeze(1)
         q = self.critics(s, f["act"])
         loss_q = nn.MSELoss()(q, target.detach())
-        self.critic_optimizer.zero_grad(set_to_none=False)
+        torch._foreach_zero_(self._cgrads)
         loss_q.backward()
         self._allreduce_grads(self.critics)
         self.critic_optimizer.step()
-        loss_a = -self.critics(s, self.actors(s)).mean()
-        self.actor_optimizer.zero_grad(set_to_none=False)
-        loss_a.backward()
+        # the actor loss back-propagates through the critic only for d/da: the reference also
+        # accumulates critic weight gradients there, which the next critic zero_grad discards
+        for p in self.critics.parameters():
+            p.requires_grad_(False)
+        try:
+            loss_a = -self.critics(s, self.actors(s)).mean()
+            torch._foreach_zero_(self._agrads)
+            loss_a.backward()
+        finally:
+            for p in self.critics.parameters():
+                p.requires_grad_(True)
         self._allreduce_grads(self.actors)
         self.actor_optimizer.step()
         self._soft_update()
@@ -267,6 +277,7 @@ class MADDPG:
         return self._static[key]
 
     def _sampled_core(self, rep, B, idx=None):
+        self._init_grads()
         bidx, rows = self._buffers(rep, B)
         if idx is None:
             ops.replay_sample(rep.meta, B, rep.seed, rep.counter, bidx)
@@ -280,6 +291,8 @@ class MADDPG:
             for p in m.parameters():
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
+        self._agrads = [p.grad for p in self.actors.parameters()]
+        self._cgrads = [p.grad for p in self.critics.parameters()]
 
     def capture(self, B, rep):
         """Capture one update (sample -> gather -> critic step -> actor step -> soft update) into a HIP
