@@ -76,6 +76,19 @@ int aac_uam_auto_reset(aac_uam *env, const uint8_t *env_done_dev, const aac_uam_
  * over the no-spawn-subtracted regions on the start's side of the runway. */
 int aac_uam_bank_build(int32_t n, int32_t N, uint64_t seed, double *start, double *goal, int32_t *clouds);
 
+/* Batched choose_action of the UAM learner (UAM/maddpg:597-676) on the fp64 matrix cores:
+ * ActorNetwork_TwoPortion (UAM/nets:167-190) over R = E * N rows own double[R][7], radar
+ * double[R][18] with torch nn.Linear weights (w1 [64][7], w2 [64][18], w3 [128][128], w4 [2][128],
+ * row-major, float64), then (noisy != 0) + randn * var and clamp to [-1, 1], var from the row's
+ * env episode[r / N] (get_custom_linear_scaling_factor, UAM/maddpg:1399-1406); counter is a
+ * device uint64 incremented after the launch.  out double[R][2]. */
+int aac_uam_actor(const double *own, const double *radar, int32_t R, const double *w1, const double *b1,
+                  const double *w2, const double *b2, const double *w3, const double *b3, const double *w4,
+                  const double *b4, double *out, int32_t N, const int32_t *episode, int32_t eps_end,
+                  double noise_start, double noise_end, uint64_t seed, uint64_t *counter, int32_t noisy,
+                  void *stream);
+const char *aac_uam_actor_last_error(void);
+
 /* Device-to-device copies of the state (NULL = skip), for tests and the reference facade. */
 int aac_uam_get_state(aac_uam *env, double *pos, double *vel, double *pre_pos, double *pre_vel, double *goal,
                       double *start, double *heading, uint8_t *reach, double *clouds, int32_t *cloud_kind,

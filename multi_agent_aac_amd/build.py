@@ -15,7 +15,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("AAC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["csrc/aac_env.hip", "csrc/aac_learn.hip", "csrc/aac_fused.hip", "csrc/aac_gru.hip", "csrc/aac_mpe.hip",
-           "csrc/aac_uam.hip", "csrc/aac_host.cpp"]
+           "csrc/aac_uam.hip", "csrc/aac_uam_actor.hip", "csrc/aac_host.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
          f"--offload-arch={ARCH}"]
 LIB = os.path.join(HERE, "libaac_env.so")

@@ -1,0 +1,202 @@
+// aac_uam_actor.hip -- the UAM learner's batched choose_action on the fp64 matrix cores
+// (include/aac_uam.h ``aac_uam_actor``).
+//
+// ActorNetwork_TwoPortion (UAM/nets:167-190) in float64 for every aircraft of every env, then the
+// exploration noise of choose_action (UAM/maddpg:597-676: act + randn * var, clamp to [-1, 1],
+// var = get_custom_linear_scaling_factor of the env's own episode, UAM/maddpg:1399-1406):
+//   h_o = relu(W1 own + b1) (7 -> 64), h_r = relu(W2 radar + b2) (18 -> 64),
+//   h = relu(W3 [h_o | h_r] + b3) (128 -> 128), a = tanh(W4 h + b4) (128 -> 2).
+// One wave per 16-row block: v_mfma_f64_16x16x4_f64 for the three wide layers (A fragments of
+// the input rows from global memory, then from the wave's LDS slab of [h_o | h_r]; B fragments
+// of the weights from L1 / L2, shared by four column tiles at a time so four accumulators are
+// in flight), the 128 -> 2 output layer as per-lane partial dots reduced over the 16 lanes that
+// hold one row.  The torch form of the same forward is ~13 launches with 64- and 128-wide
+// float64 intermediates in HBM.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <string>
+
+#include "../../include/aac_uam.h"
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int HLD = 132;     // LDS row stride (doubles) of a wave's 16 x 128 hidden slab
+
+thread_local std::string g_aerr;
+
+__host__ __device__ inline uint64_t amix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct ActorArgs {
+    const double *own, *radar, *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4;
+    double *out;
+    int R, N;
+    const int32_t *episode;
+    int eps_end, noisy;
+    double noise_start, noise_end;
+    uint64_t seed;
+    const uint64_t *counter;
+};
+
+// C tile of one 16-wide column block of a layer with K-contiguous weight rows W[o][k]: A
+// fragments from ``a_of(k)`` (this lane's row l & 15), four column tiles at once
+template <int KSTEPS, typename AF>
+__device__ __forceinline__ void layer4(const double *W, int ldw, int K, int o0, int lane, AF a_of, d4 acc[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+    const int kl = lane >> 4, ol = lane & 15;
+#pragma unroll 4
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int k = 4 * s + kl;
+        const double a = a_of(k);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const double b = k < K ? W[(size_t)(o0 + 16 * c + ol) * ldw + k] : 0.0;
+            acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) uam_actor_kernel(ActorArgs A) {
+    __shared__ double slab[4][16 * HLD];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double *H = slab[w];
+    const int rl = lane & 15, kl = lane >> 4;
+    const uint64_t ctr = A.noisy ? *A.counter : 0;
+    const int nblk = (A.R + 15) / 16;
+    for (int blk = blockIdx.x * 4 + w; blk < nblk; blk += gridDim.x * 4) {
+        // the slab is rewritten below; this wave's reads of the previous block come first (the
+        // LDS executes one wave's instructions in order, the clobber keeps the compiler's order)
+        asm volatile("" ::: "memory");
+        const int r0 = blk * 16;
+        const int ra = r0 + rl;                      // this lane's A row
+        const bool rin = ra < A.R;
+        d4 acc[4];
+        // h_o = relu(W1 own + b1): K = 7 (2 steps), 64 outputs = four column tiles
+        layer4<2>(A.w1, 7, 7, 0, lane, [&](int k) { return (rin && k < 7) ? A.own[(size_t)ra * 7 + k] : 0.0; }, acc);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = 16 * c + rl;
+                const double v = acc[c][j] + A.b1[col];
+                H[(kl + 4 * j) * HLD + col] = v > 0.0 ? v : 0.0;
+            }
+        // h_r = relu(W2 radar + b2): K = 18 (5 steps)
+        layer4<5>(A.w2, 18, 18, 0, lane, [&](int k) { return (rin && k < 18) ? A.radar[(size_t)ra * 18 + k] : 0.0; },
+                  acc);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = 16 * c + rl;
+                const double v = acc[c][j] + A.b2[col];
+                H[(kl + 4 * j) * HLD + 64 + col] = v > 0.0 ? v : 0.0;
+            }
+        asm volatile("" ::: "memory");      // slab writes before the other lanes' A reads
+        // h = relu(W3 [h_o | h_r] + b3) in two passes of four column tiles; the output layer's
+        // partial dots p[o][j] (row kl + 4 j) accumulate over this lane's 8 columns
+        double p0[4] = {0.0, 0.0, 0.0, 0.0}, p1[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            layer4<32>(A.w3, 128, 128, 64 * half, lane, [&](int k) { return H[rl * HLD + k]; }, acc);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int col = 64 * half + 16 * c + rl;
+                const double bb = A.b3[col], u0 = A.w4[col], u1 = A.w4[128 + col];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    double v = acc[c][j] + bb;
+                    v = v > 0.0 ? v : 0.0;
+                    p0[j] = fma(u0, v, p0[j]);
+                    p1[j] = fma(u1, v, p1[j]);
+                }
+            }
+        }
+        // reduce over the 16 lanes of a row group (lane & 15), then lane (rl = 0) of group kl
+        // finishes rows kl + 4 j
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                p0[j] += __shfl_xor(p0[j], m, 64);
+                p1[j] += __shfl_xor(p1[j], m, 64);
+            }
+        if (rl < 4) {
+            // lane rl of group kl writes row kl + 4 rl (selects, not a dynamic register index)
+            const double s0 = rl == 0 ? p0[0] : (rl == 1 ? p0[1] : (rl == 2 ? p0[2] : p0[3]));
+            const double s1 = rl == 0 ? p1[0] : (rl == 1 ? p1[1] : (rl == 2 ? p1[2] : p1[3]));
+            const int r = r0 + kl + 4 * rl;
+            if (r < A.R) {
+                double a0 = tanh(s0 + A.b4[0]), a1 = tanh(s1 + A.b4[1]);
+                if (A.noisy) {
+                    const int e = r / A.N;
+                    const int ep = A.episode ? A.episode[e] : 1;
+                    double var;
+                    if (ep <= A.eps_end) {
+                        const double slope = (A.noise_end - A.noise_start) / (double)(A.eps_end - 1);
+                        var = A.noise_start + slope * (double)(ep - 1);
+                    } else {
+                        var = A.noise_end;
+                    }
+                    const uint64_t h1 = amix64(amix64(amix64(A.seed) ^ ctr) ^ (uint64_t)(2 * (int64_t)r));
+                    const uint64_t h2 = amix64(h1 ^ 0xD1B54A32D192ED03ull);
+                    const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
+                    const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+                    const double rr = sqrt(-2.0 * log(u1));
+                    a0 = fmin(fmax(a0 + rr * cos(6.283185307179586 * u2) * var, -1.0), 1.0);
+                    a1 = fmin(fmax(a1 + rr * sin(6.283185307179586 * u2) * var, -1.0), 1.0);
+                }
+                A.out[2 * (size_t)r] = a0;
+                A.out[2 * (size_t)r + 1] = a1;
+            }
+        }
+    }
+}
+
+__global__ void actor_counter_kernel(uint64_t *counter) { *counter += 1; }
+
+}  // namespace
+
+extern "C" {
+
+const char *aac_uam_actor_last_error(void) { return g_aerr.c_str(); }
+
+int aac_uam_actor(const double *own, const double *radar, int32_t R, const double *w1, const double *b1,
+                  const double *w2, const double *b2, const double *w3, const double *b3, const double *w4,
+                  const double *b4, double *out, int32_t N, const int32_t *episode, int32_t eps_end,
+                  double noise_start, double noise_end, uint64_t seed, uint64_t *counter, int32_t noisy,
+                  void *stream) {
+    if (R <= 0) return 0;
+    if (!own || !radar || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !w4 || !b4 || !out || N <= 0) {
+        g_aerr = "aac_uam_actor: null argument or N <= 0";
+        return AAC_E_INVALID;
+    }
+    if (noisy && (!counter || eps_end < 2)) {
+        g_aerr = "aac_uam_actor: noisy needs a counter and eps_end >= 2";
+        return AAC_E_INVALID;
+    }
+    ActorArgs A{own, radar, w1, b1, w2, b2, w3, b3, w4, b4, out, R, N, episode, eps_end, noisy ? 1 : 0,
+                noise_start, noise_end, seed, counter};
+    const int nblk = (R + 15) / 16;
+    int wgs = (nblk + 3) / 4;
+    wgs = wgs > 2048 ? 2048 : wgs;
+    hipLaunchKernelGGL(uam_actor_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A);
+    if (noisy) hipLaunchKernelGGL(actor_counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_aerr = std::string("aac_uam_actor: ") + hipGetErrorString(e);
+        return AAC_E_HIP;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -18,10 +18,13 @@ transitions per env step into a device fp64 ring), ``update`` (one update_myown,
 captured HIP graph).  Reference API (drop-in for UAM/main, E = 1): ``choose_action``,
 ``update_myown``, ``memory.push/sample/len``, ``save_model``, ``load_model``.
 
-Compute: torch fp64 GEMMs (hipBLASLt / rocBLAS drive the fp64 MFMA) and fused elementwise kernels;
-the sampler is the replay kernel of aac_learn.hip (``aac_replay_sample``).  Nothing runs on the CPU.
+Compute: ``act`` is one HIP launch (``aac_uam_actor``: the three wide layers on the fp64 matrix
+cores, output layer, tanh, noise and clamp fused); the update is torch fp64 GEMMs on the matrix
+cores and fused elementwise kernels, captured as one HIP graph; the sampler is the replay kernel
+of aac_learn.hip (``aac_replay_sample``).  Nothing runs on the CPU.
 """
 import copy
+import ctypes
 import os
 from collections import namedtuple
 
@@ -29,7 +32,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, uam
 
 F64 = torch.float64
 ROW = 7 + 18 + 2 + 1 + 1 + 7 + 18           # [own | radar | a | r | done | own' | radar']
@@ -205,8 +208,8 @@ class MADDPG:
         self._graph = None
         self._graph_B = None
         self._static = {}
-        self._noise_gen = torch.Generator(device=self.device)
-        self._noise_gen.manual_seed(int(seed or 0) * 7919 + 1)
+        self.noise_seed = int(seed or 0) * 7919 + 1
+        self.noise_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
 
     # ------------------------------------------------------------------ batched API
     def attach_replay(self, capacity, seed=0):
@@ -216,14 +219,25 @@ class MADDPG:
     @torch.no_grad()
     def act(self, own, radar, episode, noisy=True, eps_end=10000, noise_start=1.0):
         """choose_action (UAM/maddpg:597-676) for every aircraft: tanh actor + N(0, var^2) noise with
-        var from each env's own episode counter, clamped to [-1, 1].  own (E, N, 7), radar (E, N, 18)."""
+        var from each env's own episode counter, clamped to [-1, 1].  own (E, N, 7), radar (E, N, 18)
+        float64; one ``aac_uam_actor`` launch (fp64 matrix cores, noise fused)."""
         E, N = own.shape[0], own.shape[1]
-        a = self.actors([own.reshape(-1, 7), radar.reshape(-1, 18)]).view(E, N, 2)
-        if noisy:
-            var = noise_scale(episode, eps_end, noise_start).view(E, 1, 1)
-            z = torch.randn(a.shape, dtype=F64, device=a.device, generator=self._noise_gen)
-            a = torch.clamp(a + z * var, -1.0, 1.0)
-        return a
+        for t, w in ((own, 7), (radar, 18)):
+            assert t.is_contiguous() and t.dtype == F64 and t.device == self.device and t.shape[-1] == w
+        if episode is not None:
+            assert episode.dtype == torch.int32 and episode.numel() == E
+        out = torch.empty(E, N, 2, dtype=F64, device=self.device)
+        a = self.actors
+        ws = [a.own_fc[0].weight, a.own_fc[0].bias, a.own_grid[0].weight, a.own_grid[0].bias,
+              a.merge_feature[0].weight, a.merge_feature[0].bias, a.act_out[0].weight, a.act_out[0].bias]
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None   # noqa: E731
+        rc = uam.lib().aac_uam_actor(p(own), p(radar), E * N, *[p(w) for w in ws], p(out), N, p(episode),
+                                     int(eps_end), float(noise_start), 0.0, ctypes.c_uint64(self.noise_seed),
+                                     p(self.noise_counter), int(bool(noisy)),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"aac_uam_actor failed: {uam.lib().aac_uam_actor_last_error().decode()}")
+        return out
 
     def _soft_update(self):
         """soft_update (UAM/maddpg:21-25): target <- target (1 - tau) + source tau, one foreach

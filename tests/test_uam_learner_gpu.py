@@ -75,12 +75,27 @@ def test_act_and_noise_schedule(native_lib):
     ep = torch.ones(32, dtype=torch.int32, device=DEV)
     a0 = m.act(own, radar, ep, noisy=False)
     ref = m.actors([own.view(-1, 7), radar.view(-1, 18)]).view(32, 5, 2)
-    assert torch.equal(a0, ref) and a0.dtype == torch.float64
+    # aac_uam_actor (fp64 MFMA) vs the torch module: same float64 forward, summation order aside
+    torch.testing.assert_close(a0, ref, rtol=0, atol=1e-13)
+    assert a0.dtype == torch.float64
     ep[:] = 20000       # past eps_end = 10000: var = 0, no noise (UAM/maddpg:1399-1406)
-    assert torch.equal(m.act(own, radar, ep, noisy=True), torch.clamp(ref, -1, 1))
+    torch.testing.assert_close(m.act(own, radar, ep, noisy=True), torch.clamp(a0, -1, 1), rtol=0, atol=0)
     ep[:] = 1
     an = m.act(own, radar, ep, noisy=True)
     assert an.abs().max() <= 1 and not torch.equal(an, a0)
+
+
+@pytest.mark.parametrize("R", [1, 15, 16, 17, 1000, 131072])
+def test_actor_kernel_rows(native_lib, R):
+    """aac_uam_actor over ragged row counts (partial 16-row blocks, one row, the config-5 size)
+    against the float64 torch module."""
+    m, _ = _model()
+    g = torch.Generator(device=DEV).manual_seed(R)
+    own = torch.rand(R, 1, 7, dtype=torch.float64, device=DEV, generator=g) * 2 - 1
+    radar = torch.rand(R, 1, 18, dtype=torch.float64, device=DEV, generator=g) * 5
+    a = m.act(own, radar, None, noisy=False)
+    ref = m.actors([own.view(-1, 7), radar.view(-1, 18)]).view(R, 1, 2)
+    torch.testing.assert_close(a, ref, rtol=0, atol=1e-13)
 
 
 def test_reference_surface(native_lib, tmp_path):
