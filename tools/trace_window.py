@@ -1,0 +1,24 @@
+"""Per-step kernel time of the last K steps of a rocprofv3 kernel trace, steps delimited by a
+marker kernel (default the env step kernel): python tools/trace_window.py run_kernel_trace.csv
+[K] [marker]"""
+import collections
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+marker = sys.argv[3] if len(sys.argv) > 3 else "::step_kernel("
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+a, b = idx[-K - 1], idx[-1]
+seg = rows[a:b]
+busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg) / 1e3
+wall = (int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
+print(f"last {K} steps: {len(seg) / K:.1f} launches/step, kernel time {busy / K:.1f} us/step, "
+      f"wall {wall / K:.1f} us/step (GPU busy {100 * busy / wall:.1f} %)")
+agg = collections.defaultdict(lambda: [0.0, 0])
+for r in seg:
+    agg[r["Kernel_Name"][:100]][0] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 / K
+    agg[r["Kernel_Name"][:100]][1] += 1
+for n, (t, c) in sorted(agg.items(), key=lambda x: -x[1][0]):
+    print(f"{t:8.1f} us/step {c / K:5.1f} calls/step {t * K / c:7.1f} us/call  {n}")
