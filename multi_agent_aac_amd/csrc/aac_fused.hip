@@ -57,6 +57,7 @@ struct GProb {
     int amode, bmode;          // fragment load modes LV / LS / LT / LW
     int deep;                  // 4-deep prefetch ring (long chains) or none
     int wide;                  // one tile per wave, four adjacent tiles per workgroup
+    int vec;                   // the epilogue may read / write 4 columns at once (16-B aligned rows)
     int tiles_n, w_begin;      // first workgroup of this product
 };
 
@@ -84,6 +85,44 @@ __device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, in
         v = v * (1.0f - t * t);
     }
     C[(size_t)m * P.ldc + n] = v;
+}
+
+// Four adjacent columns n..n+3 of row m (n % 4 == 0): one 16-B load of the addend / mask / bias
+// and one 16-B store when the product allows it (P.vec, every column real), else element-wise.
+__device__ __forceinline__ void epilogue4(const GProb &P, float *C, float *cx, int m, int n, const float v[4]) {
+    if (m >= P.M) return;
+    if (!P.vec || n + 3 >= P.N - P.ones) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) epilogue(P, C, cx, m, n + t, v[t]);
+        return;
+    }
+#ifdef AAC_DBG_NO_STORE
+    if (v[0] != 1234.5678f) return;
+#endif
+    f4 x = {v[0], v[1], v[2], v[3]};
+    if (P.addend) x += *reinterpret_cast<const f4 *>(P.addend + (size_t)m * P.ldadd + n);
+    if (P.bias) x += *reinterpret_cast<const f4 *>(P.bias + n);
+    if (P.act == 1) {
+        x.x = x.x > 0.0f ? x.x : 0.0f;
+        x.y = x.y > 0.0f ? x.y : 0.0f;
+        x.z = x.z > 0.0f ? x.z : 0.0f;
+        x.w = x.w > 0.0f ? x.w : 0.0f;
+    } else if (P.act == 2) {
+        x = f4{tanhf(x.x), tanhf(x.y), tanhf(x.z), tanhf(x.w)};
+    }
+    if (P.mact) {
+        const f4 t = *reinterpret_cast<const f4 *>(P.mask + (size_t)m * P.ldmask + n);
+        if (P.mact == 1) {
+            x.x = t.x > 0.0f ? x.x : 0.0f;
+            x.y = t.y > 0.0f ? x.y : 0.0f;
+            x.z = t.z > 0.0f ? x.z : 0.0f;
+            x.w = t.w > 0.0f ? x.w : 0.0f;
+        } else {
+            x = f4{x.x * (1.0f - t.x * t.x), x.y * (1.0f - t.y * t.y), x.z * (1.0f - t.z * t.z),
+                   x.w * (1.0f - t.w * t.w)};
+        }
+    }
+    *reinterpret_cast<f4 *>(C + (size_t)m * P.ldc + n) = x;
 }
 
 // Fragment load modes of an operand whose rows are the MFMA row index (m for A, n for B):
@@ -227,7 +266,7 @@ __device__ __forceinline__ void tile_mma(const GProb &P, int m0, int n0, int c0,
 
 // One workgroup's share of product P with (16T)x(16T) wave tiles.
 template <int T, int DEPTH>
-__device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4][64]) {
+__device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4][64], float *tile) {
     constexpr int TW = 16 * T;
     const int s = local % P.ks;
     const int w = threadIdx.x >> 6;
@@ -279,17 +318,48 @@ __device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4
     auto row_of = [&](int i, int rho) { return pa ? m0 + T * rho + i : m0 + 16 * i + rho; };
     auto col_of = [&](int j, int c) { return pb ? n0 + T * c + j : n0 + 16 * j + c; };
     if (P.wide) {
+        // stage the wave's tile in its quarter of the reduction buffer at its true (row, col)
+        // position, then write whole 16-B row segments (the fragment layout would store single
+        // floats, 64 B per row group)
+        float *st = reinterpret_cast<float *>(red[w]);
 #pragma unroll
         for (int i = 0; i < T; ++i)
 #pragma unroll
             for (int j = 0; j < T; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    epilogue(P, C, cx, row_of(i, lk * 4 + r), col_of(j, lr), acc[i][j][r]);
+                    st[(row_of(i, lk * 4 + r) - m0) * TW + (col_of(j, lr) - n0)] = acc[i][j][r];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");       // one wave's LDS operations run in order
+#pragma unroll
+        for (int q = 0; q < TW * TW / 256; ++q) {
+            const int idx = q * 64 + lane;
+            const int rr = idx / (TW / 4), c4 = (idx % (TW / 4)) * 4;
+            const f4 x = *reinterpret_cast<const f4 *>(st + rr * TW + c4);
+            const float v[4] = {x.x, x.y, x.z, x.w};
+            epilogue4(P, C, cx, m0 + rr, n0 + c4, v);
+        }
         return;
     }
     // reduce the four waves' partial tiles in wave order, four 16x16 blocks per round; in round
     // r wave q finishes block 4r + q
+    if (T == 2) {
+        // one round; the reduced tile is staged at its true (row, col) positions so that every
+        // thread writes one 16-B row segment (the fragment layout would store single floats)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[w][q][lane] = acc[q / T][q % T];
+        __syncthreads();
+        const f4 v = ((red[0][w][lane] + red[1][w][lane]) + red[2][w][lane]) + red[3][w][lane];
+        const int i = w / T, j = w % T;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tile[(row_of(i, lk * 4 + r) - m0) * TW + (col_of(j, lr) - n0)] = v[r];
+        __syncthreads();
+        const int rr = threadIdx.x / (TW / 4), c4 = (threadIdx.x % (TW / 4)) * 4;
+        const f4 x = *reinterpret_cast<const f4 *>(tile + rr * TW + c4);
+        const float vv[4] = {x.x, x.y, x.z, x.w};
+        epilogue4(P, C, cx, m0 + rr, n0 + c4, vv);
+        return;
+    }
 #pragma unroll
     for (int r0 = 0; r0 < T * T; r0 += 4) {
 #pragma unroll
@@ -306,6 +376,7 @@ __device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4
 template <int DEPTH>
 __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     __shared__ f4 red[4][4][64];       // [wave][block of the round][lane]
+    __shared__ float tile[32 * 32];    // the reduced 32x32 tile, row-major, for 16-B stores
 #ifdef AAC_DBG_EMPTY                   // timing probes only: the launch floor of this grid
     if (g.n > 0) return;
 #endif
@@ -313,7 +384,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     int pi = 0;
     while (pi + 1 < g.n && wg >= g.p[pi + 1].w_begin) ++pi;
     const GProb &P = g.p[pi];
-    gemm_tile<2, DEPTH>(P, wg - P.w_begin, red);
+    gemm_tile<2, DEPTH>(P, wg - P.w_begin, red, tile);
 }
 
 // ------------------------------------------------------------------------------ optimiser
@@ -772,6 +843,7 @@ const int g_depth = std::min(2, std::max(1, env_int("AAC_GEMM_DEPTH", 2)));
 const int g_deep_tiles = env_int("AAC_GEMM_DEEP_TILES", 1024);
 const int g_wide_tiles = env_int("AAC_GEMM_WIDE_TILES", 2048);
 const int g_lw = env_int("AAC_GEMM_LW", 1);                  // row-contiguous operands by 4T-B loads
+const int g_vec = env_int("AAC_GEMM_VEC", 1);                // 16-B epilogue rows
 int g_dump = env_int("AAC_GEMM_DUMP", 0);      // print the plans of the first g_dump launches
 
 int plan(const aac_gemm_prob *in, int n, GBatch &g) {
@@ -812,6 +884,9 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
                         : (!s.ones && s.ldb % 4 == 0 && s.K % 4 == 0 && aligned16(s.B) ? LV : LS);
         const int tm = (s.M + WT - 1) / WT, tn = (s.N + WT - 1) / WT;
         d.tiles_n = tn;
+        d.vec = g_vec && (!s.C || (aligned16(s.C) && s.ldc % 4 == 0)) && (!s.addend || (aligned16(s.addend) && s.ldadd % 4 == 0)) &&
+                (!s.mask || (aligned16(s.mask) && s.ldmask % 4 == 0)) && (!s.bias || aligned16(s.bias)) &&
+                (ks <= 1 || (s.split_stride % 4 == 0));
         // large products need no K cut inside a workgroup: one tile per wave
         d.wide = ks == 1 && tm * tn >= g_wide_tiles;
         {

@@ -26,6 +26,9 @@ CASES = [  # M, N, K, ta, tb, ones, act, mact, addend
     (5120, 2, 256, 0, 1, 0, 2, 0, False),
     (5120, 64, 64, 0, 0, 0, 0, 1, True),
     (97, 129, 33, 1, 1, 0, 0, 2, False),
+    (25600, 256, 192, 0, 1, 0, 1, 0, True),      # >= 2048 tiles: one tile per wave (wide), 16-B epilogue
+    (20480, 130, 64, 0, 1, 0, 2, 1, False),      # wide, unaligned rows: element-wise epilogue
+    (20480, 100, 64, 0, 1, 0, 1, 0, True),       # wide, 16-B rows with a ragged last column group
 ]
 
 
