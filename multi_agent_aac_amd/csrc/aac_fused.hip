@@ -434,6 +434,7 @@ __global__ void sum_partials_kernel(float *out, const float *__restrict__ gpart,
 
 // ------------------------------------------------------------------------------ critic head
 using aacw::wsum;
+using aacw::wsum_n;
 
 
 __global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, int ldh, int M,
@@ -524,16 +525,44 @@ __global__ void __launch_bounds__(256) actor_out_bwd_kernel(const float *__restr
 constexpr int WS = 68;
 __device__ __forceinline__ float matvec_row(const float *w, const f4 *x4, int lane) {
     const f4 *wr = reinterpret_cast<const f4 *>(w + lane * WS);
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;     // four independent chains
+    // four independent chains as two packed pairs: the (x, y) and (z, w) halves of the 16-B LDS
+    // reads are register pairs already, so each step is two v_pk_fma_f32 with no operand moves
+    // (four scalar chains made the compiler re-pair them, ~3x the VALU instructions)
+    f2 p = {0.0f, 0.0f}, q = {0.0f, 0.0f};
 #pragma unroll
     for (int o4 = 0; o4 < 16; ++o4) {
         const f4 a = wr[o4], b = x4[o4];
-        a0 = fmaf(a.x, b.x, a0);
-        a1 = fmaf(a.y, b.y, a1);
-        a2 = fmaf(a.z, b.z, a2);
-        a3 = fmaf(a.w, b.w, a3);
+        p = __builtin_elementwise_fma(a.xy, b.xy, p);
+        q = __builtin_elementwise_fma(a.zw, b.zw, q);
     }
-    return (a0 + a1) + (a2 + a3);
+    return (p.x + p.y) + (q.x + q.y);
+}
+
+// Weight staging: a 64x64 row-major matrix is 1024 float4 loads, four per thread.  Every load of
+// the workgroup's share is issued before the first LDS store (stage_load for all matrices, then
+// stage_store): interleaved, the compiler waits on each load before its store and the staging
+// pays one memory round trip per 512 floats, ~10 us before the first row.
+__device__ __forceinline__ void stage_load(const float *src, f4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e4 = threadIdx.x + 256 * i;
+        v[i] = *reinterpret_cast<const f4 *>(src + (e4 >> 4) * 64 + (e4 & 15) * 4);
+    }
+}
+
+__device__ __forceinline__ void stage_store(float *dst, const f4 (&v)[4], bool transpose) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e4 = threadIdx.x + 256 * i, r = e4 >> 4, c = (e4 & 15) * 4;
+        if (transpose) {
+            dst[(c + 0) * WS + r] = v[i].x;
+            dst[(c + 1) * WS + r] = v[i].y;
+            dst[(c + 2) * WS + r] = v[i].z;
+            dst[(c + 3) * WS + r] = v[i].w;
+        } else {
+            *reinterpret_cast<f4 *>(dst + r * WS + c) = v[i];
+        }
+    }
 }
 
 template <int KM>
@@ -547,12 +576,6 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
     __shared__ f4 wq4[64 * WS / 4], wv4[64 * WS / 4];
     __shared__ f4 buf4[4][16];
     float *wqs = reinterpret_cast<float *>(wq4), *wvs = reinterpret_cast<float *>(wv4);
-    for (int e = threadIdx.x; e < 64 * 16; e += 256) {
-        const int row = e >> 4, c4 = (e & 15) * 4;
-        *reinterpret_cast<f4 *>(wqs + row * WS + c4) = *reinterpret_cast<const f4 *>(Wqk + row * 64 + c4);
-        *reinterpret_cast<f4 *>(wvs + row * WS + c4) = *reinterpret_cast<const f4 *>(Wv + row * 64 + c4);
-    }
-    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     float *buf = reinterpret_cast<float *>(buf4[wv]);
@@ -574,6 +597,15 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
         }
     };
     if (r < R) fetch(r);
+    // the first row loads above are in flight while the weights stage
+    {
+        f4 a[4], b[4];
+        stage_load(Wqk, a);
+        stage_load(Wv, b);
+        stage_store(wqs, a, false);
+        stage_store(wvs, b, false);
+    }
+    __syncthreads();
     for (; r < R; r += nwaves) {
         float nb[KM][6];
         const float ev = e_n;
@@ -634,13 +666,6 @@ __global__ void __launch_bounds__(256) attn_block_kernel(const float *__restrict
 // (k_j.q = x_j.(Wk^T q) and sum a_j v_j = Wv sum a_j x_j), so the [rows*K][128] k|v tensor and
 // its three GEMMs (forward, dW_kv, dx) are never formed; the weight gradients dWv = dv^T xb,
 // dWk = q^T dqk, dWq = dq^T e_o are GEMM products of the saved rows.
-__device__ __forceinline__ void stage_w(float *dst, const float *src, bool transpose) {
-    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        dst[(transpose ? c : r) * WS + (transpose ? r : c)] = src[e];
-    }
-}
-
 template <int KM>
 __global__ void __launch_bounds__(256) attn_train_fwd_kernel(const float *__restrict__ eo, int lde,
                                                              const float *__restrict__ xn,
@@ -654,17 +679,16 @@ __global__ void __launch_bounds__(256) attn_train_fwd_kernel(const float *__rest
     __shared__ f4 buf4[4][16];
     float *wq = reinterpret_cast<float *>(w4[0]), *wkt = reinterpret_cast<float *>(w4[1]),
           *wv = reinterpret_cast<float *>(w4[2]);
-    stage_w(wq, Wq, false);
-    stage_w(wkt, Wk, true);
-    stage_w(wv, Wv, false);
-    __syncthreads();
     const int lane = threadIdx.x & 63, wvi = threadIdx.x >> 6;
     float *buf = reinterpret_cast<float *>(buf4[wvi]);
     const int nwaves = gridDim.x * 4;
     int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wvi);
     // software pipeline over the wave's rows: the next row's e_o / x_j / mask are loaded while
     // the current row is computed
-    float e_n = 0.0f, x_n[KM], m_n[KM];
+    // (small K keeps the six raw features of each neighbour slot: summing them inside fetch would
+    // wait for the prefetch right where it is issued)
+    constexpr bool RAW = KM <= 8;
+    float e_n = 0.0f, x_n[KM], m_n[KM], nb_n[RAW ? KM : 1][6];
     auto fetch = [&](int rr) {
         e_n = eo[(size_t)rr * lde + lane];
 #pragma unroll
@@ -672,13 +696,39 @@ __global__ void __launch_bounds__(256) attn_train_fwd_kernel(const float *__rest
             if (j >= K) continue;
             x_n[j] = xn[((size_t)rr * K + j) * 64 + lane];
             const float *nb = nei + ((size_t)rr * K + j) * 6;
-            float sum = nb[0];
+            if constexpr (RAW) {
 #pragma unroll
-            for (int i = 1; i < 6; ++i) sum += nb[i];
-            m_n[j] = sum;
+                for (int i = 0; i < 6; ++i) nb_n[j][i] = nb[i];
+            } else {
+                float sum = nb[0];
+#pragma unroll
+                for (int i = 1; i < 6; ++i) sum += nb[i];
+                m_n[j] = sum;
+            }
+        }
+    };
+    auto mask_sum = [&](int j) {
+        if constexpr (RAW) {
+            float sum = nb_n[j][0];
+#pragma unroll
+            for (int i = 1; i < 6; ++i) sum += nb_n[j][i];
+            return sum;
+        } else {
+            return m_n[j];
         }
     };
     if (r < R) fetch(r);
+    // the first row loads above are in flight while the weights stage
+    {
+        f4 a[4], b[4], c[4];
+        stage_load(Wq, a);
+        stage_load(Wk, b);
+        stage_load(Wv, c);
+        stage_store(wq, a, false);
+        stage_store(wkt, b, true);
+        stage_store(wv, c, false);
+    }
+    __syncthreads();
     for (; r < R; r += nwaves) {
         // keep the weight rows in LDS (re-read per row) instead of 192 hoisted VGPRs: occupancy
         asm volatile("" ::: "memory");
@@ -687,7 +737,7 @@ __global__ void __launch_bounds__(256) attn_train_fwd_kernel(const float *__rest
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
             x[j] = x_n[j];
-            msum[j] = m_n[j];
+            msum[j] = j < K ? mask_sum(j) : 0.0f;
         }
         if (r + nwaves < R) fetch(r + nwaves);
         buf[lane] = ev;
@@ -745,10 +795,6 @@ __global__ void __launch_bounds__(256) attn_train_bwd_kernel(const float *__rest
     __shared__ f4 buf4[4][16];
     float *wvt = reinterpret_cast<float *>(w4[0]), *wk = reinterpret_cast<float *>(w4[1]),
           *wqt = reinterpret_cast<float *>(w4[2]);
-    stage_w(wvt, Wv, true);
-    stage_w(wk, Wk, false);
-    stage_w(wqt, Wq, true);
-    __syncthreads();
     const int lane = threadIdx.x & 63, wvi = threadIdx.x >> 6;
     float *buf = reinterpret_cast<float *>(buf4[wvi]);
     const int nwaves = gridDim.x * 4;
@@ -767,6 +813,17 @@ __global__ void __launch_bounds__(256) attn_train_bwd_kernel(const float *__rest
         }
     };
     if (r < R) fetch(r);
+    // the first row loads above are in flight while the weights stage
+    {
+        f4 a[4], b[4], c[4];
+        stage_load(Wv, a);
+        stage_load(Wk, b);
+        stage_load(Wq, c);
+        stage_store(wvt, a, true);
+        stage_store(wk, b, false);
+        stage_store(wqt, c, true);
+    }
+    __syncthreads();
     for (; r < R; r += nwaves) {
         asm volatile("" ::: "memory");     // weight rows stay in LDS (see the forward)
         const float dvv = dv_n, qk = qk_n, e = e_n, dc = dc_n;
@@ -802,6 +859,314 @@ __global__ void __launch_bounds__(256) attn_train_bwd_kernel(const float *__rest
         buf[lane] = dq;
         const float t = matvec_row(wqt, buf4[wvi], lane);
         deo_out[(size_t)r * 64 + lane] = e > 0.0f ? dc + t : 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------------------ MFMA training attention
+// The same forward / backward with the three 64x64 projections on v_mfma_f32_16x16x4_f32 (K <= 8).
+// A workgroup takes 16 rows per block and wave w owns output features 16w..16w+15 of every
+// projection.  The projections run transposed (Y^T = W X^T, the block's rows on the MFMA's n axis),
+// so a result lands with lane & 15 = row and four consecutive features per lane (16-B stores), and
+// the next projection reads it back from a [feature][row] LDS image as its B operand.  The weight
+// fragments (16 floats per projection per lane) are loaded once per workgroup; the per-row form
+// above re-reads each 16 KB weight matrix from LDS for every row (LDS-bound).  In step s, lane
+// group h = lane >> 4 carries k index 16h + s, so fragments that are contiguous along k are four
+// 16-B loads.  The softmax stage keeps the per-row form (wave w: rows 4w..4w+3, lane = feature);
+// its neighbour rows are loaded at the start of the block so their latency hides under the
+// projections.
+#ifdef AAC_ATTN_STAMPS
+// phase timestamps of workgroup 0 (probe builds only: tools/attn_stamps.sh)
+__device__ unsigned long long g_attn_st[16];
+#define ASTAMP(i)                                                                                        \
+    do {                                                                                                  \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_attn_st[i] = __builtin_amdgcn_s_memtime();           \
+    } while (0)
+#else
+#define ASTAMP(i) \
+    do {          \
+    } while (0)
+#endif
+constexpr int TS = 17;          // row stride of the [feature][16 rows] LDS images (conflict-free reads)
+constexpr int QS = 68;          // row stride of the [16 rows][feature] LDS images (16-B aligned rows)
+
+__device__ __forceinline__ void ld16(const float *p, float (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f4 t = *reinterpret_cast<const f4 *>(p + 4 * i);
+        v[4 * i] = t.x;
+        v[4 * i + 1] = t.y;
+        v[4 * i + 2] = t.z;
+        v[4 * i + 3] = t.w;
+    }
+}
+
+// weight fragments: 16 scalar loads (the parameter views of the flat buffers need not be 16-B aligned)
+__device__ __forceinline__ void ld16w(const float *p, float (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = p[i];
+}
+
+// one 16x16 output tile over k = 64: a k-ordered f32 fma chain per element
+__device__ __forceinline__ f4 mfma_k64(const float (&a)[16], const float (&b)[16]) {
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+    return acc;
+}
+
+// B fragments from a [feature][row] LDS image
+__device__ __forceinline__ void lds_bfrag(const float *img, int h, int n, float (&b)[16]) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) b[s] = img[(16 * h + s) * TS + n];
+}
+
+// the six neighbour features of slot `lane` of row `row` (lanes >= K hold zeros), for the mask sum
+__device__ __forceinline__ void ld_nei6(const float *nei, int row, int K, int lane, float (&nb)[6]) {
+    if (lane < K) {
+        const f2 *p = reinterpret_cast<const f2 *>(nei + ((size_t)row * K + lane) * 6);
+        const f2 a = p[0], b = p[1], c = p[2];
+        nb[0] = a.x;
+        nb[1] = a.y;
+        nb[2] = b.x;
+        nb[3] = b.y;
+        nb[4] = c.x;
+        nb[5] = c.y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) nb[i] = 0.0f;
+    }
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256) attn_mfma_fwd_kernel(const float *__restrict__ eo, int lde,
+                                                            const float *__restrict__ xn,
+                                                            const float *__restrict__ nei,
+                                                            const float *__restrict__ Wq, const float *__restrict__ Wk,
+                                                            const float *__restrict__ Wv, float *__restrict__ q_out,
+                                                            float *__restrict__ qk_out, float *__restrict__ alpha,
+                                                            float *__restrict__ xb_out, float *__restrict__ vout,
+                                                            int ldv, int R, int K) {
+    __shared__ float sQ[64 * TS], sX[64 * TS];
+    __shared__ f4 sQK4[16 * QS / 4];
+    float *sQK = reinterpret_cast<float *>(sQK4);
+    ASTAMP(0);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
+    const int fo = 16 * w + 4 * h;                   // this lane's four output features
+    const int nblk = (R + 15) / 16;
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int r0 = blk * 16, r = r0 + n;
+        const bool rin = r < R;
+        const int rc = rin ? r : R - 1;
+        // loads in the order the stages consume them (the wave's load counter retires in order):
+        // e_o rows and Wq fragments, then Wk (stage 2), the softmax stage's rows, Wv (stage 3).
+        // Out-of-range rows / slots read a clamped in-range address; a row >= R only feeds its own
+        // (discarded) MFMA column, and slots j >= K are masked where they are consumed (a select
+        // here would wait for each load right after issuing it).
+        // A fragments: q^T = Wq e^T (A = Wq[o][k]), qk^T = Wk^T q^T (A = Wk[o][i] at [i][o]), v^T = Wv xb^T
+        float b[16], aq[16], ak[16], av[16];
+        ld16(eo + (size_t)rc * lde + 16 * h, b);
+        ld16w(Wq + (16 * w + n) * 64 + 16 * h, aq);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) ak[s] = Wk[(16 * h + s) * 64 + 16 * w + n];
+        float x[4][KM], nb[4][6];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = r0 + 4 * w + i;
+            const bool ok = row < R;
+            const int rr = ok ? row : R - 1;
+#pragma unroll
+            for (int j = 0; j < KM; ++j) x[i][j] = xn[((size_t)rr * K + (j < K ? j : K - 1)) * 64 + lane];
+            const f2 *pn = reinterpret_cast<const f2 *>(nei + ((size_t)rr * K + (lane < K ? lane : K - 1)) * 6);
+            const f2 n0 = pn[0], n1 = pn[1], n2 = pn[2];
+            nb[i][0] = n0.x;
+            nb[i][1] = n0.y;
+            nb[i][2] = n1.x;
+            nb[i][3] = n1.y;
+            nb[i][4] = n2.x;
+            nb[i][5] = n2.y;
+        }
+        ld16w(Wv + (16 * w + n) * 64 + 16 * h, av);
+        // q^T = Wq e_o^T
+        f4 acc = mfma_k64(aq, b);
+        ASTAMP(1);
+        if (rin) *reinterpret_cast<f4 *>(q_out + (size_t)r * 64 + fo) = acc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sQ[(fo + j) * TS + n] = acc[j];
+        __syncthreads();
+        // qk^T = Wk^T q^T
+        ASTAMP(2);
+        lds_bfrag(sQ, h, n, b);
+        acc = mfma_k64(ak, b);
+        if (rin) *reinterpret_cast<f4 *>(qk_out + (size_t)r * 64 + fo) = acc;
+        *reinterpret_cast<f4 *>(sQK + n * QS + fo) = acc;
+        __syncthreads();
+        ASTAMP(3);
+        // masked softmax and xb = sum_j a_j x_j for the wave's four rows at once, lane = feature: the
+        // 4 KM scores are one batched DPP reduction, and slots j >= K (zero x, zero mask) drop out
+        // arithmetically, so the stage has no branches on K
+        {
+            float p[4 * KM], qk4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) qk4[i] = sQK[(4 * w + i) * QS + lane];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    x[i][j] = j < K ? x[i][j] : 0.0f;
+                    p[i * KM + j] = x[i][j] * qk4[i];
+                }
+            wsum_n(p);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int rl = 4 * w + i, row = r0 + rl;
+                float ms = nb[i][0];
+#pragma unroll
+                for (int t = 1; t < 6; ++t) ms += nb[i][t];
+                float sc[KM];
+                float mx = -INFINITY;
+                unsigned valid = 0;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    sc[j] = p[i * KM + j] / 8.0f;
+                    const bool v =
+                        j < K && __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ms), j)) != 0.0f;
+                    valid |= (v ? 1u : 0u) << j;
+                    mx = (v && sc[j] > mx) ? sc[j] : mx;
+                }
+                float den = 0.0f;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    const float e = (valid >> j & 1) ? __expf(sc[j] - mx) : 0.0f;
+                    sc[j] = e;
+                    den += e;
+                }
+                float xb = 0.0f, al = 0.0f;
+                const float inv = 1.0f / den;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    const float a = (valid >> j & 1) ? sc[j] * inv : 0.0f;
+                    xb = fmaf(a, x[i][j], xb);
+                    al = lane == j ? a : al;
+                }
+                if (row < R) {
+                    if (lane < K) alpha[(size_t)row * K + lane] = al;
+                    xb_out[(size_t)row * 64 + lane] = xb;
+                }
+                sX[lane * TS + rl] = xb;
+            }
+        }
+        __syncthreads();
+        ASTAMP(4);
+        // v^T = Wv xb^T
+        lds_bfrag(sX, h, n, b);
+        acc = mfma_k64(av, b);
+        if (rin) *reinterpret_cast<f4 *>(vout + (size_t)r * ldv + fo) = acc;
+        ASTAMP(5);
+    }
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256) attn_mfma_bwd_kernel(const float *__restrict__ dv, int lddv,
+                                                            const float *__restrict__ xn,
+                                                            const float *__restrict__ alpha,
+                                                            const float *__restrict__ qk_in,
+                                                            const float *__restrict__ eo, int lde,
+                                                            const float *__restrict__ dcat_o, int ldd,
+                                                            const float *__restrict__ Wq, const float *__restrict__ Wk,
+                                                            const float *__restrict__ Wv, float *__restrict__ dxn,
+                                                            float *__restrict__ dqk_out, float *__restrict__ dq_out,
+                                                            float *__restrict__ deo_out, int R, int K) {
+    __shared__ float sA[64 * TS], sB[64 * TS];
+    __shared__ f4 sD4[16 * QS / 4];
+    float *sD = reinterpret_cast<float *>(sD4);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
+    const int fo = 16 * w + 4 * h;
+    const int nblk = (R + 15) / 16;
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int r0 = blk * 16, r = r0 + n;
+        const bool rin = r < R;
+        const int rc = rin ? r : R - 1;
+        // loads in consumption order (see the forward): dv rows + Wv^T, the softmax-backward rows,
+        // Wk, Wq^T, and the e_o / dcat_o rows of the last stage
+        // dxb^T = Wv^T dv^T (A = Wv[o][i] at [i][o]), dq^T = Wk dqk^T (A = Wk[o][i]), t^T = Wq^T dq^T
+        float b[16], avt[16], ak[16], aqt[16];
+        ld16(dv + (size_t)rc * lddv + 16 * h, b);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) avt[s] = Wv[(16 * h + s) * 64 + 16 * w + n];
+        float x[4][KM], al[4][KM], qkv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = r0 + 4 * w + i;
+            const int rr = row < R ? row : R - 1;
+            qkv[i] = qk_in[(size_t)rr * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                const int jj = j < K ? j : K - 1;
+                x[i][j] = xn[((size_t)rr * K + jj) * 64 + lane];
+                al[i][j] = alpha[(size_t)rr * K + jj];
+            }
+        }
+        ld16w(Wk + (16 * w + n) * 64 + 16 * h, ak);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) aqt[s] = Wq[(16 * h + s) * 64 + 16 * w + n];
+        const f4 e = *reinterpret_cast<const f4 *>(eo + (size_t)rc * lde + fo);
+        const f4 dc = *reinterpret_cast<const f4 *>(dcat_o + (size_t)rc * ldd + fo);
+        // dxb^T = Wv^T dv^T
+        f4 acc = mfma_k64(avt, b);
+        *reinterpret_cast<f4 *>(sD + n * QS + fo) = acc;
+        __syncthreads();
+        // softmax backward for the wave's four rows at once, lane = feature (batched da sums; slots
+        // j >= K get zero alpha, so they add nothing)
+        {
+            float p[4 * KM], dxb4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dxb4[i] = sD[(4 * w + i) * QS + lane];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    al[i][j] = j < K ? al[i][j] : 0.0f;
+                    p[i * KM + j] = x[i][j] * dxb4[i];
+                }
+            wsum_n(p);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int rl = 4 * w + i, row = r0 + rl;
+                const float dxb = dxb4[i], qk = qkv[i];
+                float S = 0.0f;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) S += al[i][j] * p[i * KM + j];
+                float dqk = 0.0f;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    const float ds = al[i][j] * (p[i * KM + j] - S) / 8.0f;
+                    const float g = al[i][j] * dxb + ds * qk;
+                    if (j < K && row < R) dxn[((size_t)row * K + j) * 64 + lane] = x[i][j] > 0.0f ? g : 0.0f;
+                    dqk = fmaf(ds, x[i][j], dqk);
+                }
+                if (row < R) dqk_out[(size_t)row * 64 + lane] = dqk;
+                sA[lane * TS + rl] = dqk;
+            }
+        }
+        __syncthreads();
+        // dq^T = Wk dqk^T
+        lds_bfrag(sA, h, n, b);
+        acc = mfma_k64(ak, b);
+        if (rin) *reinterpret_cast<f4 *>(dq_out + (size_t)r * 64 + fo) = acc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sB[(fo + j) * TS + n] = acc[j];
+        __syncthreads();
+        // de_o = (dcat_o + Wq^T dq) * (e_o > 0)
+        lds_bfrag(sB, h, n, b);
+        acc = mfma_k64(aqt, b);
+        if (rin) {
+            f4 o;
+            o.x = e.x > 0.0f ? dc.x + acc.x : 0.0f;
+            o.y = e.y > 0.0f ? dc.y + acc.y : 0.0f;
+            o.z = e.z > 0.0f ? dc.z + acc.z : 0.0f;
+            o.w = e.w > 0.0f ? dc.w + acc.w : 0.0f;
+            *reinterpret_cast<f4 *>(deo_out + (size_t)r * 64 + fo) = o;
+        }
     }
 }
 
@@ -978,18 +1343,45 @@ int aac_actor_out_bwd(const float *df, int32_t ldf, const float *wenc, int32_t d
     return 0;
 }
 
+// MFMA training attention: 16-row blocks, a workgroup walks blocks after loading its weight fragments
+const int g_attn_mfma = env_int("AAC_ATTN_MFMA", 1);
+static int mfma_attn_grid(int R) {
+    static const int cap = std::max(1, env_int("AAC_ATTN_WGS", 1024));
+    const int nblk = (R + 15) / 16;
+    return nblk < cap ? nblk : cap;
+}
+
 static int attn_grid(int R) {
-    int wgs = (R + 15) / 16;          // ~4 rows per wave
+    static const int rows = std::max(4, env_int("AAC_ATTN_ROWS", 16));
+    int wgs = (R + rows - 1) / rows;  // ~4 rows per wave
     return wgs < 1 ? 1 : (wgs > 2048 ? 2048 : wgs);
 }
+
+#ifdef AAC_ATTN_STAMPS
+int aac_attn_stamps(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_st), sizeof(g_attn_st)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int aac_attn_train_fwd(const float *eo, int32_t lde, const float *xn, const float *nei, const float *Wq,
                        const float *Wk, const float *Wv, float *q, float *qk, float *alpha, float *xb, float *vout,
                        int32_t ldv, int32_t R, int32_t K, void *stream) {
     if (R <= 0) return 0;
     if (K < 1 || K > 32) return ffail("attn_train_fwd: 1 <= K <= 32");
-    const dim3 grid(attn_grid(R)), block(256);
     hipStream_t st = (hipStream_t)stream;
+    if (g_attn_mfma && K <= 8 && aligned16(eo) && lde % 4 == 0 && aligned16(q) &&
+        aligned16(qk) && aligned16(vout) && ldv % 4 == 0 && (reinterpret_cast<uintptr_t>(nei) & 7) == 0) {
+        const dim3 g(mfma_attn_grid(R)), b(256);
+        if (K <= 4)
+            hipLaunchKernelGGL(attn_mfma_fwd_kernel<4>, g, b, 0, st, eo, lde, xn, nei, Wq, Wk, Wv, q, qk, alpha, xb,
+                               vout, ldv, R, K);
+        else
+            hipLaunchKernelGGL(attn_mfma_fwd_kernel<8>, g, b, 0, st, eo, lde, xn, nei, Wq, Wk, Wv, q, qk, alpha, xb,
+                               vout, ldv, R, K);
+        FHIP(hipGetLastError());
+        return 0;
+    }
+    const dim3 grid(attn_grid(R)), block(256);
 #define ATF(KM) hipLaunchKernelGGL(attn_train_fwd_kernel<KM>, grid, block, 0, st, eo, lde, xn, nei, Wq, Wk, Wv, q, qk, \
                                    alpha, xb, vout, ldv, R, K)
     if (K <= 4) ATF(4);
@@ -1007,8 +1399,20 @@ int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const flo
                        void *stream) {
     if (R <= 0) return 0;
     if (K < 1 || K > 32) return ffail("attn_train_bwd: 1 <= K <= 32");
-    const dim3 grid(attn_grid(R)), block(256);
     hipStream_t st = (hipStream_t)stream;
+    if (g_attn_mfma && K <= 8 && aligned16(dv) && lddv % 4 == 0 && aligned16(eo) && lde % 4 == 0 && aligned16(dcat_o) &&
+        ldd % 4 == 0 && aligned16(dq) && aligned16(deo)) {
+        const dim3 g(mfma_attn_grid(R)), b(256);
+        if (K <= 4)
+            hipLaunchKernelGGL(attn_mfma_bwd_kernel<4>, g, b, 0, st, dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq,
+                               Wk, Wv, dxn, dqk, dq, deo, R, K);
+        else
+            hipLaunchKernelGGL(attn_mfma_bwd_kernel<8>, g, b, 0, st, dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq,
+                               Wk, Wv, dxn, dqk, dq, deo, R, K);
+        FHIP(hipGetLastError());
+        return 0;
+    }
+    const dim3 grid(attn_grid(R)), block(256);
 #define ATB(KM) hipLaunchKernelGGL(attn_train_bwd_kernel<KM>, grid, block, 0, st, dv, lddv, xn, alpha, qk, eo, lde, \
                                    dcat_o, ldd, Wq, Wk, Wv, dxn, dqk, dq, deo, R, K)
     if (K <= 4) ATB(4);

@@ -19,6 +19,27 @@ __device__ __forceinline__ float wsum(float x) {
     DPP_STEP(x, 0x143);  // row_bcast:31
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
+
+// N independent wave sums with each DPP step applied to all N values before the next: the same
+// per-value order as wsum (bit-identical results), with the step latencies overlapped
+template <int N>
+__device__ __forceinline__ void wsum_n(float (&v)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) DPP_STEP(v[k], 0xb1);
+#pragma unroll
+    for (int k = 0; k < N; ++k) DPP_STEP(v[k], 0x4e);
+#pragma unroll
+    for (int k = 0; k < N; ++k) DPP_STEP(v[k], 0x124);
+#pragma unroll
+    for (int k = 0; k < N; ++k) DPP_STEP(v[k], 0x128);
+#pragma unroll
+    for (int k = 0; k < N; ++k) DPP_STEP(v[k], 0x142);
+#pragma unroll
+    for (int k = 0; k < N; ++k) DPP_STEP(v[k], 0x143);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v[k]), 63));
+}
 #undef DPP_STEP
 
 }  // namespace aacw

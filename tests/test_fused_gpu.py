@@ -245,7 +245,7 @@ def test_fused_act_matches_actor_module(native_lib):
     np.testing.assert_allclose(got.cpu(), want.detach().cpu(), atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("K", [1, 4, 7])
+@pytest.mark.parametrize("K", [1, 4, 7, 12])       # K <= 8: MFMA kernels; 12: per-row kernels
 def test_attn_train_fwd_bwd_matches_autograd(native_lib, K):
     """Training attention kernels (in-kernel q / k / v projections) against fp64 autograd of the
     reference form (ATT/nets:186-210): v_att, and the gradients into x_j, q and e_o."""
