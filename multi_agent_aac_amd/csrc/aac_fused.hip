@@ -1170,6 +1170,103 @@ __global__ void __launch_bounds__(256) attn_mfma_bwd_kernel(const float *__restr
     }
 }
 
+// Inference attention block (aac_attn_block, K <= 4) on the same transposed 16-row MFMA scheme:
+// qk^T = Wqk e_o^T, then x_j = relu(Wn nei_j + bn), the masked softmax and xb per row (lane =
+// feature, the wave's four rows at once), then v^T = Wv xb^T.  The neighbour rows (6 floats per
+// slot, the same in every lane) are loaded at the start of the block.
+template <int KM>
+__global__ void __launch_bounds__(256) attn_mfma_block_kernel(const float *__restrict__ eo, int lde,
+                                                              const float *__restrict__ nei,
+                                                              const float *__restrict__ Wn,
+                                                              const float *__restrict__ bn,
+                                                              const float *__restrict__ Wqk,
+                                                              const float *__restrict__ Wv, float *__restrict__ out,
+                                                              int ldo, int R, int K) {
+    __shared__ float sX[64 * TS];
+    __shared__ f4 sQK4[16 * QS / 4];
+    float *sQK = reinterpret_cast<float *>(sQK4);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
+    const int fo = 16 * w + 4 * h;
+    float wn[6];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) wn[t] = Wn[lane * 6 + t];
+    const float bnl = bn[lane];
+    const int nblk = (R + 15) / 16;
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int r0 = blk * 16, r = r0 + n;
+        const bool rin = r < R;
+        const int rc = rin ? r : R - 1;
+        // loads in consumption order: e_o rows + Wqk, the neighbour rows, Wv (clamped addresses:
+        // rows >= R only feed their own discarded column, slots j >= K are masked at use)
+        float b[16], aq[16], av[16];
+        ld16(eo + (size_t)rc * lde + 16 * h, b);
+        ld16w(Wqk + (16 * w + n) * 64 + 16 * h, aq);
+        float nb[4][KM][6];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = r0 + 4 * w + i, rr = row < R ? row : R - 1;
+#pragma unroll
+            for (int j = 0; j < KM; ++j)
+#pragma unroll
+                for (int t = 0; t < 6; ++t) nb[i][j][t] = nei[((size_t)rr * K + (j < K ? j : K - 1)) * 6 + t];
+        }
+        ld16w(Wv + (16 * w + n) * 64 + 16 * h, av);
+        // qk^T = Wqk e_o^T
+        f4 acc = mfma_k64(aq, b);
+        *reinterpret_cast<f4 *>(sQK + n * QS + fo) = acc;
+        __syncthreads();
+        {
+            float p[4 * KM], x[4][KM];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float qk = sQK[(4 * w + i) * QS + lane];
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    float hh = bnl;
+#pragma unroll
+                    for (int t = 0; t < 6; ++t) hh = fmaf(wn[t], nb[i][j][t], hh);
+                    x[i][j] = (j < K && hh > 0.0f) ? hh : 0.0f;
+                    p[i * KM + j] = x[i][j] * qk;
+                }
+            }
+            wsum_n(p);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float sc[KM];
+                float mx = -INFINITY;
+                unsigned valid = 0;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    float sum = nb[i][j][0];
+#pragma unroll
+                    for (int t = 1; t < 6; ++t) sum += nb[i][j][t];
+                    sc[j] = p[i * KM + j] / 8.0f;
+                    const bool v = j < K && sum != 0.0f;
+                    valid |= (v ? 1u : 0u) << j;
+                    mx = (v && sc[j] > mx) ? sc[j] : mx;
+                }
+                float den = 0.0f;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    const float e = (valid >> j & 1) ? __expf(sc[j] - mx) : 0.0f;
+                    sc[j] = e;
+                    den += e;
+                }
+                const float inv = 1.0f / den;
+                float xb = 0.0f;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) xb = fmaf((valid >> j & 1) ? sc[j] * inv : 0.0f, x[i][j], xb);
+                sX[lane * TS + 4 * w + i] = xb;
+            }
+        }
+        __syncthreads();
+        // v^T = Wv xb^T
+        lds_bfrag(sX, h, n, b);
+        acc = mfma_k64(av, b);
+        if (rin) *reinterpret_cast<f4 *>(out + (size_t)r * ldo + fo) = acc;
+    }
+}
+
 // ------------------------------------------------------------------------------ gather
 struct SFields {
     float *dst[16];
@@ -1428,6 +1525,12 @@ int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *
                    const float *Wqk, const float *Wv, float *out, int32_t ldo, int32_t R, int32_t K, void *stream) {
     if (R <= 0) return 0;
     if (K < 1 || K > 32) return ffail("attn_block: 1 <= K <= 32");
+    if (g_attn_mfma && K <= 4 && aligned16(eo) && lde % 4 == 0 && aligned16(out) && ldo % 4 == 0) {
+        hipLaunchKernelGGL(attn_mfma_block_kernel<4>, dim3(mfma_attn_grid(R)), dim3(256), 0, (hipStream_t)stream, eo,
+                           lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
+        FHIP(hipGetLastError());
+        return 0;
+    }
     // ~16 rows per wave: the 34 KB weight staging per workgroup stays small next to the rows
     int wgs = (R + 63) / 64;
     wgs = wgs < 1 ? 1 : (wgs > 2048 ? 2048 : wgs);

@@ -40,7 +40,10 @@ def main():
                                      P(xb), P(vout), 128, R, K)
     bw = lambda: fused.attn_train_bwd(P(dv), 128, P(xn), P(alpha), P(qk), P(eo), 192, P(dcat), 192, P(Wq),  # noqa
                                       P(Wk), P(Wv), P(dxn), P(dqk), P(dq), P(deo), R, K)
-    print(f"R={R} K={K} rows/wg={os.environ.get('AAC_ATTN_ROWS', 16)} fwd {timed(f):.2f} us  bwd {timed(bw):.2f} us")
+    Wn, bn, wqk, out = r(64, 6) / 2, r(64) / 8, r(64, 64) / 8, torch.empty(R, 64, device=d)
+    blk = lambda: fused.attn_block(P(eo), 192, P(nei), P(Wn), P(bn), P(wqk), P(Wv), P(out), 64, R, K)  # noqa: E731
+    print(f"R={R} K={K} rows/wg={os.environ.get('AAC_ATTN_ROWS', 16)} fwd {timed(f):.2f} us  bwd {timed(bw):.2f} us"
+          f"  block {timed(blk):.2f} us")
 
 
 if __name__ == "__main__":
