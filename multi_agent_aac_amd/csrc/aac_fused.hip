@@ -1301,8 +1301,12 @@ int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
     return v ? atoi(v) : dflt;
 }
+// (depth 3 / 4 rings measured slower: 1.296 / 1.353 vs 1.235 ms per bench step)
 const int g_depth = std::min(2, std::max(1, env_int("AAC_GEMM_DEPTH", 2)));
-const int g_deep_tiles = env_int("AAC_GEMM_DEEP_TILES", 1024);
+// the ring on every product with a chain > 2 chunks: 1.263 -> 1.230 ms per step since the
+// epilogue / attention changes (it had measured slower on small products before them)
+const int g_deep_tiles = env_int("AAC_GEMM_DEEP_TILES", 0);
+const int g_deep_chain = env_int("AAC_GEMM_DEEP_CHAIN", 2);     // ring only for chains longer than this
 const int g_wide_tiles = env_int("AAC_GEMM_WIDE_TILES", 2048);
 const int g_lw = env_int("AAC_GEMM_LW", 1);                  // row-contiguous operands by 4T-B loads
 const int g_vec = env_int("AAC_GEMM_VEC", 1);                // 16-B epilogue rows
@@ -1355,9 +1359,9 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
             const int nch = (s.K + KC - 1) / KC;
             const int per = (nch + ks - 1) / ks;
             const int chain = d.wide ? per : (per + 3) / 4;      // chunks per wave
-            // measured (tools/mb_gemm.py): the prefetch ring only pays on large products; elsewhere
-            // the occupancy of the ring-free kernel hides more latency
-            d.deep = g_depth > 1 && chain > 2 && tm * tn >= g_deep_tiles;
+            // the prefetch ring for chains longer than g_deep_chain chunks (whole-step A/B,
+            // tools/knob_sweep.sh; a tile-count threshold is kept as a knob)
+            d.deep = g_depth > 1 && chain > g_deep_chain && tm * tn >= g_deep_tiles;
         }
         d.w_begin = waves;          // in workgroups
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
