@@ -15,7 +15,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("AAC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["csrc/aac_env.hip", "csrc/aac_learn.hip", "csrc/aac_fused.hip", "csrc/aac_gru.hip", "csrc/aac_mpe.hip",
-           "csrc/aac_uam.hip", "csrc/aac_uam_actor.hip", "csrc/aac_host.cpp"]
+           "csrc/aac_uam.hip", "csrc/aac_uam_actor.hip", "csrc/aac_uam_learn.hip", "csrc/aac_host.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
          f"--offload-arch={ARCH}"]
 LIB = os.path.join(HERE, "libaac_env.so")
@@ -30,7 +30,7 @@ def _stale(target, deps):
 
 def build(force=False, verbose=False):
     srcs = [os.path.join(HERE, s) for s in SOURCES if os.path.exists(os.path.join(HERE, s))]
-    deps = srcs + [os.path.join(ROOT, "include", h) for h in ("aac_env.h", "aac_learn.h", "aac_fused.h", "aac_gru.h", "aac_mpe.h", "aac_uam.h")]
+    deps = srcs + [os.path.join(ROOT, "include", h) for h in ("aac_env.h", "aac_learn.h", "aac_fused.h", "aac_gru.h", "aac_mpe.h", "aac_uam.h", "aac_uam_learn.h")]
     deps += [os.path.join(HERE, "csrc", h) for h in ("aac_wave.h", "aac_geom.h")]
     deps = [d for d in deps if os.path.exists(d)]
     if not force and not _stale(LIB, deps):

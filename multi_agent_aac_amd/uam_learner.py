@@ -162,6 +162,245 @@ def _init_adam_state(opt):
                             "exp_avg_sq": torch.zeros_like(p, memory_format=torch.preserve_format)}
 
 
+_LL = None
+
+
+def _learn_lib():
+    """The fused-learner entry points of libaac_env.so (include/aac_uam_learn.h)."""
+    global _LL
+    if _LL is None:
+        from . import fused
+        L = uam.lib()
+        vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        L.aac_uam_learn_last_error.restype = ctypes.c_char_p
+        L.aac_gemm64_batch.argtypes = [ctypes.POINTER(fused.GemmProb), i32, vp]
+        L.aac_uam_gather.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+        L.aac_uam_head.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, i32, dbl, vp, vp, vp, vp]
+        L.aac_adam64_sum.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, vp]
+        L.aac_uam_polyak.argtypes = [vp, vp, i64, dbl, vp, vp, vp, i32, vp, vp]
+        _LL = L
+    return _LL
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {_learn_lib().aac_uam_learn_last_error().decode()}")
+
+
+def p64(t, off=0):
+    """Device address of float64 element ``off`` of tensor ``t``."""
+    return None if t is None else t.data_ptr() + 8 * off
+
+
+def prob64(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=0, mask=None, ldmask=0, mact=0, ones=0,
+           cextra=None, ksplit=1, split_stride=0):
+    """One float64 product C[M][N] = mact(act(op(A) op(B) + bias)) (aac_gemm64_prob; addresses as ints)."""
+    from . import fused
+    return fused.GemmProb(A, B, C, bias, None, mask, cextra, split_stride, M, N + ones, K, lda, ldb, ldc, 0, ldmask,
+                          ta, tb, act, mact, ones, ksplit)
+
+
+def _rebind(params, flat):
+    """Copy the parameters into ``flat`` (in order) and make each ``param.data`` a view of it."""
+    o = 0
+    for p in params:
+        n = p.numel()
+        flat[o:o + n].copy_(p.data.reshape(-1))
+        p.data = flat[o:o + n].view_as(p.data)
+        o += n
+    return o
+
+
+class FusedUamUpdate:
+    """update_myown of UAM/maddpg:304-595 on the device as ~20 launches (include/aac_uam_learn.h):
+    grouped float64 products on the fp64 matrix cores with fused bias / ReLU / tanh epilogues and
+    relu' / tanh' backward masks, weight gradients as KS partial copies over the B sampled rows
+    (bias gradients from a virtual ones column), the critic head with the TD target / mse / -mean Q
+    gradients, fused Adam on the partial sums, and one soft-update kernel for both targets.
+
+    Parameters of the four networks live in two flat float64 buffers ([critic | actor] and the
+    targets), which the torch modules view, so ``save_model`` / ``load_model`` / the torch path see
+    the same weights.  The Adam moments of this path are its own (flat ``m1`` / ``m2``, one step
+    counter), initialised from the torch optimisers' state."""
+    KS = 8
+
+    def __init__(self, m, B, rep):
+        self.m, self.B, self.rep = m, int(B), rep
+        dev = m.device
+        z = lambda *s: torch.zeros(*s, dtype=F64, device=dev)   # noqa: E731
+        cp, ap = list(m.critics.parameters()), list(m.actors.parameters())
+        nC, nA = sum(p.numel() for p in cp), sum(p.numel() for p in ap)
+        self.nC, self.nA = nC, nA
+        self.flat, self.tflat = z(nC + nA), z(nC + nA)
+        _rebind(cp + ap, self.flat)
+        _rebind(list(m.critics_target.parameters()) + list(m.actors_target.parameters()), self.tflat)
+        self.m1, self.m2 = z(nC + nA), z(nC + nA)
+        self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the torch optimisers' moments (if they stepped) carry over
+        o, steps = 0, []
+        for opt, ps in ((m.critic_optimizer, cp), (m.actor_optimizer, ap)):
+            for p in ps:
+                st = opt.state.get(p, {})
+                n = p.numel()
+                if "exp_avg" in st:
+                    self.m1[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                    self.m2[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                    steps.append(int(st["step"].item()))
+                o += n
+        if steps:
+            self.step.fill_(steps[0])
+        self.lr_c = m.critic_optimizer.param_groups[0]["lr"]
+        self.lr_a = m.actor_optimizer.param_groups[0]["lr"]
+        self.betas = m.critic_optimizer.param_groups[0]["betas"]
+        self.eps = m.critic_optimizer.param_groups[0]["eps"]
+        self.gc, self.ga = z(self.KS, nC), z(self.KS, nA)
+        B = self.B
+        self.idx = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.rows, self.xc, self.xt, self.xp = z(B, ROW), z(B, 9), z(B, 9), z(B, 9)
+        self.ha1t, self.ha2t, self.hc1t, self.hc2t = z(B, 128), z(B, 128), z(B, 128), z(B, 256)
+        self.hc1, self.hc2, self.dh1, self.dh2 = z(B, 128), z(B, 256), z(B, 128), z(B, 256)
+        self.ha1, self.ha2, self.hp1, self.hp2 = z(B, 128), z(B, 128), z(B, 128), z(B, 256)
+        self.dp1, self.dp2, self.dout, self.dha1, self.dha2 = z(B, 64), z(B, 256), z(B, 2), z(B, 128), z(B, 128)
+        self.y, self.dq, self.lq, self.la, self.loss = z(B), z(B), z(B), z(B), z(2)
+        self._launches = self._build()
+
+    def _offsets(self, module, base):
+        out, o = {}, base
+        for name, p in module.named_parameters():
+            out[name] = o
+            o += p.numel()
+        return out
+
+    def _build(self):
+        m, B, KS, L = self.m, self.B, self.KS, _learn_lib()
+        from . import fused
+        nC, nA = self.nC, self.nA
+        oc = self._offsets(m.critics, 0)
+        oa = self._offsets(m.actors, nC)
+        F, T = self.flat, self.tflat
+        c = {k: p64(F, v) for k, v in oc.items()}
+        a = {k: p64(F, v) for k, v in oa.items()}
+        ct = {k: p64(T, v) for k, v in oc.items()}
+        at = {k: p64(T, v) for k, v in oa.items()}
+        gc = {k: p64(self.gc, v) for k, v in oc.items()}
+        ga = {k: p64(self.ga, v - nC) for k, v in oa.items()}
+        R, P = self.rows, p64
+        own, g, g2 = P(R), P(R, 7), P(R, 36)
+        xc, xt, xp = P(self.xc), P(self.xt), P(self.xp)
+        RELU, TANH = 1, 2
+        Wc = lambda d, k: d[k + ".0.weight"]      # noqa: E731
+        Bc = lambda d, k: d[k + ".0.bias"]        # noqa: E731
+
+        def lin(A, lda, W, bias, C, ldc, K, N, act, M=B):
+            return prob64(A, W, C, M, N, K, lda, K, ldc, tb=1, bias=bias, act=act)
+
+        def wgrad(dY, lddy, X, ldx, M, N, Cw, Cb, stride):
+            # dW[M][N] = dY^T X over the B rows (K split into KS copies), bias gradient from the ones column
+            return prob64(dY, X, Cw, M, N, B, lddy, ldx, N, ta=1, ones=1, cextra=Cb, ksplit=KS, split_stride=stride)
+
+        def gemm(probs):
+            arr = (fused.GemmProb * len(probs))(*probs)
+            n = len(probs)
+            return lambda: _ok(L.aac_gemm64_batch(arr, n, fused._stream()), "aac_gemm64_batch")
+
+        st = self
+        launches = [
+            # replay sample + gather (UAM/maddpg:330-345)
+            lambda: ops.replay_sample(st.rep.meta, B, st.rep.seed, st.rep.counter, st.idx),
+            lambda: _ok(L.aac_uam_gather(P(st.rep.ring), st.idx.data_ptr(), B, P(R), xc, xt, xp, fused._stream()),
+                        "aac_uam_gather"),
+            # first layers of the target actor, the critic (both inputs), the target critic's radar
+            # encoder and the actor (actor weights are unchanged until the actor step)
+            gemm([lin(xt, 9, Wc(at, "own_fc"), Bc(at, "own_fc"), P(st.ha1t), 128, 7, 64, RELU),
+                  lin(g2, ROW, Wc(at, "own_grid"), Bc(at, "own_grid"), P(st.ha1t, 64), 128, 18, 64, RELU),
+                  lin(g2, ROW, Wc(ct, "SA_grid"), Bc(ct, "SA_grid"), P(st.hc1t, 64), 128, 18, 64, RELU),
+                  lin(xc, 9, Wc(c, "SA_fc"), Bc(c, "SA_fc"), P(st.hc1), 128, 9, 64, RELU),
+                  lin(g, ROW, Wc(c, "SA_grid"), Bc(c, "SA_grid"), P(st.hc1, 64), 128, 18, 64, RELU),
+                  lin(own, ROW, Wc(a, "own_fc"), Bc(a, "own_fc"), P(st.ha1), 128, 7, 64, RELU),
+                  lin(g, ROW, Wc(a, "own_grid"), Bc(a, "own_grid"), P(st.ha1, 64), 128, 18, 64, RELU)]),
+            gemm([lin(P(st.ha1t), 128, Wc(at, "merge_feature"), Bc(at, "merge_feature"), P(st.ha2t), 128, 128, 128,
+                      RELU),
+                  lin(P(st.hc1), 128, Wc(c, "merge_fc_grid"), Bc(c, "merge_fc_grid"), P(st.hc2), 256, 128, 256, RELU),
+                  lin(P(st.ha1), 128, Wc(a, "merge_feature"), Bc(a, "merge_feature"), P(st.ha2), 128, 128, 128,
+                      RELU)]),
+            # tanh action layers: target actions into xt[:, 7:9], policy actions into xp[:, 7:9]
+            gemm([lin(P(st.ha2t), 128, Wc(at, "act_out"), Bc(at, "act_out"), P(st.xt, 7), 9, 128, 2, TANH),
+                  lin(P(st.ha2), 128, Wc(a, "act_out"), Bc(a, "act_out"), P(st.xp, 7), 9, 128, 2, TANH)]),
+            gemm([lin(xt, 9, Wc(ct, "SA_fc"), Bc(ct, "SA_fc"), P(st.hc1t), 128, 9, 64, RELU)]),
+            gemm([lin(P(st.hc1t), 128, Wc(ct, "merge_fc_grid"), Bc(ct, "merge_fc_grid"), P(st.hc2t), 256, 128, 256,
+                      RELU)]),
+            # TD target r + gamma Q'(s', a')(1 - done) and the mse gradient (UAM/maddpg:346-380)
+            lambda: _ok(L.aac_uam_head(P(st.hc2t), B, Wc(ct, "out_feature_q"), Bc(ct, "out_feature_q"), 2, P(st.y),
+                                       P(R, 27), P(R, 28), ROW, float(m.GAMMA), None, None, None, fused._stream()),
+                        "aac_uam_head"),
+            lambda: _ok(L.aac_uam_head(P(st.hc2), B, Wc(c, "out_feature_q"), Bc(c, "out_feature_q"), 0, P(st.y),
+                                       None, None, 0, 0.0, P(st.dq), P(st.dh2), P(st.lq), fused._stream()),
+                        "aac_uam_head"),
+            # critic weight gradients and the backward into the merge layer's input
+            gemm([wgrad(P(st.dq), 1, P(st.hc2), 256, 1, 256, gc["out_feature_q.0.weight"], gc["out_feature_q.0.bias"],
+                        nC),
+                  wgrad(P(st.dh2), 256, P(st.hc1), 128, 256, 128, gc["merge_fc_grid.0.weight"],
+                        gc["merge_fc_grid.0.bias"], nC),
+                  prob64(P(st.dh2), Wc(c, "merge_fc_grid"), P(st.dh1), B, 128, 256, 256, 128, 128,
+                         mask=P(st.hc1), ldmask=128, mact=RELU)]),
+            gemm([wgrad(P(st.dh1), 128, xc, 9, 64, 9, gc["SA_fc.0.weight"], gc["SA_fc.0.bias"], nC),
+                  wgrad(P(st.dh1, 64), 128, g, ROW, 64, 18, gc["SA_grid.0.weight"], gc["SA_grid.0.bias"], nC)]),
+            lambda: _ok(L.aac_adam64_sum(P(F), P(st.gc), KS, P(st.m1), P(st.m2), nC, st.lr_c, st.betas[0],
+                                         st.betas[1], st.eps, st.step.data_ptr(), 1, fused._stream()),
+                        "aac_adam64_sum"),
+            # actor step: -mean Q(s, pi(s)) through the updated critic (UAM/maddpg:389-512)
+            gemm([lin(xp, 9, Wc(c, "SA_fc"), Bc(c, "SA_fc"), P(st.hp1), 128, 9, 64, RELU),
+                  lin(g, ROW, Wc(c, "SA_grid"), Bc(c, "SA_grid"), P(st.hp1, 64), 128, 18, 64, RELU)]),
+            gemm([lin(P(st.hp1), 128, Wc(c, "merge_fc_grid"), Bc(c, "merge_fc_grid"), P(st.hp2), 256, 128, 256,
+                      RELU)]),
+            lambda: _ok(L.aac_uam_head(P(st.hp2), B, Wc(c, "out_feature_q"), Bc(c, "out_feature_q"), 1, P(st.y),
+                                       None, None, 0, 0.0, None, P(st.dp2), P(st.la), fused._stream()),
+                        "aac_uam_head"),
+            # d/d(own-encoder input) of the critic, first 64 features only (the action columns)
+            gemm([prob64(P(st.dp2), Wc(c, "merge_fc_grid"), P(st.dp1), B, 64, 256, 256, 128, 64,
+                         mask=P(st.hp1), ldmask=128, mact=RELU)]),
+            # da = dx V1[:, 7:9], times tanh' of the policy action
+            gemm([prob64(P(st.dp1), Wc(c, "SA_fc") + 8 * 7, P(st.dout), B, 2, 64, 64, 9, 2,
+                         mask=P(st.xp, 7), ldmask=9, mact=TANH)]),
+            gemm([prob64(P(st.dout), Wc(a, "act_out"), P(st.dha2), B, 128, 2, 2, 128, 128,
+                         mask=P(st.ha2), ldmask=128, mact=RELU),
+                  wgrad(P(st.dout), 2, P(st.ha2), 128, 2, 128, ga["act_out.0.weight"], ga["act_out.0.bias"], nA)]),
+            gemm([prob64(P(st.dha2), Wc(a, "merge_feature"), P(st.dha1), B, 128, 128, 128, 128, 128,
+                         mask=P(st.ha1), ldmask=128, mact=RELU),
+                  wgrad(P(st.dha2), 128, P(st.ha1), 128, 128, 128, ga["merge_feature.0.weight"],
+                        ga["merge_feature.0.bias"], nA)]),
+            gemm([wgrad(P(st.dha1), 128, own, ROW, 64, 7, ga["own_fc.0.weight"], ga["own_fc.0.bias"], nA),
+                  wgrad(P(st.dha1, 64), 128, g, ROW, 64, 18, ga["own_grid.0.weight"], ga["own_grid.0.bias"], nA)]),
+            lambda: _ok(L.aac_adam64_sum(P(F, nC), P(st.ga), KS, P(st.m1, nC), P(st.m2, nC), nA, st.lr_a,
+                                         st.betas[0], st.betas[1], st.eps, st.step.data_ptr(), 1, fused._stream()),
+                        "aac_adam64_sum"),
+            # soft update of both targets (UAM/maddpg:21-25), the shared step counter and the losses
+            lambda: _ok(L.aac_uam_polyak(P(T), P(F), nC + nA, float(m.tau), st.step.data_ptr(), P(st.lq), P(st.la),
+                                         B, P(st.loss), fused._stream()), "aac_uam_polyak"),
+        ]
+        return launches
+
+    def run(self, idx=None):
+        """One update from the replay (or the given sampled indices); returns (loss_q, loss_a)."""
+        if idx is None:
+            for f in self._launches:
+                f()
+        else:
+            self.idx.copy_(idx.reshape(-1).to(torch.int32))
+            for f in self._launches[1:]:
+                f()
+        return self.loss[0], self.loss[1]
+
+    def capture(self):
+        """One update as a HIP graph (raw launches only: nothing to warm up, no state to restore)."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for f in self._launches:
+                f()
+        self.graph = g
+        return g
+
+
 class MADDPG:
     """UAM/maddpg:35-181 with the default flags (shared actor + shared single critic, float64)."""
 
@@ -210,6 +449,9 @@ class MADDPG:
         self._static = {}
         self.noise_seed = int(seed or 0) * 7919 + 1
         self.noise_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # update() path on one GPU: the fused float64 learner (FusedUamUpdate), else torch autograd
+        self.fused_learner = self.device.type == "cuda" and os.environ.get("AAC_UAM_FUSED", "1") != "0"
+        self._fu = None
 
     # ------------------------------------------------------------------ batched API
     def attach_replay(self, capacity, seed=0):
@@ -341,12 +583,26 @@ class MADDPG:
         rep = replay if replay is not None else (self.replay if self.replay is not None else self.memory.dev)
         if len(rep) < B:
             raise ValueError(f"replay holds {len(rep)} transitions, cannot sample {B} distinct rows")
+        if idx is None and use_graph and self.device.type == "cuda" and self.world == 1 and self.fused_learner:
+            fu = self.fused(B, rep)
+            if getattr(fu, "graph", None) is None:
+                fu.capture()
+            fu.graph.replay()
+            return fu.loss[0], fu.loss[1]
         if idx is None and use_graph and self.device.type == "cuda" and self.world == 1:
             if self._graph is None or self._graph_B != B or self._graph_rep != id(rep):
                 self.capture(B, rep)
             self._graph.replay()
             return self._graph_out
         return self._sampled_core(rep, B, idx)
+
+    def fused(self, B, rep):
+        """The FusedUamUpdate of (B, replay), built on first use.  Building it moves the parameters
+        into flat buffers (the modules keep views), so a torch-path graph captured before is dropped."""
+        if self._fu is None or self._fu.B != B or self._fu.rep is not rep:
+            self._graph = None
+            self._fu = FusedUamUpdate(self, B, rep)
+        return self._fu
 
     # ------------------------------------------------------------------ reference API
     def choose_action(self, state, cur_total_step, cur_episode, step, mini_noise_eps, noise_start_level,

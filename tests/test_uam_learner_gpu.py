@@ -57,8 +57,10 @@ def test_update_matches_cpu_restatement(native_lib):
 
 
 def test_graph_replay_equals_eager(native_lib):
+    """The torch-autograd path: captured graph == eager, three updates."""
     m1, rep1 = _model(seed=4)
     m2, rep2 = _model(seed=4)
+    m1.fused_learner = False
     for _ in range(3):
         m1.update(64, use_graph=True)
         m2.update(64, use_graph=False)
@@ -66,6 +68,98 @@ def test_graph_replay_equals_eager(native_lib):
     for p, q in zip(list(m1.actors.parameters()) + list(m1.critics_target.parameters()),
                     list(m2.actors.parameters()) + list(m2.critics_target.parameters())):
         np.testing.assert_allclose(p.detach().cpu().numpy(), q.detach().cpu().numpy(), rtol=0, atol=1e-14)
+
+
+def test_fused_update_matches_cpu_restatement(native_lib):
+    """The fused float64 learner (FusedUamUpdate, include/aac_uam_learn.h) against the CPU
+    restatement: two updates on the same sampled rows, losses and all four networks within 1e-10."""
+    from multi_agent_aac_amd import uam_learner as L
+    m, rep = _model(seed=6)
+    a, c, at, ct = _ref_from(m)
+    oa = torch.optim.Adam(a.parameters(), lr=1e-4)
+    oc = torch.optim.Adam(c.parameters(), lr=1e-4)
+    fu = m.fused(64, rep)
+    rng = np.random.default_rng(1)
+    for it in range(2):
+        idx = torch.as_tensor(rng.choice(len(rep), 64, replace=False), dtype=torch.int32, device=DEV)
+        lq, la = fu.run(idx)
+        rows = rep.ring[idx.long()].cpu()
+        b = {k: rows[:, s:e] for k, (s, e) in L.SLICES.items()}
+        b["rew"], b["done"] = b["rew"][:, 0], b["done"][:, 0]
+        rq, ra = R.ref_update(a, c, at, ct, oa, oc, b)
+        assert abs(float(lq) - rq) < 1e-10 and abs(float(la) - ra) < 1e-10, (float(lq), rq, float(la), ra)
+    for mine, ref in ((m.actors, a), (m.critics, c), (m.actors_target, at), (m.critics_target, ct)):
+        for (k, p), (_, q) in zip(mine.state_dict().items(), ref.state_dict().items()):
+            np.testing.assert_allclose(p.cpu().numpy(), q.numpy(), rtol=0, atol=1e-10, err_msg=k)
+
+
+def test_fused_graph_equals_eager_and_torch_path(native_lib):
+    """update() replays the fused learner's graph: bit-equal to its eager launches, and within
+    1e-12 of the torch-autograd path on the same sampled rows (same replay sampler stream)."""
+    m1, rep1 = _model(seed=5)
+    m2, rep2 = _model(seed=5)
+    m3, rep3 = _model(seed=5)
+    m3.fused_learner = False
+    f2 = m2.fused(64, rep2)
+    for _ in range(3):
+        m1.update(64, use_graph=True)
+        f2.run()
+        m3.update(64, use_graph=False)
+    torch.cuda.synchronize()
+    ps = lambda m: list(m.actors.parameters()) + list(m.critics.parameters()) + list(m.critics_target.parameters())  # noqa
+    for p, q, t in zip(ps(m1), ps(m2), ps(m3)):
+        assert torch.equal(p, q)
+        np.testing.assert_allclose(p.detach().cpu().numpy(), t.detach().cpu().numpy(), rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_gemm64_products(native_lib, case):
+    """aac_gemm64_batch against float64 torch: transposes, ragged tiles, epilogues, the ones column
+    and split-K partial copies, several products in one launch."""
+    from multi_agent_aac_amd import fused
+    from multi_agent_aac_amd import uam_learner as L
+    g = torch.Generator(device=DEV).manual_seed(case)
+    rnd = lambda *s: torch.randn(*s, dtype=torch.float64, device=DEV, generator=g)   # noqa: E731
+    specs = [  # (M, N, K, ta, tb, act, mact, ones, ks)
+        [(512, 64, 7, 0, 1, 1, 0, 0, 1), (512, 256, 128, 0, 1, 1, 0, 0, 1), (37, 19, 5, 0, 0, 2, 0, 0, 1)],
+        [(256, 128, 512, 1, 0, 0, 0, 1, 8), (1, 256, 512, 1, 0, 0, 0, 1, 8)],
+        [(512, 128, 256, 0, 0, 0, 1, 0, 1), (512, 2, 64, 0, 0, 0, 2, 0, 1)],
+        [(64, 9, 512, 1, 0, 0, 0, 1, 8), (64, 18, 513, 1, 0, 0, 0, 1, 3)],
+        [(17, 33, 65, 1, 1, 2, 1, 0, 1), (100, 3, 1, 0, 0, 1, 0, 0, 1)],
+        [(512, 128, 2, 0, 0, 0, 1, 0, 1), (2, 128, 512, 1, 0, 0, 0, 1, 8)],
+    ][case]
+    probs, checks, keep = [], [], []
+    for M, N, K, ta, tb, act, mact, ones, ks in specs:
+        A = rnd(K, M) if ta else rnd(M, K)
+        Bm = rnd(N, K) if tb else rnd(K, N)
+        opA, opB = (A.t() if ta else A), (Bm.t() if tb else Bm)
+        bias = rnd(N) if (act and ks == 1) else None
+        mask = rnd(M, N) if mact else None
+        stride = M * N + M
+        C = torch.full((ks * stride,), 7.0, dtype=torch.float64, device=DEV)
+        cx = C[M * N:] if ones else None
+        probs.append(L.prob64(L.p64(A), L.p64(Bm), L.p64(C), M, N, K, M if ta else K, K if tb else N, N, ta=ta,
+                              tb=tb, bias=L.p64(bias), act=act, mask=L.p64(mask), ldmask=N, mact=mact, ones=ones,
+                              cextra=L.p64(cx), ksplit=ks, split_stride=stride if ks > 1 else 0))
+        keep += [A, Bm, C, bias, mask]
+        want = opA @ opB
+        if bias is not None:
+            want = want + bias
+        want = torch.relu(want) if act == 1 else (torch.tanh(want) if act == 2 else want)
+        if mact == 1:
+            want = want * (mask > 0)
+        elif mact == 2:
+            want = want * (1 - mask * mask)
+        checks.append((C, M, N, ks, stride, ones, want, opA.sum(1)))
+    arr = (fused.GemmProb * len(probs))(*probs)
+    L._ok(L._learn_lib().aac_gemm64_batch(arr, len(probs), fused._stream()), "gemm64")
+    torch.cuda.synchronize()
+    for C, M, N, ks, stride, ones, want, rowsum in checks:
+        parts = C.view(ks, stride) if ks > 1 else C[:stride].view(1, stride)
+        got = parts[:, :M * N].sum(0).view(M, N)
+        torch.testing.assert_close(got, want, rtol=1e-12, atol=1e-12)
+        if ones:
+            torch.testing.assert_close(parts[:, M * N:].sum(0), rowsum, rtol=1e-12, atol=1e-12)
 
 
 def test_act_and_noise_schedule(native_lib):
