@@ -68,9 +68,9 @@ int aac_adam64_sum(double *param, const double *gpart, int32_t nsplit, double *e
                    int64_t n, double lr, double beta1, double beta2, double eps, const int32_t *step,
                    int32_t step_add, void *stream);
 
-/* target[i] += tau (src[i] - target[i]) over n parameters (torch._foreach_lerp_); then one
- * thread adds 1 to *step and writes loss[0] = mean(lq[0..B)), loss[1] = -mean(la[0..B)) summed
- * in row order (lq / la / loss may be NULL). */
+/* target[i] += tau (src[i] - target[i]) over n parameters (torch._foreach_lerp_); then one wave
+ * adds 1 to *step and writes loss[0] = mean(lq[0..B)), loss[1] = -mean(la[0..B)) with a fixed
+ * summation order (lq / la / loss may be NULL). */
 int aac_uam_polyak(double *target, const double *src, int64_t n, double tau, int32_t *step, const double *lq,
                    const double *la, int32_t B, double *loss, void *stream);
 

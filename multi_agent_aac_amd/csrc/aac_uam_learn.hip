@@ -70,23 +70,29 @@ __device__ __forceinline__ i4 rsrc64(const double *p) {
 __device__ __forceinline__ double ld64(i4 r, int off) { return __builtin_bit_cast(double, buf_load_2i(r, off, 0, 0)); }
 
 __global__ void __launch_bounds__(256) gemm64_kernel(Q64Batch g) {
-    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+    // the wave index is made wave-uniform so the product's fields are scalar loads (a per-lane
+    // index turns every field access into a vector load with its own wait)
+    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (gw >= g.waves) return;
     int pi = 0;
     while (pi + 1 < g.n && gw >= g.p[pi + 1].w_begin) ++pi;
     const Q64 &P = g.p[pi];
+    const int K = P.K, ks = P.ks;
     const int local = gw - P.w_begin;
-    const int s = local % P.ks, tile = local / P.ks;
+    const int s = local % ks, tile = local / ks;
     const int m0 = (tile / P.tiles_n) * 16, n0 = (tile % P.tiles_n) * 16;
     const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
     const int nreal = P.N - P.ones;
-    const int nst = (P.K + 3) / 4, per = (nst + P.ks - 1) / P.ks;
+    const int nst = (K + 3) / 4, per = (nst + ks - 1) / ks;
     const int st0 = s * per, st1 = min(nst, st0 + per);
     const i4 ra = rsrc64(P.A), rb = rsrc64(P.B);
     const int m = m0 + r, n = n0 + r;
     const bool mok = m < P.M, nok = n < nreal, isone = P.ones && n == nreal;
-    auto aoff = [&](int k) { return (mok && k < P.K) ? (P.ta ? k * P.lda + m : m * P.lda + k) * 8 : OOB; };
-    auto boff = [&](int k) { return (nok && k < P.K) ? (P.tb ? n * P.ldb + k : k * P.ldb + n) * 8 : OOB; };
+    // op(A)[m][k] = base_a + k * sa, op(B)[k][n] = base_b + k * sb (element offsets)
+    const int sa = P.ta ? P.lda : 1, base_a = P.ta ? m : m * P.lda;
+    const int sb = P.tb ? 1 : P.ldb, base_b = P.tb ? n * P.ldb : n;
+    auto aoff = [&](int k) { return (mok && k < K) ? (base_a + k * sa) * 8 : OOB; };
+    auto boff = [&](int k) { return (nok && k < K) ? (base_b + k * sb) * 8 : OOB; };
     d4 acc = {0.0, 0.0, 0.0, 0.0};
     double a0[G], b0[G], a1[G], b1[G];
     auto load = [&](int sg, double(&a)[G], double(&b)[G]) {
@@ -103,7 +109,7 @@ __global__ void __launch_bounds__(256) gemm64_kernel(Q64Batch g) {
         for (int q = 0; q < G; ++q) {
             const int st = sg + q;
             if (st >= st1) break;                    // wave-uniform
-            const double bv = isone ? ((4 * st + kq < P.K) ? 1.0 : 0.0) : b[q];
+            const double bv = isone ? ((4 * st + kq < K) ? 1.0 : 0.0) : b[q];
             acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], bv, acc, 0, 0, 0);
         }
     };
@@ -225,16 +231,26 @@ __global__ void uam_polyak_kernel(double *tgt, const double *__restrict__ src, i
         const double t = tgt[i];
         tgt[i] = t + tau * (src[i] - t);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (step) *step += 1;
-        if (loss) {
-            double sq = 0.0, sa = 0.0;
-            for (int r = 0; r < B; ++r) {
-                if (lq) sq += lq[r];
-                if (la) sa += la[r];
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        // the loss means: lane-strided partial sums then a fixed xor tree (deterministic; a single
+        // thread walking the rows costs one dependent load latency per row, ~80 us at B = 512)
+        const int lane = threadIdx.x;
+        double sq = 0.0, sa = 0.0;
+        for (int r = lane; r < B; r += 64) {
+            if (lq) sq += lq[r];
+            if (la) sa += la[r];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            sq += __shfl_xor(sq, o, 64);
+            sa += __shfl_xor(sa, o, 64);
+        }
+        if (lane == 0) {
+            if (step) *step += 1;
+            if (loss) {
+                loss[0] = sq / B;
+                loss[1] = -(sa / B);
             }
-            loss[0] = sq / B;
-            loss[1] = -(sa / B);
         }
     }
 }
