@@ -9,6 +9,7 @@
  *                     fused epilogue, ``ones`` bias-gradient column and ``ksplit`` partial copies
  *                     as aac_gemm_batch (include/aac_fused.h); the struct is aac_gemm_prob with
  *                     double pointers.
+ *   aac_uam_push      one replay row per aircraft into the device ring.
  *   aac_uam_gather    sampled replay rows -> the learner's input layouts.
  *   aac_uam_head      the critic's 256 -> 1 output layer per row with the TD target, the mse
  *                     gradient or the -mean Q gradient, and the per-row loss terms.
@@ -45,6 +46,14 @@ typedef struct {
 const char *aac_uam_learn_last_error(void);
 
 int aac_gemm64_batch(const aac_gemm64_prob *probs, int32_t n, void *stream);
+
+/* Appends M transitions (one per aircraft) to the float64 replay ring at slots (pos + i) % capacity
+ * as rows [own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18]; done is uint8 (done_u8 = 1)
+ * or float64.  Replaces UamReplay.push_batch's torch.cat (UAM/main:582-603 pushes one Experience
+ * per aircraft). */
+int aac_uam_push(double *ring, int64_t capacity, int64_t pos, int64_t M, const double *own, const double *radar,
+                 const double *act, const double *rew, const void *done, int32_t done_u8, const double *nown,
+                 const double *nradar, void *stream);
 
 /* Replay rows ring[idx[b]] (row width 54: own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18,
  * uam_learner.ROW) -> rows[b][54], xc[b] = [own | a] (9), xt[b][0:7] = own', xp[b][0:7] = own. */

@@ -13,6 +13,7 @@
 // weight gradients split K = B into partial copies summed by the Adam kernel in fixed order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -255,6 +256,30 @@ __global__ void uam_polyak_kernel(double *tgt, const double *__restrict__ src, i
     }
 }
 
+// one replay row per aircraft (UamReplay.push_batch): element (i, c) of the M new rows, ring slot
+// (pos + i) % capacity; done is uint8 (env output) or float64
+__global__ void uam_push_kernel(double *ring, int64_t capacity, int64_t pos, int64_t M, const double *__restrict__ own,
+                                const double *__restrict__ radar, const double *__restrict__ act,
+                                const double *__restrict__ rew, const void *__restrict__ done, int done_u8,
+                                const double *__restrict__ nown, const double *__restrict__ nradar) {
+    const int64_t total = M * 54;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e / 54;
+        const int c = (int)(e - i * 54);
+        double v;
+        if (c < 7) v = own[i * 7 + c];
+        else if (c < 25) v = radar[i * 18 + (c - 7)];
+        else if (c < 27) v = act[i * 2 + (c - 25)];
+        else if (c == 27) v = rew[i];
+        else if (c == 28) v = done_u8 ? (double)static_cast<const uint8_t *>(done)[i] : static_cast<const double *>(done)[i];
+        else if (c < 36) v = nown[i * 7 + (c - 29)];
+        else v = nradar[i * 18 + (c - 36)];
+        int64_t slot = pos + i;
+        if (slot >= capacity) slot -= capacity;
+        ring[slot * 54 + c] = v;
+    }
+}
+
 int grid_of(int64_t n) {
     const int64_t b = (n + 255) / 256;
     return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
@@ -304,6 +329,19 @@ int aac_gemm64_batch(const aac_gemm64_prob *in, int32_t n, void *stream) {
     }
     g.waves = (int)waves;
     hipLaunchKernelGGL(gemm64_kernel, dim3((g.waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, g);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_uam_push(double *ring, int64_t capacity, int64_t pos, int64_t M, const double *own, const double *radar,
+                 const double *act, const double *rew, const void *done, int32_t done_u8, const double *nown,
+                 const double *nradar, void *stream) {
+    if (M <= 0) return 0;
+    if (!ring || !own || !radar || !act || !rew || !done || !nown || !nradar) return lfail("uam_push: NULL argument");
+    if (M > capacity || pos < 0 || pos >= capacity) return lfail("uam_push: M > capacity or pos out of range");
+    const int64_t blocks = std::min<int64_t>((M * 54 + 255) / 256, 8192);
+    hipLaunchKernelGGL(uam_push_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ring, capacity, pos,
+                       M, own, radar, act, rew, done, done_u8, nown, nradar);
     LHIP(hipGetLastError());
     return 0;
 }

@@ -101,19 +101,34 @@ class UamReplay:
         return self.size
 
     def push_batch(self, own, radar, act, rew, done, n_own, n_radar):
-        """E x N transitions (leading dims flattened) in one row-assembly launch per ring segment."""
-        cols = [own.reshape(-1, 7), radar.reshape(-1, 18), act.reshape(-1, 2), rew.reshape(-1, 1),
-                done.reshape(-1, 1), n_own.reshape(-1, 7), n_radar.reshape(-1, 18)]
-        M = cols[0].shape[0]
+        """E x N transitions (leading dims flattened): one aac_uam_push launch for contiguous device
+        float64 inputs (done uint8 or float64), else a row-assembly launch per ring segment."""
+        M = own.numel() // 7
         if M > self.capacity:
             raise ValueError("one push larger than the replay capacity")
+        ts = (own, radar, act, rew, n_own, n_radar)
+        if (self.device.type == "cuda" and all(t.is_cuda and t.dtype == F64 and t.is_contiguous() for t in ts)
+                and done.is_cuda and done.is_contiguous() and done.dtype in (torch.uint8, F64)
+                and rew.numel() == M and done.numel() == M):
+            from . import fused
+            p = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
+            _ok(_learn_lib().aac_uam_push(p(self.ring), self.capacity, self.pos, M, p(own), p(radar), p(act), p(rew),
+                                          p(done), int(done.dtype == torch.uint8), p(n_own), p(n_radar),
+                                          fused._stream()), "aac_uam_push")
+            self._advance(M)
+            return
+        cols = [own.reshape(-1, 7), radar.reshape(-1, 18), act.reshape(-1, 2), rew.reshape(-1, 1),
+                done.reshape(-1, 1), n_own.reshape(-1, 7), n_radar.reshape(-1, 18)]
         cols = [c if c.dtype == F64 else c.to(F64) for c in cols]
         p = self.pos
         first = min(M, self.capacity - p)
         torch.cat([c[:first] for c in cols], dim=1, out=self.ring[p:p + first])
         if first < M:
             torch.cat([c[first:] for c in cols], dim=1, out=self.ring[:M - first])
-        self.pos = (p + M) % self.capacity
+        self._advance(M)
+
+    def _advance(self, M):
+        self.pos = (self.pos + M) % self.capacity
         self.size = min(self.size + M, self.capacity)
         self.meta[0] = self.pos          # device-side copies of the host counters (no sync)
         self.meta[1] = self.size
@@ -178,6 +193,7 @@ def _learn_lib():
         L.aac_uam_head.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, i32, dbl, vp, vp, vp, vp]
         L.aac_adam64_sum.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, vp]
         L.aac_uam_polyak.argtypes = [vp, vp, i64, dbl, vp, vp, vp, i32, vp, vp]
+        L.aac_uam_push.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp]
         _LL = L
     return _LL
 

@@ -212,3 +212,29 @@ def test_reference_surface(native_lib, tmp_path):
     m2.load_model([str(tmp_path / "episode_3_actor_net.pth")])
     for p, q in zip(m.actors.parameters(), m2.actors.parameters()):
         assert torch.equal(p, q)
+
+
+@pytest.mark.parametrize("done_u8", [True, False])
+def test_replay_push_kernel(native_lib, done_u8):
+    """aac_uam_push (one launch, ring wrap-around in the kernel) writes the same rows as the
+    torch.cat row assembly, bit for bit."""
+    from multi_agent_aac_amd import uam_learner as L
+    cap, M = 100, 40
+    rep = L.UamReplay(cap, DEV, seed=1)
+    want = torch.zeros(cap, L.ROW, dtype=torch.float64)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    pos = 0
+    for it in range(4):           # 160 rows through a 100-row ring: two wraps
+        f = lambda *s: torch.randn(*s, dtype=torch.float64, device=DEV, generator=g)   # noqa: E731
+        own, radar, act, rew, nown, nradar = f(8, 5, 7), f(8, 5, 18), f(8, 5, 2), f(8, 5), f(8, 5, 7), f(8, 5, 18)
+        done = (torch.rand(8, 5, device=DEV, generator=g) > 0.5)
+        done = done.to(torch.uint8) if done_u8 else done.double()
+        rep.push_batch(own, radar, act, rew, done, nown, nradar)
+        rows = torch.cat([own.reshape(-1, 7), radar.reshape(-1, 18), act.reshape(-1, 2), rew.reshape(-1, 1),
+                          done.reshape(-1, 1).double(), nown.reshape(-1, 7), nradar.reshape(-1, 18)], 1).cpu()
+        for i in range(M):
+            want[(pos + i) % cap] = rows[i]
+        pos = (pos + M) % cap
+    assert rep.pos == pos and len(rep) == cap
+    assert torch.equal(rep.ring.cpu(), want)
+    assert rep.meta.tolist() == [pos, cap]
