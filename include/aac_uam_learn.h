@@ -49,11 +49,12 @@ int aac_gemm64_batch(const aac_gemm64_prob *probs, int32_t n, void *stream);
 
 /* Appends M transitions (one per aircraft) to the float64 replay ring at slots (pos + i) % capacity
  * as rows [own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18]; done is uint8 (done_u8 = 1)
- * or float64.  Replaces UamReplay.push_batch's torch.cat (UAM/main:582-603 pushes one Experience
- * per aircraft). */
+ * or float64.  meta (may be NULL) receives the ring's new [pos, size] = [(pos + M) % capacity,
+ * min(size + M, capacity)] for the device sampler.  Replaces UamReplay.push_batch's torch.cat
+ * (UAM/main:582-603 pushes one Experience per aircraft). */
 int aac_uam_push(double *ring, int64_t capacity, int64_t pos, int64_t M, const double *own, const double *radar,
                  const double *act, const double *rew, const void *done, int32_t done_u8, const double *nown,
-                 const double *nradar, void *stream);
+                 const double *nradar, int64_t *meta, int64_t size, void *stream);
 
 /* Replay rows ring[idx[b]] (row width 54: own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18,
  * uam_learner.ROW) -> rows[b][54], xc[b] = [own | a] (9), xt[b][0:7] = own', xp[b][0:7] = own. */

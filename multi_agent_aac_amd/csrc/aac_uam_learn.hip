@@ -256,27 +256,47 @@ __global__ void uam_polyak_kernel(double *tgt, const double *__restrict__ src, i
     }
 }
 
-// one replay row per aircraft (UamReplay.push_batch): element (i, c) of the M new rows, ring slot
-// (pos + i) % capacity; done is uint8 (env output) or float64
-__global__ void uam_push_kernel(double *ring, int64_t capacity, int64_t pos, int64_t M, const double *__restrict__ own,
-                                const double *__restrict__ radar, const double *__restrict__ act,
-                                const double *__restrict__ rew, const void *__restrict__ done, int done_u8,
-                                const double *__restrict__ nown, const double *__restrict__ nradar) {
-    const int64_t total = M * 54;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = e / 54;
-        const int c = (int)(e - i * 54);
-        double v;
-        if (c < 7) v = own[i * 7 + c];
-        else if (c < 25) v = radar[i * 18 + (c - 7)];
-        else if (c < 27) v = act[i * 2 + (c - 25)];
-        else if (c == 27) v = rew[i];
-        else if (c == 28) v = done_u8 ? (double)static_cast<const uint8_t *>(done)[i] : static_cast<const double *>(done)[i];
-        else if (c < 36) v = nown[i * 7 + (c - 29)];
-        else v = nradar[i * 18 + (c - 36)];
-        int64_t slot = pos + i;
-        if (slot >= capacity) slot -= capacity;
-        ring[slot * 54 + c] = v;
+// one replay row per aircraft (UamReplay.push_batch): a workgroup assembles 64 rows in LDS from
+// coalesced reads of the seven sources, then writes them as 64 x 54 contiguous doubles (two ring
+// segments at the wrap); thread 0 of workgroup 0 stores the ring's new [pos, size] (meta).
+// done is uint8 (env output) or float64.
+constexpr int PR = 64;            // rows per workgroup
+__global__ void __launch_bounds__(256) uam_push_kernel(double *ring, int64_t capacity, int64_t pos, int M,
+                                                       const double *__restrict__ own, const double *__restrict__ radar,
+                                                       const double *__restrict__ act, const double *__restrict__ rew,
+                                                       const void *__restrict__ done, int done_u8,
+                                                       const double *__restrict__ nown,
+                                                       const double *__restrict__ nradar, int64_t *meta,
+                                                       int64_t new_pos, int64_t new_size) {
+    __shared__ double t[PR * 54];
+    const int r0 = blockIdx.x * PR, nr = min(PR, M - r0), tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0 && meta) {
+        meta[0] = new_pos;
+        meta[1] = new_size;
+    }
+    auto stage = [&](const double *src, int w, int c0) {
+        for (int e = tid; e < nr * w; e += 256) {
+            const int rr = e / w;
+            t[rr * 54 + c0 + (e - rr * w)] = src[(size_t)r0 * w + e];
+        }
+    };
+    stage(own, 7, 0);
+    stage(radar, 18, 7);
+    stage(act, 2, 25);
+    stage(rew, 1, 27);
+    for (int e = tid; e < nr; e += 256)
+        t[e * 54 + 28] = done_u8 ? (double)static_cast<const uint8_t *>(done)[r0 + e]
+                                 : static_cast<const double *>(done)[r0 + e];
+    stage(nown, 7, 29);
+    stage(nradar, 18, 36);
+    __syncthreads();
+    int64_t slot = pos + r0;
+    if (slot >= capacity) slot -= capacity;
+    const int first = (int)min<int64_t>(nr, capacity - slot);     // rows before the wrap
+    for (int e = tid; e < nr * 54; e += 256) {
+        const int rr = e / 54;
+        double *dst = rr < first ? ring + slot * 54 : ring - (int64_t)first * 54;
+        dst[e] = t[e];
     }
 }
 
@@ -335,13 +355,14 @@ int aac_gemm64_batch(const aac_gemm64_prob *in, int32_t n, void *stream) {
 
 int aac_uam_push(double *ring, int64_t capacity, int64_t pos, int64_t M, const double *own, const double *radar,
                  const double *act, const double *rew, const void *done, int32_t done_u8, const double *nown,
-                 const double *nradar, void *stream) {
+                 const double *nradar, int64_t *meta, int64_t size, void *stream) {
     if (M <= 0) return 0;
     if (!ring || !own || !radar || !act || !rew || !done || !nown || !nradar) return lfail("uam_push: NULL argument");
     if (M > capacity || pos < 0 || pos >= capacity) return lfail("uam_push: M > capacity or pos out of range");
-    const int64_t blocks = std::min<int64_t>((M * 54 + 255) / 256, 8192);
-    hipLaunchKernelGGL(uam_push_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ring, capacity, pos,
-                       M, own, radar, act, rew, done, done_u8, nown, nradar);
+    if (M >= (int64_t)1 << 30) return lfail("uam_push: too many rows in one push");
+    const int64_t np = (pos + M) % capacity, ns = std::min<int64_t>(size + M, capacity);
+    hipLaunchKernelGGL(uam_push_kernel, dim3((unsigned)((M + PR - 1) / PR)), dim3(256), 0, (hipStream_t)stream, ring,
+                       capacity, pos, (int)M, own, radar, act, rew, done, done_u8, nown, nradar, meta, np, ns);
     LHIP(hipGetLastError());
     return 0;
 }

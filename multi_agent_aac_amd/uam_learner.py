@@ -114,8 +114,8 @@ class UamReplay:
             p = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
             _ok(_learn_lib().aac_uam_push(p(self.ring), self.capacity, self.pos, M, p(own), p(radar), p(act), p(rew),
                                           p(done), int(done.dtype == torch.uint8), p(n_own), p(n_radar),
-                                          fused._stream()), "aac_uam_push")
-            self._advance(M)
+                                          p(self.meta), self.size, fused._stream()), "aac_uam_push")
+            self._advance(M, meta=False)       # the kernel wrote meta
             return
         cols = [own.reshape(-1, 7), radar.reshape(-1, 18), act.reshape(-1, 2), rew.reshape(-1, 1),
                 done.reshape(-1, 1), n_own.reshape(-1, 7), n_radar.reshape(-1, 18)]
@@ -127,11 +127,12 @@ class UamReplay:
             torch.cat([c[first:] for c in cols], dim=1, out=self.ring[:M - first])
         self._advance(M)
 
-    def _advance(self, M):
+    def _advance(self, M, meta=True):
         self.pos = (self.pos + M) % self.capacity
         self.size = min(self.size + M, self.capacity)
-        self.meta[0] = self.pos          # device-side copies of the host counters (no sync)
-        self.meta[1] = self.size
+        if meta:
+            self.meta[0] = self.pos          # device-side copies of the host counters (no sync)
+            self.meta[1] = self.size
 
     def fields(self, rows):
         return {k: rows[:, a:b] for k, (a, b) in SLICES.items()}
@@ -193,7 +194,7 @@ def _learn_lib():
         L.aac_uam_head.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, i32, dbl, vp, vp, vp, vp]
         L.aac_adam64_sum.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, vp]
         L.aac_uam_polyak.argtypes = [vp, vp, i64, dbl, vp, vp, vp, i32, vp, vp]
-        L.aac_uam_push.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp]
+        L.aac_uam_push.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp, i64, vp]
         _LL = L
     return _LL
 
