@@ -1308,6 +1308,11 @@ const int g_depth = std::min(2, std::max(1, env_int("AAC_GEMM_DEPTH", 2)));
 const int g_deep_tiles = env_int("AAC_GEMM_DEEP_TILES", 0);
 const int g_deep_chain = env_int("AAC_GEMM_DEEP_CHAIN", 2);     // ring only for chains longer than this
 const int g_wide_tiles = env_int("AAC_GEMM_WIDE_TILES", 2048);
+// wide mode for one-chunk products with >= g_wide_kch_tiles tiles: within run-to-run noise on
+// configs 3 / 4 (knob_sweep: 1.230 vs 1.230-1.236 ms, 0.687 vs 0.687-0.689 ms), so off by default;
+// with small products too (128 tiles) the GRU step got 2 % slower
+const int g_wide_kch = env_int("AAC_GEMM_WIDE_KCH", 0);
+const int g_wide_kch_tiles = env_int("AAC_GEMM_WIDE_KCH_TILES", 512);
 const int g_lw = env_int("AAC_GEMM_LW", 1);                  // row-contiguous operands by 4T-B loads
 const int g_vec = env_int("AAC_GEMM_VEC", 1);                // 16-B epilogue rows
 int g_dump = env_int("AAC_GEMM_DUMP", 0);      // print the plans of the first g_dump launches
@@ -1353,8 +1358,10 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         d.vec = g_vec && (!s.C || (aligned16(s.C) && s.ldc % 4 == 0)) && (!s.addend || (aligned16(s.addend) && s.ldadd % 4 == 0)) &&
                 (!s.mask || (aligned16(s.mask) && s.ldmask % 4 == 0)) && (!s.bias || aligned16(s.bias)) &&
                 (ks <= 1 || (s.split_stride % 4 == 0));
-        // large products need no K cut inside a workgroup: one tile per wave
-        d.wide = ks == 1 && tm * tn >= g_wide_tiles;
+        // large products need no K cut inside a workgroup: one tile per wave; nor do short chains
+        // (<= g_wide_kch chunks), where splitting K leaves waves idle and adds the LDS reduction
+        const int nch_all = (s.K + KC - 1) / KC;
+        d.wide = ks == 1 && (tm * tn >= g_wide_tiles || (nch_all <= g_wide_kch && tm * tn >= g_wide_kch_tiles));
         {
             const int nch = (s.K + KC - 1) / KC;
             const int per = (nch + ks - 1) / ks;
