@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 
@@ -162,6 +163,157 @@ __global__ void __launch_bounds__(256) uam_actor_kernel(ActorArgs A) {
     }
 }
 
+// Weights-stationary form (the default): a workgroup keeps every weight fragment it needs in
+// registers and walks 16-row blocks.  The layers run transposed (h^T = W x^T, the block's rows on
+// the MFMA's n axis; A = weight fragments, B = activations), so wave w owns output features
+// 16w..16w+15 of the two 64-wide encoders and 32w..32w+31 of the 128-wide merge layer, and the
+// activations pass between layers through a [feature][row] LDS image.  The per-block form above
+// re-reads the 128 KB merge weights from L2 for every 16 rows (~1 GB per launch at 131 072 rows).
+constexpr int TI = 17;                       // row stride of the [feature][16 rows] image
+
+__device__ __forceinline__ double row_noise(const ActorArgs &A, int r, uint64_t ctr, double &n1) {
+    const int e = r / A.N;
+    const int ep = A.episode ? A.episode[e] : 1;
+    double var;
+    if (ep <= A.eps_end) {
+        const double slope = (A.noise_end - A.noise_start) / (double)(A.eps_end - 1);
+        var = A.noise_start + slope * (double)(ep - 1);
+    } else {
+        var = A.noise_end;
+    }
+    const uint64_t h1 = amix64(amix64(amix64(A.seed) ^ ctr) ^ (uint64_t)(2 * (int64_t)r));
+    const uint64_t h2 = amix64(h1 ^ 0xD1B54A32D192ED03ull);
+    const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
+    const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+    const double rr = sqrt(-2.0 * log(u1));
+    n1 = rr * sin(6.283185307179586 * u2) * var;
+    return rr * cos(6.283185307179586 * u2) * var;
+}
+
+__global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
+    __shared__ double sH[128 * TI];          // [h_o | h_r] of the block, [feature][row]
+    __shared__ double sP[4][16][2];          // per-wave partial output dots
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
+    const uint64_t ctr = A.noisy ? *A.counter : 0;
+    // A fragments (lane: output row 16 t + n of the tile, k slot kq of each 4-step)
+    double a1[2], a2[5], a3[2][32];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int k = 4 * s + kq;
+        a1[s] = k < 7 ? A.w1[(16 * w + n) * 7 + k] : 0.0;
+    }
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int k = 4 * s + kq;
+        a2[s] = k < 18 ? A.w2[(16 * w + n) * 18 + k] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 32; ++s) a3[t][s] = A.w3[(32 * w + 16 * t + n) * 128 + 4 * s + kq];
+    // epilogue constants of this lane's outputs: feature 16 t + kq + 4 j of a tile (f64 C layout)
+    double c1[4], c2[4], c3[2][4], u0[2][4], u1[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        c1[j] = A.b1[16 * w + kq + 4 * j];
+        c2[j] = A.b2[16 * w + kq + 4 * j];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int o = 32 * w + 16 * t + kq + 4 * j;
+            c3[t][j] = A.b3[o];
+            u0[t][j] = A.w4[o];
+            u1[t][j] = A.w4[128 + o];
+        }
+    }
+    const double b40 = A.b4[0], b41 = A.b4[1];
+    const int nblk = (A.R + 15) / 16;
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int r0 = blk * 16, r = r0 + n;
+        const int rc = r < A.R ? r : A.R - 1;            // rows past R feed only their own column
+        double bo[2], br[5];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int k = 4 * s + kq;
+            bo[s] = A.own[(size_t)rc * 7 + (k < 7 ? k : 6)];
+        }
+#pragma unroll
+        for (int s = 0; s < 5; ++s) {
+            const int k = 4 * s + kq;
+            br[s] = A.radar[(size_t)rc * 18 + (k < 18 ? k : 17)];
+        }
+        // h_o^T = relu(W1 own^T + b1), h_r^T = relu(W2 radar^T + b2): padded k slots have a zero A
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bo[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double v = acc[j] + c1[j];
+            sH[(16 * w + kq + 4 * j) * TI + n] = v > 0.0 ? v : 0.0;
+        }
+        acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 5; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], br[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double v = acc[j] + c2[j];
+            sH[(64 + 16 * w + kq + 4 * j) * TI + n] = v > 0.0 ? v : 0.0;
+        }
+        __syncthreads();
+        // h^T = relu(W3 [h_o | h_r]^T + b3), two output tiles per wave, then this lane's share of
+        // the 128 -> 2 output layer
+        d4 h0 = {0.0, 0.0, 0.0, 0.0}, h1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 32; ++s) {
+            const double b = sH[(4 * s + kq) * TI + n];
+            h0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a3[0][s], b, h0, 0, 0, 0);
+            h1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a3[1][s], b, h1, 0, 0, 0);
+        }
+        double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double v = h0[j] + c3[0][j];
+            v = v > 0.0 ? v : 0.0;
+            p0 = fma(u0[0][j], v, p0);
+            p1 = fma(u1[0][j], v, p1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double v = h1[j] + c3[1][j];
+            v = v > 0.0 ? v : 0.0;
+            p0 = fma(u0[1][j], v, p0);
+            p1 = fma(u1[1][j], v, p1);
+        }
+        // sum over the four lane groups that hold row n, then over the waves in order
+        p0 += __shfl_xor(p0, 16, 64);
+        p1 += __shfl_xor(p1, 16, 64);
+        p0 += __shfl_xor(p0, 32, 64);
+        p1 += __shfl_xor(p1, 32, 64);
+        if (kq == 0) {
+            sP[w][n][0] = p0;
+            sP[w][n][1] = p1;
+        }
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            const int rr = r0 + threadIdx.x;
+            if (rr < A.R) {
+                const double s0 = ((sP[0][threadIdx.x][0] + sP[1][threadIdx.x][0]) + sP[2][threadIdx.x][0]) +
+                                  sP[3][threadIdx.x][0];
+                const double s1 = ((sP[0][threadIdx.x][1] + sP[1][threadIdx.x][1]) + sP[2][threadIdx.x][1]) +
+                                  sP[3][threadIdx.x][1];
+                double x0 = tanh(s0 + b40), x1 = tanh(s1 + b41);
+                if (A.noisy) {
+                    double e1;
+                    const double e0 = row_noise(A, rr, ctr, e1);
+                    x0 = fmin(fmax(x0 + e0, -1.0), 1.0);
+                    x1 = fmin(fmax(x1 + e1, -1.0), 1.0);
+                }
+                A.out[2 * (size_t)rr] = x0;
+                A.out[2 * (size_t)rr + 1] = x1;
+            }
+        }
+    }
+}
+
 __global__ void actor_counter_kernel(uint64_t *counter) { *counter += 1; }
 
 }  // namespace
@@ -187,9 +339,22 @@ int aac_uam_actor(const double *own, const double *radar, int32_t R, const doubl
     ActorArgs A{own, radar, w1, b1, w2, b2, w3, b3, w4, b4, out, R, N, episode, eps_end, noisy ? 1 : 0,
                 noise_start, noise_end, seed, counter};
     const int nblk = (R + 15) / 16;
-    int wgs = (nblk + 3) / 4;
-    wgs = wgs > 2048 ? 2048 : wgs;
-    hipLaunchKernelGGL(uam_actor_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A);
+    static const int per_block = [] {
+        const char *v = getenv("AAC_UAM_ACTOR_V1");
+        return v && atoi(v) != 0;
+    }();
+    if (per_block) {
+        int wgs = (nblk + 3) / 4;
+        wgs = wgs > 2048 ? 2048 : wgs;
+        hipLaunchKernelGGL(uam_actor_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A);
+    } else {
+        static const int cap = [] {
+            const char *v = getenv("AAC_UAM_ACTOR_WGS");
+            return v ? atoi(v) : 256;     // one workgroup per CU (300 VGPRs: one wave per SIMD)
+        }();
+        const int wgs = nblk < cap ? nblk : cap;
+        hipLaunchKernelGGL(uam_actor_ws_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A);
+    }
     if (noisy) hipLaunchKernelGGL(actor_counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
