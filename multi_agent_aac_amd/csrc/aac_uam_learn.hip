@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/aac_uam_learn.h"
@@ -51,6 +52,7 @@ struct Q64 {
     int64_t sstride;
     int M, N, K, lda, ldb, ldc, ldadd, ldmask, ta, tb, act, mact, ones, ks;
     int tiles_n, w_begin;           // w_begin in waves
+    int kw;                         // waves per tile: 1, or 4 (a workgroup splits K and reduces in LDS)
 };
 
 struct Q64Batch {
@@ -71,6 +73,7 @@ __device__ __forceinline__ i4 rsrc64(const double *p) {
 __device__ __forceinline__ double ld64(i4 r, int off) { return __builtin_bit_cast(double, buf_load_2i(r, off, 0, 0)); }
 
 __global__ void __launch_bounds__(256) gemm64_kernel(Q64Batch g) {
+    __shared__ d4 red[4][64];
     // the wave index is made wave-uniform so the product's fields are scalar loads (a per-lane
     // index turns every field access into a vector load with its own wait)
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -78,14 +81,17 @@ __global__ void __launch_bounds__(256) gemm64_kernel(Q64Batch g) {
     int pi = 0;
     while (pi + 1 < g.n && gw >= g.p[pi + 1].w_begin) ++pi;
     const Q64 &P = g.p[pi];
-    const int K = P.K, ks = P.ks;
-    const int local = gw - P.w_begin;
+    const int K = P.K, ks = P.ks, kw = P.kw;
+    const int local = (gw - P.w_begin) / kw, wq = (gw - P.w_begin) % kw;     // tile-split, quarter
     const int s = local % ks, tile = local / ks;
     const int m0 = (tile / P.tiles_n) * 16, n0 = (tile % P.tiles_n) * 16;
     const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
     const int nreal = P.N - P.ones;
     const int nst = (K + 3) / 4, per = (nst + ks - 1) / ks;
-    const int st0 = s * per, st1 = min(nst, st0 + per);
+    // kw = 4: the workgroup's four waves take consecutive quarters of the split's steps
+    const int per4 = (per + kw - 1) / kw;
+    const int sq0 = s * per, se = min(nst, sq0 + per);
+    const int st0 = min(se, sq0 + wq * per4), st1 = min(se, st0 + per4);
     const i4 ra = rsrc64(P.A), rb = rsrc64(P.B);
     const int m = m0 + r, n = n0 + r;
     const bool mok = m < P.M, nok = n < nreal, isone = P.ones && n == nreal;
@@ -121,6 +127,13 @@ __global__ void __launch_bounds__(256) gemm64_kernel(Q64Batch g) {
         if (sg + G >= st1) break;
         load(sg + 2 * G, a0, b0);
         comp(sg + G, a1, b1);
+    }
+    if (kw > 1) {
+        // the four quarters in wave order; wave 0 finishes the tile
+        red[wq][lane] = acc;
+        __syncthreads();
+        if (wq != 0) return;
+        acc = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
     }
     double *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
     double *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
@@ -300,6 +313,14 @@ __global__ void __launch_bounds__(256) uam_push_kernel(double *ring, int64_t cap
     }
 }
 
+int env_i(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+const int g_kw4 = env_i("AAC_GEMM64_KW4", 1);
+const int g_kw4_steps = env_i("AAC_GEMM64_KW4_STEPS", 16);
+const int g_kw4_tiles = env_i("AAC_GEMM64_KW4_TILES", 1024);
+
 int grid_of(int64_t n) {
     const int64_t b = (n + 255) / 256;
     return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
@@ -343,8 +364,13 @@ int aac_gemm64_batch(const aac_gemm64_prob *in, int32_t n, void *stream) {
         d.ta = s.ta; d.tb = s.tb; d.act = s.act; d.mact = s.mact; d.ones = s.ones; d.ks = ks;
         const int tm = (s.M + 15) / 16, tn = (s.N + 15) / 16;
         d.tiles_n = tn;
+        // long chains over few tiles: four waves per tile (K quarters, LDS reduction), the tile's
+        // waves aligned to one workgroup
+        const int steps = ((s.K + 3) / 4 + ks - 1) / ks;
+        d.kw = (g_kw4 && steps >= g_kw4_steps && (int64_t)tm * tn * ks <= g_kw4_tiles) ? 4 : 1;
+        if (d.kw == 4) waves = (waves + 3) / 4 * 4;
         d.w_begin = (int)waves;
-        waves += (int64_t)tm * tn * ks;
+        waves += (int64_t)tm * tn * ks * d.kw;
         if (waves > (1 << 26)) return lfail(who + "too many tiles");
     }
     g.waves = (int)waves;
