@@ -98,6 +98,11 @@ int aac_uam_set_state(aac_uam *env, const double *pos, const double *vel, const 
                       const uint8_t *reach, const double *clouds, const int32_t *cloud_kind, const int32_t *cloud_tgt,
                       const int32_t *step, const uint8_t *top2, void *stream);
 
+/* Diagnostic (tests): n random segments of length len against a 64-gon of radius r, the radar's
+ * fast ray-vs-polygon paths against the full 64-edge clip; *bad = cases whose hit flag or t differ
+ * in any bit.  Synchronous (allocates, launches on the null stream, copies back). */
+int aac_uam_ray_gon_check(int64_t n, uint64_t seed, double r, double len, uint64_t *bad);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,19 @@ struct UReset {
     uint64_t seed;
 };
 
+#ifdef AAC_UAM_STAMPS
+// phase timestamps of the first 64 workgroups of uam_step_kernel (probe builds only)
+__device__ unsigned long long g_uam_st[64][16];
+#define USTAMP(i)                                                                                     \
+    do {                                                                                               \
+        if (blockIdx.x < 64 && threadIdx.x == 0) g_uam_st[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define USTAMP(i) \
+    do {          \
+    } while (0)
+#endif
+
 struct Lds {
     double2 pos[MAXA], vel[MAXA], ppos[MAXA], pvel[MAXA], goal[MAXA];
     double heading[MAXA];
@@ -88,22 +101,11 @@ __device__ inline double bearing(double xh, double yh, double xi, double yi) {
     return th < 0 ? -th : 360 - th;
 }
 
-// nearest point of segment c->e on the boundary of the clockwise GEOS 64-gon(p, r): the entry if c
-// is outside, the exit if c is inside (LineString.intersection(polygon.boundary), UAM/env:1429-1486)
-__device__ bool ray_gon_boundary(double cx, double cy, double ex, double ey, double px, double py, double r,
-                                 double &tout) {
+// Full Cyrus-Beck clip of segment c->e against the clockwise GEOS 64-gon(p, r): the entry if c is
+// outside, the exit if c is inside (LineString.intersection(polygon.boundary), UAM/env:1429-1486)
+__device__ bool ray_gon_boundary_full(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                      double &tout) {
     const double ddx = ex - cx, ddy = ey - cy;
-    {   // exact pre-filter: the 64-gon lies within the circle of radius r (1 + 1e-15) around p
-        const double wx = px - cx, wy = py - cy;
-        double tt = (wx * ddx + wy * ddy) / (ddx * ddx + ddy * ddy);
-        tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
-        const double qx = tt * ddx - wx, qy = tt * ddy - wy;
-        if (qx * qx + qy * qy > (r + 1e-6) * (r + 1e-6)) return false;
-    }
-    {   // c outside the circumscribed circle: the boundary point is the entry (aac_geom.h window clip)
-        const double wx = px - cx, wy = py - cy;
-        if (wx * wx + wy * wy > r * r * (1.0 + 1e-9)) return ray_poly_entry(cx, cy, ex, ey, px, py, r, tout);
-    }
     double tin = -INFINITY, tex = INFINITY;
     double vx = px + r * c_tab.circ_c[0], vy = py + r * c_tab.circ_s[0];
     for (int k = 0; k < 64; ++k) {
@@ -133,6 +135,58 @@ __device__ bool ray_gon_boundary(double cx, double cy, double ex, double ey, dou
     if (tex < 0.0 || tex > 1.0) return false;   // polygon behind, or the segment ends inside
     tout = tex;
     return true;
+}
+
+// The same result with fast paths (inv_l2 = 1 / |e - c|^2 of the ray):
+//  * exact pre-filter: the 64-gon lies within the circle of radius r around p, so a segment that
+//    passes farther than r + 1e-6 from p misses it (the reciprocal's rounding is far below 1e-6);
+//  * c outside the circumscribed circle: the entry by the window clip of aac_geom.h;
+//  * c inside the inscribed circle (so inside the polygon): every edge has a < 0, no entering edge
+//    gives t >= 0, and the result is the exit min(-a/b) over the leaving edges.  The exit point lies
+//    on the edge the ray crosses, within half an edge (pi/64) of the ray's exit angle from the
+//    circumscribed circle, so the six edges around that angle hold the minimum: same vertices, same
+//    arithmetic as the full clip, whose value it returns.
+//  * anything else (c in the thin annulus between the circles): the full clip.
+__device__ bool ray_gon_boundary(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                 double inv_l2, double &tout) {
+    const double ddx = ex - cx, ddy = ey - cy;
+    const double wx = px - cx, wy = py - cy;
+    {
+        double tt = (wx * ddx + wy * ddy) * inv_l2;
+        tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
+        const double qx = tt * ddx - wx, qy = tt * ddy - wy;
+        if (qx * qx + qy * qy > (r + 1e-6) * (r + 1e-6)) return false;
+    }
+    const double w2 = wx * wx + wy * wy;
+    if (w2 > r * r * (1.0 + 1e-9)) return ray_poly_entry(cx, cy, ex, ey, px, py, r, tout);
+    const double ap = r * c_tab.apothem;
+    if (w2 < ap * ap * (1.0 - 1e-9)) {
+        const double L = sqrt(ddx * ddx + ddy * ddy);
+        const double s0 = (wx * ddx + wy * ddy) / L;
+        const double h2 = w2 - s0 * s0;
+        const double to = (s0 + sqrt(fmax(r * r - h2, 0.0))) / L;      // circumscribed-circle exit
+        const float phi = atan2f((float)(cy + to * ddy - py), (float)(cx + to * ddx - px));
+        const int i0 = (int)lrintf(-phi * (64.0f / 6.28318530717958647f));
+        double tex = INFINITY;
+#pragma unroll
+        for (int dk = -3; dk <= 2; ++dk) {
+            const int k = (i0 + dk) & 63, k1 = (k + 1) & 63;
+            const double vx = px + r * c_tab.circ_c[k], vy = py + r * c_tab.circ_s[k];
+            const double qx = px + r * c_tab.circ_c[k1], qy = py + r * c_tab.circ_s[k1];
+            const double exx = qx - vx, eyy = qy - vy;
+            const double a = exx * (cy - vy) - eyy * (cx - vx);
+            const double b = exx * ddy - eyy * ddx;
+            if (b > 0.0) {
+                const double t = -a / b;
+                tex = t < tex ? t : tex;
+            }
+        }
+        if (tex == INFINITY) return ray_gon_boundary_full(cx, cy, ex, ey, px, py, r, tout);
+        if (tex > 1.0) return false;
+        tout = tex;
+        return true;
+    }
+    return ray_gon_boundary_full(cx, cy, ex, ey, px, py, r, tout);
 }
 
 // segment c->e vs the finite bound segment x = lx, y in [y0, y1] (UAM/env:1413-1427)
@@ -184,13 +238,17 @@ __device__ void dist_row(const UArgs &A, const Lds &S, int la, int base) {
     }
 }
 
-// (2) neighbour order of aircraft la: get_current_agent_nei(queue=True) is a stable sort by
-// np.linalg.norm distance, i.e. rank_j = #{k : d_k < d_j or (d_k == d_j and k < j)}
-__device__ void order_phase(const UArgs &A, Lds &S, int la, int i) {
+// (2) neighbour order: get_current_agent_nei(queue=True) is a stable sort by np.linalg.norm
+// distance, i.e. rank_j = #{k : d_k < d_j or (d_k == d_j and k < j)}.  One (aircraft, neighbour)
+// pair per work item over the whole workgroup (one thread per aircraft left three quarters of the
+// threads idle on the N^2 comparisons: ~57 k cycles per workgroup at N = 16).
+__device__ void order_phase(const UArgs &A, Lds &S, int nag) {
     const int N = A.N;
-    const double *row = s_dist + (size_t)la * N;
-    for (int j = 0; j < N; ++j) {
-        if (j == i) continue;
+    for (int w = threadIdx.x; w < nag * N; w += BLOCK) {
+        const int la = w / N, j = w - la * N;
+        const int le = la / N, i = la - le * N;
+        if (!S.active[le] || j == i) continue;
+        const double *row = s_dist + (size_t)la * N;
         const double dj = row[j];
         int rank = 0;
         for (int k = 0; k < N; ++k) {
@@ -207,6 +265,7 @@ __device__ double radar_ray(const UArgs &A, const Lds &S, int le, int base, int 
     const double2 p = S.pos[base + i];
     const double cx = p.x, cy = p.y;
     const double ex = cx + A.radar_len * c_tab.ray_c[r], ey = cy + A.radar_len * c_tab.ray_s[r];
+    const double inv_l2 = 1.0 / ((ex - cx) * (ex - cx) + (ey - cy) * (ey - cy));
     double best = gdist(ex, ey, cx, cy), d, t;
     const double *rw = c_world.runway;
     if (ray_square(cx, cy, ex, ey, rw[0], rw[1], rw[2], rw[3], d) && d < best) best = d;
@@ -217,7 +276,7 @@ __device__ double radar_ray(const UArgs &A, const Lds &S, int le, int base, int 
     if (ray_hseg(cx, cy, ex, ey, b[2], b[0], b[1], d) && d < best) best = d;
     for (int k = 0; k < 2; ++k) {
         const double2 c = S.cl[le][k];
-        if (ray_gon_boundary(cx, cy, ex, ey, c.x, c.y, c_world.radius[k], t)) {
+        if (ray_gon_boundary(cx, cy, ex, ey, c.x, c.y, c_world.radius[k], inv_l2, t)) {
             d = gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy);
             if (d < best) best = d;
         }
@@ -225,7 +284,7 @@ __device__ double radar_ray(const UArgs &A, const Lds &S, int le, int base, int 
     for (int j = 0; j < A.N; ++j) {
         if (j == i) continue;
         const double2 q = S.pos[base + j];
-        if (ray_gon_boundary(cx, cy, ex, ey, q.x, q.y, A.pb, t)) {
+        if (ray_gon_boundary(cx, cy, ex, ey, q.x, q.y, A.pb, inv_l2, t)) {
             d = gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy);
             if (d < best) best = d;
         }
@@ -319,7 +378,7 @@ __global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 
     const int N = A.N, K = A.K;
     const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x; USTAMP(0);
     const int le = t / N, i = t - le * N;
     const int e = e0 + le;
     const bool active = (t < nag) && (e < A.E);
@@ -392,13 +451,13 @@ __global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 
         lds_agent(S, t, np, nv, pp, pv, A.goal[ai], hd);
         S.reach[t] = reach;
     }
-    __syncthreads();
+    __syncthreads(); USTAMP(1);
     if (active) dist_row(A, S, t, base);
-    __syncthreads();
-    if (active) order_phase(A, S, t, i);
-    __syncthreads();
+    __syncthreads(); USTAMP(2);
+    order_phase(A, S, nag);
+    __syncthreads(); USTAMP(3);
     radar_phase(A, S, e0, nag);
-    __syncthreads();
+    __syncthreads(); USTAMP(4);
 
     // ---- (4) observation; the goal touch of every aircraft first (UAM/env:3929-3936)
     if (active) {
@@ -406,7 +465,7 @@ __global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 
         const double2 g = S.goal[t];
         if (gons_meet(g.x - np.x, g.y - np.y, A.pb + 1.0, false)) S.reach[t] = 1;
     }
-    __syncthreads();
+    __syncthreads(); USTAMP(5);
 
     // ---- (5) ss_reward_Mar_changeskin predicates of aircraft i (UAM/env:3937-4486)
     if (active) {
@@ -480,7 +539,7 @@ __global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 
         if (kind == 3) S.reach[t] = 1;
         A.reach[ai] = S.reach[t];
     }
-    __syncthreads();
+    __syncthreads(); USTAMP(6);
 
     // ---- (6) per env, aircraft in order: the coefficient doubling persists over later aircraft
     //      of the same call (UAM/env:4320, :4546); done, bbc, termination (UAM/main:624-637)
@@ -530,6 +589,7 @@ __global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 
         A.step[eq] = st;
         A.env_done[eq] = (uint8_t)((A.episode_length < st) || any_done || all_reach);
     }
+    USTAMP(15);
 }
 
 // ------------------------------------------------------------------------------ reset
@@ -596,11 +656,36 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     __syncthreads();
     if (active) dist_row(A, S, t, base);
     __syncthreads();
-    if (active) order_phase(A, S, t, i);
+    order_phase(A, S, nag);
     __syncthreads();
     radar_phase(A, S, e0, nag);
     __syncthreads();
     if (active) observe(A, S, e, t, base, i);
+}
+
+// exactness check of ray_gon_boundary's fast paths against the full clip (aac_uam_ray_gon_check):
+// random segments of radar length from points around a 64-gon, focused on the inside / annulus /
+// near-tangent cases; counts results that differ in the hit flag or any bit of t
+__global__ void ray_gon_check_kernel(int64_t n, uint64_t seed, double r, double len, unsigned long long *bad) {
+    unsigned long long nb = 0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t h1 = mix64(seed ^ (uint64_t)q), h2 = mix64(h1), h3 = mix64(h2);
+        const double u1 = (double)(h1 >> 11) * (1.0 / 9007199254740992.0);
+        const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+        const double u3 = (double)(h3 >> 11) * (1.0 / 9007199254740992.0);
+        // origin radius: half the cases inside the polygon, the rest up to 3 r (entry / miss / annulus)
+        const double rad = (q & 1) ? r * u1 : r * 3.0 * u1;
+        const double ang = 6.283185307179586 * u2, dir = 6.283185307179586 * u3;
+        const double px = 1.25, py = -0.75;
+        const double cx = px + rad * cos(ang), cy = py + rad * sin(ang);
+        const double ex = cx + len * cos(dir), ey = cy + len * sin(dir);
+        const double inv_l2 = 1.0 / ((ex - cx) * (ex - cx) + (ey - cy) * (ey - cy));
+        double t1 = -7.0, t2 = -7.0;
+        const bool a = ray_gon_boundary(cx, cy, ex, ey, px, py, r, inv_l2, t1);
+        const bool b = ray_gon_boundary_full(cx, cy, ex, ey, px, py, r, t2);
+        if (a != b || (a && __double_as_longlong(t1) != __double_as_longlong(t2))) ++nb;
+    }
+    if (nb) atomicAdd(bad, nb);
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -763,6 +848,26 @@ static int check_uout(const aac_uam_out *o) {
 }
 
 extern "C" {
+
+int aac_uam_ray_gon_check(int64_t n, uint64_t seed, double r, double len, uint64_t *bad) {
+    if (n <= 0 || !bad || r <= 0.0 || len <= 0.0) return ufail(AAC_E_INVALID, "ray_gon_check: bad argument");
+    unsigned long long *d = nullptr;
+    UCHK(hipMalloc((void **)&d, sizeof(unsigned long long)));
+    UCHK(hipMemset(d, 0, sizeof(unsigned long long)));
+    hipLaunchKernelGGL(ray_gon_check_kernel, dim3(2048), dim3(256), 0, 0, n, seed, r, len, d);
+    UCHK(hipGetLastError());
+    unsigned long long hcount = 0;
+    UCHK(hipMemcpy(&hcount, d, sizeof(hcount), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    *bad = hcount;
+    return AAC_OK;
+}
+
+#ifdef AAC_UAM_STAMPS
+int aac_uam_stamps(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_uam_st), sizeof(g_uam_st)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char *aac_uam_last_error(void) { return g_uerr.c_str(); }
 

@@ -175,3 +175,19 @@ def test_uam_facade_loop(native_lib):
         if env.episode_over(step):
             assert over
             break
+
+
+@pytest.mark.parametrize("r", [0.5, 1.0, 3.0])      # aircraft pB, go-around aircraft, cloud
+def test_ray_gon_fast_paths_exact(native_lib, r):
+    """The radar's ray-vs-64-gon fast paths (exact pre-filter, entry window, inside-polygon exit
+    window) against the full 64-edge clip on 4M random segments around the polygon: the same hit
+    flag and the same t to the last bit (aac_uam_ray_gon_check)."""
+    import ctypes
+    from multi_agent_aac_amd import uam
+    L = uam.lib()
+    L.aac_uam_ray_gon_check.argtypes = [ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_double,
+                                        ctypes.POINTER(ctypes.c_uint64)]
+    for ln in (U.RADAR_DIST, 0.7 * r):
+        bad = ctypes.c_uint64(99)
+        assert L.aac_uam_ray_gon_check(4_000_000, 11, r, float(ln), ctypes.byref(bad)) == 0
+        assert bad.value == 0, (r, ln, bad.value)
