@@ -210,7 +210,7 @@ class Trainer:
         else:
             self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
         self.env.auto_reset(n.env_done, out=n)
-        self.episode.add_(n.env_done.to(torch.int32))
+        self.episode.add_(n.env_done)      # int32 += uint8 in one launch
         self.cur, self.nxt = n, c
         if update and len(self.replay) > self.B:
             self.model.update(self.B, use_graph=not NO_GRAPH, want_stats=False)
@@ -252,7 +252,7 @@ class UamTrainer:
             self.env_events.append((ev0, ev1))
         self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
         self.env.auto_reset(n.env_done, out=n)
-        self.episode.add_(n.env_done.to(torch.int32))
+        self.episode.add_(n.env_done)      # int32 += uint8 in one launch
         self.cur, self.nxt = n, c
         if update and len(self.replay) > self.B:
             self.model.update(self.B, use_graph=not NO_GRAPH)

@@ -9,6 +9,7 @@
  *                        sample = uniform without replacement like random.sample (ATT/mem:19)
  *   aac_adam_flat        torch.optim.Adam step (ATT/maddpg:93-94, :387, :425) on one flat buffer
  *   aac_polyak_flat      soft_update (ATT/maddpg:18-22) on one flat buffer
+ *   aac_polyak_flat_step the same, advancing the optimiser step counter in the same launch
  *   aac_noise_clamp      choose_action exploration: act + randn * var, clamp [-1, 1]
  *                        (ATT/maddpg:476-500, var schedule :563-570)
  * Conventions as in aac_env.h: plain device pointers, ``stream`` = hipStream_t as void*, 0 = ok.
@@ -59,6 +60,10 @@ int aac_adam_flat_at(float *param, const float *grad, float *exp_avg, float *exp
                      float beta1, float beta2, float eps, const int32_t *step, int32_t step_add, void *stream);
 /* tgt = (1 - tau) * tgt + tau * src */
 int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *stream);
+/* Same, and *step += step_add in the same launch (the optimiser step counter of this network,
+ * advanced once per captured update after every Adam step that reads it; NULL: no counter). */
+int aac_polyak_flat_step(float *tgt, const float *src, int64_t n, float tau, int32_t *step, int32_t step_add,
+                         void *stream);
 
 /* Fused activation backward + bias gradient of y = act(x W^T + b) (nn.Linear + ReLU/Tanh of
  * ATT/nets:180-184, ATT/nets:699-701): gm = gy * act'(y) (rows of O at the given strides; gm may

@@ -257,7 +257,11 @@ __global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_
     }
 }
 
-__global__ void polyak_kernel(float *tgt, const float *src, int64_t n, float keep, float tau) {
+// step (optional): the optimiser's device step counter, advanced by step_add in the same launch
+// (the Polyak step is the last reader-free point of an update, ATT/maddpg:436-438)
+__global__ void polyak_kernel(float *tgt, const float *src, int64_t n, float keep, float tau, int32_t *step,
+                              int32_t step_add) {
+    if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += step_add;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float a = keep * tgt[i];
         const float b = tau * src[i];
@@ -481,9 +485,14 @@ int aac_adam_flat_at(float *p, const float *g, float *m, float *v, int64_t n, fl
 }
 
 int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *stream) {
+    return aac_polyak_flat_step(tgt, src, n, tau, nullptr, 0, stream);
+}
+
+int aac_polyak_flat_step(float *tgt, const float *src, int64_t n, float tau, int32_t *step, int32_t step_add,
+                         void *stream) {
     const float keep = (float)(1.0 - (double)tau);
     hipLaunchKernelGGL(polyak_kernel, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, tgt, src, n,
-                       keep, tau);
+                       keep, tau, step, step_add);
     LHIP(hipGetLastError());
     return 0;
 }

@@ -391,10 +391,9 @@ class FusedUpdate:
                           + self._actor_step(i, A, C)
                           + self._adam(m.actor_optimizer, m.fa, self.ga, self.SPLIT_ACTOR, i + 1)
                           for i in range(N)]
-        self.post = [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau),
-                     lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau),
-                     lambda: m.critic_optimizer.step_t.add_(N),
-                     lambda: m.actor_optimizer.step_t.add_(N)]
+        # the Polyak launches also advance the optimisers' step counters (no separate add kernels)
+        self.post = [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau, m.critic_optimizer.step_t, N),
+                     lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau, m.actor_optimizer.step_t, N)]
         self.n_launches = len(self.pre) + sum(len(it) for it in self.iters) + len(self.post)
 
     def _adam(self, opt, flat, gpart, ns, step_add):

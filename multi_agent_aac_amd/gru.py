@@ -325,10 +325,9 @@ class GruUpdate:
             + wgrad_probs(P(self.dcat_a), 64, 128, radar, 0, 18, 18, gA, "Wg", "bg", 64, B, N))
         L += self._adam(m.actor_optimizer, m.fa)
         # ---------------- soft update of every target (WGRU/maddpg:318-322)
-        L += [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau),
-              lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau),
-              lambda: m.critic_optimizer.step_t.add_(1),
-              lambda: m.actor_optimizer.step_t.add_(1)]
+        # (the Polyak launches also advance the optimisers' step counters)
+        L += [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau, m.critic_optimizer.step_t, 1),
+              lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau, m.actor_optimizer.step_t, 1)]
         self.L = L
 
     def ops(self):

@@ -30,6 +30,7 @@ def lib():
         L.aac_replay_gather.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp]
         L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
         L.aac_polyak_flat.argtypes = [vp, vp, i64, f32, vp]
+        L.aac_polyak_flat_step.argtypes = [vp, vp, i64, f32, vp, i32, vp]
         L.aac_noise_clamp.argtypes = [vp, i32, i32, vp, i32, f32, f32, u64, vp, vp, vp]
         L.aac_act_bgrad.argtypes = [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, vp]
         L.aac_bias_act.argtypes = [vp, vp, i64, i32, i32, vp]
@@ -119,8 +120,13 @@ def adam_flat(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999
                              eps, _p(step), _s()), "aac_adam_flat")
 
 
-def polyak_flat(target, source, tau):
-    _chk(lib().aac_polyak_flat(_p(target), _p(source), target.numel(), tau, _s()), "aac_polyak_flat")
+def polyak_flat(target, source, tau, step=None, step_add=0):
+    """soft_update (ATT/maddpg:18-22); with ``step`` (device int32) also ``step += step_add``."""
+    if step is None:
+        _chk(lib().aac_polyak_flat(_p(target), _p(source), target.numel(), tau, _s()), "aac_polyak_flat")
+    else:
+        _chk(lib().aac_polyak_flat_step(_p(target), _p(source), target.numel(), tau, _p(step), step_add, _s()),
+             "aac_polyak_flat_step")
 
 
 def noise_clamp(act, episode, eps_end, noise_start, seed, counter, noise_out=None, noise_end=0.0):

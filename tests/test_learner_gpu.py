@@ -108,6 +108,10 @@ def test_adam_polyak_flat(native_lib):
     td = tgt.to(DEV)
     ops.polyak_flat(td, src.to(DEV), 0.01)
     np.testing.assert_allclose(td.cpu(), want, atol=1e-7, rtol=1e-6)
+    # the counter-advancing form: same soft update, step += 5 in the same launch
+    td2 = tgt.to(DEV)
+    ops.polyak_flat(td2, src.to(DEV), 0.01, step, 5)
+    assert torch.equal(td2, td) and int(step.item()) == 10
 
 
 def test_noise_clamp_schedule(native_lib):
