@@ -479,6 +479,8 @@ def main():
     traffic = None
     tsrc = None
     tpath = os.path.join(ROOT, "profiles", "uam_env_pmc.json") if uam else a.traffic
+    if not uam and tpath and N != 5:     # per-N env PMC files (config 4: env_step_pmc_n8.json)
+        tpath = tpath.replace(".json", f"_n{N}.json")
     if tpath and os.path.exists(tpath):
         with open(tpath) as f:
             t = json.load(f)
