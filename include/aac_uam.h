@@ -70,6 +70,10 @@ int aac_uam_step(aac_uam *env, const double *actions_dev, const aac_uam_out *out
 int aac_uam_set_bank(aac_uam *env, const double *start, const double *goal, const int32_t *clouds, int32_t n,
                      uint64_t seed);
 int aac_uam_auto_reset(aac_uam *env, const uint8_t *env_done_dev, const aac_uam_out *out, void *stream);
+/* Process-wide: on != 0 (default, unless AAC_UAM_RESET_CONTIGUOUS=1) the auto-reset first packs the
+ * resetting envs into an ordered list (one extra launch) so every reset workgroup holds epb of
+ * them; 0 resets over contiguous env ranges.  Results are identical either way. */
+void aac_uam_set_reset_compact(int32_t on);
 
 /* Host: draw n episodes with the reference's rules (UAM/env:575-747, UAM/util:165-237): cloud
  * choices, starts in the two start zones re-drawn until > 3 pB from earlier starts, ends uniform

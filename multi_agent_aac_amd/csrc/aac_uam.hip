@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <algorithm>
 #include <vector>
@@ -62,6 +63,8 @@ struct UReset {
     const int32_t *clouds;    // [E][2] explicit or [n][2] bank
     int32_t bank_n;
     uint64_t seed;
+    const int32_t *list;      // [count, env...] of the resetting envs (uam_compact_kernel); NULL:
+                              // workgroup b takes envs b*epb ... (mask-filtered)
 };
 
 #ifdef AAC_UAM_STAMPS
@@ -292,11 +295,11 @@ __device__ double radar_ray(const UArgs &A, const Lds &S, int le, int base, int 
     return best;
 }
 
-__device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag) {
+__device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag, const int32_t *emap = nullptr) {
     for (int w = threadIdx.x; w < nag * NRAY; w += BLOCK) {
         const int la = w / NRAY, r = w - la * NRAY;
         const int le = la / A.N, i = la - le * A.N;
-        const int e = e0 + le;
+        const int e = emap ? emap[le] : e0 + le;
         if (e >= A.E || !S.active[le]) continue;
         const double v = radar_ray(A, S, le, le * A.N, i, r);
         S.rad[la][r] = v;
@@ -599,23 +602,34 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
     const int t = threadIdx.x;
+    // local env slot -> env: contiguous, or the compacted list of resetting envs (so that every
+    // workgroup that runs has epb envs to reset instead of the few of its contiguous range)
+    __shared__ int32_t emap[MAXA];
     if (t < A.epb) {
-        const int eq = e0 + t;
-        S.active[t] = (eq < A.E) && (R.mask == nullptr || R.mask[eq] != 0);
+        if (R.list) {
+            const int q = e0 + t;
+            const bool on = q < R.list[0];
+            emap[t] = on ? R.list[1 + q] : 0;
+            S.active[t] = on;
+        } else {
+            const int eq = e0 + t;
+            emap[t] = eq;
+            S.active[t] = (eq < A.E) && (R.mask == nullptr || R.mask[eq] != 0);
+        }
     }
     __syncthreads();
     int any = 0;
     for (int k = 0; k < A.epb; ++k) any |= S.active[k];
     if (!any) return;
     const int le = t / N, i = t - le * N;
-    const int e = e0 + le;
+    const int e = emap[le < A.epb ? le : 0];
     const bool active = (t < nag) && (e < A.E) && S.active[le];
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
     // which episode each resetting env takes (bank: a fresh draw per reset)
     __shared__ int32_t src[MAXA];
     if (t < A.epb && S.active[t]) {
-        const int eq = e0 + t;
+        const int eq = emap[t];
         if (R.mode == 1) {
             const int ep = A.episode[eq] + 1;
             A.episode[eq] = ep;
@@ -627,7 +641,7 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     __syncthreads();
     // clouds (UAM/env:576-703)
     if (t < 2 * A.epb && S.active[t >> 1]) {
-        const int lq = t >> 1, k = t & 1, eq = e0 + lq;
+        const int lq = t >> 1, k = t & 1, eq = emap[lq];
         const int kind = R.clouds[src[lq] * 2 + k];
         const double2 c = k == 0 ? make_double2(c_world.cloud_start[kind][0], c_world.cloud_start[kind][1])
                                  : make_double2(c_world.path[kind][0][0], c_world.path[kind][0][1]);
@@ -658,9 +672,39 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     __syncthreads();
     order_phase(A, S, nag);
     __syncthreads();
-    radar_phase(A, S, e0, nag);
+    radar_phase(A, S, e0, nag, emap);
     __syncthreads();
     if (active) observe(A, S, e, t, base, i);
+}
+
+// ordered list of the envs whose done flag is set: rlist = [count, e...] (ascending), one
+// workgroup (a ballot + wave-prefix per 1024 envs), so the reset launch can pack epb resetting
+// envs per workgroup
+__global__ void __launch_bounds__(1024) uam_compact_kernel(const uint8_t *__restrict__ mask, int E, int32_t *rlist) {
+    __shared__ int wsum[16];
+    __shared__ int base_s;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) base_s = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < E; c0 += 1024) {
+        const int e = c0 + threadIdx.x;
+        const bool a = e < E && mask[e] != 0;
+        const unsigned long long b = __ballot(a);
+        const int pre = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(b);
+        __syncthreads();
+        int off = base_s;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        if (a) rlist[1 + off + pre] = e;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int k = 0; k < 16; ++k) tot += wsum[k];
+            base_s += tot;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rlist[0] = base_s;
 }
 
 // exactness check of ray_gon_boundary's fast paths against the full clip (aac_uam_ray_gon_check):
@@ -690,6 +734,11 @@ __global__ void ray_gon_check_kernel(int64_t n, uint64_t seed, double r, double 
 
 // ------------------------------------------------------------------------------ host side
 thread_local std::string g_uerr;
+// AAC_UAM_RESET_CONTIGUOUS=1: auto-reset over contiguous env ranges (no compaction; A/B and tests)
+bool g_no_compact = [] {
+    const char *v = getenv("AAC_UAM_RESET_CONTIGUOUS");
+    return v && v[0] == '1';
+}();
 
 int ufail(int code, const std::string &msg) {
     g_uerr = msg;
@@ -791,6 +840,7 @@ struct aac_uam {
     int32_t *bank_clouds;
     int32_t bank_n;
     uint64_t bank_seed;
+    int32_t *rlist;           // [1 + E]: compacted resetting envs of the last auto-reset
 };
 
 static size_t dist_bytes(const aac_uam *h) { return sizeof(double) * (size_t)h->epb * h->cfg.N * h->cfg.N; }
@@ -892,7 +942,7 @@ int aac_uam_create(const aac_uam_cfg *cfg, int device, aac_uam **out) {
     if (st == hipSuccess) st = hipMemset(h->p, 0, (n) * sizeof(*h->p));
     ALLOC(pos, EN) ALLOC(vel, EN) ALLOC(pre_pos, EN) ALLOC(pre_vel, EN) ALLOC(goal, EN) ALLOC(start, EN)
     ALLOC(heading, EN) ALLOC(reach, EN) ALLOC(top2, EN * 2) ALLOC(clouds, E * 2) ALLOC(cloud_kind, E * 2)
-    ALLOC(cloud_tgt, E) ALLOC(step, E) ALLOC(episode, E)
+    ALLOC(cloud_tgt, E) ALLOC(step, E) ALLOC(episode, E) ALLOC(rlist, E + 1)
 #undef ALLOC
     if (st == hipSuccess) {
         Tab t;
@@ -916,7 +966,7 @@ void aac_uam_destroy(aac_uam *h) {
     if (!h) return;
     void *ptrs[] = {h->pos,   h->vel,        h->pre_pos,   h->pre_vel, h->goal,    h->start,      h->clouds,
                     h->heading, h->reach,    h->top2,      h->cloud_kind, h->cloud_tgt, h->step, h->episode,
-                    h->bank_start, h->bank_goal, h->bank_clouds};
+                    h->bank_start, h->bank_goal, h->bank_clouds, h->rlist};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -977,6 +1027,8 @@ int aac_uam_set_bank(aac_uam *h, const double *start, const double *goal, const 
     return AAC_OK;
 }
 
+void aac_uam_set_reset_compact(int32_t on) { g_no_compact = on == 0; }
+
 int aac_uam_auto_reset(aac_uam *h, const uint8_t *env_done, const aac_uam_out *o, void *stream) {
     if (!h) return ufail(AAC_E_INVALID, "null handle");
     if (!h->bank_n) return ufail(AAC_E_STATE, "no episode bank installed (aac_uam_set_bank)");
@@ -988,6 +1040,12 @@ int aac_uam_auto_reset(aac_uam *h, const uint8_t *env_done, const aac_uam_out *o
     R.clouds = h->bank_clouds;
     R.bank_n = h->bank_n;
     R.seed = h->bank_seed;
+    if (env_done && !g_no_compact) {
+        hipLaunchKernelGGL(uam_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, env_done, h->cfg.E,
+                           h->rlist);
+        UCHK(hipGetLastError());
+        R.list = h->rlist;
+    }
     return launch_reset(h, R, o, stream);
 }
 

@@ -26,7 +26,7 @@ N_RAYS = 18
 BOUND = (0.0, 40.0, 0.0, 40.0)               # UAM/params:32-36
 EXPORTS = ("aac_uam_create", "aac_uam_destroy", "aac_uam_last_error", "aac_uam_reset", "aac_uam_step",
            "aac_uam_set_bank", "aac_uam_auto_reset", "aac_uam_bank_build", "aac_uam_get_state",
-           "aac_uam_set_state", "aac_uam_actor", "aac_uam_actor_last_error")
+           "aac_uam_set_state", "aac_uam_actor", "aac_uam_actor_last_error", "aac_uam_set_reset_compact")
 
 
 class UamCfg(ctypes.Structure):
@@ -55,6 +55,8 @@ def lib():
         L.aac_uam_step.argtypes = [vp, vp, ctypes.POINTER(UamOut), vp]
         L.aac_uam_set_bank.argtypes = [vp, vp, vp, vp, i32, ctypes.c_uint64]
         L.aac_uam_auto_reset.argtypes = [vp, vp, ctypes.POINTER(UamOut), vp]
+        L.aac_uam_set_reset_compact.argtypes = [i32]
+        L.aac_uam_set_reset_compact.restype = None
         L.aac_uam_bank_build.argtypes = [i32, i32, ctypes.c_uint64, vp, vp, vp]
         L.aac_uam_get_state.argtypes = [vp] + [vp] * 13 + [vp]
         L.aac_uam_set_state.argtypes = [vp] + [vp] * 13 + [vp]

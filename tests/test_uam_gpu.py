@@ -191,3 +191,44 @@ def test_ray_gon_fast_paths_exact(native_lib, r):
         bad = ctypes.c_uint64(99)
         assert L.aac_uam_ray_gon_check(4_000_000, 11, r, float(ln), ctypes.byref(bad)) == 0
         assert bad.value == 0, (r, ln, bad.value)
+
+
+@pytest.mark.parametrize("N", [16, 5])
+def test_uam_compact_reset_bit_exact(native_lib, N):
+    """The auto-reset over the compacted list of done envs (default) is bit-identical to the reset
+    over contiguous env ranges: two envs from the same bank and actions, one per mode, compared on
+    every output and state tensor after each step + auto-reset (E not a multiple of epb: ragged tail)."""
+    from multi_agent_aac_amd import uam
+    E = 1003
+    bank = uam.build_bank(2048, N, seed=9)
+    envs = []
+    for _ in range(2):
+        env = uam.BatchedUAM(E, N, neighbours=True)
+        env.set_bank(bank, seed=77)
+        envs.append(env)
+    rng = np.random.default_rng(4)
+    lib = uam.lib()
+    resets = 0
+    try:
+        for mode, env in zip((1, 0), envs):
+            lib.aac_uam_set_reset_compact(mode)
+            env.auto_reset()
+        for k in range(12):
+            act = torch.from_numpy(rng.uniform(-1, 1, (E, N, 2))).to(DEV)
+            for mode, env in zip((1, 0), envs):
+                lib.aac_uam_set_reset_compact(mode)
+                env.step(act)
+                env.auto_reset(env.bufs.env_done)
+            torch.cuda.synchronize()
+            resets += int(envs[0].bufs.env_done.sum())
+            a, b = envs
+            for name in a.bufs.__dict__:
+                x, y = getattr(a.bufs, name), getattr(b.bufs, name)
+                if isinstance(x, torch.Tensor):
+                    assert torch.equal(x, y), (k, name)
+            sa, sb = a.get_state(), b.get_state()
+            for key in sa:
+                assert torch.equal(sa[key], sb[key]), (k, key)
+    finally:
+        lib.aac_uam_set_reset_compact(1)
+    assert resets > 0
