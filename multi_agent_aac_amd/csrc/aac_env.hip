@@ -18,10 +18,12 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/aac_env.h"
 #include "aac_geom.h"
+#include "aac_wave.h"
 
 #define BLOCK 256
 #define MAX_MAP_BYTES 8192
@@ -55,6 +57,8 @@ struct ResetArgs {
     int32_t bank_n;
     uint64_t seed;
     int32_t *episode;         // [E] per-env episode counter (bank mode)
+    const int32_t *list;      // [count, env...] of the resetting envs (env_compact_kernel); NULL:
+                              // workgroup b takes envs b*epb ... (mask-filtered)
 };
 
 // LineString([p0,p1]).buffer(pB) meets one of the 4 infinite bound lines (ATT/env:2507)
@@ -240,11 +244,12 @@ __device__ inline void load_maps(const Args &A, Lds &S) {
 }
 
 // all radar rays of the workgroup's (active) agents: one work item per (agent, ray)
-__device__ inline void radar_phase(const Args &A, const Lds &S, int e0, int nagents, bool check_active) {
+__device__ inline void radar_phase(const Args &A, const Lds &S, int e0, int nagents, bool check_active,
+                                   const int32_t *emap = nullptr) {
     for (int w = threadIdx.x; w < nagents * NRAY; w += BLOCK) {
         const int la = w / NRAY, r = w - la * NRAY;
         const int le = la / A.N, i = la - le * A.N;
-        const int e = e0 + le;
+        const int e = emap ? emap[le] : e0 + le;
         if (e >= A.E) continue;
         if (check_active && !S.active[le]) continue;
         const uint8_t *occ = S.occ + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
@@ -419,17 +424,27 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
     const int t = threadIdx.x;
-    // which of this workgroup's envs reset; skip the whole workgroup if none (the common case)
+    // which envs this workgroup resets (contiguous range, or its slots of the packed list of the
+    // done envs); skip the whole workgroup if none (the common case)
+    __shared__ int32_t emap[BLOCK];
     if (t < A.epb) {
-        const int e = e0 + t;
-        S.active[t] = (e < A.E) && (R.mask == nullptr || R.mask[e] != 0);
+        if (R.list) {
+            const int q = e0 + t;
+            const bool on = q < R.list[0];
+            emap[t] = on ? R.list[1 + q] : 0;
+            S.active[t] = on;
+        } else {
+            const int e = e0 + t;
+            emap[t] = e;
+            S.active[t] = (e < A.E) && (R.mask == nullptr || R.mask[e] != 0);
+        }
     }
     __syncthreads();
     int any = 0;
     for (int k = 0; k < A.epb; ++k) any |= S.active[k];
     if (!any) return;
     const int le = t / N, i = t - le * N;
-    const int e = e0 + le;
+    const int e = emap[le < A.epb ? le : 0];
     const bool active = (t < nag) && (e < A.E) && S.active[le];
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
@@ -441,7 +456,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         // the last of 4096).
         const int lane = t & 63, wv = t >> 6;
         for (int lq = wv; lq < A.epb; lq += BLOCK / 64) {
-            const int eq = e0 + lq;
+            const int eq = emap[lq];
             if (eq >= A.E || !S.active[lq]) continue;
             const int ep = R.episode[eq] + 1;
             const int bq = lq * N;
@@ -507,12 +522,22 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         S.goal[t] = A.goal[ai];
     }
     __syncthreads();   // map_idx (explicit mode) written above is read by the radar phase below
-    radar_phase(A, S, e0, nag, true);
+    radar_phase(A, S, e0, nag, true, emap);
     if (active) observe_agent(A, S, e, i, base);
+}
+
+// ordered list of the done envs for the packed auto-reset (aacw::compact_flags)
+__global__ void __launch_bounds__(1024) env_compact_kernel(const uint8_t *__restrict__ mask, int E, int32_t *rlist) {
+    aacw::compact_flags(mask, E, rlist);
 }
 
 // ------------------------------------------------------------------------------ host side
 thread_local std::string g_err;
+// AAC_ENV_RESET_CONTIGUOUS=1: auto-reset over contiguous env ranges (no packing; A/B and tests)
+bool g_env_no_compact = [] {
+    const char *v = getenv("AAC_ENV_RESET_CONTIGUOUS");
+    return v && v[0] == '1';
+}();
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -538,6 +563,7 @@ struct aac_env {
     int32_t *bank_cnt;
     int32_t bank_n;
     uint64_t bank_seed;
+    int32_t *rlist;           // [1 + E]: packed resetting envs of the last auto-reset
 };
 
 static Args make_args(const aac_env *h, const aac_step_out *o) {
@@ -627,6 +653,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     ALLOC(pos, EN) ALLOC(vel, EN) ALLOC(pre_pos, EN) ALLOC(pre_vel, EN) ALLOC(goal, EN)
     ALLOC(wp, EN * h->W) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
+    ALLOC(rlist, (size_t)c.E + 1)
     ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
 #undef ALLOC
     if (st == hipSuccess) st = hipMemcpy(h->occ, c.occ, (size_t)c.n_maps * c.grid_w * c.grid_h, hipMemcpyHostToDevice);
@@ -646,7 +673,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
 void aac_env_destroy(aac_env *h) {
     if (!h) return;
     void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->wp, h->wp_cur, h->wp_cnt, h->wall,
-                    h->reach, h->step, h->map_idx, h->episode, h->occ, h->bank_start, h->bank_wp, h->bank_cnt};
+                    h->reach, h->step, h->map_idx, h->episode, h->occ, h->bank_start, h->bank_wp, h->bank_cnt, h->rlist};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -724,10 +751,18 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
     R.bank_n = h->bank_n;
     R.seed = h->bank_seed;
     R.episode = h->episode;
+    if (env_done && !g_env_no_compact) {
+        hipLaunchKernelGGL(env_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, env_done, h->cfg.E,
+                           h->rlist);
+        HIPCHK(hipGetLastError());
+        R.list = h->rlist;
+    }
     hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A, R);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
+
+void aac_env_set_reset_compact(int32_t on) { g_env_no_compact = on == 0; }
 
 #define CPY(dst, src, n)                                                                                  \
     if (dst && src) HIPCHK(hipMemcpyAsync((void *)(dst), (const void *)(src), (n), hipMemcpyDeviceToDevice, \

@@ -25,6 +25,7 @@
 
 #include "../../include/aac_uam.h"
 #include "aac_geom.h"
+#include "aac_wave.h"
 
 #define BLOCK 256
 #define MAXA 64   // aircraft per workgroup
@@ -677,34 +678,9 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     if (active) observe(A, S, e, t, base, i);
 }
 
-// ordered list of the envs whose done flag is set: rlist = [count, e...] (ascending), one
-// workgroup (a ballot + wave-prefix per 1024 envs), so the reset launch can pack epb resetting
-// envs per workgroup
+// ordered list of the done envs for the packed auto-reset (aacw::compact_flags)
 __global__ void __launch_bounds__(1024) uam_compact_kernel(const uint8_t *__restrict__ mask, int E, int32_t *rlist) {
-    __shared__ int wsum[16];
-    __shared__ int base_s;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) base_s = 0;
-    __syncthreads();
-    for (int c0 = 0; c0 < E; c0 += 1024) {
-        const int e = c0 + threadIdx.x;
-        const bool a = e < E && mask[e] != 0;
-        const unsigned long long b = __ballot(a);
-        const int pre = __popcll(b & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[w] = __popcll(b);
-        __syncthreads();
-        int off = base_s;
-        for (int k = 0; k < w; ++k) off += wsum[k];
-        if (a) rlist[1 + off + pre] = e;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int tot = 0;
-            for (int k = 0; k < 16; ++k) tot += wsum[k];
-            base_s += tot;
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) rlist[0] = base_s;
+    aacw::compact_flags(mask, E, rlist);
 }
 
 // exactness check of ray_gon_boundary's fast paths against the full clip (aac_uam_ray_gon_check):

@@ -42,4 +42,34 @@ __device__ __forceinline__ void wsum_n(float (&v)[N]) {
 }
 #undef DPP_STEP
 
+// ordered list of the envs whose flag is set: rlist = [count, e...] (ascending).  Called by ONE
+// workgroup of 1024 threads (a ballot + wave prefix per 1024 envs), so that an auto-reset launch
+// can pack its workgroups with resetting envs instead of walking contiguous env ranges.
+__device__ inline void compact_flags(const uint8_t *__restrict__ mask, int E, int32_t *rlist) {
+    __shared__ int wsum[16];
+    __shared__ int base_s;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) base_s = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < E; c0 += 1024) {
+        const int e = c0 + threadIdx.x;
+        const bool a = e < E && mask[e] != 0;
+        const unsigned long long b = __ballot(a);
+        const int pre = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(b);
+        __syncthreads();
+        int off = base_s;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        if (a) rlist[1 + off + pre] = e;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int k = 0; k < 16; ++k) tot += wsum[k];
+            base_s += tot;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rlist[0] = base_s;
+}
+
 }  // namespace aacw

@@ -144,3 +144,41 @@ def test_event_coverage(native_lib, occ):
         _cmp_step(env.bufs, co, f"t{t}")
         seen |= int(np.bitwise_or.reduce(co.mask.ravel()))
     assert seen & 0b11011 == 0b11011, bin(seen)   # bound, drone, building, wp all exercised
+
+
+def test_packed_auto_reset_bit_exact(native_lib, occ):
+    """The auto-reset over the packed list of done envs (default) is bit-identical to the reset
+    over contiguous env ranges: two envs, same OD bank and actions, one per mode, compared on every
+    output and state tensor after each step + auto-reset (E not a multiple of epb: ragged tail)."""
+    from multi_agent_aac_amd import _native, world
+    E, N = 1001, 5
+    bank = world.ODBank(occ, n_pairs=4096, seed=6, max_wp=W_DEFAULT)
+    envs = [_env(E, N, occ, 2) for _ in range(2)]
+    for env in envs:
+        env.set_od_bank(bank, seed=99)
+    lib = _native.lib()
+    rng = np.random.default_rng(8)
+    resets = 0
+    try:
+        for mode, env in zip((1, 0), envs):
+            lib.aac_env_set_reset_compact(mode)
+            env.auto_reset(None)
+        for k in range(30):
+            act = torch.from_numpy(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)).to("cuda")
+            for mode, env in zip((1, 0), envs):
+                lib.aac_env_set_reset_compact(mode)
+                env.step(act)
+                env.auto_reset(env.bufs.env_done)
+            torch.cuda.synchronize()
+            resets += int(envs[0].bufs.env_done.sum())
+            a, b = envs
+            for name in a.bufs.__dict__:
+                x, y = getattr(a.bufs, name), getattr(b.bufs, name)
+                if isinstance(x, torch.Tensor):
+                    assert torch.equal(x, y), (k, name)
+            sa, sb = a.get_state(), b.get_state()
+            for key in sa:
+                assert torch.equal(sa[key], sb[key]), (k, key)
+    finally:
+        lib.aac_env_set_reset_compact(1)
+    assert resets > 0
