@@ -43,33 +43,40 @@ __device__ __forceinline__ void wsum_n(float (&v)[N]) {
 #undef DPP_STEP
 
 // ordered list of the envs whose flag is set: rlist = [count, e...] (ascending).  Called by ONE
-// workgroup of 1024 threads (a ballot + wave prefix per 1024 envs), so that an auto-reset launch
-// can pack its workgroups with resetting envs instead of walking contiguous env ranges.
+// workgroup of 1024 threads; each thread owns 8 consecutive envs of a 8192-env tile (one pass at
+// E <= 8192): local count, wave prefix by shuffles, wave totals through LDS.  An auto-reset launch
+// then packs its workgroups with resetting envs instead of walking contiguous env ranges.
 __device__ inline void compact_flags(const uint8_t *__restrict__ mask, int E, int32_t *rlist) {
+    constexpr int PER = 8, TILE = 1024 * PER;
     __shared__ int wsum[16];
-    __shared__ int base_s;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) base_s = 0;
-    __syncthreads();
-    for (int c0 = 0; c0 < E; c0 += 1024) {
-        const int e = c0 + threadIdx.x;
-        const bool a = e < E && mask[e] != 0;
-        const unsigned long long b = __ballot(a);
-        const int pre = __popcll(b & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[w] = __popcll(b);
-        __syncthreads();
-        int off = base_s;
-        for (int k = 0; k < w; ++k) off += wsum[k];
-        if (a) rlist[1 + off + pre] = e;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int tot = 0;
-            for (int k = 0; k < 16; ++k) tot += wsum[k];
-            base_s += tot;
+    int base = 0;
+    for (int t0 = 0; t0 < E; t0 += TILE) {
+        const int e0 = t0 + threadIdx.x * PER;
+        unsigned bits = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) bits |= (e0 + k < E && mask[e0 + k] != 0) ? (1u << k) : 0u;
+        const int c = __popc(bits);
+        int incl = c;     // inclusive prefix over the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += v;
         }
+        if (lane == 63) wsum[w] = incl;
         __syncthreads();
+        int off = base + incl - c, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            const int s = wsum[k];
+            if (k < w) off += s;
+            tot += s;
+        }
+        for (int k = 0; k < PER; ++k)
+            if (bits & (1u << k)) rlist[1 + off++] = e0 + k;
+        base += tot;
+        __syncthreads();     // wsum is rewritten by the next tile
     }
-    if (threadIdx.x == 0) rlist[0] = base_s;
+    if (threadIdx.x == 0) rlist[0] = base;
 }
 
 }  // namespace aacw

@@ -193,13 +193,12 @@ def test_ray_gon_fast_paths_exact(native_lib, r):
         assert bad.value == 0, (r, ln, bad.value)
 
 
-@pytest.mark.parametrize("N", [16, 5])
-def test_uam_compact_reset_bit_exact(native_lib, N):
+@pytest.mark.parametrize("N,E", [(16, 1003), (5, 9001)])     # 9001: more than one 8192-env packing tile
+def test_uam_compact_reset_bit_exact(native_lib, N, E):
     """The auto-reset over the compacted list of done envs (default) is bit-identical to the reset
     over contiguous env ranges: two envs from the same bank and actions, one per mode, compared on
     every output and state tensor after each step + auto-reset (E not a multiple of epb: ragged tail)."""
     from multi_agent_aac_amd import uam
-    E = 1003
     bank = uam.build_bank(2048, N, seed=9)
     envs = []
     for _ in range(2):
