@@ -184,9 +184,9 @@ class Trainer:
         self.env_events = []
 
     def env_episode_view(self):
-        # per-env episode counter lives in the native handle; a device tensor mirror drives the
-        # noise schedule (env e's own episode index, ATT/maddpg:476-477)
-        return torch.ones(self.E, dtype=torch.int32, device="cuda")
+        # the env's own per-env episode counter (advanced by each auto-reset; 1 after the first)
+        # drives the noise schedule (env e's own episode index, ATT/maddpg:476-477)
+        return self.env.use_episode_buffer(torch.zeros(self.E, dtype=torch.int32, device="cuda"))
 
     def step(self, update=True, time_env=False):
         c, n = self.cur, self.nxt
@@ -210,7 +210,6 @@ class Trainer:
         else:
             self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
         self.env.auto_reset(n.env_done, out=n)
-        self.episode.add_(n.env_done)      # int32 += uint8 in one launch
         self.cur, self.nxt = n, c
         if update and len(self.replay) > self.B:
             self.model.update(self.B, use_graph=not NO_GRAPH, want_stats=False)
@@ -236,8 +235,8 @@ class UamTrainer:
         self.replay = self.model.attach_replay(memory, seed=seed)
         self.cur = self.env.alloc_buffers()
         self.nxt = self.env.alloc_buffers()
-        self.episode = torch.ones(E, dtype=torch.int32, device="cuda")
-        self.env.auto_reset(None, out=self.cur)
+        self.episode = self.env.use_episode_buffer(torch.zeros(E, dtype=torch.int32, device="cuda"))
+        self.env.auto_reset(None, out=self.cur)      # episode counters -> 1
         self.env_events = []
 
     def step(self, update=True, time_env=False):
@@ -252,7 +251,6 @@ class UamTrainer:
             self.env_events.append((ev0, ev1))
         self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
         self.env.auto_reset(n.env_done, out=n)
-        self.episode.add_(n.env_done)      # int32 += uint8 in one launch
         self.cur, self.nxt = n, c
         if update and len(self.replay) > self.B:
             self.model.update(self.B, use_graph=not NO_GRAPH)

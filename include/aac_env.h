@@ -93,6 +93,10 @@ int aac_env_auto_reset(aac_env *env, const uint8_t *env_done_dev, const aac_step
  * launch) so that each reset workgroup holds epb of them; 0 (default, unless AAC_ENV_RESET_PACKED=1)
  * resets over contiguous env ranges.  Results are identical either way. */
 void aac_env_set_reset_compact(int32_t on);
+/* From now on the per-env episode counter (int32[E], advanced by every auto-reset of an env) lives
+ * in the caller's device buffer episode_dev (the current counts are copied into it); the caller
+ * keeps it alive while the handle exists.  A trainer's noise schedule can read it directly. */
+int aac_env_use_episode_buffer(aac_env *env, int32_t *episode_dev);
 
 /* State export / import (device pointers, each may be NULL to skip). */
 int aac_env_get_state(aac_env *env, double *pos, double *vel, double *pre_pos, double *pre_vel, double *goal,

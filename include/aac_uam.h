@@ -74,6 +74,10 @@ int aac_uam_auto_reset(aac_uam *env, const uint8_t *env_done_dev, const aac_uam_
  * resetting envs into an ordered list (one extra launch) so every reset workgroup holds epb of
  * them; 0 resets over contiguous env ranges.  Results are identical either way. */
 void aac_uam_set_reset_compact(int32_t on);
+/* From now on the per-env episode counter (int32[E], advanced by every auto-reset of an env) lives
+ * in the caller's device buffer episode_dev (the current counts are copied into it); the caller
+ * keeps it alive while the handle exists. */
+int aac_uam_use_episode_buffer(aac_uam *env, int32_t *episode_dev);
 
 /* Host: draw n episodes with the reference's rules (UAM/env:575-747, UAM/util:165-237): cloud
  * choices, starts in the two start zones re-drawn until > 3 pB from earlier starts, ends uniform

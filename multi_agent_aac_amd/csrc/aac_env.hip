@@ -560,6 +560,7 @@ struct aac_env {
     int K, D0, W, epb, blocks;
     double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp;
     int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx, *episode;
+    int32_t *episode_own;     // the handle's own counter buffer (episode may be a caller's buffer)
     uint8_t *reach, *occ;
     double2 *bank_start, *bank_wp;
     int32_t *bank_cnt;
@@ -656,6 +657,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     ALLOC(wp, EN * h->W) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
     ALLOC(rlist, (size_t)c.E + 1)
+    h->episode_own = h->episode;
     ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
 #undef ALLOC
     if (st == hipSuccess) st = hipMemcpy(h->occ, c.occ, (size_t)c.n_maps * c.grid_w * c.grid_h, hipMemcpyHostToDevice);
@@ -675,7 +677,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
 void aac_env_destroy(aac_env *h) {
     if (!h) return;
     void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->wp, h->wp_cur, h->wp_cnt, h->wall,
-                    h->reach, h->step, h->map_idx, h->episode, h->occ, h->bank_start, h->bank_wp, h->bank_cnt, h->rlist};
+                    h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt, h->rlist};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -765,6 +767,15 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
 }
 
 void aac_env_set_reset_compact(int32_t on) { g_env_no_compact = on == 0; }
+
+int aac_env_use_episode_buffer(aac_env *h, int32_t *episode_dev) {
+    if (!h || !episode_dev) return fail(AAC_E_INVALID, "null argument");
+    HIPCHK(hipSetDevice(h->device));
+    if (episode_dev != h->episode)
+        HIPCHK(hipMemcpy(episode_dev, h->episode, sizeof(int32_t) * (size_t)h->cfg.E, hipMemcpyDeviceToDevice));
+    h->episode = episode_dev;
+    return AAC_OK;
+}
 
 #define CPY(dst, src, n)                                                                                  \
     if (dst && src) HIPCHK(hipMemcpyAsync((void *)(dst), (const void *)(src), (n), hipMemcpyDeviceToDevice, \

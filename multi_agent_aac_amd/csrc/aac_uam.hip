@@ -817,6 +817,7 @@ struct aac_uam {
     int32_t bank_n;
     uint64_t bank_seed;
     int32_t *rlist;           // [1 + E]: compacted resetting envs of the last auto-reset
+    int32_t *episode_own;     // the handle's own counter buffer (episode may be a caller's buffer)
 };
 
 static size_t dist_bytes(const aac_uam *h) { return sizeof(double) * (size_t)h->epb * h->cfg.N * h->cfg.N; }
@@ -919,6 +920,7 @@ int aac_uam_create(const aac_uam_cfg *cfg, int device, aac_uam **out) {
     ALLOC(pos, EN) ALLOC(vel, EN) ALLOC(pre_pos, EN) ALLOC(pre_vel, EN) ALLOC(goal, EN) ALLOC(start, EN)
     ALLOC(heading, EN) ALLOC(reach, EN) ALLOC(top2, EN * 2) ALLOC(clouds, E * 2) ALLOC(cloud_kind, E * 2)
     ALLOC(cloud_tgt, E) ALLOC(step, E) ALLOC(episode, E) ALLOC(rlist, E + 1)
+    h->episode_own = h->episode;
 #undef ALLOC
     if (st == hipSuccess) {
         Tab t;
@@ -941,7 +943,7 @@ int aac_uam_create(const aac_uam_cfg *cfg, int device, aac_uam **out) {
 void aac_uam_destroy(aac_uam *h) {
     if (!h) return;
     void *ptrs[] = {h->pos,   h->vel,        h->pre_pos,   h->pre_vel, h->goal,    h->start,      h->clouds,
-                    h->heading, h->reach,    h->top2,      h->cloud_kind, h->cloud_tgt, h->step, h->episode,
+                    h->heading, h->reach,    h->top2,      h->cloud_kind, h->cloud_tgt, h->step, h->episode_own,
                     h->bank_start, h->bank_goal, h->bank_clouds, h->rlist};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -1004,6 +1006,15 @@ int aac_uam_set_bank(aac_uam *h, const double *start, const double *goal, const 
 }
 
 void aac_uam_set_reset_compact(int32_t on) { g_no_compact = on == 0; }
+
+int aac_uam_use_episode_buffer(aac_uam *h, int32_t *episode_dev) {
+    if (!h || !episode_dev) return ufail(AAC_E_INVALID, "null argument");
+    UCHK(hipSetDevice(h->device));
+    if (episode_dev != h->episode)
+        UCHK(hipMemcpy(episode_dev, h->episode, sizeof(int32_t) * (size_t)h->cfg.E, hipMemcpyDeviceToDevice));
+    h->episode = episode_dev;
+    return AAC_OK;
+}
 
 int aac_uam_auto_reset(aac_uam *h, const uint8_t *env_done, const aac_uam_out *o, void *stream) {
     if (!h) return ufail(AAC_E_INVALID, "null handle");

@@ -155,6 +155,15 @@ class BatchedEnv:
                       "aac_env_set_od_bank")
         self.bank = bank
 
+    def use_episode_buffer(self, episode: torch.Tensor):
+        """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E],
+        on this device): a trainer's noise schedule then reads it with no per-step update."""
+        assert episode.dtype == torch.int32 and episode.shape == (self.E,) and episode.is_contiguous()
+        assert episode.device == self.device
+        _native.check(_native.lib().aac_env_use_episode_buffer(self._h, _ptr(episode)), "aac_env_use_episode_buffer")
+        self._episode_buf = episode
+        return episode
+
     def auto_reset(self, env_done=None, out: Optional[StepBuffers] = None):
         """Redraw OD from the device bank for envs with env_done != 0 (None = all envs)."""
         out = out or self.bufs

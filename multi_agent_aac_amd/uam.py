@@ -26,7 +26,8 @@ N_RAYS = 18
 BOUND = (0.0, 40.0, 0.0, 40.0)               # UAM/params:32-36
 EXPORTS = ("aac_uam_create", "aac_uam_destroy", "aac_uam_last_error", "aac_uam_reset", "aac_uam_step",
            "aac_uam_set_bank", "aac_uam_auto_reset", "aac_uam_bank_build", "aac_uam_get_state",
-           "aac_uam_set_state", "aac_uam_actor", "aac_uam_actor_last_error", "aac_uam_set_reset_compact")
+           "aac_uam_set_state", "aac_uam_actor", "aac_uam_actor_last_error", "aac_uam_set_reset_compact",
+           "aac_uam_use_episode_buffer")
 
 
 class UamCfg(ctypes.Structure):
@@ -57,6 +58,7 @@ def lib():
         L.aac_uam_auto_reset.argtypes = [vp, vp, ctypes.POINTER(UamOut), vp]
         L.aac_uam_set_reset_compact.argtypes = [i32]
         L.aac_uam_set_reset_compact.restype = None
+        L.aac_uam_use_episode_buffer.argtypes = [vp, vp]
         L.aac_uam_bank_build.argtypes = [i32, i32, ctypes.c_uint64, vp, vp, vp]
         L.aac_uam_get_state.argtypes = [vp] + [vp] * 13 + [vp]
         L.aac_uam_set_state.argtypes = [vp] + [vp] * 13 + [vp]
@@ -212,6 +214,14 @@ class BatchedUAM:
         _chk(lib().aac_uam_set_bank(self._h, bank.start.ctypes.data, bank.goal.ctypes.data, bank.clouds.ctypes.data,
                                     bank.n, ctypes.c_uint64(seed)), "aac_uam_set_bank")
         self.bank = bank
+
+    def use_episode_buffer(self, episode: torch.Tensor):
+        """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E])."""
+        assert episode.dtype == torch.int32 and episode.shape == (self.E,) and episode.is_contiguous()
+        assert episode.is_cuda
+        _chk(lib().aac_uam_use_episode_buffer(self._h, _ptr(episode)), "aac_uam_use_episode_buffer")
+        self._episode_buf = episode
+        return episode
 
     def auto_reset(self, env_done=None, out: Optional[UamBuffers] = None):
         """Reset every env with env_done != 0 (None = all) to a fresh bank episode."""

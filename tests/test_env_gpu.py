@@ -182,3 +182,22 @@ def test_packed_auto_reset_bit_exact(native_lib, occ):
     finally:
         lib.aac_env_set_reset_compact(0)
     assert resets > 0
+
+
+def test_episode_buffer_counts_resets(native_lib, occ):
+    """aac_env_use_episode_buffer: the caller's tensor holds the per-env episode counter, 1 after the
+    first auto-reset, + env_done after every later one (what bench.py's noise schedule reads)."""
+    from multi_agent_aac_amd import world
+    E, N = 300, 5
+    env = _env(E, N, occ, 2)
+    env.set_od_bank(world.ODBank(occ, n_pairs=2048, seed=3, max_wp=W_DEFAULT), seed=4)
+    ep = env.use_episode_buffer(torch.zeros(E, dtype=torch.int32, device="cuda"))
+    env.auto_reset(None)
+    want = torch.ones(E, dtype=torch.int32, device="cuda")
+    rng = np.random.default_rng(1)
+    for _ in range(20):
+        env.step(torch.from_numpy(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)).to("cuda"))
+        want += env.bufs.env_done.to(torch.int32)
+        env.auto_reset(env.bufs.env_done)
+    torch.cuda.synchronize()
+    assert torch.equal(ep, want) and int(want.max()) > 1

@@ -231,3 +231,20 @@ def test_uam_compact_reset_bit_exact(native_lib, N, E):
     finally:
         lib.aac_uam_set_reset_compact(1)
     assert resets > 0
+
+
+def test_uam_episode_buffer_counts_resets(native_lib):
+    from multi_agent_aac_amd import uam
+    E, N = 257, 8
+    env = uam.BatchedUAM(E, N)
+    env.set_bank(uam.build_bank(1024, N, seed=2), seed=3)
+    ep = env.use_episode_buffer(torch.zeros(E, dtype=torch.int32, device=DEV))
+    env.auto_reset()
+    want = torch.ones(E, dtype=torch.int32, device=DEV)
+    rng = np.random.default_rng(5)
+    for _ in range(10):
+        env.step(torch.from_numpy(rng.uniform(-1, 1, (E, N, 2))).to(DEV))
+        want += env.bufs.env_done.to(torch.int32)
+        env.auto_reset(env.bufs.env_done)
+    torch.cuda.synchronize()
+    assert torch.equal(ep, want) and int(want.max()) > 1
