@@ -95,8 +95,9 @@ int aac_env_auto_reset(aac_env *env, const uint8_t *env_done_dev, const aac_step
 void aac_env_set_reset_compact(int32_t on);
 /* From now on the per-env episode counter (int32[E], advanced by every auto-reset of an env) lives
  * in the caller's device buffer episode_dev (the current counts are copied into it); the caller
- * keeps it alive while the handle exists.  A trainer's noise schedule can read it directly. */
-int aac_env_use_episode_buffer(aac_env *env, int32_t *episode_dev);
+ * keeps it alive while the handle exists.  A trainer's noise schedule can read it directly.  The copy
+ * is enqueued on `stream` (ordered after the caller's pending resets and its fill of the buffer). */
+int aac_env_use_episode_buffer(aac_env *env, int32_t *episode_dev, void *stream);
 
 /* State export / import (device pointers, each may be NULL to skip). */
 int aac_env_get_state(aac_env *env, double *pos, double *vel, double *pre_pos, double *pre_vel, double *goal,

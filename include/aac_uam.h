@@ -76,8 +76,8 @@ int aac_uam_auto_reset(aac_uam *env, const uint8_t *env_done_dev, const aac_uam_
 void aac_uam_set_reset_compact(int32_t on);
 /* From now on the per-env episode counter (int32[E], advanced by every auto-reset of an env) lives
  * in the caller's device buffer episode_dev (the current counts are copied into it); the caller
- * keeps it alive while the handle exists. */
-int aac_uam_use_episode_buffer(aac_uam *env, int32_t *episode_dev);
+ * keeps it alive while the handle exists.  The copy is enqueued on `stream`. */
+int aac_uam_use_episode_buffer(aac_uam *env, int32_t *episode_dev, void *stream);
 
 /* Host: draw n episodes with the reference's rules (UAM/env:575-747, UAM/util:165-237): cloud
  * choices, starts in the two start zones re-drawn until > 3 pB from earlier starts, ends uniform

@@ -60,7 +60,7 @@ def lib():
     L.aac_env_auto_reset.argtypes = [vp, vp, ctypes.POINTER(StepOut), vp]
     L.aac_env_set_reset_compact.argtypes = [ctypes.c_int32]
     L.aac_env_set_reset_compact.restype = None
-    L.aac_env_use_episode_buffer.argtypes = [vp, vp]
+    L.aac_env_use_episode_buffer.argtypes = [vp, vp, vp]
     L.aac_env_get_state.argtypes = [vp] + [vp] * 12 + [vp]
     L.aac_env_set_state.argtypes = [vp] + [vp] * 12 + [vp]
     L.aac_astar.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32]

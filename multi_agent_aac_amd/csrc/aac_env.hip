@@ -768,11 +768,13 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
 
 void aac_env_set_reset_compact(int32_t on) { g_env_no_compact = on == 0; }
 
-int aac_env_use_episode_buffer(aac_env *h, int32_t *episode_dev) {
+int aac_env_use_episode_buffer(aac_env *h, int32_t *episode_dev, void *stream) {
     if (!h || !episode_dev) return fail(AAC_E_INVALID, "null argument");
     HIPCHK(hipSetDevice(h->device));
+    // on the caller's stream: ordered after its pending auto-resets and its fill of episode_dev
     if (episode_dev != h->episode)
-        HIPCHK(hipMemcpy(episode_dev, h->episode, sizeof(int32_t) * (size_t)h->cfg.E, hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpyAsync(episode_dev, h->episode, sizeof(int32_t) * (size_t)h->cfg.E, hipMemcpyDeviceToDevice,
+                              (hipStream_t)stream));
     h->episode = episode_dev;
     return AAC_OK;
 }

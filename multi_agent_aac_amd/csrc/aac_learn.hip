@@ -177,6 +177,27 @@ __global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B
     // B (DeviceReplay.sample_batch / the learners' plans), this only keeps a bad call in bounds
     const int64_t size = meta[1] > 0 ? meta[1] : 1;
     const uint64_t ctr = *counter;
+    if (size < 2 * (int64_t)B) {
+        // few spare rows (size < 2B <= 8192, the first updates after the len(memory) > B guard): a
+        // redraw then hits a free row with probability (size - B) / size per round, so draw exactly
+        // instead -- a partial Fisher-Yates shuffle of [0, size) in LDS (uniform ordered sample
+        // without replacement, as random.sample), one thread, B swaps
+        const int n = (int)size;
+        for (int s = threadIdx.x; s < n; s += 1024) keys[s] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int m = B < n ? B : n;
+            for (int i = 0; i < m; ++i) {
+                const int j = i + (int)draw(seed, ctr, i, 0, n - i);
+                const int t = keys[i];
+                keys[i] = keys[j];
+                keys[j] = t;
+            }
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < B; idx += 1024) out[idx] = keys[idx < n ? idx : idx % n];
+        return;
+    }
     const int nv = (B + 1023) / 1024;
     int val[4], att[4];
     for (int u = 0; u < nv; ++u) {

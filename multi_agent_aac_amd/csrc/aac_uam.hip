@@ -1007,11 +1007,13 @@ int aac_uam_set_bank(aac_uam *h, const double *start, const double *goal, const 
 
 void aac_uam_set_reset_compact(int32_t on) { g_no_compact = on == 0; }
 
-int aac_uam_use_episode_buffer(aac_uam *h, int32_t *episode_dev) {
+int aac_uam_use_episode_buffer(aac_uam *h, int32_t *episode_dev, void *stream) {
     if (!h || !episode_dev) return ufail(AAC_E_INVALID, "null argument");
     UCHK(hipSetDevice(h->device));
+    // on the caller's stream: ordered after its pending auto-resets and its fill of episode_dev
     if (episode_dev != h->episode)
-        UCHK(hipMemcpy(episode_dev, h->episode, sizeof(int32_t) * (size_t)h->cfg.E, hipMemcpyDeviceToDevice));
+        UCHK(hipMemcpyAsync(episode_dev, h->episode, sizeof(int32_t) * (size_t)h->cfg.E, hipMemcpyDeviceToDevice,
+                            (hipStream_t)stream));
     h->episode = episode_dev;
     return AAC_OK;
 }

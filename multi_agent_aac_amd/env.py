@@ -160,7 +160,8 @@ class BatchedEnv:
         on this device): a trainer's noise schedule then reads it with no per-step update."""
         assert episode.dtype == torch.int32 and episode.shape == (self.E,) and episode.is_contiguous()
         assert episode.device == self.device
-        _native.check(_native.lib().aac_env_use_episode_buffer(self._h, _ptr(episode)), "aac_env_use_episode_buffer")
+        _native.check(_native.lib().aac_env_use_episode_buffer(self._h, _ptr(episode), _stream()),
+                      "aac_env_use_episode_buffer")
         self._episode_buf = episode
         return episode
 

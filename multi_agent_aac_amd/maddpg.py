@@ -320,6 +320,10 @@ class MADDPG:
         if len(self.memory) <= self.batch_size:
             return None, None, single_eps_critic_cal_record
         if i_episode % UPDATE_EVERY != 0:
+            # The fused plan advances both Adam step counters inside its Polyak launches
+            # (fused.FusedUpdate.post), so an update that skipped the soft update would also skip the
+            # counter increment and mis-bias-correct the next Adam steps.  Supporting UPDATE_EVERY > 1
+            # needs a standalone counter advance (ops.polyak_flat with tau = 0, or an add) there.
             raise NotImplementedError("soft update every call (UPDATE_EVERY=1) as ATT/params:29")
         stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev)
         c_loss = [s[0] for s in stats]
@@ -340,12 +344,3 @@ class MADDPG:
         self.fa_t.data.copy_(self.fa.data)
         self.fc_t.data.copy_(self.fc.data)
 
-
-def smoke_check():
-    """One tiny batched update on cuda:0 against the torch-CPU restatement (used by smoke())."""
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    if root not in sys.path:
-        sys.path.insert(0, root)
-    from oracle import learner_ref
-    learner_ref.check_one_update(MADDPG, device="cuda", N=3, B=64, E=32, tol=1e-4)

@@ -58,7 +58,7 @@ def lib():
         L.aac_uam_auto_reset.argtypes = [vp, vp, ctypes.POINTER(UamOut), vp]
         L.aac_uam_set_reset_compact.argtypes = [i32]
         L.aac_uam_set_reset_compact.restype = None
-        L.aac_uam_use_episode_buffer.argtypes = [vp, vp]
+        L.aac_uam_use_episode_buffer.argtypes = [vp, vp, vp]
         L.aac_uam_bank_build.argtypes = [i32, i32, ctypes.c_uint64, vp, vp, vp]
         L.aac_uam_get_state.argtypes = [vp] + [vp] * 13 + [vp]
         L.aac_uam_set_state.argtypes = [vp] + [vp] * 13 + [vp]
@@ -218,8 +218,8 @@ class BatchedUAM:
     def use_episode_buffer(self, episode: torch.Tensor):
         """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E])."""
         assert episode.dtype == torch.int32 and episode.shape == (self.E,) and episode.is_contiguous()
-        assert episode.is_cuda
-        _chk(lib().aac_uam_use_episode_buffer(self._h, _ptr(episode)), "aac_uam_use_episode_buffer")
+        assert episode.device == self.device
+        _chk(lib().aac_uam_use_episode_buffer(self._h, _ptr(episode), _stream()), "aac_uam_use_episode_buffer")
         self._episode_buf = episode
         return episode
 

@@ -237,35 +237,18 @@ class FusedUamUpdate:
 
     Parameters of the four networks live in two flat float64 buffers ([critic | actor] and the
     targets), which the torch modules view, so ``save_model`` / ``load_model`` / the torch path see
-    the same weights.  The Adam moments of this path are its own (flat ``m1`` / ``m2``, one step
-    counter), initialised from the torch optimisers' state."""
+    the same weights.  The Adam moments are flat buffers too (``m1`` / ``m2``, one int32 step
+    counter), owned by the MADDPG object (``MADDPG._flat_state``) so every plan -- any B, any
+    replay -- and the torch-autograd path continue from the same optimiser state."""
     KS = 8
 
     def __init__(self, m, B, rep):
         self.m, self.B, self.rep = m, int(B), rep
         dev = m.device
         z = lambda *s: torch.zeros(*s, dtype=F64, device=dev)   # noqa: E731
-        cp, ap = list(m.critics.parameters()), list(m.actors.parameters())
-        nC, nA = sum(p.numel() for p in cp), sum(p.numel() for p in ap)
-        self.nC, self.nA = nC, nA
-        self.flat, self.tflat = z(nC + nA), z(nC + nA)
-        _rebind(cp + ap, self.flat)
-        _rebind(list(m.critics_target.parameters()) + list(m.actors_target.parameters()), self.tflat)
-        self.m1, self.m2 = z(nC + nA), z(nC + nA)
-        self.step = torch.zeros(1, dtype=torch.int32, device=dev)
-        # the torch optimisers' moments (if they stepped) carry over
-        o, steps = 0, []
-        for opt, ps in ((m.critic_optimizer, cp), (m.actor_optimizer, ap)):
-            for p in ps:
-                st = opt.state.get(p, {})
-                n = p.numel()
-                if "exp_avg" in st:
-                    self.m1[o:o + n].copy_(st["exp_avg"].reshape(-1))
-                    self.m2[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
-                    steps.append(int(st["step"].item()))
-                o += n
-        if steps:
-            self.step.fill_(steps[0])
+        fs = m._flat_state()
+        self.nC, self.nA = nC, nA = fs["nC"], fs["nA"]
+        self.flat, self.tflat, self.m1, self.m2, self.step = fs["flat"], fs["tflat"], fs["m1"], fs["m2"], fs["step"]
         self.lr_c = m.critic_optimizer.param_groups[0]["lr"]
         self.lr_a = m.actor_optimizer.param_groups[0]["lr"]
         self.betas = m.critic_optimizer.param_groups[0]["betas"]
@@ -469,6 +452,8 @@ class MADDPG:
         # update() path on one GPU: the fused float64 learner (FusedUamUpdate), else torch autograd
         self.fused_learner = self.device.type == "cuda" and os.environ.get("AAC_UAM_FUSED", "1") != "0"
         self._fu = None
+        self._fstate = None         # shared flat parameter / Adam state (``_flat_state``)
+        self._opt_steps = []
 
     # ------------------------------------------------------------------ batched API
     def attach_replay(self, capacity, seed=0):
@@ -520,6 +505,11 @@ class MADDPG:
             na = self.actors_target(s2)
             q_next = self.critics_target(s2, na).squeeze()
             target = (f["rew"][:, 0] + self.GAMMA * q_next * (1 - f["done"][:, 0])).unsqueeze(1)
+        if self._fstate is not None:
+            # the fused plans count Adam steps in one int32 counter: mirror it into the torch
+            # optimisers' per-parameter step tensors, and advance it after the two steps below
+            torch._foreach_copy_(self._opt_steps, [self._fstate["step"].to(torch.float32).reshape(())]
+                                 * len(self._opt_steps))
         q = self.critics(s, f["act"])
         loss_q = nn.MSELoss()(q, target.detach())
         torch._foreach_zero_(self._cgrads)
@@ -539,6 +529,8 @@ class MADDPG:
                 p.requires_grad_(True)
         self._allreduce_grads(self.actors)
         self.actor_optimizer.step()
+        if self._fstate is not None:
+            self._fstate["step"].add_(1)
         self._soft_update()
         return loss_q.detach(), loss_a.detach()
 
@@ -612,6 +604,44 @@ class MADDPG:
             self._graph.replay()
             return self._graph_out
         return self._sampled_core(rep, B, idx)
+
+    def _flat_state(self):
+        """Flat float64 parameter / target / Adam-moment buffers and the shared int32 Adam step
+        counter, built once.  The modules' parameters and the torch optimisers' ``exp_avg`` /
+        ``exp_avg_sq`` become views of them (moments the torch path already accumulated carry over),
+        so the fused plans and the torch-autograd path share one optimiser state; the torch path
+        copies the counter into its per-parameter ``step`` tensors before stepping (``_core``)."""
+        if self._fstate is not None:
+            return self._fstate
+        dev = self.device
+        cp, ap = list(self.critics.parameters()), list(self.actors.parameters())
+        nC, nA = sum(p.numel() for p in cp), sum(p.numel() for p in ap)
+        z = lambda n: torch.zeros(n, dtype=F64, device=dev)   # noqa: E731
+        flat, tflat, m1, m2 = z(nC + nA), z(nC + nA), z(nC + nA), z(nC + nA)
+        _rebind(cp + ap, flat)
+        _rebind(list(self.critics_target.parameters()) + list(self.actors_target.parameters()), tflat)
+        step = torch.zeros(1, dtype=torch.int32, device=dev)
+        o, steps = 0, []
+        for opt, ps in ((self.critic_optimizer, cp), (self.actor_optimizer, ap)):
+            for p in ps:
+                n = p.numel()
+                st = opt.state.setdefault(p, {})
+                if "exp_avg" in st:
+                    m1[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                    m2[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                    steps.append(int(st["step"].item()))
+                st["exp_avg"] = m1[o:o + n].view_as(p)
+                st["exp_avg_sq"] = m2[o:o + n].view_as(p)
+                if "step" not in st:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+                o += n
+        if steps:
+            step.fill_(steps[0])
+        self._graph = None          # a torch-path graph captured before holds the old storages
+        self._fstate = dict(nC=nC, nA=nA, flat=flat, tflat=tflat, m1=m1, m2=m2, step=step)
+        self._opt_steps = [st["step"] for opt in (self.critic_optimizer, self.actor_optimizer)
+                           for st in opt.state.values()]
+        return self._fstate
 
     def fused(self, B, rep):
         """The FusedUamUpdate of (B, replay), built on first use.  Building it moves the parameters

@@ -125,11 +125,16 @@ def random_transitions(E, N, seed, zero_nei_frac=0.1):
                 rew=rew, done=done, n_own=r(E, N, D0), n_radar=torch.rand(E, N, 18, generator=g) * 15, n_nei=n_nei)
 
 
-def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=0, iters=1):
-    """Device learner vs this restatement on identical weights and batches; raises on mismatch."""
+def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=0, iters=1, eps=1e-8,
+                     param_tol=None):
+    """Device learner vs this restatement on identical weights and batches; raises on mismatch.
+    Q, targets and losses are compared at ``tol``; parameters at ``param_tol`` (default ``tol``).
+    ``eps`` is Adam's epsilon on both sides: where a gradient is rounding noise (|g| << eps) Adam's
+    step is ~lr g / eps instead of +-lr, so a larger eps makes the parameters compare the gradients."""
     m = MADDPG_cls([6 + 4 * (N - 1), 18, 6], [6 + 4 * (N - 1), 18, 6], 2, n_agents=N, device=device, seed=seed,
                    memory_length=4 * E, batch_size=B)
     rep = m.attach_replay(4 * E)
+    m.actor_optimizer.eps = m.critic_optimizer.eps = eps
     D0 = 6 + 4 * (N - 1)
     actor, critic = RefActor([D0, 18, 6], 2), RefCritic([D0, 18, 6], N, 2)
     actor.load_state_dict(m.actors.reference_state_dict())
@@ -155,6 +160,9 @@ def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=
             b = {k: v[i.long()].clone() for k, v in host.items()}
             b["done"] = b["done"].to(torch.float32)
             batches.append(b)
+        if opts is None:
+            opts = (torch.optim.Adam(actor.parameters(), lr=1e-3, eps=eps),
+                    torch.optim.Adam(critic.parameters(), lr=1e-3, eps=eps))
         rstats, opts = ref_update(actor, critic, actor_t, critic_t, batches, opts=opts)
         for (lq, la, q, tg), (rlq, rla, rq, rtg) in zip(stats, rstats):
             if not torch.allclose(q.cpu().squeeze(1), rq.squeeze(1), atol=tol, rtol=tol):
@@ -169,6 +177,6 @@ def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=
                       (m.critics_target.reference_state_dict(), critic_t.state_dict())):
         for k in ref:
             d = float((mine[k] - ref[k]).abs().max())
-            if d > tol:
+            if d > (tol if param_tol is None else param_tol):
                 raise AssertionError(f"param {k} differs by {d}")
     return True

@@ -74,3 +74,16 @@ def bank_draw(bank_start, n_bank, seed, e, episode, N, pb=2.5):
                 break
         idx.append(k)
     return idx
+
+
+def uam_oracle_steps(pre, acts, N):
+    """Worker for the config-5 parity test (spawned process, numpy only): one oracle/uam_ref.py
+    step per env of ``pre`` (a device state dict sliced to the checked envs) from that exact
+    pre-step state.  Returns [(obs, reward, done, check_goal, bbc, mask, over, post_state)]."""
+    from oracle import uam_ref as U
+    out = []
+    for e in range(len(acts)):
+        o = U.env_from_state(pre, e, N)
+        res = o.full_step(acts[e])
+        out.append(tuple(res) + (U.state_of(o),))
+    return out

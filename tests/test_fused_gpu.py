@@ -232,17 +232,24 @@ def test_attn_block_matches_reference_attention(native_lib, K):
     np.testing.assert_allclose(out.cpu().double(), want, atol=2e-5, rtol=1e-5)
 
 
-def test_fused_act_matches_actor_module(native_lib):
+def test_fused_act_matches_ref_actor(native_lib):
+    """The fused HIP choose_action forward (encoders, aac_attn_block, merge, tanh) at config 2's
+    size (E = 1024 envs x N = 5 agents) against oracle/learner_ref.RefActor, the CPU restatement of
+    ActorNetwork_ATT_TwoPortion (ATT/nets:177-213), loaded with the same reference state_dict."""
     from multi_agent_aac_amd.maddpg import MADDPG
     m = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=5, device=DEV, seed=3)
-    torch.manual_seed(5)
-    E = 300
-    own, radar = torch.randn(E, 5, 22, device=DEV), torch.rand(E, 5, 18, device=DEV) * 15
-    nei = torch.randn(E, 5, 4, 6, device=DEV)
-    nei[::7, :, 1] = 0.0
-    got = m.act(own, radar, nei, noisy=False).clone()
-    want = m.actors([own, radar, nei])
-    np.testing.assert_allclose(got.cpu(), want.detach().cpu(), atol=1e-5, rtol=1e-5)
+    ref = learner_ref.RefActor([22, 18, 6], 2)
+    ref.load_state_dict({k: v.cpu() for k, v in m.actors.reference_state_dict().items()})
+    g = torch.Generator().manual_seed(5)
+    E, N = 1024, 5
+    own, radar = torch.randn(E, N, 22, generator=g), torch.rand(E, N, 18, generator=g) * 15
+    nei = torch.randn(E, N, 4, 6, generator=g)
+    nei[::7, :, 1] = 0.0                         # masked neighbours
+    nei[5, 2] = 0.0                              # an all-masked attention row
+    got = m.act(own.to(DEV), radar.to(DEV), nei.to(DEV), noisy=False).clone()
+    with torch.no_grad():
+        want = learner_ref.actor_rows(ref, own, radar, nei)
+    np.testing.assert_allclose(got.cpu(), want, atol=1e-5, rtol=1e-5)
 
 
 @pytest.mark.parametrize("K", [1, 4, 7, 12])       # K <= 8: MFMA kernels; 12: per-row kernels

@@ -86,6 +86,30 @@ def test_replay_push_gather_sample(native_lib):
     assert torch.equal(first, rep.batch_buffers(512)[0])
 
 
+@pytest.mark.parametrize("extra", [0, 1, 7, 1023, 1024])
+def test_sampler_distinct_on_small_ring(native_lib, extra):
+    """size = B + extra rows (the first updates after the len(memory) > B guard): every batch holds
+    B distinct in-range rows (size < 2B takes the exact partial Fisher-Yates path; 1024 = 2B the
+    redraw path), and each row is drawn about equally often."""
+    from multi_agent_aac_amd.memory import DeviceReplay
+    N, D0, B = 3, 14, 1024
+    rep = DeviceReplay(4096, N, D0, device=DEV, seed=5)
+    tr = learner_ref.random_transitions(B + extra, N, 1)
+    rep.push_batch(*[tr[k].to(DEV).contiguous() for k in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
+                                                           "n_own", "n_radar", "n_nei")])
+    size = B + extra
+    counts = np.zeros(size)
+    for _ in range(40):
+        rep.sample_batch(B)
+        ids = rep.batch_buffers(B)[0].cpu().numpy()
+        assert len(np.unique(ids)) == B and ids.min() >= 0 and ids.max() < size
+        counts[ids] += 1
+    if extra >= 7:
+        expected = 40 * B / size
+        chi2 = ((counts - expected) ** 2 / expected).sum()
+        assert chi2 < size + 6 * np.sqrt(2 * size), chi2
+
+
 def test_adam_polyak_flat(native_lib):
     from multi_agent_aac_amd import ops
     torch.manual_seed(0)

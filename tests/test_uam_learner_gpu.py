@@ -238,3 +238,38 @@ def test_replay_push_kernel(native_lib, done_u8):
     assert rep.pos == pos and len(rep) == cap
     assert torch.equal(rep.ring.cpu(), want)
     assert rep.meta.tolist() == [pos, cap]
+
+
+def test_adam_state_shared_across_plans_and_torch_path(native_lib):
+    """The fused plans of different B and the torch-autograd path continue from one optimiser state
+    (MADDPG._flat_state): update(B=64) and update(B=128) (graph-replayed fused plans, indices from
+    the device sampler) then a torch-path update, all against the CPU restatement with one pair of
+    torch.optim.Adam (a rebuilt plan used to restart from the stale torch moments)."""
+    from multi_agent_aac_amd import uam_learner as L
+    m, rep = _model(seed=8)
+    a, c, at, ct = _ref_from(m)
+    oa = torch.optim.Adam(a.parameters(), lr=1e-4)
+    oc = torch.optim.Adam(c.parameters(), lr=1e-4)
+
+    def ref_step(idx):
+        rows = rep.ring[idx.long()].cpu()
+        b = {k: rows[:, s:e] for k, (s, e) in L.SLICES.items()}
+        b["rew"], b["done"] = b["rew"][:, 0], b["done"][:, 0]
+        return R.ref_update(a, c, at, ct, oa, oc, b)
+
+    for B in (64, 128, 64):
+        lq, la = m.update(B, use_graph=True)
+        idx = m.fused(B, rep).idx.clone()
+        rq, ra = ref_step(idx)
+        assert abs(float(lq) - rq) < 1e-10 * max(1, abs(rq)) and abs(float(la) - ra) < 1e-10 * max(1, abs(ra))
+    idx = torch.as_tensor(np.random.default_rng(2).choice(len(rep), 96, replace=False), dtype=torch.int32,
+                          device=DEV)
+    lq, la = m.update(96, use_graph=False, idx=idx)           # torch-autograd path
+    rq, ra = ref_step(idx)
+    assert abs(float(lq) - rq) < 1e-10 * max(1, abs(rq)) and abs(float(la) - ra) < 1e-10 * max(1, abs(ra))
+    lq, la = m.update(128, use_graph=True)                    # and back to a fused plan
+    rq, ra = ref_step(m.fused(128, rep).idx.clone())
+    assert abs(float(lq) - rq) < 1e-10 * max(1, abs(rq)) and abs(float(la) - ra) < 1e-10 * max(1, abs(ra))
+    for mine, ref in ((m.actors, a), (m.critics, c), (m.actors_target, at), (m.critics_target, ct)):
+        for (k, p), (_, q) in zip(mine.state_dict().items(), ref.state_dict().items()):
+            np.testing.assert_allclose(p.cpu().numpy(), q.numpy(), rtol=0, atol=1e-10, err_msg=k)
