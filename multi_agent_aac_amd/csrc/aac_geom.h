@@ -208,6 +208,13 @@ __device__ bool ray_square(double cx, double cy, double ex, double ey, double x0
                            double &dout) {
     double ddx = ex - cx, ddy = ey - cy;
     double tx0, tx1, ty0, ty1;
+    // a ray running along an edge from a start point on that edge: the intersection with the
+    // boundary is a segment through c, so the distance is 0 (GEOS line.intersection(boundary))
+    if ((ddx == 0.0 && (cx == x0 || cx == x1) && cy >= y0 && cy <= y1) ||
+        (ddy == 0.0 && (cy == y0 || cy == y1) && cx >= x0 && cx <= x1)) {
+        dout = 0.0;
+        return true;
+    }
     if (ddx == 0.0) {
         if (cx < x0 || cx > x1) return false;
         tx0 = -INFINITY;

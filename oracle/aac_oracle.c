@@ -183,6 +183,12 @@ static int ray_poly_entry(double cx, double cy, double ex, double ey, double px,
 static int ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1, double *dout) {
     double ddx = ex - cx, ddy = ey - cy;
     double tx0, tx1, ty0, ty1;
+    /* a ray along an edge from a start point on that edge: distance 0 (OM/env:1105-1116) */
+    if ((ddx == 0.0 && (cx == x0 || cx == x1) && cy >= y0 && cy <= y1) ||
+        (ddy == 0.0 && (cy == y0 || cy == y1) && cx >= x0 && cx <= x1)) {
+        *dout = 0.0;
+        return 1;
+    }
     if (ddx == 0.0) {
         if (cx < x0 || cx > x1) return 0;
         tx0 = -INFINITY; tx1 = INFINITY;

@@ -224,6 +224,10 @@ def ray_square_crossing(cx, cy, ex, ey, x0, x1, y0, y1):
     (OM/env:1117-1126: ``line.intersection(polygon.boundary)`` then ``distance``)."""
     ddx = ex - cx
     ddy = ey - cy
+    # a ray running along an edge from a start point on that edge: line.intersection(boundary) is
+    # a segment through c, so the distance is 0
+    if (ddx == 0.0 and cx in (x0, x1) and y0 <= cy <= y1) or (ddy == 0.0 and cy in (y0, y1) and x0 <= cx <= x1):
+        return 0.0
     if ddx == 0.0:
         if cx < x0 or cx > x1:
             return None
@@ -322,3 +326,76 @@ def segment_convex_entry_exact(c, e, poly):
         if t_lo > t_hi:
             return None
     return t_lo
+
+
+def _seg_seg_first_t_exact(c, d, a, b):
+    """Exact smallest t in [0, 1] with c + t d on the closed segment a-b (Fractions), or None.
+    Collinear overlaps give the first overlapping parameter."""
+    ex, ey = b[0] - a[0], b[1] - a[1]
+    den = d[0] * ey - d[1] * ex
+    wx, wy = a[0] - c[0], a[1] - c[1]
+    if den != 0:
+        t = (wx * ey - wy * ex) / den
+        s = (wx * d[1] - wy * d[0]) / den
+        return t if (0 <= t <= 1 and 0 <= s <= 1) else None
+    if wx * d[1] - wy * d[0] != 0:
+        return None                      # parallel, not collinear
+    dd = d[0] * d[0] + d[1] * d[1]
+    ta = (wx * d[0] + wy * d[1]) / dd    # parameters of a and b along c + t d
+    tb = ((b[0] - c[0]) * d[0] + (b[1] - c[1]) * d[1]) / dd
+    lo, hi = (ta, tb) if ta <= tb else (tb, ta)
+    lo, hi = max(lo, Fraction(0)), min(hi, Fraction(1))
+    return lo if lo <= hi else None
+
+
+def ray_square_boundary_t_exact(c, e, x0, x1, y0, y1):
+    """Exact parameter of the point of segment c->e on the square's boundary nearest to c (the
+    reference's ``line.intersection(polygon.boundary)`` + ``distance``, OM/env:1105-1116), or None:
+    the union of the segment's exact intersections with the four closed edges."""
+    cc, ee = _fr(c), _fr(e)
+    d = (ee[0] - cc[0], ee[1] - cc[1])
+    X0, X1, Y0, Y1 = Fraction(x0), Fraction(x1), Fraction(y0), Fraction(y1)
+    best = None
+    for a, b in (((X0, Y0), (X1, Y0)), ((X1, Y0), (X1, Y1)), ((X1, Y1), (X0, Y1)), ((X0, Y1), (X0, Y0))):
+        t = _seg_seg_first_t_exact(cc, d, a, b)
+        if t is not None and (best is None or t < best):
+            best = t
+    return best
+
+
+def ray_line_t_exact(c, e, axis, value):
+    """Exact parameter of segment c->e on the bound line {axis = value} (a LineString from -9999 to
+    9999, ATT/env:143-146, OM/env:1117-1141), or None."""
+    cc, ee = _fr(c), _fr(e)
+    d = (ee[0] - cc[0], ee[1] - cc[1])
+    v = Fraction(value)
+    a = (v, Fraction(-9999)) if axis == 0 else (Fraction(-9999), v)
+    b = (v, Fraction(9999)) if axis == 0 else (Fraction(9999), v)
+    return _seg_seg_first_t_exact(cc, d, a, b)
+
+
+def segment_hits_polygon_exact(p, q, poly):
+    """Closed segment p-q meets the closed polygon ``poly`` (exact orientation tests on the float
+    vertices): some polygon edge touches or crosses the segment, or the segment lies inside."""
+    P, Q = _fr(p), _fr(q)
+    V = [_fr(v) for v in poly]
+
+    def orient(a, b, c):
+        v = (b[0] - a[0]) * (c[1] - a[1]) - (b[1] - a[1]) * (c[0] - a[0])
+        return (v > 0) - (v < 0)
+
+    def on_seg(a, b, c):       # c collinear with a-b: within its box
+        return min(a[0], b[0]) <= c[0] <= max(a[0], b[0]) and min(a[1], b[1]) <= c[1] <= max(a[1], b[1])
+
+    n = len(V)
+    for k in range(n):
+        a, b = V[k], V[(k + 1) % n]
+        o1, o2, o3, o4 = orient(P, Q, a), orient(P, Q, b), orient(a, b, P), orient(a, b, Q)
+        if o1 != o2 and o3 != o4:
+            return True
+        if (o1 == 0 and on_seg(P, Q, a)) or (o2 == 0 and on_seg(P, Q, b)) or \
+                (o3 == 0 and on_seg(a, b, P)) or (o4 == 0 and on_seg(a, b, Q)):
+            return True
+    # no boundary contact: inside iff P is inside (convex ring, either orientation)
+    s = [orient(V[k], V[(k + 1) % n], P) for k in range(n)]
+    return all(x >= 0 for x in s) or all(x <= 0 for x in s)

@@ -1,5 +1,6 @@
-"""Extract the reference's fixed-OD fixtures (MA_ver1/fixedDrone_3drones.xlsx, fixedDrone_5_adj.xlsx)
-into tests/golden/fixed_od.json.  The xlsx files are read as zipped sheet XML (data only; nothing
+"""Extract the reference's fixed-OD fixtures (all seven MA_ver1/*.xlsx: fixedDrone.xlsx,
+fixedDrone_2_drone.xlsx, fixedDrone_3drones.xlsx, fixedDrone_3dronesV2.xlsx, fixedDrone_3drones_2.xlsx,
+fixedDrone_5_adj.xlsx, reward_test.xlsx) into tests/golden/fixed_od.json.  The xlsx files are read as zipped sheet XML (data only; nothing
 from the reference is executed).  Parsing follows reset_world_fixedOD (ATT/env:513-614): numeric gx/gy
 is one goal; string cells "x1; x2" / "y1; y2" hold two waypoints, read exactly as the reference does
 (x from the first token of each cell, y from the second, ATT/env:225-227 pattern)."""
@@ -10,6 +11,8 @@ import sys
 import zipfile
 
 REF = "/root/reference/MA_ver1"
+FILES = ("fixedDrone.xlsx", "fixedDrone_2_drone.xlsx", "fixedDrone_3drones.xlsx", "fixedDrone_3dronesV2.xlsx",
+         "fixedDrone_3drones_2.xlsx", "fixedDrone_5_adj.xlsx", "reward_test.xlsx")
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixed_od.json")
 
 
@@ -42,7 +45,7 @@ def parse(rows):
 
 def main():
     data = {}
-    for name in ("fixedDrone_3drones.xlsx", "fixedDrone_5_adj.xlsx"):
+    for name in FILES:
         header, rows = read_rows(os.path.join(REF, name))
         data[name] = {"header": header, "agents": parse(rows)}
     with open(OUT, "w") as f:

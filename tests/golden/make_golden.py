@@ -92,6 +92,16 @@ def main():
     scen["rand5_drones"] = run(occ, 5, [rand_od(5) for _ in range(4)], 0, T=30, actions="random", seed=1)
     scen["rand8_obstacles"] = run(occ, 8, [rand_od(8) for _ in range(3)], 1, T=30, actions="random", seed=2)
     scen["ctrl5_combined"] = run(occ, 5, [rand_od(5) for _ in range(4)], 2, T=60, actions="controller")
+    # the remaining reference fixtures (appended: the scenarios above keep their random streams).
+    # fixedDrone_2_drone / fixedDrone_3drones_2 are head-on pairs: the go-to-waypoint controller
+    # flies them into each other (drone collision, bbc[2] / bbc[3])
+    for name, key, mode, T in (("headon2", "fixedDrone_2_drone.xlsx", 2, 40),
+                               ("headon2_long", "fixedDrone_3drones_2.xlsx", 0, 60),
+                               ("fixed5_all", "fixedDrone.xlsx", 0, 60),
+                               ("fixed3v2", "fixedDrone_3dronesV2.xlsx", 1, 60)):
+        ag = fixed[key]["agents"]
+        od = ([tuple(a["start"]) for a in ag], [a["goals"] for a in ag])
+        scen[name] = run(occ, len(ag), [od], mode, T=T)
     for k, v in scen.items():
         np.savez_compressed(os.path.join(HERE, f"env_{k}.npz"), **v)
         m = np.bitwise_or.reduce(v["mask"].ravel())

@@ -20,7 +20,8 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 ATOL = 1e-5
 
 
-@pytest.mark.parametrize("name", ["fixed3", "fixed5", "rand5_drones", "rand8_obstacles", "ctrl5_combined"])
+@pytest.mark.parametrize("name", ["fixed3", "fixed5", "rand5_drones", "rand8_obstacles", "ctrl5_combined",
+                                  "headon2", "headon2_long", "fixed5_all", "fixed3v2"])
 def test_goldens_through_abi(native_lib, name):
     from multi_agent_aac_amd.env import BatchedEnv
     g = np.load(os.path.join(GOLDEN, f"env_{name}.npz"))

@@ -15,6 +15,8 @@ from oracle.consts import BOUND
 from tests.helpers import W_DEFAULT, draw_env_od, pack_od
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+GOLDENS = ["fixed3", "fixed5", "rand5_drones", "rand8_obstacles", "ctrl5_combined", "headon2", "headon2_long",
+           "fixed5_all", "fixed3v2"]
 
 
 def _fma(a, b, c):
@@ -86,7 +88,27 @@ def test_fixed_od_fixture_matches_reference_rows():
     assert a3[0]["start"] == [508.7, 339.3] and a3[0]["goals"] == [[536.0, 356.0], [560.0, 340.0]]
     assert a3[1] == {"start": [480.0, 346.0], "goals": [[600.0, 360.0]]}
     assert len(fx["fixedDrone_5_adj.xlsx"]["agents"]) == 5
+    # all seven MA_ver1 fixtures, including the head-on pair and the one-drone reward test
+    assert sorted(fx) == sorted(["fixedDrone.xlsx", "fixedDrone_2_drone.xlsx", "fixedDrone_3drones.xlsx",
+                                 "fixedDrone_3dronesV2.xlsx", "fixedDrone_3drones_2.xlsx", "fixedDrone_5_adj.xlsx",
+                                 "reward_test.xlsx"])
+    assert fx["fixedDrone_2_drone.xlsx"]["agents"] == [{"start": [560.0, 320.0], "goals": [[580.0, 370.0]]},
+                                                       {"start": [580.0, 370.0], "goals": [[560.0, 320.0]]}]
+    assert fx["fixedDrone_3dronesV2.xlsx"]["agents"][0] == {"start": [570.0, 300.0], "goals": [[588.0, 382.0]]}
+    assert len(fx["fixedDrone.xlsx"]["agents"]) == 5 and len(fx["reward_test.xlsx"]["agents"]) == 1
 
+
+def test_headon_golden_collides():
+    """fixedDrone_2_drone.xlsx flown head-on by the go-to-goal controller: the episode ends on the
+    drone-collision branch (ATT/env:2228-2236, :2537-2545) at the first step with |p0 - p1| <= 2 pB,
+    both agents get the -20 crash (team sum) and bbc[2] is set."""
+    g = np.load(os.path.join(GOLDEN, "env_headon2.npz"))
+    d = np.linalg.norm(g["pos"][:, 0, 0] - g["pos"][:, 0, 1], axis=-1)
+    t = int(np.argmax(d <= 5.0))
+    assert d[t] <= 5.0 and (d[:t] > 5.0).all()
+    assert (g["mask"][t, 0] & 2).all() and g["done"][t, 0].all() and g["env_done"][t, 0] == 1
+    assert g["bbc"][t, 0, 2] == 1 and (g["mask"][:t] & 2).sum() == 0
+    assert (g["reward"][t, 0] <= -40.0).all()
 
 # ---------------------------------------------------------------- closed forms vs exact
 def test_goal_closed_form_vs_exact():
@@ -135,6 +157,106 @@ def test_bound_crash_python_vs_c_and_edges():
     # moving along +x next to the top line: cap vertex at angle pi/2 is at y + 2.5
     assert c_oracle.bound_crash(500.0, 382.5, 501.0, 382.5)
     assert not c_oracle.bound_crash(500.0, 382.5 - 1e-9, 501.0, 382.5 - 1e-9)
+
+
+def _near_bound_capsules(rng, n):
+    """Swept capsules (pre_pos -> pos, |step| <= vmax dt = 2.5) placed so that one extent lies within
+    ~1e-12 m of a bound line (both sides of the tie), plus stationary circles."""
+    out = []
+    for k in range(n):
+        side = k % 4
+        ang = rng.uniform(0, 2 * math.pi)
+        L = 0.0 if k % 7 == 0 else rng.uniform(0, 2.5)
+        p0 = np.array([rng.uniform(470, 665), rng.uniform(270, 370)])
+        p1 = p0 + L * np.array([math.cos(ang), math.sin(ang)])
+        mnx, mxx, mny, mxy = geos.capsule_extents(p0, p1, 2.5)
+        ext, target = ((mnx, BOUND[0]), (mxx, BOUND[1]), (mny, BOUND[2]), (mxy, BOUND[3]))[side]
+        shift = (target - ext) + rng.choice([-1, 1]) * rng.uniform(0, 1e-12) * (k % 3 != 0)
+        v = np.zeros(2)
+        v[side // 2] = shift
+        out.append((tuple(p0 + v), tuple(p1 + v)))
+    return out
+
+
+def test_capsule_closed_form_vs_exact():
+    """Bound crash (ATT/env:2172-2173, :2507): the swept capsule polygon meets one of the four bound
+    LineStrings (-9999 .. 9999, ATT/env:143-146).  Independent exact formulation: the capsule's
+    actual GEOS float vertices (geos.capsule_vertices) against each LineString by exact orientation
+    tests in rational arithmetic (segment_hits_polygon_exact: edge crossings / touches); compared
+    with the extent closed form of the python oracle and of the C oracle (the kernel's form), at
+    positions within 1e-12 m of every bound line on both sides."""
+    rng = np.random.default_rng(31)
+    lines = [((BOUND[0], -9999.0), (BOUND[0], 9999.0)), ((BOUND[1], -9999.0), (BOUND[1], 9999.0)),
+             ((-9999.0, BOUND[2]), (9999.0, BOUND[2])), ((-9999.0, BOUND[3]), (9999.0, BOUND[3]))]
+    hits = 0
+    cases = _near_bound_capsules(rng, 240)
+    for p0, p1 in cases:
+        verts = geos.capsule_vertices(p0, p1, 2.5)
+        exact = any(geos.segment_hits_polygon_exact(a, b, verts) for a, b in lines)
+        assert geos.bound_crash(p0, p1, BOUND) == exact, (p0, p1)
+        assert bool(c_oracle.bound_crash(p0[0], p0[1], p1[0], p1[1])) == exact, (p0, p1)
+        hits += exact
+    assert 40 < hits < 200, hits        # both outcomes at the ties
+
+
+def test_radar_obstacle_vs_exact(occ):
+    """Obstacle radar (OM/env:1085-1141): per ray, the distance to the nearest point of
+    segment(c, e) on the boundary of any occupied 10 m cell or on a bound LineString, else the ray
+    length.  Independent exact formulation: the segment's exact intersections with every cell edge
+    and bound line in rational arithmetic (ray_square_boundary_t_exact / ray_line_t_exact), the
+    nearest parameter t; compared with the python oracle's closed form (hit / no hit identical,
+    distance within 1e-12 m) and the C oracle's obstacle-mode radar after a reset (float32, 1e-5).
+    Rays are aimed within 1e-12 m of cell corners (grazing) and parallel to cell edges as well as
+    at random."""
+    env = env_ref.ScalarEnv(2, occ, radar_mode=env_ref.RADAR_OBSTACLES)
+    rng = np.random.default_rng(32)
+    corners = [(cx + sx * 5.0, cy + sy * 5.0) for cx, cy in env.cells for sx in (-1, 1) for sy in (-1, 1)]
+    centres = []
+    for k in range(120):
+        deg = 20 * int(rng.integers(0, 18))
+        u = (math.cos(math.radians(deg)), math.sin(math.radians(deg)))
+        if k % 3 == 0:             # graze a corner: start behind it along the ray, nudged sideways
+            qx, qy = corners[int(rng.integers(len(corners)))]
+            s_ = rng.uniform(1, 14)
+            off = rng.choice([-1e-12, 0.0, 1e-12])
+            centres.append((qx - s_ * u[0] - off * u[1], qy - s_ * u[1] + off * u[0]))
+        elif k % 3 == 1:           # along a cell edge line
+            cx, cy = env.cells[int(rng.integers(len(env.cells)))]
+            centres.append((cx + 5.0 * rng.choice([-1, 1]), cy + rng.uniform(-20, 20)))
+        else:
+            centres.append((rng.uniform(456, 679), rng.uniform(256, 384)))
+    n_hit = 0
+    for c in centres:
+        for deg in range(0, 360, 20):
+            e = env._ray_end(c, deg)
+            length = geos.point_dist(e[0], e[1], c[0], c[1])
+            best = None
+            for cx, cy in env.cells:
+                t = geos.ray_square_boundary_t_exact(c, e, cx - 5.0, cx + 5.0, cy - 5.0, cy + 5.0)
+                if t is not None and (best is None or t < best):
+                    best = t
+            for axis, val in ((0, BOUND[0]), (0, BOUND[1]), (1, BOUND[2]), (1, BOUND[3])):
+                t = geos.ray_line_t_exact(c, e, axis, float(val))
+                if t is not None and (best is None or t < best):
+                    best = t
+            got = env._radar_obstacles(c, e, length)
+            if best is None or best == 1:
+                assert got == length, (c, deg, got)
+            else:
+                want = float(best) * length
+                assert abs(got - want) < 1e-12, (c, deg, got, want)
+                n_hit += 1
+    assert n_hit > 300
+    # the C oracle (the kernel's arithmetic) on the same centres, two agents per env
+    E = len(centres) // 2
+    st = np.array(centres[:2 * E]).reshape(E, 2, 2)
+    wps = np.tile(st[:, :, None, :], (1, 1, W_DEFAULT, 1))
+    co = c_oracle.BatchedOracle(E, 2, occ, W=W_DEFAULT, radar_mode=1)
+    co.reset(st, wps, np.ones((E, 2), np.int32))
+    for e_ in range(E):
+        env.reset([tuple(st[e_, 0]), tuple(st[e_, 1])], [[list(st[e_, 0])], [list(st[e_, 1])]])
+        for i in range(2):
+            np.testing.assert_allclose(co.radar[e_, i], env.radar(i).astype(np.float32), rtol=0, atol=1e-5)
 
 
 def test_radar_entry_vs_exact():
@@ -193,7 +315,7 @@ def test_scalar_vs_c_oracle(occ, mode, N):
             assert np.array_equal(co.pos[e], np.array([env.all_agents[i].pos for i in range(N)]))
 
 
-@pytest.mark.parametrize("name", ["fixed3", "fixed5", "rand5_drones", "rand8_obstacles", "ctrl5_combined"])
+@pytest.mark.parametrize("name", GOLDENS)
 def test_c_oracle_reproduces_goldens(name):
     g = np.load(os.path.join(GOLDEN, f"env_{name}.npz"))
     E, N = g["start"].shape[:2]
@@ -208,7 +330,7 @@ def test_c_oracle_reproduces_goldens(name):
 
 def test_golden_event_coverage():
     bits = 0
-    for name in ("fixed3", "fixed5", "rand5_drones", "rand8_obstacles", "ctrl5_combined"):
+    for name in GOLDENS:
         g = np.load(os.path.join(GOLDEN, f"env_{name}.npz"))
         bits |= int(np.bitwise_or.reduce(g["mask"].ravel()))
     assert bits == 0b111111 or bits & 0b111110 == 0b111110

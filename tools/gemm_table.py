@@ -1,0 +1,79 @@
+"""Per-launch table (graph-replayed) of the fused learner's grouped GEMM launches (config 3 by default): products,
+FLOPs, isolated duration (each launch replayed 20x back to back after one full update), TF/s.
+
+python tools/gemm_table.py [--agents 5] [--batch 1024] [--model att|gru]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import learner_ref  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--agents", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--model", default="att")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    from multi_agent_aac_amd.fused import GemmLaunch
+    N, B = a.agents, a.batch
+    D0 = 6 + 4 * (N - 1)
+    if a.model == "gru":
+        from multi_agent_aac_amd.gru import MADDPG
+        from oracle import gru_ref
+        m = MADDPG([6, 18, 6], [6, 18, 6], 2, 64, 10, n_agents=N, device="cuda", seed=1, batch_size=B)
+        rep = m.attach_replay(8192, seed=1)
+        keys = ("s_own", "s_radar", "s_nei", "act", "rew", "done", "n_own", "n_radar", "n_nei", "h_cur", "h_next")
+        for p in range(2):
+            tr = gru_ref.random_gru_transitions(4096, N, p)
+            rep.push_batch(*[tr[k].cuda().contiguous() for k in keys])
+        fu = m._plan(B)
+        ops = fu.ops()
+    else:
+        from multi_agent_aac_amd.maddpg import MADDPG
+        m = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, device="cuda", seed=1, batch_size=B)
+        rep = m.attach_replay(8192, seed=1)
+        for p in range(2):
+            tr = learner_ref.random_transitions(4096, N, p)
+            rep.push_batch(*[tr[k].cuda().contiguous() for k in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
+                                                                   "n_own", "n_radar", "n_nei")])
+        fu = m._fused_plan(B)
+        ops = fu.ops()
+    for op in ops:
+        op()
+    torch.cuda.synchronize()
+    tot_t, tot_f = 0.0, 0.0
+    rows = []
+    for k, op in enumerate(ops):
+        if not isinstance(op, GemmLaunch):
+            continue
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        op()
+        g = torch.cuda.CUDAGraph()        # device time, no host launch cost (as in the bench's replay)
+        with torch.cuda.graph(g):
+            for _ in range(a.reps):
+                op()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.reps * 1e3
+        shapes = " ".join(f"{p.M}x{p.N - p.ones}{'+1' if p.ones else ''}x{p.K}{'/' + str(p.ksplit) if p.ksplit > 1 else ''}"
+                          f"{'T' if p.ta else ''}{'t' if p.tb else ''}" for p in op.arr)
+        rows.append((us, op.flops, k, shapes))
+        tot_t += us
+        tot_f += op.flops
+    for us, fl, k, shapes in rows:
+        print(f"{k:3d} {us:7.1f} us {fl / 1e9:6.3f} GF {fl / us / 1e6:6.1f} TF/s  {shapes}")
+    print(f"total {tot_t:.1f} us over {len(rows)} launches, {tot_f / 1e9:.2f} GF, {tot_f / tot_t / 1e6:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
