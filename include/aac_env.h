@@ -85,6 +85,13 @@ int aac_env_step(aac_env *env, const float *actions_dev, const aac_step_out *out
  * start [P][2], wps [P][W][2], cnt [P]; one entry = one agent's (start, A* waypoint list). */
 int aac_env_set_od_bank(aac_env *env, const double *start, const double *wps, const int32_t *cnt,
                         int32_t n_pairs, uint64_t seed);
+/* Multi-map form (MADDPG_ownENV_randomOD_radar_multipleMap: random_map_idx =
+ * random.randrange(len(world_map_2D_collection)) per episode, ma_main:464-465): one bank per map of
+ * the handle's map stack, concatenated map-major (n_per_map[m] entries for map m).  Each auto-reset
+ * draws the env's map uniformly, then its agents' ODs from that map's bank; the env's map_idx is
+ * updated.  aac_env_set_od_bank is this with n_maps = 1 (it refuses a handle with n_maps > 1). */
+int aac_env_set_od_banks(aac_env *env, int32_t n_maps, const double *start, const double *wps, const int32_t *cnt,
+                         const int32_t *n_per_map, uint64_t seed);
 
 /* Re-draws the OD of every env with env_done_dev[e] != 0 from the bank (reference rule: starts
  * more than 2 pB apart, ATT/env:258-268) and overwrites those envs' rows of ``out``. */

@@ -58,6 +58,11 @@ const char *aac_fused_last_error(void);
 /* n <= AAC_GEMM_MAX products in one launch. */
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream);
 
+/* Diagnostic builds only (-DAAC_GEMM_STAMPS): per-workgroup stamps of the last gemm launch,
+ * 5 uint64 per workgroup [memrealtime entry, memtime entry, memtime after MFMA loop, memtime exit,
+ * memrealtime exit]; returns -1 in a normal build. */
+int aac_gemm_stamps(unsigned long long *out, int32_t n_wg);
+
 /* torch.optim.Adam step (as aac_adam_flat_at) whose gradient is the fixed-order sum of nsplit
  * partial copies gpart[s*n + i]; grad_out (may be NULL) receives that sum. */
 int aac_adam_flat_sum(float *param, const float *gpart, int32_t nsplit, float *grad_out, float *exp_avg,

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("AAC_LIB") or os.path.join(_HERE, "libaac_env.so")
 
 EXPORTS = (
     "aac_env_create", "aac_env_destroy", "aac_last_error", "aac_env_reset", "aac_env_step",
-    "aac_env_set_od_bank", "aac_env_auto_reset", "aac_env_set_reset_compact", "aac_env_use_episode_buffer", "aac_env_get_state", "aac_env_set_state",
+    "aac_env_set_od_bank", "aac_env_set_od_banks", "aac_env_auto_reset", "aac_env_set_reset_compact", "aac_env_use_episode_buffer", "aac_env_get_state", "aac_env_set_state",
     "aac_astar", "aac_od_bank_build",
 )
 
@@ -57,6 +57,7 @@ def lib():
     L.aac_env_reset.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.POINTER(StepOut), vp]
     L.aac_env_step.argtypes = [vp, vp, ctypes.POINTER(StepOut), vp]
     L.aac_env_set_od_bank.argtypes = [vp, vp, vp, vp, i32, ctypes.c_uint64]
+    L.aac_env_set_od_banks.argtypes = [vp, i32, vp, vp, vp, vp, ctypes.c_uint64]
     L.aac_env_auto_reset.argtypes = [vp, vp, ctypes.POINTER(StepOut), vp]
     L.aac_env_set_reset_compact.argtypes = [ctypes.c_int32]
     L.aac_env_set_reset_compact.restype = None

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "../../include/aac_env.h"
 #include "aac_geom.h"
@@ -55,6 +56,8 @@ struct ResetArgs {
     const double2 *bank_start, *bank_wp;
     const int32_t *bank_cnt;
     int32_t bank_n;
+    const int32_t *bank_off;  // [bank_maps + 1] first entry of each map's bank (multi-map)
+    int32_t bank_maps;        // 1: one bank, every env on map 0; > 1: map drawn per episode
     uint64_t seed;
     int32_t *episode;         // [E] per-env episode counter (bank mode)
     const int32_t *list;      // [count, env...] of the resetting envs (env_compact_kernel); NULL:
@@ -460,13 +463,22 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
             if (eq >= A.E || !S.active[lq]) continue;
             const int ep = R.episode[eq] + 1;
             const int bq = lq * N;
+            // multipleMap variant: random_map_idx = random.randrange(len(world_map_2D_collection)) per
+            // episode (multipleMap/ma_main:464-465), then the OD from that map's bank
+            int mp = 0, boff = 0, bn = R.bank_n;
+            if (R.bank_maps > 1) {
+                mp = (int)(mix64(mix64(mix64(R.seed ^ 0x6d61705f64726177ull ^ (uint64_t)eq) ^ (uint64_t)ep)) %
+                           (uint64_t)R.bank_maps);
+                boff = R.bank_off[mp];
+                bn = R.bank_off[mp + 1] - boff;
+            }
             for (int a = 0; a < N; ++a) {
                 int chosen = -1, last = 0;
                 for (int att0 = 0; att0 < 4096 && chosen < 0; att0 += 64) {
                     const int att = att0 + lane;
                     const uint64_t key =
                         mix64(mix64(mix64(R.seed ^ (uint64_t)eq) ^ (uint64_t)ep) ^ ((uint64_t)a * 65536ull + att));
-                    const int idx = (int)(key % (uint64_t)R.bank_n);
+                    const int idx = boff + (int)(key % (uint64_t)bn);
                     const double2 sp = R.bank_start[idx];
                     bool ok = true;
                     for (int b = 0; b < a; ++b) {
@@ -485,7 +497,10 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             }
-            if (lane == 0) R.episode[eq] = ep;
+            if (lane == 0) {
+                R.episode[eq] = ep;
+                if (A.map_idx) A.map_idx[eq] = mp;
+            }
         }
     }
     __syncthreads();
@@ -521,7 +536,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         S.pvel[t] = z;
         S.goal[t] = A.goal[ai];
     }
-    __syncthreads();   // map_idx (explicit mode) written above is read by the radar phase below
+    __syncthreads();   // map_idx (explicit or drawn) written above is read by the radar phase below
     radar_phase(A, S, e0, nag, true, emap);
     if (active) observe_agent(A, S, e, i, base);
 }
@@ -563,8 +578,8 @@ struct aac_env {
     int32_t *episode_own;     // the handle's own counter buffer (episode may be a caller's buffer)
     uint8_t *reach, *occ;
     double2 *bank_start, *bank_wp;
-    int32_t *bank_cnt;
-    int32_t bank_n;
+    int32_t *bank_cnt, *bank_off;
+    int32_t bank_n, bank_maps;
     uint64_t bank_seed;
     int32_t *rlist;           // [1 + E]: packed resetting envs of the last auto-reset
 };
@@ -677,7 +692,8 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
 void aac_env_destroy(aac_env *h) {
     if (!h) return;
     void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->wp, h->wp_cur, h->wp_cnt, h->wall,
-                    h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt, h->rlist};
+                    h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt,
+                    h->bank_off, h->rlist};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -721,23 +737,42 @@ int aac_env_reset(aac_env *h, const uint8_t *mask, const double *start, const do
     return AAC_OK;
 }
 
-int aac_env_set_od_bank(aac_env *h, const double *start, const double *wps, const int32_t *cnt, int32_t n,
-                        uint64_t seed) {
-    if (!h || !start || !wps || !cnt || n <= 0) return fail(AAC_E_INVALID, "bad OD bank");
+int aac_env_set_od_banks(aac_env *h, int32_t n_maps, const double *start, const double *wps, const int32_t *cnt,
+                         const int32_t *n_per_map, uint64_t seed) {
+    if (!h || !start || !wps || !cnt || !n_per_map || n_maps < 1) return fail(AAC_E_INVALID, "bad OD banks");
+    if (n_maps != h->cfg.n_maps) return fail(AAC_E_INVALID, "one OD bank per map (n_maps of the handle)");
+    std::vector<int32_t> off(n_maps + 1, 0);
+    for (int m = 0; m < n_maps; ++m) {
+        if (n_per_map[m] <= 0) return fail(AAC_E_INVALID, "empty OD bank");
+        off[m + 1] = off[m] + n_per_map[m];
+    }
+    const int32_t n = off[n_maps];
     for (int32_t k = 0; k < n; ++k)
         if (cnt[k] < 1 || cnt[k] > h->W) return fail(AAC_E_INVALID, "OD bank waypoint count out of [1, W]");
     HIPCHK(hipSetDevice(h->device));
-    if (h->bank_start) { (void)hipFree(h->bank_start); (void)hipFree(h->bank_wp); (void)hipFree(h->bank_cnt); }
-    h->bank_start = nullptr; h->bank_wp = nullptr; h->bank_cnt = nullptr;
+    if (h->bank_start) {
+        (void)hipFree(h->bank_start); (void)hipFree(h->bank_wp); (void)hipFree(h->bank_cnt); (void)hipFree(h->bank_off);
+    }
+    h->bank_start = nullptr; h->bank_wp = nullptr; h->bank_cnt = nullptr; h->bank_off = nullptr;
     HIPCHK(hipMalloc((void **)&h->bank_start, sizeof(double2) * n));
     HIPCHK(hipMalloc((void **)&h->bank_wp, sizeof(double2) * (size_t)n * h->W));
     HIPCHK(hipMalloc((void **)&h->bank_cnt, sizeof(int32_t) * n));
+    HIPCHK(hipMalloc((void **)&h->bank_off, sizeof(int32_t) * (n_maps + 1)));
     HIPCHK(hipMemcpy(h->bank_start, start, sizeof(double2) * n, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->bank_wp, wps, sizeof(double2) * (size_t)n * h->W, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->bank_cnt, cnt, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->bank_off, off.data(), sizeof(int32_t) * (n_maps + 1), hipMemcpyHostToDevice));
     h->bank_n = n;
+    h->bank_maps = n_maps;
     h->bank_seed = seed;
     return AAC_OK;
+}
+
+int aac_env_set_od_bank(aac_env *h, const double *start, const double *wps, const int32_t *cnt, int32_t n,
+                        uint64_t seed) {
+    if (!h || !start || !wps || !cnt || n <= 0) return fail(AAC_E_INVALID, "bad OD bank");
+    if (h->cfg.n_maps != 1) return fail(AAC_E_INVALID, "n_maps > 1: install one OD bank per map (aac_env_set_od_banks)");
+    return aac_env_set_od_banks(h, 1, start, wps, cnt, &n, seed);
 }
 
 int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *o, void *stream) {
@@ -753,6 +788,8 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
     R.bank_wp = h->bank_wp;
     R.bank_cnt = h->bank_cnt;
     R.bank_n = h->bank_n;
+    R.bank_off = h->bank_off;
+    R.bank_maps = h->bank_maps;
     R.seed = h->bank_seed;
     R.episode = h->episode;
     if (env_done && !g_env_no_compact) {

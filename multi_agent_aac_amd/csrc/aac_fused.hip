@@ -66,6 +66,21 @@ struct GBatch {
     int n, waves;
 };
 
+#ifdef AAC_GEMM_STAMPS
+// diagnostic build only (tools/gemm_stamps.py): per-workgroup phase stamps of one launch, wave 0
+// lane 0: [s_memrealtime at entry, s_memtime at entry / after the MFMA loop / at exit, XCC id]
+constexpr int STAMP_WG = 16384;
+__device__ unsigned long long g_gemm_st[STAMP_WG][5];
+#define GSTAMP(k, v)                                                                                       \
+    do {                                                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < STAMP_WG) g_gemm_st[blockIdx.x][k] = (v);                   \
+    } while (0)
+#else
+#define GSTAMP(k, v) \
+    do {             \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, int m, int n, float v) {
     if (m >= P.M || n >= P.N) return;
 #ifdef AAC_DBG_NO_STORE      // timing probes only (tools/gemm_probe.sh): keep the value live, store ~never
@@ -311,6 +326,7 @@ __device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4
         TM(LT, LV) TM(LT, LS) TM(LT, LT) TM(LT, LW) TM(LW, LV) TM(LW, LS) TM(LW, LT) TM(LW, LW)
     }
 #undef TM
+    GSTAMP(2, __builtin_amdgcn_s_memtime());
     float *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
     float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
     // output row / column of element (block, position) of the tile (LW operands permute them)
@@ -373,6 +389,7 @@ __device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4
     }
 }
 
+
 template <int DEPTH>
 __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     __shared__ f4 red[4][4][64];       // [wave][block of the round][lane]
@@ -380,11 +397,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
 #ifdef AAC_DBG_EMPTY                   // timing probes only: the launch floor of this grid
     if (g.n > 0) return;
 #endif
+    GSTAMP(0, __builtin_amdgcn_s_memrealtime());
+    GSTAMP(1, __builtin_amdgcn_s_memtime());
     const int wg = blockIdx.x;
     int pi = 0;
     while (pi + 1 < g.n && wg >= g.p[pi + 1].w_begin) ++pi;
     const GProb &P = g.p[pi];
     gemm_tile<2, DEPTH>(P, wg - P.w_begin, red, tile);
+    GSTAMP(3, __builtin_amdgcn_s_memtime());
+    GSTAMP(4, __builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------------------------ optimiser
@@ -1392,6 +1413,18 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
 extern "C" {
 
 const char *aac_fused_last_error(void) { return f_err.c_str(); }
+
+// diagnostic builds with -DAAC_GEMM_STAMPS: copy the per-workgroup stamps of the last gemm launch
+int aac_gemm_stamps(unsigned long long *out, int32_t n_wg) {
+#ifdef AAC_GEMM_STAMPS
+    FHIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gemm_st), sizeof(unsigned long long) * 5 * std::min(n_wg, STAMP_WG)));
+    return 0;
+#else
+    (void)out;
+    (void)n_wg;
+    return ffail("built without AAC_GEMM_STAMPS");
+#endif
+}
 
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
     GBatch g{};

@@ -150,9 +150,19 @@ class BatchedEnv:
         return out
 
     def set_od_bank(self, bank, seed=0):
-        _native.check(_native.lib().aac_env_set_od_bank(self._h, bank.start.ctypes.data, bank.wps.ctypes.data,
-                                                        bank.cnt.ctypes.data, bank.n_pairs, ctypes.c_uint64(seed)),
-                      "aac_env_set_od_bank")
+        """Install the device OD bank for auto-reset: a ``world.ODBank`` (one map), or a
+        ``world.MapBanks`` for a map stack (each auto-reset draws the env's map, then its OD)."""
+        if isinstance(bank, _world.MapBanks):
+            if bank.n_maps != self.occ.shape[0]:
+                raise ValueError(f"{bank.n_maps} banks for {self.occ.shape[0]} maps")
+            _native.check(_native.lib().aac_env_set_od_banks(self._h, bank.n_maps, bank.start.ctypes.data,
+                                                             bank.wps.ctypes.data, bank.cnt.ctypes.data,
+                                                             bank.counts.ctypes.data, ctypes.c_uint64(seed)),
+                          "aac_env_set_od_banks")
+        else:
+            _native.check(_native.lib().aac_env_set_od_bank(self._h, bank.start.ctypes.data, bank.wps.ctypes.data,
+                                                            bank.cnt.ctypes.data, bank.n_pairs,
+                                                            ctypes.c_uint64(seed)), "aac_env_set_od_bank")
         self.bank = bank
 
     def use_episode_buffer(self, episode: torch.Tensor):

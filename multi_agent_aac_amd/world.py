@@ -135,3 +135,21 @@ class ODBank:
                 wps[e, a] = self.wps[k]
                 cnt[e, a] = self.cnt[k]
         return start, wps, cnt
+
+
+class MapBanks:
+    """One ``ODBank`` per map of a stack (the multipleMap variant draws the map per episode,
+    multipleMap/ma_main:464-465, then the OD from that map, ATT/env:251-347), concatenated
+    map-major for ``aac_env_set_od_banks``."""
+
+    def __init__(self, occ_stack, n_pairs=65536, seed=2026, max_wp=32, bound=BOUND, cell=CELL):
+        occ_stack = np.asarray(occ_stack, dtype=np.uint8)
+        assert occ_stack.ndim == 3
+        self.banks = [ODBank(o, n_pairs=n_pairs, seed=seed + 7919 * m, max_wp=max_wp, bound=bound, cell=cell)
+                      for m, o in enumerate(occ_stack)]
+        self.n_maps, self.max_wp = len(self.banks), max_wp
+        self.start = np.ascontiguousarray(np.concatenate([b.start for b in self.banks]))
+        self.wps = np.ascontiguousarray(np.concatenate([b.wps for b in self.banks]))
+        self.cnt = np.ascontiguousarray(np.concatenate([b.cnt for b in self.banks]))
+        self.counts = np.array([b.n_pairs for b in self.banks], dtype=np.int32)
+        self.offsets = np.concatenate([[0], np.cumsum(self.counts)]).astype(np.int64)

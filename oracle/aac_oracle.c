@@ -31,7 +31,8 @@ typedef struct {
     int32_t episode_length;
     int32_t gw, gh;             /* occupancy grid (x-major [i*gh + j]) */
     double bound[4];
-    const uint8_t *occ;
+    const uint8_t *occ;         /* n_maps stacked grids [m][i*gh + j] */
+    int32_t n_maps;             /* multipleMap variant: env e reads map map_idx[e] */
 } oc_cfg;
 
 typedef struct {
@@ -42,7 +43,14 @@ typedef struct {
     uint8_t *reach;                          /* E*N reach_target latch */
     int32_t *wall;                           /* E*N collide_wall_count */
     int32_t *step;                           /* E */
+    int32_t *map_idx;                        /* E (NULL: every env on map 0) */
 } oc_state;
+
+/* the occupancy grid of env e (MADDPG_ownENV_randomOD_radar_multipleMap: one map per episode) */
+static const uint8_t *env_occ(const oc_cfg *c, const oc_state *s, int e) {
+    const int m = s->map_idx ? s->map_idx[e] : 0;
+    return c->occ + (size_t)(m >= 0 && m < (c->n_maps > 0 ? c->n_maps : 1) ? m : 0) * c->gw * c->gh;
+}
 
 typedef struct {
     float *own, *radar, *nei, *reward;       /* E*N*D0, E*N*18, E*N*K*6, E*N */
@@ -228,7 +236,8 @@ static int ray_hline(double cx, double cy, double ex, double ey, double ly, doub
     return 1;
 }
 
-static double radar_obstacles(const oc_cfg *c, double cx, double cy, double ex, double ey, double len) {
+static double radar_obstacles(const oc_cfg *c, const uint8_t *occ, double cx, double cy, double ex, double ey,
+                              double len) {
     double mind = len, d;
     const double *b = c->bound;
     double gx0 = ceil(b[0] / 10.0) * 10.0, gy0 = ceil(b[2] / 10.0) * 10.0;
@@ -241,7 +250,7 @@ static double radar_obstacles(const oc_cfg *c, double cx, double cy, double ex, 
     if (j1 > c->gh - 1) j1 = c->gh - 1;
     for (int i = i0; i <= i1; ++i)
         for (int j = j0; j <= j1; ++j) {
-            if (!c->occ[i * c->gh + j]) continue;
+            if (!occ[i * c->gh + j]) continue;
             double qx = gx0 + 10.0 * i, qy = gy0 + 10.0 * j;
             if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, &d) && d <= mind) mind = d;
         }
@@ -361,7 +370,7 @@ static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e) {
                     if (d < shortest) { shortest = d; dd = d; }
                 }
             }
-            if (c->radar_mode != 0) dob = radar_obstacles(c, px, py, ex, ey, len);
+            if (c->radar_mode != 0) dob = radar_obstacles(c, env_occ(c, s, e), px, py, ex, ey, len);
             double v = c->radar_mode == 0 ? dd : (c->radar_mode == 1 ? dob : (dd < dob ? dd : dob));
             o->radar[ai * NRAY + r] = (float)v;
         }
@@ -422,7 +431,7 @@ void oc_step(const oc_cfg *c, oc_state *s, const float *act, oc_out *o) {
                 for (int ii = ci - 1; ii <= ci + 1 && !building; ++ii)
                     for (int jj = cj - 1; jj <= cj + 1; ++jj) {
                         if (ii < 0 || jj < 0 || ii >= c->gw || jj >= c->gh) continue;
-                        if (!c->occ[ii * c->gh + jj]) continue;
+                        if (!env_occ(c, s, e)[ii * c->gh + jj]) continue;
                         if (building_hit(px, py, gx0 + 10.0 * ii, gy0 + 10.0 * jj, pb)) { building = 1; break; }
                     }
             }
@@ -468,7 +477,7 @@ void oc_step(const oc_cfg *c, oc_state *s, const float *act, oc_out *o) {
 
 /* reset selected envs to the given OD and write their observation (env:199-405) */
 void oc_reset(const oc_cfg *c, oc_state *s, const uint8_t *env_mask, const double *start, const double *wps,
-              const int32_t *wp_cnt, oc_out *o) {
+              const int32_t *wp_cnt, const int32_t *map_idx, oc_out *o) {
     init_tables();
     const int N = c->N;
     for (int e = 0; e < c->E; ++e) {
@@ -489,6 +498,7 @@ void oc_reset(const oc_cfg *c, oc_state *s, const uint8_t *env_mask, const doubl
             s->wall[ai] = 0;
         }
         s->step[e] = 0;
+        if (s->map_idx) s->map_idx[e] = map_idx ? map_idx[e] : 0;
         observe_env(c, s, o, e);
     }
 }

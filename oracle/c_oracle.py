@@ -26,12 +26,13 @@ class _Cfg(ctypes.Structure):
     _fields_ = [("E", ctypes.c_int32), ("N", ctypes.c_int32), ("W", ctypes.c_int32),
                 ("radar_mode", ctypes.c_int32), ("compat", ctypes.c_int32), ("team_reward", ctypes.c_int32),
                 ("episode_length", ctypes.c_int32), ("gw", ctypes.c_int32), ("gh", ctypes.c_int32),
-                ("bound", ctypes.c_double * 4), ("occ", ctypes.c_void_p)]
+                ("bound", ctypes.c_double * 4), ("occ", ctypes.c_void_p), ("n_maps", ctypes.c_int32)]
 
 
 class _State(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in
-                ("pos", "vel", "pre_pos", "pre_vel", "goal", "wp", "wp_cur", "wp_cnt", "reach", "wall", "step")]
+                ("pos", "vel", "pre_pos", "pre_vel", "goal", "wp", "wp_cur", "wp_cnt", "reach", "wall", "step",
+                 "map_idx")]
 
 
 class _Out(ctypes.Structure):
@@ -51,7 +52,7 @@ def lib():
         _lib = ctypes.CDLL(_SO)
         _lib.oc_step.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(_State), ctypes.c_void_p, ctypes.POINTER(_Out)]
         _lib.oc_reset.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(_State), ctypes.c_void_p, ctypes.c_void_p,
-                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(_Out)]
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(_Out)]
         _lib.oc_observe.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(_State), ctypes.POINTER(_Out)]
         _lib.oc_bound_crash.argtypes = [ctypes.c_double] * 4 + [ctypes.c_void_p]
         for f in (_lib.oc_goal_reached, _lib.oc_building_hit):
@@ -69,10 +70,11 @@ class BatchedOracle:
         self.E, self.N, self.W = E, N, W
         self.K = N - 1
         self.D0 = 6 + 4 * self.K
-        self.occ = np.ascontiguousarray(occ, dtype=np.uint8)
+        occ = np.asarray(occ, dtype=np.uint8)
+        self.occ = np.ascontiguousarray(occ[None] if occ.ndim == 2 else occ)      # [n_maps][gw][gh]
         self.cfg = _Cfg(E, N, W, radar_mode, 1 if compat else 0, 1 if team_reward else 0, episode_length,
-                        self.occ.shape[0],
-                        self.occ.shape[1], (ctypes.c_double * 4)(*[float(b) for b in bound]), _p(self.occ))
+                        self.occ.shape[1], self.occ.shape[2], (ctypes.c_double * 4)(*[float(b) for b in bound]),
+                        _p(self.occ), self.occ.shape[0])
         z = lambda *s, dt=np.float64: np.zeros(s, dtype=dt)
         self.pos, self.vel, self.pre_pos, self.pre_vel, self.goal = (z(E, N, 2) for _ in range(5))
         self.wp = z(E, N, W, 2)
@@ -81,8 +83,10 @@ class BatchedOracle:
         self.reach = z(E, N, dt=np.uint8)
         self.wall = z(E, N, dt=np.int32)
         self.step_count = z(E, dt=np.int32)
+        self.map_idx = z(E, dt=np.int32)
         self.state = _State(*[_p(a) for a in (self.pos, self.vel, self.pre_pos, self.pre_vel, self.goal, self.wp,
-                                               self.wp_cur, self.wp_cnt, self.reach, self.wall, self.step_count)])
+                                               self.wp_cur, self.wp_cnt, self.reach, self.wall, self.step_count,
+                                               self.map_idx)])
         self.own = z(E, N, self.D0, dt=np.float32)
         self.radar = z(E, N, N_RAYS, dt=np.float32)
         self.nei = z(E, N, self.K, 6, dt=np.float32)
@@ -100,13 +104,17 @@ class BatchedOracle:
                                            self.env_done, self.bbc, self.tcpa, self.dcpa, self.conf_cur,
                                            self.conf_pre)])
 
-    def reset(self, start, wps, wp_cnt, env_mask=None):
+    def reset(self, start, wps, wp_cnt, env_mask=None, map_idx=None):
+        """Install OD (and, with a map stack, each env's map) for the masked envs (all if None)."""
+        if map_idx is not None:
+            map_idx = np.ascontiguousarray(map_idx, dtype=np.int32)
+            assert map_idx.shape == (self.E,) and map_idx.min() >= 0 and map_idx.max() < self.occ.shape[0]
         start = np.ascontiguousarray(start, dtype=np.float64)
         wps = np.ascontiguousarray(wps, dtype=np.float64)
         wp_cnt = np.ascontiguousarray(wp_cnt, dtype=np.int32)
         m = None if env_mask is None else np.ascontiguousarray(env_mask, dtype=np.uint8)
         lib().oc_reset(ctypes.byref(self.cfg), ctypes.byref(self.state), _p(m), _p(start), _p(wps), _p(wp_cnt),
-                       ctypes.byref(self.out))
+                       _p(map_idx), ctypes.byref(self.out))
 
     def step(self, actions):
         a = np.ascontiguousarray(actions, dtype=np.float32)

@@ -53,14 +53,23 @@ def mix64(x):
     return x ^ (x >> 31)
 
 
-def bank_draw(bank_start, n_bank, seed, e, episode, N, pb=2.5):
-    """Python restatement of the auto-reset draw (starts pairwise > 2 pB apart)."""
+MAP_DRAW_KEY = 0x6d61705f64726177
+
+
+def map_draw(seed, e, episode, n_maps):
+    """The auto-reset's per-episode map of env e with per-map banks (csrc/aac_env.hip reset_kernel)."""
+    return mix64(mix64(mix64(seed ^ MAP_DRAW_KEY ^ e) ^ episode)) % n_maps
+
+
+def bank_draw(bank_start, n_bank, seed, e, episode, N, pb=2.5, off=0):
+    """Python restatement of the auto-reset draw (starts pairwise > 2 pB apart) from the bank
+    entries off .. off + n_bank - 1."""
     idx = []
     for a in range(N):
         k = 0
         for att in range(4096):
             key = mix64(mix64(mix64(seed ^ e) ^ episode) ^ (a * 65536 + att))
-            k = key % n_bank
+            k = off + key % n_bank
             s = bank_start[k]
             ok = True
             for b in idx:
