@@ -100,6 +100,9 @@ int aac_env_auto_reset(aac_env *env, const uint8_t *env_done_dev, const aac_step
  * launch) so that each reset workgroup holds epb of them; 0 (default, unless AAC_ENV_RESET_PACKED=1)
  * resets over contiguous env ranges.  Results are identical either way. */
 void aac_env_set_reset_compact(int32_t on);
+/* Diagnostic builds only (-DAAC_ENV_STAMPS): per-workgroup phase stamps of the last step launch
+ * (7 uint64 per workgroup); returns an error in a normal build. */
+int aac_env_stamps(unsigned long long *out, int32_t n_wg);
 /* From now on the per-env episode counter (int32[E], advanced by every auto-reset of an env) lives
  * in the caller's device buffer episode_dev (the current counts are copied into it); the caller
  * keeps it alive while the handle exists.  A trainer's noise schedule can read it directly.  The copy

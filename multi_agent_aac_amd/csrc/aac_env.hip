@@ -14,6 +14,7 @@
 // ATT/env:2105-2618 ss_reward, ATT/main:448-462 termination, ATT/env:199-405 reset.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -28,6 +29,11 @@
 
 #define BLOCK 256
 #define MAX_MAP_BYTES 8192
+#ifndef AAC_ENV_MIN_WAVES         // minimum waves per SIMD the step kernel is compiled for: 4 keeps
+#define AAC_ENV_MIN_WAVES 4       // 4 workgroups per CU resident (179 -> 128 VGPRs, a few spilled to
+#endif                            // scratch on cold paths); 2 waves: 1.75x slower at 262 144 envs
+// observation rows staged in LDS for coalesced 16-B stores (floats per workgroup, else direct)
+#define OBS_STAGE_FLOATS 2560
 
 namespace {
 
@@ -132,18 +138,22 @@ struct Lds {
     uint8_t flags[BLOCK];   // bit0 done, bit1 check_goal, bit2 reach, bit3 bound, bit4 drone, bit5 last==nearest
     uint8_t active[BLOCK];  // per local env (reset kernel)
     int32_t idx[BLOCK];
-    uint8_t occ[MAX_MAP_BYTES];
+    alignas(16) float obs[OBS_STAGE_FLOATS];   // the workgroup's own | nei rows (step kernel, when they fit)
 };
+// the occupancy maps follow the static LDS image as dynamic LDS (n_maps * gw * gh bytes)
+extern __shared__ uint8_t s_maps[];
 
 // own + neighbour observation and tdCPA of agent i of env e (ATT/env:1285-1469)
-__device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int base) {
+__device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int base, float *own = nullptr,
+                              float *nei = nullptr) {
     const int N = A.N, K = A.K;
     const size_t ai = (size_t)e * N + i;
     const double *b = A.bound;
     const double pb = A.pb, vmax = A.vmax;
     const double2 p = S.pos[base + i], v = S.vel[base + i];
     const double px = p.x, py = p.y;
-    float *own = A.own + ai * A.D0;
+    if (!own) own = A.own + ai * A.D0;          // rows in global memory, or staged in LDS
+    if (!nei) nei = A.nei + ai * K * 6;
     double npx = -1 + (px - b[0]) * A.xs, npy = -1 + (py - b[2]) * A.ys;
     const double2 g = S.goal[base + i];
     double ngx = 2 * ((g.x - b[0]) / (b[1] - b[0])) - 1, ngy = 2 * ((g.y - b[2]) / (b[3] - b[2])) - 1;
@@ -169,7 +179,7 @@ __device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int bas
         }
         own[8 + 4 * kk] = (float)(w.x / vmax);
         own[9 + 4 * kk] = (float)(w.y / vmax);
-        float *nb = A.nei + (ai * K + kk) * 6;
+        float *nb = nei + kk * 6;
         nb[0] = (float)(2 * ((dx - dxm) / (dxM - dxm)) - 1);
         nb[1] = (float)(2 * ((dy - dym) / (dyM - dym)) - 1);
         double g0, g1;
@@ -241,9 +251,9 @@ __device__ float radar_ray(const Args &A, const Lds &S, int i, int r, int base, 
     return (float)val;
 }
 
-__device__ inline void load_maps(const Args &A, Lds &S) {
+__device__ inline void load_maps(const Args &A) {
     const int bytes = A.n_maps * A.gw * A.gh;
-    for (int k = threadIdx.x; k < bytes; k += BLOCK) S.occ[k] = A.occ[k];
+    for (int k = threadIdx.x; k < bytes; k += BLOCK) s_maps[k] = A.occ[k];
 }
 
 // all radar rays of the workgroup's (active) agents: one work item per (agent, ray)
@@ -255,8 +265,35 @@ __device__ inline void radar_phase(const Args &A, const Lds &S, int e0, int nage
         const int e = emap ? emap[le] : e0 + le;
         if (e >= A.E) continue;
         if (check_active && !S.active[le]) continue;
-        const uint8_t *occ = S.occ + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
+        const uint8_t *occ = s_maps + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
         A.radar[((size_t)e * A.N + i) * NRAY + r] = radar_ray(A, S, i, r, le * A.N, occ);
+    }
+}
+
+#ifdef AAC_ENV_STAMPS
+// diagnostic build only (tools/env_stamps.py): per-workgroup s_memtime at entry, after kinematics,
+// after the radar, after the agent phase and at exit, plus s_memrealtime at entry / exit
+constexpr int ESTAMP_WG = 65536;
+__device__ unsigned long long g_env_st[ESTAMP_WG][7];
+#define ESTAMP(k, v)                                                                                    \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_env_st[blockIdx.x][k] = (v);                \
+    } while (0)
+#else
+#define ESTAMP(k, v) \
+    do {             \
+    } while (0)
+#endif
+
+// copy n floats from LDS to global memory with 16-B stores where the destination allows
+__device__ inline void store_rows(float *dst, const float *src, int n) {
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        const int n4 = n >> 2;
+        for (int k = threadIdx.x; k < n4; k += BLOCK)
+            reinterpret_cast<float4 *>(dst)[k] = reinterpret_cast<const float4 *>(src)[k];
+        for (int k = 4 * n4 + threadIdx.x; k < n; k += BLOCK) dst[k] = src[k];
+    } else {
+        for (int k = threadIdx.x; k < n; k += BLOCK) dst[k] = src[k];
     }
 }
 
@@ -264,7 +301,7 @@ __device__ inline void radar_phase(const Args &A, const Lds &S, int e0, int nage
 // Phases: (1) kinematics, one thread per agent; (2) radar, one work item per (agent, ray) over
 // all 256 threads; (3) observation + ss_reward predicates, one thread per agent; (4) team reward
 // and episode termination, one thread per env.
-__global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__restrict__ act) {
+__global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args A, const float2 *__restrict__ act) {
     __shared__ Lds S;
     const int N = A.N;
     const int nag = A.epb * N;
@@ -275,11 +312,20 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
     const bool active = (t < nag) && (e < A.E);
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
-    load_maps(A, S);
+    ESTAMP(0, __builtin_amdgcn_s_memrealtime());
+    ESTAMP(1, __builtin_amdgcn_s_memtime());
+    load_maps(A);
 
     // ---- a1: kinematics (ATT/env:2639-2713)
-    double2 np = make_double2(0.0, 0.0), pp = np;
+    double2 np = make_double2(0.0, 0.0), pp = np, w0 = np;
+    int cur = 0, wcnt = 0;
+    uint8_t reach = 0;
     if (active) {
+        // the agent phase's own state, loaded now: its latency hides under the radar phase
+        // (the barriers below order LDS only, so these loads stay in flight across them)
+        cur = A.wp_cur[ai];
+        wcnt = A.wp_cnt[ai];
+        reach = A.reach[ai];
         pp = A.pos[ai];
         const double2 pv = A.vel[ai];
         const float2 a = act[ai];
@@ -302,18 +348,27 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
         S.ppos[t] = pp;
         S.pvel[t] = pv;
         S.goal[t] = A.goal[ai];
+        w0 = A.wp[(size_t)ai * A.W + cur];
     }
-    __syncthreads();
+    aacw::lds_barrier();
+    ESTAMP(2, __builtin_amdgcn_s_memtime());
 #ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
     radar_phase(A, S, e0, nag, false);
 #endif
+#ifdef AAC_ENV_STAMPS
+    aacw::lds_barrier();
+#endif
+    ESTAMP(3, __builtin_amdgcn_s_memtime());
+    const int D0 = A.D0, K6 = A.K * 6;
+    const bool stage = nag * (D0 + K6) <= OBS_STAGE_FLOATS;     // uniform
 #ifdef AAC_DBG_SKIP_AGENT
     if (false) {
 #else
     if (active) {
 #endif
-        const uint8_t *occ = S.occ + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
-        observe_agent(A, S, e, i, base);
+        const uint8_t *occ = s_maps + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
+        if (stage) observe_agent(A, S, e, i, base, S.obs + t * D0, S.obs + nag * D0 + t * K6);
+        else observe_agent(A, S, e, i, base);
 
         // ---- ss_reward (ATT/env:2133-2603)
         const double px = np.x, py = np.y, pb = A.pb;
@@ -357,8 +412,6 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
         if (building) A.wall[ai] += 1;
         const double2 g = S.goal[t];
         const int goal = goal_reached(px, py, g.x, g.y, pb);
-        const int cur = A.wp_cur[ai];
-        const double2 w0 = A.wp[(size_t)ai * A.W + cur];
         const int wpf = gdist(px, py, w0.x, w0.y) < 5;
         double before = npnorm(pp.x - g.x, pp.y - g.y);
         double after = npnorm(px - g.x, py - g.y);
@@ -368,7 +421,6 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
         int done = 0, cg = 0;
         uint8_t fl = 0;
         double r;
-        uint8_t reach = A.reach[ai];
         if (bnd) {
             r = ((0.0 - 20) - 0.0) - 0;
             done = 1;
@@ -384,7 +436,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
             reach = 1;
             A.reach[ai] = 1;
         } else {
-            if (wpf && A.wp_cnt[ai] - cur > 1) A.wp_cur[ai] = cur + 1;
+            if (wpf && wcnt - cur > 1) A.wp_cur[ai] = cur + 1;
             r = dtg - pen;
         }
         if (cg) m |= 32;
@@ -394,7 +446,13 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
         A.done[ai] = (uint8_t)done;
         A.mask[ai] = m;
     }
-    __syncthreads();
+    aacw::lds_barrier();
+    ESTAMP(4, __builtin_amdgcn_s_memtime());
+    if (stage) {      // the workgroup's rows are contiguous in own / nei: whole 16-B stores
+        const int nv = (e0 + A.epb <= A.E ? A.epb : A.E - e0) * N;
+        store_rows(A.own + (size_t)e0 * N * D0, S.obs, nv * D0);
+        store_rows(A.nei + (size_t)e0 * N * K6, S.obs + nag * D0, nv * K6);
+    }
     if (active) {
         double team = A.team_reward ? pairwise_sum(&S.rew[base], N) : S.rew[t];
         A.reward[ai] = (float)team;
@@ -418,6 +476,8 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Args A, const float2 *__res
             A.env_done[e] = (uint8_t)((A.episode_length < st) || any_done || all_goal || all_reach);
         }
     }
+    ESTAMP(5, __builtin_amdgcn_s_memtime());
+    ESTAMP(6, __builtin_amdgcn_s_memrealtime());
 }
 
 // ---------------------------------------------------------------------- reset / auto-reset
@@ -451,7 +511,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     const bool active = (t < nag) && (e < A.E) && S.active[le];
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
-    load_maps(A, S);
+    load_maps(A);
     if (R.mode == 1) {
         // draw N OD entries; starts pairwise > 2 pB apart (ATT/env:258-268).  One wave per
         // resetting env: the 64 lanes test 64 consecutive attempts of agent a at once and the
@@ -584,6 +644,9 @@ struct aac_env {
     int32_t *rlist;           // [1 + E]: packed resetting envs of the last auto-reset
 };
 
+// dynamic LDS of the step / reset kernels: the handle's occupancy maps
+static size_t map_bytes(const aac_env *h) { return (size_t)h->cfg.n_maps * h->cfg.grid_w * h->cfg.grid_h; }
+
 static Args make_args(const aac_env *h, const aac_step_out *o) {
     Args A;
     const aac_env_cfg &c = h->cfg;
@@ -712,7 +775,7 @@ int aac_env_step(aac_env *h, const float *actions, const aac_step_out *o, void *
     if (rc) return rc;
     if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return fail(AAC_E_INVALID, "step outputs");
     Args A = make_args(h, o);
-    hipLaunchKernelGGL(step_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A,
+    hipLaunchKernelGGL(step_kernel, dim3(h->blocks), dim3(BLOCK), map_bytes(h), (hipStream_t)stream, A,
                        reinterpret_cast<const float2 *>(actions));
     HIPCHK(hipGetLastError());
     return AAC_OK;
@@ -732,7 +795,7 @@ int aac_env_reset(aac_env *h, const uint8_t *mask, const double *start, const do
     R.cnt = cnt;
     R.map_idx = map_idx;
     R.episode = h->episode;
-    hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A, R);
+    hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), map_bytes(h), (hipStream_t)stream, A, R);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
@@ -798,12 +861,24 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
         HIPCHK(hipGetLastError());
         R.list = h->rlist;
     }
-    hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), 0, (hipStream_t)stream, A, R);
+    hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), map_bytes(h), (hipStream_t)stream, A, R);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
 
 void aac_env_set_reset_compact(int32_t on) { g_env_no_compact = on == 0; }
+
+int aac_env_stamps(unsigned long long *out, int32_t n_wg) {
+#ifdef AAC_ENV_STAMPS
+    const size_t n = sizeof(unsigned long long) * 7 * (size_t)std::min(n_wg, ESTAMP_WG);
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_env_st), n));
+    return AAC_OK;
+#else
+    (void)out;
+    (void)n_wg;
+    return fail(AAC_E_STATE, "built without AAC_ENV_STAMPS");
+#endif
+}
 
 int aac_env_use_episode_buffer(aac_env *h, int32_t *episode_dev, void *stream) {
     if (!h || !episode_dev) return fail(AAC_E_INVALID, "null argument");

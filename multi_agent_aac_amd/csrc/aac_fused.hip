@@ -62,8 +62,10 @@ struct GProb {
 };
 
 struct GBatch {
-    GProb p[AAC_GEMM_MAX];
+    int wb[AAC_GEMM_MAX];      // first workgroup of each product (INT_MAX past n): the product
+                               // select reads these 64 B with independent scalar loads
     int n, waves;
+    GProb p[AAC_GEMM_MAX];
 };
 
 #ifdef AAC_GEMM_STAMPS
@@ -400,8 +402,11 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     GSTAMP(0, __builtin_amdgcn_s_memrealtime());
     GSTAMP(1, __builtin_amdgcn_s_memtime());
     const int wg = blockIdx.x;
+    // product of this workgroup: count the products that start at or before it (wb is ascending,
+    // wb[0] = 0); independent loads instead of a dependent scan of the kernel arguments
     int pi = 0;
-    while (pi + 1 < g.n && wg >= g.p[pi + 1].w_begin) ++pi;
+#pragma unroll
+    for (int k = 1; k < AAC_GEMM_MAX; ++k) pi += wg >= g.wb[k] ? 1 : 0;
     const GProb &P = g.p[pi];
     gemm_tile<2, DEPTH>(P, wg - P.w_begin, red, tile);
     GSTAMP(3, __builtin_amdgcn_s_memtime());
@@ -1392,9 +1397,11 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
             d.deep = g_depth > 1 && chain > g_deep_chain && tm * tn >= g_deep_tiles;
         }
         d.w_begin = waves;          // in workgroups
+        g.wb[i] = waves;
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
     }
     g.waves = waves;
+    for (int i = n; i < AAC_GEMM_MAX; ++i) g.wb[i] = 0x7fffffff;
     if (g_dump > 0) {
         --g_dump;
         fprintf(stderr, "gemm_batch n=%d wg=%d\n", n, waves);
@@ -1418,6 +1425,8 @@ const char *aac_fused_last_error(void) { return f_err.c_str(); }
 int aac_gemm_stamps(unsigned long long *out, int32_t n_wg) {
 #ifdef AAC_GEMM_STAMPS
     FHIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gemm_st), sizeof(unsigned long long) * 5 * std::min(n_wg, STAMP_WG)));
+    static unsigned long long zero[STAMP_WG][5];
+    FHIP(hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_st), zero, sizeof(zero)));
     return 0;
 #else
     (void)out;

@@ -79,4 +79,13 @@ __device__ inline void compact_flags(const uint8_t *__restrict__ mask, int E, in
     if (threadIdx.x == 0) rlist[0] = base;
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for its
+// global loads in flight (__syncthreads waits for both), so loads issued before it keep going
+// across the barrier.  Use where the barrier protects LDS data only.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 }  // namespace aacw

@@ -321,6 +321,9 @@ class FusedUpdate:
     # or B*N*K rows, critic K = B rows.  AAC_SPLIT_ACTOR / AAC_SPLIT_CRITIC override (tuning).
     SPLIT_ACTOR = int(os.environ.get("AAC_SPLIT_ACTOR", "32"))
     SPLIT_CRITIC = int(os.environ.get("AAC_SPLIT_CRITIC", "8"))
+    # world == 1: run the critic step of iteration i+1 beside the actor step of iteration i on a
+    # second stream of the captured graph (AAC_OVERLAP=1; measured slower, off: DESIGN section 4)
+    OVERLAP = os.environ.get("AAC_OVERLAP", "0") == "1"
 
     def __init__(self, model, replay, B):
         self.m, self.rep, self.B = model, replay, B
@@ -351,7 +354,7 @@ class FusedUpdate:
         # critic-step activation sets [f, h, dq, dh, df]: [0] is shared with the actor step; world > 1
         # runs the critic step of iteration i+1 beside the actor step of i, in set [1]
         self.cbuf = [(self.f, self.h, self.dq, self.dh, self.df)]
-        if model.world > 1:
+        if model.world > 1 or self.OVERLAP:
             self.cbuf.append((z(B, 128 * N), z(B, 256), z(B), z(B, 256), z(B, 128 * N)))
         R = B * N
         self.dout, self.dha = z(R, 2), z(R, 256)
@@ -383,8 +386,12 @@ class FusedUpdate:
         self.pre += critic_forward(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
         self.pre.append(lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),
                                             done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y)))
+        self.segs = None
         if m.world > 1:
             self.iters = self._pipelined(A, C)
+        elif self.OVERLAP:
+            self.segs = self._overlapped(A, C)
+            self.iters = [a + b + j for a, b, j in self.segs]
         else:
             self.iters = [self._critic_step(i, A, C, self.cbuf[0], fuse_actor_fwd=True)
                           + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, i + 1)
@@ -399,6 +406,53 @@ class FusedUpdate:
     def _adam(self, opt, flat, gpart, ns, step_add):
         """world == 1: the Adam step sums the split-K partial copies itself."""
         return [lambda: adam_sum(opt, gpart, ns, step_add, grad_out=flat.grad)]
+
+    def _overlapped(self, A, C):
+        """world == 1: the update as segments (branch A, branch B, join).  The critic step of
+        iteration i+1 reads the critic weights after critic Adam step i (and the fixed targets),
+        exactly what the actor step of iteration i reads, and neither reads the other's result, so
+        branch B (critic step i+1, activation set 1) runs beside branch A (actor forward + actor step
+        of iteration i, set 0) on a second stream of the captured graph; the join runs both Adam
+        steps.  Every product's arithmetic is unchanged: bit-identical to the serial order."""
+        m, N = self.m, self.N
+        SA, SC = self.SPLIT_ACTOR, self.SPLIT_CRITIC
+        copt, aopt = m.critic_optimizer, m.actor_optimizer
+        segs = [([], self._critic_step(0, A, C, self.cbuf[1], fuse_actor_fwd=False),
+                 self._adam(copt, m.fc, self.gc, SC, 1))]
+        for i in range(N):
+            a = self._actor_fwd_launches(i, A) + self._actor_step(i, A, C)
+            b, j = [], []
+            if i + 1 < N:
+                b = self._critic_step(i + 1, A, C, self.cbuf[1], fuse_actor_fwd=False)
+                j = self._adam(copt, m.fc, self.gc, SC, i + 2)
+            j = j + self._adam(aopt, m.fa, self.ga, SA, i + 1)
+            segs.append((a, b, j))
+        return segs
+
+    def run_streams(self, side):
+        """The update with branch B of every segment on ``side`` (fork / join by stream waits):
+        what the world == 1 graph captures.  Without segments: the serial launch list."""
+        cur = torch.cuda.current_stream()
+        if self.segs is None:
+            for op in self.ops():
+                op()
+            return
+        for op in self.pre:
+            op()
+        for a, b, j in self.segs:
+            if b:
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    for op in b:
+                        op()
+            for op in a:
+                op()
+            if b:
+                cur.wait_stream(side)
+            for op in j:
+                op()
+        for op in self.post:
+            op()
 
     def _pipelined(self, A, C):
         """world > 1: one gradient all-reduce per ``update_myown`` iteration boundary instead of two.

@@ -241,6 +241,16 @@ class MADDPG:
                 graphs.append(g)
             self._graph = (graphs, colls)
             self._graph_stats = fu
+        elif self.fused:
+            # one graph; the fused plan's overlapped segments put branch B on a second stream
+            fu = self._fused_plan(B)
+            side = torch.cuda.Stream()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fu.run_streams(side)
+            self._graph_stats = fu
+            self._graph = g
+            self._side = side
         else:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):

@@ -37,6 +37,10 @@ def main():
             op()
         torch.cuda.synchronize()
         buf = np.zeros((16384, 5), dtype=np.uint64)
+        L.aac_gemm_stamps(buf.ctypes.data, 16384)      # read + clear
+        ops[k - 1]()
+        op()
+        torch.cuda.synchronize()
         assert L.aac_gemm_stamps(buf.ctypes.data, 16384) == 0
         nwg = int((buf[:, 0] > 0).sum())
         st = buf[:nwg].astype(np.int64)
