@@ -124,7 +124,7 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "env_step_pmc.json"))
     p.add_argument("--gemm-traffic", default=os.path.join(ROOT, "profiles", "gemm_pmc.json"))
@@ -310,23 +310,23 @@ def _cpu_uam_worker(N, budget, wid):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(E, N, B, radar, seconds, model="att"):
-    """The C oracle env step + the torch-CPU learner restatement on the host cores (bounded sample)."""
-    import multiprocessing as mp
-    if model == "uam":
-        return cpu_baseline_uam(E, N, B, seconds)
-    from oracle import c_oracle, learner_ref  # noqa: F401  (checker / baseline only)
-    cores = len(os.sched_getaffinity(0))
-    procs = min(cores, 16)
-    per = max(1, E // procs)
-    ctx = mp.get_context("spawn")
-    budget = seconds / 2
-    with ctx.Pool(procs) as pool:
-        res = pool.starmap(_cpu_env_worker, [(per, N, radar, budget, w) for w in range(procs)])
-    steps = min(r[0] for r in res)
-    t_env = max(r[1] / r[0] for r in res)             # seconds per env step of the slowest worker
-    env_rate = procs * per * N / t_env
-    torch.set_num_threads(procs)
+def cpu_model():
+    """The host CPU model line (lscpu 'Model name'), for the baseline's core-count context."""
+    import subprocess
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def _cpu_update_time(N, B, budget, model, threads):
+    """Seconds per update_myown of the torch-CPU restatement (oracle/learner_ref.py or gru_ref.py)."""
+    from oracle import learner_ref  # noqa: F401  (checker / baseline only)
+    torch.set_num_threads(threads)
     D0 = 6 + 4 * (N - 1)
     if model == "gru":
         from oracle import gru_ref
@@ -348,14 +348,98 @@ def cpu_baseline(E, N, B, radar, seconds, model="att"):
     while time.perf_counter() - t0 < budget or n_upd == 0:
         opts = step(opts)
         n_upd += 1
-    t_upd = (time.perf_counter() - t0) / n_upd
-    t_iter = t_env * (E / (procs * per)) + t_upd
-    return {"value": E * N / t_iter, "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
-            "sample": (f"C oracle env step ({radar} radar) on {procs} processes x {per} envs x {N} agents, "
-                       f"{steps} steps ({env_rate:.3g} agent-env-steps/s env-only) + torch-CPU update_myown "
-                       f"restatement B={B} x {n_upd} ({t_upd * 1e3:.1f} ms each), {procs} threads; "
-                       f"value = {E}x{N} agent-steps / (env step + update) per iteration"),
-            "env_only": env_rate, "update_ms": t_upd * 1e3}
+    return (time.perf_counter() - t0) / n_upd, n_upd
+
+
+def cpu_baseline(E, N, B, radar, seconds, model="att"):
+    """BASELINE.md's CPU baseline on the host cores (bounded sample of the same workload): the env
+    step timed in three forms, each combined with the torch-CPU update_myown restatement as one
+    training iteration (value = E x N agent-steps / (env step + update)):
+      mode 1  reference-shaped scalar Python (oracle/env_ref.py, ATT/env's per-agent loops), one
+              process per core, each on its own envs  -- the headline ``value``
+      mode 2  vectorised NumPy over envs (oracle/env_np.py), one process, and one process per core
+      C port  the batched C restatement (oracle/aac_oracle.c), one process per core
+    Each env rate is agent-env-steps/s summed over the processes (envs are independent)."""
+    import multiprocessing as mp
+    if model == "uam":
+        return cpu_baseline_uam(E, N, B, seconds)
+    cores = len(os.sched_getaffinity(0))
+    procs = min(cores, 16)
+    ctx = mp.get_context("spawn")
+    per = max(1, E // procs)
+    slot = seconds / 5
+    with ctx.Pool(procs) as pool:
+        m1 = pool.starmap(_cpu_scalar_worker, [(N, radar, slot, w) for w in range(procs)])
+        m2 = pool.starmap(_cpu_numpy_worker, [(min(per, 256), N, radar, slot, w) for w in range(procs)])
+        cp = pool.starmap(_cpu_env_worker, [(per, N, radar, slot, w) for w in range(procs)])
+    m2_one = _cpu_numpy_worker(min(E, 512), N, radar, slot / 2, 0)
+    t_upd, n_upd = _cpu_update_time(N, B, slot, model, procs)
+
+    def mode(res, what):
+        rate = sum(envs * N * steps / sec for steps, sec, envs in res)
+        t_iter = E * N / rate + t_upd
+        return {"value": E * N / t_iter, "env_only": rate, "processes": len(res), "what": what}
+
+    modes = {"scalar_per_core": mode(m1, "oracle/env_ref.py reference-shaped per-agent Python loop"),
+             "numpy_1proc": mode([m2_one], "oracle/env_np.py vectorised over envs, one process"),
+             "numpy_per_core": mode(m2, "oracle/env_np.py vectorised over envs, one process per core"),
+             "c_port_per_core": mode(cp, "oracle/aac_oracle.c batched C restatement, one process per core")}
+    head = modes["scalar_per_core"]
+    return {"value": head["value"], "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
+            "affinity_cores": cores, "cpu_model": cpu_model(),
+            "sample": (f"mode 1: reference-shaped scalar env (oracle/env_ref.py, {radar} radar) on {procs} processes "
+                       f"x 1 env x {N} agents, {sum(r[0] for r in m1)} env steps in ~{slot:.1f} s "
+                       f"({head['env_only']:.3g} agent-env-steps/s env-only) + torch-CPU update_myown restatement "
+                       f"B={B} x {n_upd} ({t_upd * 1e3:.1f} ms each, {procs} threads); value = {E}x{N} agent-steps / "
+                       f"(env step + update) per iteration; other modes in 'modes'"),
+            "env_only": head["env_only"], "update_ms": t_upd * 1e3, "modes": modes}
+
+
+def _cpu_scalar_worker(N, radar, budget, wid):
+    """Mode 1: one reference-shaped ScalarEnv (per-agent Python, oracle/env_ref.py), random actions,
+    re-drawn OD on episode end; returns (env steps, seconds, envs)."""
+    sys.path.insert(0, ROOT)
+    from multi_agent_aac_amd import world
+    from oracle import env_ref
+    occ = world.synthetic_map(2026)
+    bank = world.ODBank(occ, n_pairs=1024, seed=wid, max_wp=32)
+    rng = np.random.default_rng(wid)
+    env = env_ref.ScalarEnv(N, occ, radar_mode={"drones": 0, "obstacles": 1, "combined": 2}[radar])
+
+    def reset():
+        st, wps, cnt = bank.sample_env_od(1, N, rng)
+        env.reset([tuple(st[0, i]) for i in range(N)], [[list(w) for w in wps[0, i, :cnt[0, i]]] for i in range(N)])
+    reset()
+    t0 = time.perf_counter()
+    steps = 0
+    while time.perf_counter() - t0 < budget or steps < 2:
+        *_, over = env.full_step(rng.uniform(-1, 1, (N, 2)).astype(np.float32))
+        if over:
+            reset()
+        steps += 1
+    return steps, time.perf_counter() - t0, 1
+
+
+def _cpu_numpy_worker(E, N, radar, budget, wid):
+    """Mode 2: E envs of the vectorised NumPy env (oracle/env_np.py) with auto-reset."""
+    sys.path.insert(0, ROOT)
+    from multi_agent_aac_amd import world
+    from oracle import env_np
+    occ = world.synthetic_map(2026)
+    bank = world.ODBank(occ, n_pairs=4096, seed=wid, max_wp=32)
+    rng = np.random.default_rng(wid)
+    env = env_np.NumpyEnv(E, N, occ, W=32, radar_mode={"drones": 0, "obstacles": 1, "combined": 2}[radar])
+    st, wps, cnt = bank.sample_env_od(E, N, rng)
+    env.reset(st, wps, cnt)
+    t0 = time.perf_counter()
+    steps = 0
+    while time.perf_counter() - t0 < budget or steps < 1:
+        out = env.step(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32))
+        done = out[6].astype(bool)
+        if done.any():
+            env.reset(st, wps, cnt, env_mask=done)
+        steps += 1
+    return steps, time.perf_counter() - t0, E
 
 
 def _cpu_env_worker(E, N, radar, budget, wid):
@@ -378,7 +462,7 @@ def _cpu_env_worker(E, N, radar, budget, wid):
         if done.any():
             co.reset(st, wps, cnt, env_mask=done.astype(np.uint8))
         steps += 1
-    return steps, time.perf_counter() - t0
+    return steps, time.perf_counter() - t0, E
 
 
 def env_microbench(E, N, radar, iters=20):

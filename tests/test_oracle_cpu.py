@@ -424,3 +424,42 @@ def test_mpe_oracle_cpu():
     assert o.shape == (3, 18)
     np.testing.assert_allclose(o[1, 10:12], p2[0] - p2[1])
     assert np.all(o[:, 14:] == 0)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_numpy_env_matches_c_oracle(occ, mode):
+    """The vectorised NumPy restatement (oracle/env_np.py, BASELINE.md's CPU-baseline mode 2) against
+    the C oracle from identical state every step: masks / done / bbc / env_done equal, obs / radar /
+    reward within 1e-5 (no FMA in NumPy: last-bit differences only)."""
+    from oracle import env_np
+    E, N = 48, 5
+    rng = np.random.default_rng(40 + mode)
+    pools = world_ref.target_pools(occ)
+    st, wps, cnt = pack_od([draw_env_od(occ, N, rng, pools) for _ in range(E)])
+    co = c_oracle.BatchedOracle(E, N, occ, W=W_DEFAULT, radar_mode=mode)
+    ne = env_np.NumpyEnv(E, N, occ, W=W_DEFAULT, radar_mode=mode)
+    co.reset(st, wps, cnt)
+    own, radar, nei = ne.reset(st, wps, cnt)
+    np.testing.assert_allclose(own, co.own, atol=1e-5)
+    np.testing.assert_allclose(radar, co.radar, atol=1e-5)
+    seen = 0
+    for t in range(30):
+        for k in ("pos", "vel", "pre_pos", "pre_vel", "wp_cur", "reach", "wall"):
+            getattr(ne, k)[...] = getattr(co, k)
+        ne.step_count[:] = co.step_count
+        act = rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)
+        co.step(act)
+        own, radar, nei, rew, done, mask, env_done, bbc = ne.step(act)
+        np.testing.assert_allclose(own, co.own, atol=1e-5, err_msg=f"t{t}")
+        np.testing.assert_allclose(radar, co.radar, atol=1e-5, err_msg=f"t{t}")
+        np.testing.assert_allclose(nei, co.nei, atol=1e-5, err_msg=f"t{t}")
+        np.testing.assert_allclose(rew, co.reward, atol=1e-5, err_msg=f"t{t}")
+        assert np.array_equal(mask, co.mask) and np.array_equal(done, co.done), t
+        assert np.array_equal(env_done, co.env_done) and np.array_equal(bbc, co.bbc), t
+        seen |= int(np.bitwise_or.reduce(co.mask.ravel()))
+        d = co.env_done.astype(bool)
+        if d.any():
+            s2, w2, c2 = pack_od([draw_env_od(occ, N, rng, pools) for _ in range(E)])
+            co.reset(s2, w2, c2, env_mask=d.astype(np.uint8))
+            ne.reset(s2, w2, c2, env_mask=d)
+    assert seen & 0b11 == 0b11
