@@ -78,6 +78,10 @@ int aac_adam64_sum(double *param, const double *gpart, int32_t nsplit, double *e
                    int64_t n, double lr, double beta1, double beta2, double eps, const int32_t *step,
                    int32_t step_add, void *stream);
 
+/* out[i] = the sum of the nsplit partial copies gpart[s*n + i] in aac_adam64_sum's order: the
+ * gradient a multi-rank update all-reduces before aac_adam64_sum(..., out, nsplit = 1, ...). */
+int aac_sum64_partials(double *out, const double *gpart, int32_t nsplit, int64_t n, void *stream);
+
 /* target[i] += tau (src[i] - target[i]) over n parameters (torch._foreach_lerp_); then one wave
  * adds 1 to *step and writes loss[0] = mean(lq[0..B)), loss[1] = -mean(la[0..B)) with a fixed
  * summation order (lq / la / loss may be NULL). */

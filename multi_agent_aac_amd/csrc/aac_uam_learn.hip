@@ -239,6 +239,24 @@ __global__ void adam64_kernel(double *p, const double *__restrict__ gpart, int n
     }
 }
 
+// the fixed-order sum of ns partial copies (the adam64_kernel order): the gradient a multi-rank
+// update all-reduces before its Adam step (aac_adam64_sum with nsplit = 1 on the result)
+__global__ void sum64_kernel(double *out, const double *__restrict__ gpart, int ns, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double gi = gpart[i];
+        int s = 1;
+        for (; s + 8 <= ns; s += 8) {
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = gpart[(int64_t)(s + u) * n + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) gi += x[u];
+        }
+        for (; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
+        out[i] = gi;
+    }
+}
+
 __global__ void uam_polyak_kernel(double *tgt, const double *__restrict__ src, int64_t n, double tau, int32_t *step,
                                   const double *lq, const double *la, int B, double *loss) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -422,6 +440,14 @@ int aac_adam64_sum(double *param, const double *gpart, int32_t nsplit, double *e
     if (nsplit < 1 || !param || !gpart || !exp_avg || !exp_avg_sq || !step) return lfail("adam64_sum: bad argument");
     hipLaunchKernelGGL(adam64_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, param, gpart, nsplit,
                        exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, step_add);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_sum64_partials(double *out, const double *gpart, int32_t nsplit, int64_t n, void *stream) {
+    if (n <= 0) return 0;
+    if (nsplit < 1 || !out || !gpart) return lfail("sum64_partials: bad argument");
+    hipLaunchKernelGGL(sum64_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, out, gpart, nsplit, n);
     LHIP(hipGetLastError());
     return 0;
 }

@@ -195,6 +195,7 @@ def _learn_lib():
         L.aac_adam64_sum.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, vp]
         L.aac_uam_polyak.argtypes = [vp, vp, i64, dbl, vp, vp, vp, i32, vp, vp]
         L.aac_uam_push.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp, i64, vp]
+        L.aac_sum64_partials.argtypes = [vp, vp, i32, i64, vp]
         _LL = L
     return _LL
 
@@ -254,6 +255,8 @@ class FusedUamUpdate:
         self.betas = m.critic_optimizer.param_groups[0]["betas"]
         self.eps = m.critic_optimizer.param_groups[0]["eps"]
         self.gc, self.ga = z(self.KS, nC), z(self.KS, nA)
+        # world > 1: the summed gradient [critic | actor] that the ranks average before each Adam step
+        self.gflat = z(nC + nA) if m.world > 1 else None
         B = self.B
         self.idx = torch.zeros(B, dtype=torch.int32, device=dev)
         self.rows, self.xc, self.xt, self.xp = z(B, ROW), z(B, 9), z(B, 9), z(B, 9)
@@ -345,9 +348,7 @@ class FusedUamUpdate:
                          mask=P(st.hc1), ldmask=128, mact=RELU)]),
             gemm([wgrad(P(st.dh1), 128, xc, 9, 64, 9, gc["SA_fc.0.weight"], gc["SA_fc.0.bias"], nC),
                   wgrad(P(st.dh1, 64), 128, g, ROW, 64, 18, gc["SA_grid.0.weight"], gc["SA_grid.0.bias"], nC)]),
-            lambda: _ok(L.aac_adam64_sum(P(F), P(st.gc), KS, P(st.m1), P(st.m2), nC, st.lr_c, st.betas[0],
-                                         st.betas[1], st.eps, st.step.data_ptr(), 1, fused._stream()),
-                        "aac_adam64_sum"),
+            *self._adam_launches(0, nC, st.gc, st.lr_c),
             # actor step: -mean Q(s, pi(s)) through the updated critic (UAM/maddpg:389-512)
             gemm([lin(xp, 9, Wc(c, "SA_fc"), Bc(c, "SA_fc"), P(st.hp1), 128, 9, 64, RELU),
                   lin(g, ROW, Wc(c, "SA_grid"), Bc(c, "SA_grid"), P(st.hp1, 64), 128, 18, 64, RELU)]),
@@ -371,14 +372,46 @@ class FusedUamUpdate:
                         ga["merge_feature.0.bias"], nA)]),
             gemm([wgrad(P(st.dha1), 128, own, ROW, 64, 7, ga["own_fc.0.weight"], ga["own_fc.0.bias"], nA),
                   wgrad(P(st.dha1, 64), 128, g, ROW, 64, 18, ga["own_grid.0.weight"], ga["own_grid.0.bias"], nA)]),
-            lambda: _ok(L.aac_adam64_sum(P(F, nC), P(st.ga), KS, P(st.m1, nC), P(st.m2, nC), nA, st.lr_a,
-                                         st.betas[0], st.betas[1], st.eps, st.step.data_ptr(), 1, fused._stream()),
-                        "aac_adam64_sum"),
+            *self._adam_launches(nC, nA, st.ga, st.lr_a),
             # soft update of both targets (UAM/maddpg:21-25), the shared step counter and the losses
             lambda: _ok(L.aac_uam_polyak(P(T), P(F), nC + nA, float(m.tau), st.step.data_ptr(), P(st.lq), P(st.la),
                                          B, P(st.loss), fused._stream()), "aac_uam_polyak"),
         ]
         return launches
+
+    def _adam_launches(self, off, n, gpart, lr):
+        """The Adam step of the network at [off, off + n) of the flat buffers.  world == 1: Adam sums
+        the KS partial copies itself.  world > 1: sum them, average over the ranks (one collective,
+        between graph segments), Adam on the average -- bit-identical to one rank when every rank
+        holds the same data."""
+        from . import fused
+        L, st, KS, P = _learn_lib(), self, self.KS, p64
+
+        def adam(src, ns):
+            return lambda: _ok(L.aac_adam64_sum(P(st.flat, off), src, ns, P(st.m1, off), P(st.m2, off), n, lr,
+                                                st.betas[0], st.betas[1], st.eps, st.step.data_ptr(), 1,
+                                                fused._stream()), "aac_adam64_sum")
+        if self.m.world == 1:
+            return [adam(P(gpart), KS)]
+        g = self.gflat[off:off + n]
+        m = self.m
+        return [lambda: _ok(L.aac_sum64_partials(P(g), P(gpart), KS, n, fused._stream()), "aac_sum64_partials"),
+                fused.Collective(lambda: m._allreduce_flat(g)),
+                adam(P(g), 1)]
+
+    def segments(self):
+        """The launch list cut at the collectives: ([segment launches], [collective])."""
+        from . import fused
+        segs, colls, cur = [], [], []
+        for f in self._launches:
+            if isinstance(f, fused.Collective):
+                segs.append(cur)
+                colls.append(f)
+                cur = []
+            else:
+                cur.append(f)
+        segs.append(cur)
+        return segs, colls
 
     def run(self, idx=None):
         """One update from the replay (or the given sampled indices); returns (loss_q, loss_a)."""
@@ -392,13 +425,25 @@ class FusedUamUpdate:
         return self.loss[0], self.loss[1]
 
     def capture(self):
-        """One update as a HIP graph (raw launches only: nothing to warm up, no state to restore)."""
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for f in self._launches:
-                f()
-        self.graph = g
-        return g
+        """One update as HIP graphs (raw launches only: nothing to warm up, no state to restore): one
+        graph, or one per segment between the gradient all-reduces when world > 1."""
+        segs, colls = self.segments()
+        graphs = []
+        for seg in segs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for f in seg:
+                    f()
+            graphs.append(g)
+        self.graphs, self.colls = graphs, colls
+        self.graph = graphs[0] if len(graphs) == 1 else None
+        return graphs
+
+    def replay(self):
+        for k, g in enumerate(self.graphs):
+            g.replay()
+            if k < len(self.colls):
+                self.colls[k]()
 
 
 class MADDPG:
@@ -488,6 +533,11 @@ class MADDPG:
         kernel per network (lerp: target + tau (source - target), the same value to rounding)."""
         for tgt, src in ((self.critics_target, self.critics), (self.actors_target, self.actors)):
             torch._foreach_lerp_(list(tgt.parameters()), [p.detach() for p in src.parameters()], self.tau)
+
+    def _allreduce_flat(self, t):
+        """Mean over the ranks of one flat float64 gradient (the fused learner's collective)."""
+        from . import parallel
+        parallel.allreduce_mean_(t, self.pg)
 
     def _allreduce_grads(self, module):
         if self.world > 1:
@@ -592,11 +642,15 @@ class MADDPG:
         rep = replay if replay is not None else (self.replay if self.replay is not None else self.memory.dev)
         if len(rep) < B:
             raise ValueError(f"replay holds {len(rep)} transitions, cannot sample {B} distinct rows")
-        if idx is None and use_graph and self.device.type == "cuda" and self.world == 1 and self.fused_learner:
+        if self.device.type == "cuda" and self.fused_learner and (self.world > 1 or (idx is None and use_graph)):
+            # the fused learner: one graph (world == 1) or one per segment between the gradient
+            # all-reduces (world > 1, also for eager calls: the torch path would all-reduce per module)
             fu = self.fused(B, rep)
-            if getattr(fu, "graph", None) is None:
+            if idx is not None or not use_graph:
+                return fu.run(idx)
+            if getattr(fu, "graphs", None) is None:
                 fu.capture()
-            fu.graph.replay()
+            fu.replay()
             return fu.loss[0], fu.loss[1]
         if idx is None and use_graph and self.device.type == "cuda" and self.world == 1:
             if self._graph is None or self._graph_B != B or self._graph_rep != id(rep):
