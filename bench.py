@@ -41,17 +41,23 @@ FP32_PEAK_TFLOPS = 157.3
 FP64_PEAK_TFLOPS = 78.6    # AMD MI355X spec sheet, dense FP64 vector / matrix (the guide lists no FP64 row)
 
 
-def env_bytes_per_agent_step(N):
-    """130 + 4 (24 + 10 (N - 1)) algorithmic HBM bytes per agent-env-step."""
+def env_bytes_per_agent_step(N, variant="att", mean_wp=None):
+    """130 + 4 (24 + 10 (N - 1)) algorithmic HBM bytes per agent-env-step.
+    WGRU variant (config 4): read pos, vel (32), action (8), goal (16), path start (16), the goal list
+    (16 per waypoint, mean_wp of them), removed-bits + count (8); write pos, vel, pre_pos (48); obs
+    own 6 + radar 18 + nei 6 (N - 1) floats; reward, done, mask (6)."""
+    if variant == "wgru":
+        return 80 + 16 * mean_wp + 48 + 4 * (24 + 6 * (N - 1)) + 6
     return 130 + 4 * (24 + 10 * (N - 1))
 
 
-def uam_bytes_per_agent_step(N):
+def uam_bytes_per_agent_step(N, tdcpa=True):
     """Algorithmic HBM bytes of one UAM agent-env-step (aac_uam.hip): read
     pos, vel, action, goal, start (5 x 16), heading (8), reach (1), top2 (2) = 91; write pos, vel,
     pre_pos, pre_vel (64), heading (8), reach (1), top2 (2) = 75; float64 observations own 7, radar
-    18, neighbours 5 (N - 1); reward 8, done 1, mask 1."""
-    return 91 + 75 + 8 * (7 + 18 + 5 * (N - 1)) + 10
+    18, neighbours 5 (N - 1); reward 8, done 1, mask 1; with tdCPA live: float64 tcpa and dcpa per
+    neighbour, int32 conf_cur and conf_pre."""
+    return 91 + 75 + 8 * (7 + 18 + 5 * (N - 1)) + 10 + ((16 * (N - 1) + 8) if tdcpa else 0)
 
 
 def uam_update_flops(B):
@@ -121,6 +127,9 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="default 1024 (att) / 512 (gru)")
     p.add_argument("--memory", type=int, default=None, help="replay rows (default 1e5; uam 2^20)")
     p.add_argument("--radar", default="combined", choices=["drones", "obstacles", "combined"])
+    p.add_argument("--maps", type=int, default=1,
+                   help="att / gru: a stack of this many synthetic maps (seeds 2026..), one drawn per env "
+                        "episode (the multipleMap variant, multipleMap/ma_main:464-465)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,22 +164,29 @@ def barrier(ws):
 class Trainer:
     """Vectorised ma_main loop on one GPU (shared by bench.py and the examples)."""
 
-    def __init__(self, E, N, B, memory, radar, seed, pg=None, model="att"):
+    def __init__(self, E, N, B, memory, radar, seed, pg=None, model="att", maps=1):
         from multi_agent_aac_amd import world
         from multi_agent_aac_amd.env import BatchedEnv
         from multi_agent_aac_amd.maddpg import MADDPG
         self.E, self.N, self.B = E, N, B
         self.gru = model == "gru"
-        self.occ = world.synthetic_map(2026)
-        self.bank = world.ODBank(self.occ, n_pairs=65536, seed=2026 + seed, max_wp=32)
-        self.env = BatchedEnv(E, N, self.occ, radar_mode=radar, max_wp=32)
+        # config 4 runs the randomOD_Wgru_radar env (obstacle radar, per-agent WGRU reward, 6-wide own
+        # rows, max_spd 10, episodes of 150 steps); configs 2-3 the one_model_att env
+        variant = "wgru" if self.gru else "att"
+        if maps > 1:      # BASELINE.md: the 8-map stack, seeds 2026..2033; one OD bank per map
+            self.occ = world.map_stack(range(2026, 2026 + maps))
+            self.bank = world.MapBanks(self.occ, n_pairs=max(8192, 65536 // maps), seed=2026 + seed, max_wp=32)
+        else:
+            self.occ = world.synthetic_map(2026)
+            self.bank = world.ODBank(self.occ, n_pairs=65536, seed=2026 + seed, max_wp=32)
+        self.env = BatchedEnv(E, N, self.occ, radar_mode=radar, max_wp=32, variant=variant)
         self.env.set_od_bank(self.bank, seed=1234 + seed)
         D0 = 6 + 4 * (N - 1)
         if self.gru:
             from multi_agent_aac_amd import gru
             # WGRU/ma_main:380-389: actor_dim = critic_dim = [6, 18, 6], 64 hidden units
             self.model = gru.MADDPG([6, 18, 6], [6, 18, 6], 2, 64, 10, n_agents=N, seed=777, batch_size=B,
-                                    memory_length=memory, process_group=pg)
+                                    memory_length=memory, process_group=pg, own_width=self.env.D0)
             self.h = torch.zeros(E, N, 64, device="cuda")
         else:
             self.model = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, seed=777, batch_size=B,
@@ -226,7 +242,8 @@ class UamTrainer:
         from multi_agent_aac_amd import uam, uam_learner
         self.E, self.N, self.B = E, N, B
         self.gru = False
-        self.env = uam.BatchedUAM(E, N, neighbours=True)
+        # tdCPA outputs live (tcpa / dcpa per neighbour, conflict counts)
+        self.env = uam.BatchedUAM(E, N, neighbours=True, tdcpa=True)
         self.env.set_bank(uam.build_bank(16384, N, seed=2026 + seed), seed=1234 + seed)
         # UAM/main:159-165: actor_dim = critic_dim = [7, (N-1)*5, 18, 6]
         dims = [7, (N - 1) * 5, 18, 6]
@@ -368,11 +385,15 @@ def cpu_baseline(E, N, B, radar, seconds, model="att"):
     ctx = mp.get_context("spawn")
     per = max(1, E // procs)
     slot = seconds / 5
+    # config 4 times the randomOD_Wgru_radar env (obstacle radar, WGRU reward), as the GPU line
+    variant = "wgru" if model == "gru" else "att"
+    if variant == "wgru":
+        radar = "obstacles"
     with ctx.Pool(procs) as pool:
-        m1 = pool.starmap(_cpu_scalar_worker, [(N, radar, slot, w) for w in range(procs)])
-        m2 = pool.starmap(_cpu_numpy_worker, [(min(per, 256), N, radar, slot, w) for w in range(procs)])
-        cp = pool.starmap(_cpu_env_worker, [(per, N, radar, slot, w) for w in range(procs)])
-    m2_one = _cpu_numpy_worker(min(E, 512), N, radar, slot / 2, 0)
+        m1 = pool.starmap(_cpu_scalar_worker, [(N, radar, slot, w, variant) for w in range(procs)])
+        m2 = pool.starmap(_cpu_numpy_worker, [(min(per, 256), N, radar, slot, w, variant) for w in range(procs)])
+        cp = pool.starmap(_cpu_env_worker, [(per, N, radar, slot, w, variant) for w in range(procs)])
+    m2_one = _cpu_numpy_worker(min(E, 512), N, radar, slot / 2, 0, variant)
     t_upd, n_upd = _cpu_update_time(N, B, slot, model, procs)
 
     def mode(res, what):
@@ -380,14 +401,15 @@ def cpu_baseline(E, N, B, radar, seconds, model="att"):
         t_iter = E * N / rate + t_upd
         return {"value": E * N / t_iter, "env_only": rate, "processes": len(res), "what": what}
 
-    modes = {"scalar_per_core": mode(m1, "oracle/env_ref.py reference-shaped per-agent Python loop"),
+    sref = "oracle/wgru_env_ref.py" if variant == "wgru" else "oracle/env_ref.py"
+    modes = {"scalar_per_core": mode(m1, f"{sref} reference-shaped per-agent Python loop"),
              "numpy_1proc": mode([m2_one], "oracle/env_np.py vectorised over envs, one process"),
              "numpy_per_core": mode(m2, "oracle/env_np.py vectorised over envs, one process per core"),
              "c_port_per_core": mode(cp, "oracle/aac_oracle.c batched C restatement, one process per core")}
     head = modes["scalar_per_core"]
     return {"value": head["value"], "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
             "affinity_cores": cores, "cpu_model": cpu_model(),
-            "sample": (f"mode 1: reference-shaped scalar env (oracle/env_ref.py, {radar} radar) on {procs} processes "
+            "sample": (f"mode 1: reference-shaped scalar env ({sref}, {radar} radar) on {procs} processes "
                        f"x 1 env x {N} agents, {sum(r[0] for r in m1)} env steps in ~{slot:.1f} s "
                        f"({head['env_only']:.3g} agent-env-steps/s env-only) + torch-CPU update_myown restatement "
                        f"B={B} x {n_upd} ({t_upd * 1e3:.1f} ms each, {procs} threads); value = {E}x{N} agent-steps / "
@@ -395,16 +417,20 @@ def cpu_baseline(E, N, B, radar, seconds, model="att"):
             "env_only": head["env_only"], "update_ms": t_upd * 1e3, "modes": modes}
 
 
-def _cpu_scalar_worker(N, radar, budget, wid):
-    """Mode 1: one reference-shaped ScalarEnv (per-agent Python, oracle/env_ref.py), random actions,
-    re-drawn OD on episode end; returns (env steps, seconds, envs)."""
+def _cpu_scalar_worker(N, radar, budget, wid, variant="att"):
+    """Mode 1: one reference-shaped ScalarEnv (per-agent Python, oracle/env_ref.py, or
+    oracle/wgru_env_ref.py for config 4), random actions, re-drawn OD on episode end; returns
+    (env steps, seconds, envs)."""
     sys.path.insert(0, ROOT)
     from multi_agent_aac_amd import world
-    from oracle import env_ref
+    from oracle import env_ref, wgru_env_ref
     occ = world.synthetic_map(2026)
     bank = world.ODBank(occ, n_pairs=1024, seed=wid, max_wp=32)
     rng = np.random.default_rng(wid)
-    env = env_ref.ScalarEnv(N, occ, radar_mode={"drones": 0, "obstacles": 1, "combined": 2}[radar])
+    if variant == "wgru":
+        env = wgru_env_ref.WgruEnv(N, occ)
+    else:
+        env = env_ref.ScalarEnv(N, occ, radar_mode={"drones": 0, "obstacles": 1, "combined": 2}[radar])
 
     def reset():
         st, wps, cnt = bank.sample_env_od(1, N, rng)
@@ -420,7 +446,7 @@ def _cpu_scalar_worker(N, radar, budget, wid):
     return steps, time.perf_counter() - t0, 1
 
 
-def _cpu_numpy_worker(E, N, radar, budget, wid):
+def _cpu_numpy_worker(E, N, radar, budget, wid, variant="att"):
     """Mode 2: E envs of the vectorised NumPy env (oracle/env_np.py) with auto-reset."""
     sys.path.insert(0, ROOT)
     from multi_agent_aac_amd import world
@@ -428,7 +454,8 @@ def _cpu_numpy_worker(E, N, radar, budget, wid):
     occ = world.synthetic_map(2026)
     bank = world.ODBank(occ, n_pairs=4096, seed=wid, max_wp=32)
     rng = np.random.default_rng(wid)
-    env = env_np.NumpyEnv(E, N, occ, W=32, radar_mode={"drones": 0, "obstacles": 1, "combined": 2}[radar])
+    env = env_np.NumpyEnv(E, N, occ, W=32, radar_mode={"drones": 0, "obstacles": 1, "combined": 2}[radar],
+                          variant=variant)
     st, wps, cnt = bank.sample_env_od(E, N, rng)
     env.reset(st, wps, cnt)
     t0 = time.perf_counter()
@@ -442,7 +469,7 @@ def _cpu_numpy_worker(E, N, radar, budget, wid):
     return steps, time.perf_counter() - t0, E
 
 
-def _cpu_env_worker(E, N, radar, budget, wid):
+def _cpu_env_worker(E, N, radar, budget, wid, variant="att"):
     sys.path.insert(0, ROOT)
     from multi_agent_aac_amd import world
     from oracle import c_oracle
@@ -450,7 +477,7 @@ def _cpu_env_worker(E, N, radar, budget, wid):
     bank = world.ODBank(occ, n_pairs=4096, seed=wid, max_wp=32)
     rng = np.random.default_rng(wid)
     mode = {"drones": 0, "obstacles": 1, "combined": 2}[radar]
-    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode, variant=variant)
     st, wps, cnt = bank.sample_env_od(E, N, rng)
     co.reset(st, wps, cnt)
     acts = rng.uniform(-1, 1, size=(8, E, N, 2)).astype(np.float32)
@@ -465,13 +492,13 @@ def _cpu_env_worker(E, N, radar, budget, wid):
     return steps, time.perf_counter() - t0, E
 
 
-def env_microbench(E, N, radar, iters=20):
+def env_microbench(E, N, radar, iters=20, variant="att"):
     """Env-only kernel throughput at large E (the HBM-roofline regime of SURVEY 8(d))."""
     from multi_agent_aac_amd import world
     from multi_agent_aac_amd.env import BatchedEnv
     occ = world.synthetic_map(2026)
     bank = world.ODBank(occ, n_pairs=65536, seed=5, max_wp=32)
-    env = BatchedEnv(E, N, occ, radar_mode=radar, max_wp=32)
+    env = BatchedEnv(E, N, occ, radar_mode=radar, max_wp=32, variant=variant)
     env.set_od_bank(bank, seed=3)
     env.auto_reset(None)
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -487,9 +514,9 @@ def env_microbench(E, N, radar, iters=20):
     torch.cuda.synchronize()
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rate = E * N / (ms * 1e-3)
-    gbs = env_bytes_per_agent_step(N) * E * N / (ms * 1e-3) / 1e9
-    return {"envs": E, "agents": N, "kernel_ms": ms, "agent_env_steps_per_s": rate, "achieved_GBs": gbs,
-            "frac": gbs / HBM_PEAK_GBS}
+    gbs = env_bytes_per_agent_step(N, variant, float(np.mean(bank.cnt))) * E * N / (ms * 1e-3) / 1e9
+    return {"envs": E, "agents": N, "variant": variant, "kernel_ms": ms, "agent_env_steps_per_s": rate,
+            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
 
 
 def uam_env_microbench(E, N, iters=10):
@@ -511,7 +538,7 @@ def uam_env_microbench(E, N, iters=10):
         env.auto_reset(env.bufs.env_done)
     torch.cuda.synchronize()
     ms = float(np.mean([x.elapsed_time(y) for x, y in ev]))
-    gbs = uam_bytes_per_agent_step(N) * E * N / (ms * 1e-3) / 1e9
+    gbs = uam_bytes_per_agent_step(N, tdcpa=False) * E * N / (ms * 1e-3) / 1e9
     return {"envs": E, "agents": N, "kernel_ms": ms, "agent_env_steps_per_s": E * N / (ms * 1e-3),
             "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
 
@@ -532,7 +559,7 @@ def main():
     if a.model == "uam":
         tr = UamTrainer(a.envs, a.agents, a.batch, a.memory, seed=rank, pg=pg)
     else:
-        tr = Trainer(a.envs, a.agents, a.batch, a.memory, a.radar, seed=rank, pg=pg, model=a.model)
+        tr = Trainer(a.envs, a.agents, a.batch, a.memory, a.radar, seed=rank, pg=pg, model=a.model, maps=a.maps)
     # pre-fill the replay to >= memory transitions (untimed), then capture the update graph
     while len(tr.replay) < min(a.memory, 100000):
         tr.step(update=False)
@@ -556,7 +583,12 @@ def main():
     upd_per_s = a.steps / dt
     uam = a.model == "uam"
     D0 = 6 + 4 * (N - 1)
-    bpa = uam_bytes_per_agent_step(N) if uam else env_bytes_per_agent_step(N)
+    if uam:
+        bpa = uam_bytes_per_agent_step(N)
+    elif tr.gru:
+        bpa = env_bytes_per_agent_step(N, "wgru", float(np.mean(tr.bank.cnt)))
+    else:
+        bpa = env_bytes_per_agent_step(N)
     achieved = bpa * a.envs * N / (env_ms * 1e-3) / 1e9
     traffic = None
     tsrc = None
@@ -566,21 +598,27 @@ def main():
     if tpath and os.path.exists(tpath):
         with open(tpath) as f:
             t = json.load(f)
-        if t.get("envs") == a.envs and t.get("agents") == N and (uam or t.get("radar") == a.radar):
+        if t.get("envs") == a.envs and t.get("agents") == N and (
+                bool(t.get("tdcpa")) if uam else (t.get("variant", "att") == ("wgru" if tr.gru else "att") and
+                                                  t.get("radar") == ("obstacles" if tr.gru else a.radar) and
+                                                  t.get("maps", 1) == a.maps)):
             traffic = t.get("hbm_bytes_per_launch")
             tsrc = os.path.relpath(tpath, ROOT)
     if uam:
         upd_fl = uam_update_flops(a.batch)
         workload = (f"tdCPA_forV2_changeskin_UAM: {N} aircraft x {a.envs} envs/GPU, drifting cloud + go-around "
-                    f"aircraft, float64 shared actor / single critic, B={a.batch}, 1 gradient iteration per update")
+                    f"aircraft, tdCPA outputs live, float64 shared actor / single critic, B={a.batch}, "
+                    f"1 gradient iteration per update")
     elif tr.gru:      # algorithmic GEMM FLOPs of the plan's launches (2 M N K per product)
         from multi_agent_aac_amd.fused import GemmLaunch
         upd_fl = sum(op.flops for op in tr.model._plan(a.batch).ops() if isinstance(op, GemmLaunch))
         workload = f"randomOD_gru_radar: {N} agents x {a.envs} envs/GPU, GRU actor, B={a.batch} MADDPG update, " \
-                   f"{a.radar} radar"
+                   f"randomOD_Wgru_radar env (obstacle radar, per-agent WGRU ss_reward, max_spd 10)"
     else:
         upd_fl = update_flops(N, D0, a.batch)
         workload = f"one_model_att: {N} agents x {a.envs} envs/GPU, B={a.batch} MADDPG update, {a.radar} radar"
+    if not uam and a.maps > 1:
+        workload += f", {a.maps}-map stack (map drawn per env episode)"
     peak = FP64_PEAK_TFLOPS if uam else FP32_PEAK_TFLOPS
     out = {
         "metric": METRIC_UAM if uam else (METRIC_GRU if tr.gru else METRIC), "value": value,
@@ -589,11 +627,11 @@ def main():
         "vs_baseline": None, "dtype": "f64 env + f64 learner" if uam else "f64 env state / f32 obs+learner",
         "data": "synthetic",
         "config": {"workload": workload, "envs_per_gpu": a.envs, "envs_total": E_total, "agents": N,
-                   "batch": a.batch, "replay": a.memory, "radar": "runway+bound+clouds+aircraft" if uam else a.radar,
+                   "batch": a.batch, "replay": a.memory, "radar": "runway+bound+clouds+aircraft" if uam else ("obstacles" if tr.gru else a.radar),
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
-                   "update_graph": (not a.no_graph) and (ws == 1 or (not uam and tr.model.fused)),
-                   "graph_segments": "one per update" if ws == 1 else (
-                       "eager (per-module all-reduce)" if uam else "cut at each of the N+1 gradient all-reduces")},
+                   "maps": 1 if uam else a.maps, "tdcpa": uam,
+                   "update_graph": (not a.no_graph) and (ws == 1 or uam or tr.gru or tr.model.fused),
+                   "graph_segments": "one per update" if ws == 1 else "cut at each gradient all-reduce"},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if (tr.gru or uam) else N),
         "env_roofline": {"kernel": "uam_step_kernel (fused UAM env step)" if uam else "step_kernel (fused env step)",
                          "bound": "hbm", "achieved": achieved,
@@ -618,7 +656,8 @@ def main():
     else:
         out["roofline"] = out["env_roofline"]
     if rank == 0 and ws == 1 and a.env_micro:
-        out["env_microbench"] = uam_env_microbench(1 << 16, N) if uam else env_microbench(a.env_micro, N, a.radar)
+        out["env_microbench"] = uam_env_microbench(1 << 16, N) if uam else env_microbench(
+            a.env_micro, N, a.radar, variant="wgru" if a.model == "gru" else "att")
     if rank == 0 and cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

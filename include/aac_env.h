@@ -11,7 +11,7 @@
  *     thread-local message readable with aac_last_error();
  *   - one handle = one device, not thread-safe (the reference is single-threaded).
  *
- * Layouts (E envs, N agents, K = N-1 neighbours, D0 = 6 + 4K, R = 18 rays, W = max_wp):
+ * Layouts (E envs, N agents, K = N-1 neighbours, D0 = 6 + 4K (6 in variant 1), R = 18 rays, W = max_wp):
  *   own  float[E][N][D0]   radar float[E][N][R]   nei float[E][N][K][6]
  *   reward float[E][N] (team sum, identical across an env's agents)
  *   done uint8[E][N]; mask uint8[E][N] bit0 bound-crash, bit1 drone-collision, bit2 goal-touch,
@@ -57,6 +57,12 @@ typedef struct {
     double bound[4];            /* xlow, xhigh, ylow, yhigh                                 */
     double cell;                /* grid length, 10 m                                        */
     const uint8_t *occ;         /* HOST: n_maps * grid_w * grid_h bytes, x-major [i][j]     */
+    int32_t variant;            /* 0: one_model_att (ATT/env); 1: randomOD_Wgru_radar (config 4,
+                                      WGRU/env:824-2131): requires radar_mode OBSTACLES,
+                                      team_reward 0, max_wp <= 32; own rows are 6 wide (D0 = 6,
+                                      scale_vel), reward per agent (WGRU/env:1666-2039), wp_cur
+                                      holds the removed-waypoint bits of the goal list, bbc =
+                                      [bound, building, 0, 0]; typically vmax 10, episode_length 150 */
 } aac_env_cfg;
 
 /* Caller-owned device output buffers of one step / reset. tcpa..conf_pre may be NULL. */

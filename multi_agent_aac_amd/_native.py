@@ -31,7 +31,7 @@ class EnvCfg(ctypes.Structure):
                 ("episode_length", i32), ("grid_w", i32), ("grid_h", i32), ("n_maps", i32),
                 ("dt", ctypes.c_double), ("acc_max", ctypes.c_double), ("vmax", ctypes.c_double),
                 ("pB", ctypes.c_double), ("radar_len", ctypes.c_double), ("bound", ctypes.c_double * 4),
-                ("cell", ctypes.c_double), ("occ", vp)]
+                ("cell", ctypes.c_double), ("occ", vp), ("variant", i32)]
 
 
 class StepOut(ctypes.Structure):

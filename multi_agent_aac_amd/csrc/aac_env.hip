@@ -12,6 +12,9 @@
 // Reference: ATT/env:2627-2713 kinematics, :758-773 neighbours, :1051-1170 radar (drones),
 // OM/env:1049-1148 radar (obstacles), :1285-1469 observation, ATT/util:308-329 tdCPA,
 // ATT/env:2105-2618 ss_reward, ATT/main:448-462 termination, ATT/env:199-405 reset.
+// variant 1 = the randomOD_Wgru_radar env of config 4 (WGRU/env:824-1054 observation, :1666-2039
+// ss_reward, :2048-2131 step, WGRU/ma_main:653-661 termination): obstacle radar, 6-wide own rows,
+// per-agent reward against the next waypoint and the reference path (oracle/wgru_env_ref.py).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,12 +41,12 @@
 namespace {
 
 struct Args {
-    int E, N, K, D0, W, radar_mode, compat, team_reward, episode_length, gw, gh, n_maps, epb;
+    int E, N, K, D0, W, radar_mode, compat, team_reward, episode_length, gw, gh, n_maps, epb, variant;
     double bound[4];
     double gx0, gy0, xs, ys;
     double dt, acc_max, vmax, pb, radar_len;
-    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp;
-    int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx;
+    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp, *start;
+    int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx;   // variant 1: wp_cur = removed-waypoint bits
     uint8_t *reach;
     const uint8_t *occ;  // n_maps * gw * gh
     float *own, *radar, *nei, *reward;
@@ -138,6 +141,7 @@ struct Lds {
     uint8_t flags[BLOCK];   // bit0 done, bit1 check_goal, bit2 reach, bit3 bound, bit4 drone, bit5 last==nearest
     uint8_t active[BLOCK];  // per local env (reset kernel)
     int32_t idx[BLOCK];
+    unsigned long long rmin[BLOCK];   // variant 1: per agent, the smallest radar distance (float64 bits)
     alignas(16) float obs[OBS_STAGE_FLOATS];   // the workgroup's own | nei rows (step kernel, when they fit)
 };
 // the occupancy maps follow the static LDS image as dynamic LDS (n_maps * gw * gh bytes)
@@ -159,8 +163,13 @@ __device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int bas
     double ngx = 2 * ((g.x - b[0]) / (b[1] - b[0])) - 1, ngy = 2 * ((g.y - b[2]) / (b[3] - b[2])) - 1;
     own[0] = (float)npx;
     own[1] = (float)npy;
-    own[2] = (float)(v.x / vmax);
-    own[3] = (float)(v.y / vmax);
+    if (A.variant) {      // scale_vel (WGRU/env:971)
+        own[2] = (float)(A.xs * v.x);
+        own[3] = (float)(A.ys * v.y);
+    } else {
+        own[2] = (float)(v.x / vmax);
+        own[3] = (float)(v.y / vmax);
+    }
     own[4] = (float)(ngx - npx);
     own[5] = (float)(ngy - npy);
     const double dxm = b[0] - b[1], dxM = b[1] - b[0], dym = b[2] - b[3], dyM = b[3] - b[2];
@@ -170,15 +179,17 @@ __device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int bas
         if (j == i) continue;
         const double2 q = S.pos[base + j], w = S.vel[base + j];
         double dx = q.x - px, dy = q.y - py;
-        if (A.compat) {
-            own[6 + 4 * kk] = (float)(-1 + (dx - b[0]) * A.xs);
-            own[7 + 4 * kk] = (float)(-1 + (dy - b[2]) * A.ys);
-        } else {
-            own[6 + 4 * kk] = (float)(A.xs * dx);
-            own[7 + 4 * kk] = (float)(A.ys * dy);
+        if (!A.variant) {     // the own row's neighbour part (ATT only; WGRU own rows are 6 wide)
+            if (A.compat) {
+                own[6 + 4 * kk] = (float)(-1 + (dx - b[0]) * A.xs);
+                own[7 + 4 * kk] = (float)(-1 + (dy - b[2]) * A.ys);
+            } else {
+                own[6 + 4 * kk] = (float)(A.xs * dx);
+                own[7 + 4 * kk] = (float)(A.ys * dy);
+            }
+            own[8 + 4 * kk] = (float)(w.x / vmax);
+            own[9 + 4 * kk] = (float)(w.y / vmax);
         }
-        own[8 + 4 * kk] = (float)(w.x / vmax);
-        own[9 + 4 * kk] = (float)(w.y / vmax);
         float *nb = nei + kk * 6;
         nb[0] = (float)(2 * ((dx - dxm) / (dxM - dxm)) - 1);
         nb[1] = (float)(2 * ((dy - dym) / (dyM - dym)) - 1);
@@ -213,7 +224,7 @@ __device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int bas
 }
 
 // one radar ray r of agent i (ATT/env:1089-1164 drones, OM/env:1089-1141 obstacles)
-__device__ float radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ) {
+__device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ) {
     const int N = A.N;
     const double pb = A.pb;
     const double2 p = S.pos[base + i];
@@ -246,9 +257,7 @@ __device__ float radar_ray(const Args &A, const Lds &S, int i, int r, int base, 
         }
     }
     if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, px, py, ex, ey, len);
-    const double val =
-        A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
-    return (float)val;
+    return A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
 }
 
 __device__ inline void load_maps(const Args &A) {
@@ -256,9 +265,10 @@ __device__ inline void load_maps(const Args &A) {
     for (int k = threadIdx.x; k < bytes; k += BLOCK) s_maps[k] = A.occ[k];
 }
 
-// all radar rays of the workgroup's (active) agents: one work item per (agent, ray)
-__device__ inline void radar_phase(const Args &A, const Lds &S, int e0, int nagents, bool check_active,
-                                   const int32_t *emap = nullptr) {
+// all radar rays of the workgroup's (active) agents: one work item per (agent, ray); rmin (variant
+// 1 step): each agent's smallest float64 distance, as an LDS atomic min on the (non-negative) bits
+__device__ inline void radar_phase(const Args &A, Lds &S, int e0, int nagents, bool check_active,
+                                   const int32_t *emap = nullptr, bool rmin = false) {
     for (int w = threadIdx.x; w < nagents * NRAY; w += BLOCK) {
         const int la = w / NRAY, r = w - la * NRAY;
         const int le = la / A.N, i = la - le * A.N;
@@ -266,8 +276,129 @@ __device__ inline void radar_phase(const Args &A, const Lds &S, int e0, int nage
         if (e >= A.E) continue;
         if (check_active && !S.active[le]) continue;
         const uint8_t *occ = s_maps + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
-        A.radar[((size_t)e * A.N + i) * NRAY + r] = radar_ray(A, S, i, r, le * A.N, occ);
+        const double d = radar_ray(A, S, i, r, le * A.N, occ);
+        A.radar[((size_t)e * A.N + i) * NRAY + r] = (float)d;
+        if (rmin) atomicMin(&S.rmin[la], (unsigned long long)__double_as_longlong(d));
     }
+}
+
+// ------------------------------------------------------------- variant 1 (randomOD_Wgru_radar)
+// GEOS algorithm::Distance::pointToSegment and LineSegment::closestPoint (oracle/geos.py)
+__device__ double point_to_segment(double px, double py, double ax, double ay, double bx, double by) {
+    if (ax == bx && ay == by) return gdist(px, py, ax, ay);
+    const double len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay);
+    const double r = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2;
+    if (r <= 0.0) return gdist(px, py, ax, ay);
+    if (r >= 1.0) return gdist(px, py, bx, by);
+    const double sv = ((ay - py) * (bx - ax) - (ax - px) * (by - ay)) / len2;
+    return fabs(sv) * sqrt(len2);
+}
+
+__device__ double2 segment_closest_point(double px, double py, double ax, double ay, double bx, double by) {
+    double f;
+    if (px == ax && py == ay) f = 0.0;
+    else if (px == bx && py == by) f = 1.0;
+    else {
+        const double dx = bx - ax, dy = by - ay;
+        f = ((px - ax) * dx + (py - ay) * dy) / (dx * dx + dy * dy);
+    }
+    if (f > 0 && f < 1) return make_double2(ax + f * (bx - ax), ay + f * (by - ay));
+    return gdist(ax, ay, px, py) < gdist(bx, by, px, py) ? make_double2(ax, ay) : make_double2(bx, by);
+}
+
+// ss_reward of one agent (WGRU/env:1666-2039): the next-waypoint search pops goal-list entries (the
+// list = the waypoints whose bit in rm is clear), progress toward that waypoint, cross-track reward
+// against the reference path start -> waypoints (reset_world :339-343), small-step and
+// near-building penalties; per-agent reward
+__device__ double wgru_reward(const Args &A, size_t ai, double2 pp, double2 p, double2 v, uint32_t rm, int cnt,
+                              double rmin, int goal, int bnd, int building, int &flag, int &done, int &cg,
+                              uint8_t &fl) {
+    const double2 *wp = A.wp + ai * A.W;
+    const double px = p.x, py = p.y, pb = A.pb;
+    int nrem = cnt - __popc(rm & (cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1u)));
+    double smallest = INFINITY;
+    double2 nx = make_double2(0.0, 0.0);
+    const uint32_t rm0 = rm;
+    for (int k = 0; k < cnt; ++k) {
+        if ((rm >> k) & 1u) continue;
+        const double2 w = wp[k];
+        const double d = gdist(px, py, w.x, w.y);
+        if (d < smallest) {
+            smallest = d;
+            nx = w;
+            if (smallest < 5) {
+                flag = 1;
+                if (nrem > 1) {
+                    rm |= 1u << k;
+                    --nrem;
+                    double best = INFINITY;
+                    for (int q = 0; q < cnt; ++q) {
+                        if ((rm >> q) & 1u) continue;
+                        const double2 u = wp[q];
+                        const double dd = gdist(u.x, u.y, px, py);
+                        if (dd < best) {
+                            best = dd;
+                            nx = u;
+                        }
+                    }
+                }
+                break;
+            }
+        }
+    }
+    if (rm != rm0) {
+        A.wp_cur[ai] = (int32_t)rm;
+        for (int k = cnt - 1; k >= 0; --k)      // goal[-1] after the pop
+            if (!((rm >> k) & 1u)) {
+                A.goal[ai] = wp[k];
+                break;
+            }
+    }
+    const double dtg = 1 * (npnorm(pp.x - nx.x, pp.y - nx.y) - npnorm(px - nx.x, py - nx.y));
+    // cross_track_error (WGRU/env:2621-2632): nearest point of the first segment at the smallest
+    // pointToSegment distance, then the point distance to it
+    double cross;
+    {
+        double best = INFINITY;
+        double2 a = A.start[ai], q = a;
+        for (int k = 0; k < cnt; ++k) {
+            const double2 b = wp[k];
+            const double d = point_to_segment(px, py, a.x, a.y, b.x, b.y);
+            if (d < best) {
+                best = d;
+                q = segment_closest_point(px, py, a.x, a.y, b.x, b.y);
+            }
+            if (best <= 0.0) break;
+            a = b;
+        }
+        cross = gdist(px, py, q.x, q.y);
+    }
+    double dref;
+    if (cross <= pb) dref = 3 * (((0 - 1) / (pb - 0)) * cross + 1);
+    else dref = -3 * 1;
+    const double thr = 2 * pb;
+    const double sp = npnorm(v.x, v.y);
+    const double clip = sp < 0 ? 0 : (sp > thr ? thr : sp);
+    const double ssp = 3 * ((thr - clip) * (1.0 / thr));
+    const double nbp = (rmin >= pb && rmin <= 5) ? 3 * (((0 - 1) / (5 - pb)) * rmin + 2) : 0;
+    double r;
+    if (bnd) {
+        r = (((((0.0 + dref) - 5) + dtg) - ssp) + 0.0) - nbp;
+        done = 1;
+        fl |= 8;
+    } else if (building) {
+        done = 1;
+        fl |= 16;
+        r = (((((0.0 + dref) - 5) + dtg) - ssp) + 0.0) - nbp;
+    } else if (goal) {
+        cg = 1;
+        r = (0.0 + 5) + 0.0;
+    } else {
+        r = 0.0;
+        if (flag && nrem > 1) r = r + 3;
+        r = (((((r + dref) + dtg) - ssp) + 0.0) - nbp) + 0.0;
+    }
+    return r;
 }
 
 #ifdef AAC_ENV_STAMPS
@@ -348,15 +479,18 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args A, 
         S.ppos[t] = pp;
         S.pvel[t] = pv;
         S.goal[t] = A.goal[ai];
-        w0 = A.wp[(size_t)ai * A.W + cur];
+        if (!A.variant) w0 = A.wp[(size_t)ai * A.W + cur];     // variant 1: cur is a bit mask
     }
+    if (A.variant) S.rmin[t] = 0x7ff0000000000000ull;       // +inf
     aacw::lds_barrier();
     ESTAMP(2, __builtin_amdgcn_s_memtime());
 #ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
-    radar_phase(A, S, e0, nag, false);
+    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0);
 #endif
 #ifdef AAC_ENV_STAMPS
     aacw::lds_barrier();
+#else
+    if (A.variant) aacw::lds_barrier();     // the agent phase reads the radar minima (uniform branch)
 #endif
     ESTAMP(3, __builtin_amdgcn_s_memtime());
     const int D0 = A.D0, K6 = A.K * 6;
@@ -389,7 +523,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args A, 
         }
         const double c_drone = 1 + (2.5 / (10 - 2.5)), m_drone = (0 - 1) / (10 - 2.5);
         double pen = 0;
-        for (int j = 0; j < N; ++j) {
+        for (int j = 0; j < N && !A.variant; ++j) {
             if (j == i) continue;
             const double2 q = S.pos[base + j];
             double d = npnorm(px - q.x, py - q.y);
@@ -412,33 +546,43 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args A, 
         if (building) A.wall[ai] += 1;
         const double2 g = S.goal[t];
         const int goal = goal_reached(px, py, g.x, g.y, pb);
-        const int wpf = gdist(px, py, w0.x, w0.y) < 5;
-        double before = npnorm(pp.x - g.x, pp.y - g.y);
-        double after = npnorm(px - g.x, py - g.y);
-        double dtg = (1 * (before - after)) / A.vmax;
         const int bnd = bound_crash(A, pp.x, pp.y, px, py);
-        uint8_t m = (uint8_t)(bnd | ((ncoll > 0) << 1) | (goal << 2) | (building << 3) | (wpf << 4));
-        int done = 0, cg = 0;
+        int done = 0, cg = 0, wpf = 0;
         uint8_t fl = 0;
         double r;
-        if (bnd) {
-            r = ((0.0 - 20) - 0.0) - 0;
-            done = 1;
-            fl |= 8;
-        } else if (ncoll > 0) {
-            r = ((0.0 - 20) - 0.0) - pen;
-            done = 1;
-            fl |= 16;
-            if (last_coll == nearest) fl |= 32;
-        } else if (goal) {
-            r = (0.0 + 20) + 0.0;
-            cg = 1;
-            reach = 1;
-            A.reach[ai] = 1;
+        if (A.variant) {
+            r = wgru_reward(A, ai, pp, np, S.vel[t], (uint32_t)cur, wcnt, __longlong_as_double((long long)S.rmin[t]),
+                            goal, bnd, building, wpf, done, cg, fl);
+            if (cg) {
+                reach = 1;
+                A.reach[ai] = 1;
+            }
         } else {
-            if (wpf && wcnt - cur > 1) A.wp_cur[ai] = cur + 1;
-            r = dtg - pen;
+            // ATT/env:2266-2603: next waypoint in range, progress toward goal[-1]
+            wpf = gdist(px, py, w0.x, w0.y) < 5;
+            const double before = npnorm(pp.x - g.x, pp.y - g.y);
+            const double after = npnorm(px - g.x, py - g.y);
+            const double dtg = (1 * (before - after)) / A.vmax;
+            if (bnd) {
+                r = ((0.0 - 20) - 0.0) - 0;
+                done = 1;
+                fl |= 8;
+            } else if (ncoll > 0) {
+                r = ((0.0 - 20) - 0.0) - pen;
+                done = 1;
+                fl |= 16;
+                if (last_coll == nearest) fl |= 32;
+            } else if (goal) {
+                r = (0.0 + 20) + 0.0;
+                cg = 1;
+                reach = 1;
+                A.reach[ai] = 1;
+            } else {
+                if (wpf && wcnt - cur > 1) A.wp_cur[ai] = cur + 1;
+                r = dtg - pen;
+            }
         }
+        uint8_t m = (uint8_t)(bnd | ((ncoll > 0) << 1) | (goal << 2) | (building << 3) | (wpf << 4));
         if (cg) m |= 32;
         fl |= (uint8_t)(done | (cg << 1) | (reach << 2));
         S.rew[t] = r;
@@ -467,10 +611,12 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args A, 
                 b2 |= (f >> 4) & 1;
                 b3 |= (f >> 5) & 1;
             }
+            // ATT: [bound, 0, drone, last contact == nearest]; variant 1: bound_building_check
+            // [bound, building] (WGRU/env:1956, :1963)
             A.bbc[4 * e + 0] = (uint8_t)b0;
-            A.bbc[4 * e + 1] = 0;
-            A.bbc[4 * e + 2] = (uint8_t)b2;
-            A.bbc[4 * e + 3] = (uint8_t)b3;
+            A.bbc[4 * e + 1] = (uint8_t)(A.variant ? b2 : 0);
+            A.bbc[4 * e + 2] = (uint8_t)(A.variant ? 0 : b2);
+            A.bbc[4 * e + 3] = (uint8_t)(A.variant ? 0 : b3);
             int st = A.step[e] + 1;
             A.step[e] = st;
             A.env_done[e] = (uint8_t)((A.episode_length < st) || any_done || all_goal || all_reach);
@@ -583,6 +729,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         const double2 z = make_double2(0.0, 0.0);
         A.pos[ai] = st;
         A.pre_pos[ai] = st;
+        A.start[ai] = st;
         A.vel[ai] = z;
         A.pre_vel[ai] = z;
         A.wp_cnt[ai] = cnt;
@@ -633,7 +780,7 @@ struct aac_env {
     aac_env_cfg cfg;
     int device;
     int K, D0, W, epb, blocks;
-    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp;
+    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp, *start;
     int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx, *episode;
     int32_t *episode_own;     // the handle's own counter buffer (episode may be a caller's buffer)
     uint8_t *reach, *occ;
@@ -663,6 +810,7 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
     A.gh = c.grid_h;
     A.n_maps = c.n_maps;
     A.epb = h->epb;
+    A.variant = c.variant;
     for (int k = 0; k < 4; ++k) A.bound[k] = c.bound[k];
     A.gx0 = std::ceil(c.bound[0] / c.cell) * c.cell;
     A.gy0 = std::ceil(c.bound[2] / c.cell) * c.cell;
@@ -679,6 +827,7 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
     A.pre_vel = h->pre_vel;
     A.goal = h->goal;
     A.wp = h->wp;
+    A.start = h->start;
     A.wp_cur = h->wp_cur;
     A.wp_cnt = h->wp_cnt;
     A.wall = h->wall;
@@ -715,6 +864,9 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     if (c.n_maps < 1 || !c.occ || c.grid_w < 1 || c.grid_h < 1) return fail(AAC_E_INVALID, "bad occupancy maps");
     if ((size_t)c.n_maps * c.grid_w * c.grid_h > MAX_MAP_BYTES) return fail(AAC_E_INVALID, "maps exceed LDS budget");
     if (c.cell != 10.0) return fail(AAC_E_INVALID, "cell must be 10 m (grid geometry of ATT/grid:138)");
+    if (c.variant < 0 || c.variant > 1) return fail(AAC_E_INVALID, "variant: 0 one_model_att, 1 randomOD_Wgru_radar");
+    if (c.variant == 1 && (c.radar_mode != AAC_RADAR_OBSTACLES || c.team_reward || c.max_wp > 32))
+        return fail(AAC_E_INVALID, "variant 1 (WGRU): obstacle radar, per-agent reward, max_wp <= 32");
     HIPCHK(hipSetDevice(device));
     aac_env *h = new aac_env();
     std::memset(h, 0, sizeof(*h));
@@ -722,7 +874,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     h->cfg.occ = nullptr;
     h->device = device;
     h->K = c.N - 1;
-    h->D0 = 6 + 4 * h->K;
+    h->D0 = c.variant ? 6 : 6 + 4 * h->K;
     h->W = c.max_wp;
     h->epb = c.N > 24 ? 1 : 24 / c.N;   // ~24 agents x 18 rays of radar work per 256-thread workgroup
     h->blocks = (c.E + h->epb - 1) / h->epb;
@@ -731,7 +883,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
 #define ALLOC(p, n)                                                       \
     if (st == hipSuccess) st = hipMalloc((void **)&h->p, (n) * sizeof(*h->p)); \
     if (st == hipSuccess) st = hipMemset(h->p, 0, (n) * sizeof(*h->p));
-    ALLOC(pos, EN) ALLOC(vel, EN) ALLOC(pre_pos, EN) ALLOC(pre_vel, EN) ALLOC(goal, EN)
+    ALLOC(pos, EN) ALLOC(vel, EN) ALLOC(pre_pos, EN) ALLOC(pre_vel, EN) ALLOC(goal, EN) ALLOC(start, EN)
     ALLOC(wp, EN * h->W) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
     ALLOC(rlist, (size_t)c.E + 1)
@@ -754,7 +906,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
 
 void aac_env_destroy(aac_env *h) {
     if (!h) return;
-    void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->wp, h->wp_cur, h->wp_cnt, h->wall,
+    void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->start, h->wp, h->wp_cur, h->wp_cnt, h->wall,
                     h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt,
                     h->bank_off, h->rlist};
     for (void *p : ptrs)

@@ -52,12 +52,19 @@ class StepBuffers:
                                  for t in (getattr(self, f.name) for f in fields(self))])
 
 
+VARIANTS = {"att": 0, "wgru": 1}
+
+
 class BatchedEnv:
-    """E x N vectorised ``one_model_att`` environment on one MI355X."""
+    """E x N vectorised ``one_model_att`` environment on one MI355X.
+
+    ``variant="wgru"``: the ``randomOD_Wgru_radar`` env of config 4 (WGRU/env:824-2131,
+    WGRU/ma_main:653-661): obstacle radar, 6-wide own rows, per-agent reward; its defaults are
+    max_spd 10 (WGRU/ma_main:409) and episode_length 150 (WGRU/ma_main:1044)."""
 
     def __init__(self, E, N, occ, radar_mode="drones", compat=True, team_reward=True, max_wp=32,
                  episode_length=50, device=None, bound=_world.BOUND, cell=_world.CELL, tdcpa=False,
-                 dt=0.5, acc_max=8.0, vmax=5.0, pB=2.5, radar_len=15.0):
+                 dt=0.5, acc_max=8.0, vmax=5.0, pB=2.5, radar_len=15.0, variant="att"):
         if not torch.cuda.is_available():
             raise RuntimeError("BatchedEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device if device is not None else "cuda")
@@ -68,7 +75,12 @@ class BatchedEnv:
             occ = occ[None]
         self.occ = np.ascontiguousarray(occ)
         self.E, self.N, self.K = int(E), int(N), int(N) - 1
-        self.D0 = 6 + 4 * self.K
+        self.variant = VARIANTS[variant]
+        if self.variant:
+            radar_mode, team_reward = "obstacles", False
+            vmax = 10.0 if vmax == 5.0 else vmax
+            episode_length = 150 if episode_length == 50 else episode_length
+        self.D0 = 6 if self.variant else 6 + 4 * self.K
         self.W = int(max_wp)
         self.tdcpa = tdcpa
         self.radar_mode = RADAR_MODES[radar_mode] if isinstance(radar_mode, str) else int(radar_mode)
@@ -81,6 +93,7 @@ class BatchedEnv:
         cfg.bound = (ctypes.c_double * 4)(*[float(b) for b in bound])
         cfg.cell = float(cell)
         cfg.occ = self.occ.ctypes.data
+        cfg.variant = self.variant
         self.cfg = cfg
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         h = ctypes.c_void_p()

@@ -399,7 +399,10 @@ class MADDPG:
 
     def __init__(self, actor_dim, critic_dim, dim_act, actor_hidden_state_size=H, gru_history_length=10, n_agents=8,
                  args=None, cr_lr=1e-3, ac_lr=1e-3, gamma=0.95, tau=0.01, device=None, seed=None, memory_length=None,
-                 batch_size=None, process_group=None):
+                 batch_size=None, process_group=None, own_width=None):
+        """own_width: the env's own-observation row width the act / replay rows use: 6 for the WGRU
+        env variant (``BatchedEnv(variant="wgru")``, WGRU/env:990), default 6 + 4 (N - 1) (the ATT
+        env's rows, of which the networks read the first actor_dim[0])."""
         from .maddpg import _Adam
         self.args = args
         self.device = torch.device(device) if device is not None else torch.device("cuda")
@@ -409,7 +412,7 @@ class MADDPG:
         self.n_actions = int(dim_act)
         assert self.n_actions == 2, "the tanh output layer of the row kernel is 2 actions wide (WGRU/nets:187)"
         self.d_own = int(actor_dim[0])                 # own-state columns the networks read (6 in WGRU/main:380)
-        self.D0 = max(self.d_own, 6 + 4 * (N - 1))     # row width of the env's own observation
+        self.D0 = max(self.d_own, int(own_width) if own_width else 6 + 4 * (N - 1))   # env own-row width
         self.n_actor_dim, self.n_critic_dim = list(actor_dim), list(critic_dim)
         if seed is not None:
             torch.manual_seed(seed)

@@ -14,6 +14,9 @@
  * Reference lines: ATT/env:2627-2713 (kinematics), :758-773 (neighbours), :1051-1170 + OM/env:
  * 1049-1148 (radar), :1285-1469 (obs), ATT/util:308-329 (tdCPA), ATT/env:2105-2618 (ss_reward),
  * ATT/main:448-462 (termination).
+ * variant = 1: the randomOD_Wgru_radar env of config 4 (oracle/wgru_env_ref.py, WGRU/env:824-1054,
+ * :1666-2039, :2048-2131, WGRU/ma_main:653-661): obstacle radar, 6-wide own rows with scale_vel,
+ * per-agent reward against the next waypoint and the reference path.
  */
 #include <math.h>
 #include <stdint.h>
@@ -33,6 +36,8 @@ typedef struct {
     double bound[4];
     const uint8_t *occ;         /* n_maps stacked grids [m][i*gh + j] */
     int32_t n_maps;             /* multipleMap variant: env e reads map map_idx[e] */
+    int32_t variant;            /* 0 one_model_att, 1 randomOD_Wgru_radar */
+    double vmax;                /* max_spd: 5 (ATT/main:150), 10 (WGRU/ma_main:409) */
 } oc_cfg;
 
 typedef struct {
@@ -44,6 +49,7 @@ typedef struct {
     int32_t *wall;                           /* E*N collide_wall_count */
     int32_t *step;                           /* E */
     int32_t *map_idx;                        /* E (NULL: every env on map 0) */
+    double *start;                           /* E*N*2 episode start (variant 1: reference path) */
 } oc_state;
 
 /* the occupancy grid of env e (MADDPG_ownENV_randomOD_radar_multipleMap: one map per episode) */
@@ -301,11 +307,12 @@ static void tdcpa(double ox, double oy, double hx, double hy, double ovx, double
 }
 
 /* ------------------------------------------------------------ observation (env:837-1493) */
-static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e) {
-    const int N = c->N, K = N - 1, D0 = 6 + 4 * K;
+/* rmin (variant 1, may be NULL): per agent, the smallest radar distance in float64 */
+static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e, double *rmin) {
+    const int N = c->N, K = N - 1, D0 = c->variant ? 6 : 6 + 4 * K;
     const double *b = c->bound;
     const double XS = (1.0 - (-1.0)) / (b[1] - b[0]), YS = (1.0 - (-1.0)) / (b[3] - b[2]);
-    const double pb = 2.5, vmax = 5.0;
+    const double pb = 2.5, vmax = c->vmax;
     for (int i = 0; i < N; ++i) {
         size_t ai = (size_t)e * N + i;
         double px = s->pos[2 * ai], py = s->pos[2 * ai + 1];
@@ -315,7 +322,8 @@ static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e) {
         double gx = s->goal[2 * ai], gy = s->goal[2 * ai + 1];
         double ngx = 2 * ((gx - b[0]) / (b[1] - b[0])) - 1, ngy = 2 * ((gy - b[2]) / (b[3] - b[2])) - 1;
         own[0] = (float)npx; own[1] = (float)npy;
-        own[2] = (float)(vx / vmax); own[3] = (float)(vy / vmax);
+        if (c->variant) { own[2] = (float)(XS * vx); own[3] = (float)(YS * vy); }   /* scale_vel */
+        else { own[2] = (float)(vx / vmax); own[3] = (float)(vy / vmax); }
         own[4] = (float)(ngx - npx); own[5] = (float)(ngy - npy);
         int kk = 0, cc = 0, cp = 0;
         for (int j = 0; j < N; ++j) {
@@ -324,15 +332,17 @@ static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e) {
             double qx = s->pos[2 * aj], qy = s->pos[2 * aj + 1];
             double wx = s->vel[2 * aj], wy = s->vel[2 * aj + 1];
             double dx = qx - px, dy = qy - py;
-            if (c->compat) {
-                own[6 + 4 * kk] = (float)(-1 + (dx - b[0]) * XS);
-                own[7 + 4 * kk] = (float)(-1 + (dy - b[2]) * YS);
-            } else {
-                own[6 + 4 * kk] = (float)(XS * dx);
-                own[7 + 4 * kk] = (float)(YS * dy);
+            if (!c->variant) {
+                if (c->compat) {
+                    own[6 + 4 * kk] = (float)(-1 + (dx - b[0]) * XS);
+                    own[7 + 4 * kk] = (float)(-1 + (dy - b[2]) * YS);
+                } else {
+                    own[6 + 4 * kk] = (float)(XS * dx);
+                    own[7 + 4 * kk] = (float)(YS * dy);
+                }
+                own[8 + 4 * kk] = (float)(wx / vmax);
+                own[9 + 4 * kk] = (float)(wy / vmax);
             }
-            own[8 + 4 * kk] = (float)(wx / vmax);
-            own[9 + 4 * kk] = (float)(wy / vmax);
             float *nb = o->nei + (ai * K + kk) * 6;
             double dxm = b[0] - b[1], dxM = b[1] - b[0], dym = b[2] - b[3], dyM = b[3] - b[2];
             nb[0] = (float)(2 * ((dx - dxm) / (dxM - dxm)) - 1);
@@ -354,6 +364,7 @@ static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e) {
         }
         if (o->conf_cur) { o->conf_cur[ai] = cc; o->conf_pre[ai] = cp; }
         /* radar */
+        double rm = INFINITY;
         for (int r = 0; r < NRAY; ++r) {
             double ex = px + 15.0 * ray_c[r], ey = py + 15.0 * ray_s[r];
             double len = gdist(ex, ey, px, py);
@@ -373,8 +384,126 @@ static void observe_env(const oc_cfg *c, oc_state *s, oc_out *o, int e) {
             if (c->radar_mode != 0) dob = radar_obstacles(c, env_occ(c, s, e), px, py, ex, ey, len);
             double v = c->radar_mode == 0 ? dd : (c->radar_mode == 1 ? dob : (dd < dob ? dd : dob));
             o->radar[ai * NRAY + r] = (float)v;
+            if (v < rm) rm = v;
+        }
+        if (rmin) rmin[i] = rm;
+    }
+}
+
+/* ------------------------------------------------ GEOS point -> LineString (oracle/geos.py) */
+static double point_to_segment(double px, double py, double ax, double ay, double bx, double by) {
+    if (ax == bx && ay == by) return gdist(px, py, ax, ay);
+    double len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay);
+    double r = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2;
+    if (r <= 0.0) return gdist(px, py, ax, ay);
+    if (r >= 1.0) return gdist(px, py, bx, by);
+    double sv = ((ay - py) * (bx - ax) - (ax - px) * (by - ay)) / len2;
+    return fabs(sv) * sqrt(len2);
+}
+
+static void segment_closest_point(double px, double py, double ax, double ay, double bx, double by, double *qx,
+                                  double *qy) {
+    double f;
+    if (px == ax && py == ay) f = 0.0;
+    else if (px == bx && py == by) f = 1.0;
+    else {
+        double dx = bx - ax, dy = by - ay;
+        f = ((px - ax) * dx + (py - ay) * dy) / (dx * dx + dy * dy);
+    }
+    if (f > 0 && f < 1) { *qx = ax + f * (bx - ax); *qy = ay + f * (by - ay); return; }
+    double d0 = gdist(ax, ay, px, py), d1 = gdist(bx, by, px, py);
+    if (d0 < d1) { *qx = ax; *qy = ay; } else { *qx = bx; *qy = by; }
+}
+
+/* cross_track_error(point, ref_line)[0] (WGRU/env:2621-2632); the path is start, wp[0..n) */
+static double cross_track(double px, double py, const double *start, const double *wp, int n) {
+    double best = INFINITY, nx = 0.0, ny = 0.0, ax = start[0], ay = start[1];
+    for (int k = 0; k < n; ++k) {
+        double bx = wp[2 * k], by = wp[2 * k + 1];
+        double d = point_to_segment(px, py, ax, ay, bx, by);
+        if (d < best) { best = d; segment_closest_point(px, py, ax, ay, bx, by, &nx, &ny); }
+        if (best <= 0.0) break;
+        ax = bx; ay = by;
+    }
+    return gdist(px, py, nx, ny);
+}
+
+/* WGRU ss_reward of agent ai (WGRU/env:1666-2039); returns the reward, sets the outputs */
+static double wgru_reward(const oc_cfg *c, oc_state *s, int e, int i, double rmin, int ncoll, int building,
+                          int *done_out, int *cg_out, uint8_t *mask_out, uint8_t *bbc) {
+    const int N = c->N;
+    const double pb = 2.5;
+    size_t ai = (size_t)e * N + i;
+    double px = s->pos[2 * ai], py = s->pos[2 * ai + 1];
+    double gx = s->goal[2 * ai], gy = s->goal[2 * ai + 1];
+    int goal = goal_reached(px, py, gx, gy, pb);
+    /* the next waypoint: remaining goal list = waypoints not flagged in wp_cur (bit k) */
+    const double *wp = s->wp + (size_t)ai * c->W * 2;
+    const int cnt = s->wp_cnt[ai];
+    uint32_t rm = (uint32_t)s->wp_cur[ai];
+    int nrem = 0;
+    for (int k = 0; k < cnt; ++k) nrem += !((rm >> k) & 1u);
+    double smallest = INFINITY, nx = 0.0, ny = 0.0;
+    int flag = 0;
+    for (int k = 0; k < cnt; ++k) {
+        if ((rm >> k) & 1u) continue;
+        double d = gdist(px, py, wp[2 * k], wp[2 * k + 1]);
+        if (d < smallest) {
+            smallest = d;
+            nx = wp[2 * k]; ny = wp[2 * k + 1];
+            if (smallest < 5) {
+                flag = 1;
+                if (nrem > 1) {
+                    rm |= 1u << k;
+                    --nrem;
+                    double best = INFINITY;
+                    for (int q = 0; q < cnt; ++q) {
+                        if ((rm >> q) & 1u) continue;
+                        double dd = gdist(wp[2 * q], wp[2 * q + 1], px, py);
+                        if (dd < best) { best = dd; nx = wp[2 * q]; ny = wp[2 * q + 1]; }
+                    }
+                }
+                break;
+            }
         }
     }
+    s->wp_cur[ai] = (int32_t)rm;
+    for (int k = cnt - 1; k >= 0; --k)         /* goal[-1] after the pop */
+        if (!((rm >> k) & 1u)) { s->goal[2 * ai] = wp[2 * k]; s->goal[2 * ai + 1] = wp[2 * k + 1]; break; }
+    double before = npnorm(s->pre_pos[2 * ai] - nx, s->pre_pos[2 * ai + 1] - ny);
+    double after = npnorm(px - nx, py - ny);
+    double dtg = 1 * (before - after);
+    double cross = cross_track(px, py, s->start + 2 * ai, wp, cnt);
+    double dref;
+    if (cross <= pb) { double m = (0 - 1) / (pb - 0); dref = 3 * (m * cross + 1); }
+    else dref = -3 * 1;
+    double thr = 2 * pb;
+    double sp = npnorm(s->vel[2 * ai], s->vel[2 * ai + 1]);
+    double clip = sp < 0 ? 0 : (sp > thr ? thr : sp);
+    double ssp = 3 * ((thr - clip) * (1.0 / thr));
+    double m2 = (0 - 1) / (5 - pb);
+    double nbp = (rmin >= pb && rmin <= 5) ? 3 * (m2 * rmin + 2) : 0;
+    int bnd = bound_crash(s->pre_pos[2 * ai], s->pre_pos[2 * ai + 1], px, py, pb, c->bound);
+    uint8_t m = (uint8_t)(bnd | ((ncoll > 0) << 1) | (goal << 2) | (building << 3) | (flag << 4));
+    int done = 0, cg = 0;
+    double r;
+    if (bnd) {
+        r = (((((0.0 + dref) - 5) + dtg) - ssp) + 0.0) - nbp;
+        done = 1; bbc[0] = 1;
+    } else if (building) {
+        done = 1; bbc[1] = 1;
+        r = (((((0.0 + dref) - 5) + dtg) - ssp) + 0.0) - nbp;
+    } else if (goal) {
+        cg = 1; s->reach[ai] = 1;
+        r = (0.0 + 5) + 0.0;
+    } else {
+        r = 0.0;
+        if (flag && nrem > 1) r = r + 3;
+        r = (((((r + dref) + dtg) - ssp) + 0.0) - nbp) + 0.0;
+    }
+    if (cg) m |= 32;
+    *done_out = done; *cg_out = cg; *mask_out = m;
+    return r;
 }
 
 /* ------------------------------------------------------------ step (env:2627 + ss_reward) */
@@ -382,8 +511,8 @@ void oc_step(const oc_cfg *c, oc_state *s, const float *act, oc_out *o) {
     init_tables();
     const int N = c->N, E = c->E;
     const double *b = c->bound;
-    const double pb = 2.5, vmax = 5.0, dt = 0.5;
-    double rew[64];
+    const double pb = 2.5, vmax = c->vmax, dt = 0.5;
+    double rew[64], rmin[64];
     for (int e = 0; e < E; ++e) {
         /* a1 kinematics */
         for (int i = 0; i < N; ++i) {
@@ -405,7 +534,7 @@ void oc_step(const oc_cfg *c, oc_state *s, const float *act, oc_out *o) {
             s->pos[2 * ai] = s->pos[2 * ai] + s->vel[2 * ai] * dt;
             s->pos[2 * ai + 1] = s->pos[2 * ai + 1] + s->vel[2 * ai + 1] * dt;
         }
-        observe_env(c, s, o, e);
+        observe_env(c, s, o, e, c->variant ? rmin : NULL);
         /* ss_reward */
         uint8_t bbc[4] = {0, 0, 0, 0};
         int all_goal = 1, any_done = 0, all_reach = 1;
@@ -436,6 +565,17 @@ void oc_step(const oc_cfg *c, oc_state *s, const float *act, oc_out *o) {
                     }
             }
             if (building) s->wall[ai] += 1;
+            if (c->variant) {
+                int done, cg;
+                uint8_t m;
+                rew[i] = wgru_reward(c, s, e, i, rmin[i], ncoll, building, &done, &cg, &m, bbc);
+                o->done[ai] = (uint8_t)done;
+                o->mask[ai] = m;
+                any_done |= done;
+                all_goal &= cg;
+                all_reach &= s->reach[ai];
+                continue;
+            }
             double gx = s->goal[2 * ai], gy = s->goal[2 * ai + 1];
             int goal = goal_reached(px, py, gx, gy, pb);
             int cur = s->wp_cur[ai];
@@ -486,6 +626,7 @@ void oc_reset(const oc_cfg *c, oc_state *s, const uint8_t *env_mask, const doubl
             size_t ai = (size_t)e * N + i;
             s->pos[2 * ai] = s->pre_pos[2 * ai] = start[2 * ai];
             s->pos[2 * ai + 1] = s->pre_pos[2 * ai + 1] = start[2 * ai + 1];
+            if (s->start) { s->start[2 * ai] = start[2 * ai]; s->start[2 * ai + 1] = start[2 * ai + 1]; }
             s->vel[2 * ai] = s->vel[2 * ai + 1] = 0.0;
             s->pre_vel[2 * ai] = s->pre_vel[2 * ai + 1] = 0.0;
             int n = wp_cnt[ai];
@@ -499,14 +640,14 @@ void oc_reset(const oc_cfg *c, oc_state *s, const uint8_t *env_mask, const doubl
         }
         s->step[e] = 0;
         if (s->map_idx) s->map_idx[e] = map_idx ? map_idx[e] : 0;
-        observe_env(c, s, o, e);
+        observe_env(c, s, o, e, NULL);
     }
 }
 
 /* observation only (no state change) */
 void oc_observe(const oc_cfg *c, oc_state *s, oc_out *o) {
     init_tables();
-    for (int e = 0; e < c->E; ++e) observe_env(c, s, o, e);
+    for (int e = 0; e < c->E; ++e) observe_env(c, s, o, e, NULL);
 }
 
 /* building / bound / goal predicate probes for tests */
@@ -521,4 +662,9 @@ int oc_goal_reached(double px, double py, double gx, double gy) {
 int oc_building_hit(double px, double py, double cx, double cy) {
     init_tables();
     return building_hit(px, py, cx, cy, 2.5);
+}
+
+/* cross-track probe for tests (variant 1 reference-path distance) */
+double oc_cross_track(double px, double py, const double *start, const double *wp, int n) {
+    return cross_track(px, py, start, wp, n);
 }

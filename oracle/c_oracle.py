@@ -26,13 +26,14 @@ class _Cfg(ctypes.Structure):
     _fields_ = [("E", ctypes.c_int32), ("N", ctypes.c_int32), ("W", ctypes.c_int32),
                 ("radar_mode", ctypes.c_int32), ("compat", ctypes.c_int32), ("team_reward", ctypes.c_int32),
                 ("episode_length", ctypes.c_int32), ("gw", ctypes.c_int32), ("gh", ctypes.c_int32),
-                ("bound", ctypes.c_double * 4), ("occ", ctypes.c_void_p), ("n_maps", ctypes.c_int32)]
+                ("bound", ctypes.c_double * 4), ("occ", ctypes.c_void_p), ("n_maps", ctypes.c_int32),
+                ("variant", ctypes.c_int32), ("vmax", ctypes.c_double)]
 
 
 class _State(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in
                 ("pos", "vel", "pre_pos", "pre_vel", "goal", "wp", "wp_cur", "wp_cnt", "reach", "wall", "step",
-                 "map_idx")]
+                 "map_idx", "start")]
 
 
 class _Out(ctypes.Structure):
@@ -57,6 +58,9 @@ def lib():
         _lib.oc_bound_crash.argtypes = [ctypes.c_double] * 4 + [ctypes.c_void_p]
         for f in (_lib.oc_goal_reached, _lib.oc_building_hit):
             f.argtypes = [ctypes.c_double] * 4
+        _lib.oc_cross_track.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int]
+        _lib.oc_cross_track.restype = ctypes.c_double
     return _lib
 
 
@@ -66,15 +70,24 @@ def _p(a):
 
 class BatchedOracle:
     def __init__(self, E, N, occ, W=32, radar_mode=0, compat=True, episode_length=EPISODE_LENGTH,
-                 bound=BOUND, with_tdcpa=False, team_reward=True):
+                 bound=BOUND, with_tdcpa=False, team_reward=True, variant="att"):
+        """variant "att" (one_model_att) or "wgru" (randomOD_Wgru_radar, config 4: obstacle radar,
+        6-wide own rows, per-agent WGRU ss_reward, max_spd 10, episode_length 150 by default)."""
         self.E, self.N, self.W = E, N, W
         self.K = N - 1
-        self.D0 = 6 + 4 * self.K
+        self.variant = {"att": 0, "wgru": 1}[variant]
+        vmax = 5.0
+        if self.variant:
+            from .wgru_env_ref import EPISODE_LENGTH as WGRU_LEN, VMAX as WGRU_VMAX
+            assert W <= 32, "the WGRU goal list is a 32-bit removal mask"
+            radar_mode, team_reward, vmax = 1, False, float(WGRU_VMAX)
+            episode_length = WGRU_LEN if episode_length == EPISODE_LENGTH else episode_length
+        self.D0 = 6 if self.variant else 6 + 4 * self.K
         occ = np.asarray(occ, dtype=np.uint8)
         self.occ = np.ascontiguousarray(occ[None] if occ.ndim == 2 else occ)      # [n_maps][gw][gh]
         self.cfg = _Cfg(E, N, W, radar_mode, 1 if compat else 0, 1 if team_reward else 0, episode_length,
                         self.occ.shape[1], self.occ.shape[2], (ctypes.c_double * 4)(*[float(b) for b in bound]),
-                        _p(self.occ), self.occ.shape[0])
+                        _p(self.occ), self.occ.shape[0], self.variant, vmax)
         z = lambda *s, dt=np.float64: np.zeros(s, dtype=dt)
         self.pos, self.vel, self.pre_pos, self.pre_vel, self.goal = (z(E, N, 2) for _ in range(5))
         self.wp = z(E, N, W, 2)
@@ -84,9 +97,10 @@ class BatchedOracle:
         self.wall = z(E, N, dt=np.int32)
         self.step_count = z(E, dt=np.int32)
         self.map_idx = z(E, dt=np.int32)
+        self.start = z(E, N, 2)
         self.state = _State(*[_p(a) for a in (self.pos, self.vel, self.pre_pos, self.pre_vel, self.goal, self.wp,
                                                self.wp_cur, self.wp_cnt, self.reach, self.wall, self.step_count,
-                                               self.map_idx)])
+                                               self.map_idx, self.start)])
         self.own = z(E, N, self.D0, dt=np.float32)
         self.radar = z(E, N, N_RAYS, dt=np.float32)
         self.nei = z(E, N, self.K, 6, dt=np.float32)
@@ -136,3 +150,10 @@ def goal_reached(px, py, gx, gy):
 
 def building_hit(px, py, cx, cy):
     return bool(lib().oc_building_hit(px, py, cx, cy))
+
+
+def cross_track(px, py, start, wps):
+    """The C oracle's WGRU cross-track distance to the path start, wps[0..n)."""
+    st = np.ascontiguousarray(start, dtype=np.float64)
+    w = np.ascontiguousarray(wps, dtype=np.float64)
+    return float(lib().oc_cross_track(px, py, _p(st), _p(w), len(w)))

@@ -8,6 +8,10 @@ operations over (env, agent, ray, neighbour / cell / edge) instead of per-agent 
 has no fused multiply-add, so ``np.linalg.norm`` (whose OpenBLAS ddot tail is an FMA) is
 ``sqrt(x*x + y*y)`` here: values may differ from the C oracle in the last bits, never in a
 decision away from a tie (tests/test_oracle_cpu.py::test_numpy_env_matches_c_oracle).
+
+``variant="wgru"``: the randomOD_Wgru_radar env of config 4 (oracle/wgru_env_ref.py, WGRU/env:824-2131,
+WGRU/ma_main:653-661) -- obstacle radar, 6-wide own rows, per-agent reward against the next waypoint and
+the reference path, the goal list as removed-waypoint bits in ``wp_cur``.
 """
 import math
 
@@ -34,9 +38,17 @@ def _norm(x, y):
 class NumpyEnv:
     """E x N envs; state arrays as the GPU handle / C oracle (SoA, float64)."""
 
-    def __init__(self, E, N, occ, W=32, radar_mode=2, compat=True, episode_length=EPISODE_LENGTH, bound=BOUND):
+    def __init__(self, E, N, occ, W=32, radar_mode=2, compat=True, episode_length=EPISODE_LENGTH, bound=BOUND,
+                 variant="att"):
         self.E, self.N, self.K, self.W = E, N, N - 1, W
-        self.D0 = 6 + 4 * self.K
+        self.wgru = variant == "wgru"
+        if self.wgru:
+            from .wgru_env_ref import EPISODE_LENGTH as WL, VMAX as WV
+            radar_mode, self.vmax = 1, float(WV)
+            episode_length = WL if episode_length == EPISODE_LENGTH else episode_length
+        else:
+            self.vmax = float(VMAX)
+        self.D0 = 6 if self.wgru else 6 + 4 * self.K
         self.mode, self.compat, self.T = radar_mode, compat, episode_length
         self.b = np.array(bound, dtype=np.float64)
         occ = np.asarray(occ, dtype=np.uint8)
@@ -46,7 +58,7 @@ class NumpyEnv:
         ii, jj = np.nonzero(occ)
         self.cells = np.stack([gx0 + 10.0 * ii, gy0 + 10.0 * jj], 1)          # occupied cell centres
         z = lambda *s: np.zeros(s)   # noqa: E731
-        self.pos, self.vel, self.pre_pos, self.pre_vel, self.goal = (z(E, N, 2) for _ in range(5))
+        self.pos, self.vel, self.pre_pos, self.pre_vel, self.goal, self.start = (z(E, N, 2) for _ in range(6))
         self.wp = z(E, N, W, 2)
         self.wp_cur = np.zeros((E, N), np.int64)
         self.wp_cnt = np.zeros((E, N), np.int64)
@@ -60,6 +72,7 @@ class NumpyEnv:
         m = np.ones(self.E, bool) if env_mask is None else np.asarray(env_mask, bool)
         self.pos[m] = start[m]
         self.pre_pos[m] = start[m]
+        self.start[m] = start[m]
         self.vel[m] = 0.0
         self.pre_vel[m] = 0.0
         self.wp[m] = wps[m]
@@ -148,26 +161,34 @@ class NumpyEnv:
         npx, npy = -1 + (p[..., 0] - b[0]) * XS, -1 + (p[..., 1] - b[2]) * YS
         ngx = 2 * ((g[..., 0] - b[0]) / (b[1] - b[0])) - 1
         ngy = 2 * ((g[..., 1] - b[2]) / (b[3] - b[2])) - 1
+        VM = self.vmax
         own = np.zeros((E, N, self.D0))
         own[..., 0], own[..., 1] = npx, npy
-        own[..., 2], own[..., 3] = v[..., 0] / VMAX, v[..., 1] / VMAX
+        if self.wgru:                                   # scale_vel (WGRU/env:971)
+            own[..., 2], own[..., 3] = XS * v[..., 0], YS * v[..., 1]
+        else:
+            own[..., 2], own[..., 3] = v[..., 0] / VM, v[..., 1] / VM
         own[..., 4], own[..., 5] = ngx - npx, ngy - npy
         q, w = p[:, self.others], v[:, self.others]                 # (E, N, K, 2)
         dx, dy = q[..., 0] - p[..., None, 0], q[..., 1] - p[..., None, 1]
         if self.compat:
-            own[..., 6::4], own[..., 7::4] = -1 + (dx - b[0]) * XS, -1 + (dy - b[2]) * YS
             g0, g1 = w[..., 1] - q[..., 0], PB - q[..., 1]
         else:
-            own[..., 6::4], own[..., 7::4] = XS * dx, YS * dy
             gq = g[:, self.others]
             g0, g1 = gq[..., 0] - q[..., 0], gq[..., 1] - q[..., 1]
-        own[..., 8::4], own[..., 9::4] = w[..., 0] / VMAX, w[..., 1] / VMAX
+        if not self.wgru:
+            if self.compat:
+                own[..., 6::4], own[..., 7::4] = -1 + (dx - b[0]) * XS, -1 + (dy - b[2]) * YS
+            else:
+                own[..., 6::4], own[..., 7::4] = XS * dx, YS * dy
+            own[..., 8::4], own[..., 9::4] = w[..., 0] / VM, w[..., 1] / VM
         dxm, dxM, dym, dyM = b[0] - b[1], b[1] - b[0], b[2] - b[3], b[3] - b[2]
         nei = np.zeros((E, N, K, 6))
         nei[..., 0], nei[..., 1] = 2 * ((dx - dxm) / (dxM - dxm)) - 1, 2 * ((dy - dym) / (dyM - dym)) - 1
         nei[..., 2], nei[..., 3] = 2 * ((g0 - dxm) / (dxM - dxm)) - 1, 2 * ((g1 - dym) / (dyM - dym)) - 1
-        nei[..., 4], nei[..., 5] = w[..., 0] / VMAX, w[..., 1] / VMAX
+        nei[..., 4], nei[..., 5] = w[..., 0] / VM, w[..., 1] / VM
         radar = np.concatenate([self._radar(slice(s, s + chunk)) for s in range(0, E, chunk)])
+        self.radar64 = radar
         return own.astype(np.float32), radar.astype(np.float32), nei.astype(np.float32)
 
     # ------------------------------------------------------------------ step
@@ -225,11 +246,14 @@ class NumpyEnv:
         self.pre_vel[:] = self.vel
         cvx, cvy = self.vel[..., 0] + a[..., 0] * DT, self.vel[..., 1] + a[..., 1] * DT
         nh = np.arctan2(cvy, cvx)
-        fast = _norm(cvx, cvy) >= VMAX
-        self.vel[..., 0] = np.where(fast, VMAX * np.cos(nh), cvx)
-        self.vel[..., 1] = np.where(fast, VMAX * np.sin(nh), cvy)
+        VM = self.vmax
+        fast = _norm(cvx, cvy) >= VM
+        self.vel[..., 0] = np.where(fast, VM * np.cos(nh), cvx)
+        self.vel[..., 1] = np.where(fast, VM * np.sin(nh), cvy)
         self.pos = self.pos + self.vel * DT
         own, radar, nei = self.observe()
+        if self.wgru:
+            return (own, radar, nei) + self._wgru_reward()
         p, N = self.pos, self.N
         q = p[:, self.others]
         dist = _norm(p[..., None, 0] - q[..., 0], p[..., None, 1] - q[..., 1])     # (E, N, K)
@@ -277,3 +301,79 @@ class NumpyEnv:
         self.step_count += 1
         env_done = (self.T < self.step_count) | done.any(1) | cg.all(1) | self.reach.all(1)
         return own, radar, nei, reward, done.astype(np.uint8), mask.astype(np.uint8), env_done.astype(np.uint8), bbc
+
+    # ------------------------------------------------------------------ WGRU ss_reward
+    def _wgru_reward(self):
+        """WGRU/env:1666-2039 over all agents (the loop forms of oracle/wgru_env_ref.py as array ops)."""
+        E, N, W = self.E, self.N, self.W
+        p, pp, v = self.pos, self.pre_pos, self.vel
+        px, py = p[..., 0], p[..., 1]
+        q = p[:, self.others]
+        dist = _norm(px[..., None] - q[..., 0], py[..., None] - q[..., 1])
+        ncoll = (dist <= PB * 2).sum(-1)
+        building = self._building()
+        self.wall += building
+        g = self.goal
+        goal = ((g[..., 0] - px)[..., None] * NRM_C + (g[..., 1] - py)[..., None] * NRM_S).max(-1) <= (PB + 1.0) * APOTHEM
+        # next waypoint (:1815-1832): the first strict running minimum below 5 stops the scan
+        k = np.arange(W)
+        rm = self.wp_cur
+        valid = (k < self.wp_cnt[..., None]) & (((rm[..., None] >> k) & 1) == 0)
+        d = np.where(valid, _norm(px[..., None] - self.wp[..., 0], py[..., None] - self.wp[..., 1]), np.inf)
+        pm = np.concatenate([np.full((E, N, 1), np.inf), np.minimum.accumulate(d, -1)[..., :-1]], -1)
+        trig = valid & (d < pm) & (d < 5)
+        flag = trig.any(-1)
+        kt = np.argmax(trig, -1)
+        nrem = valid.sum(-1)
+        pop = flag & (nrem > 1)
+        rm = np.where(pop, rm | (np.int64(1) << kt), rm)
+        nrem = nrem - pop
+        valid2 = valid & ~(pop[..., None] & (k == kt[..., None]))
+        d2 = np.where(valid2, _norm(self.wp[..., 0] - px[..., None], self.wp[..., 1] - py[..., None]), np.inf)
+        nxt_k = np.where(pop, np.argmin(d2, -1), np.where(flag, kt, np.argmin(d, -1)))
+        nxt = np.take_along_axis(self.wp, nxt_k[..., None, None].repeat(2, -1), 2)[:, :, 0]
+        self.wp_cur = rm
+        last = (W - 1) - np.argmax(valid2[..., ::-1], -1)               # goal[-1] after the pop
+        self.goal = np.take_along_axis(self.wp, last[..., None, None].repeat(2, -1), 2)[:, :, 0].copy()
+        dtg = 1 * (_norm(pp[..., 0] - nxt[..., 0], pp[..., 1] - nxt[..., 1]) - _norm(px - nxt[..., 0], py - nxt[..., 1]))
+        # cross-track distance to the path start, wp[0..cnt) (WGRU/env:2621-2632, GEOS DistanceOp)
+        P = np.concatenate([self.start[:, :, None], self.wp], 2)           # (E, N, W + 1, 2)
+        ax, ay, bx, by = P[..., :-1, 0], P[..., :-1, 1], P[..., 1:, 0], P[..., 1:, 1]
+        X, Y = px[..., None], py[..., None]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay)
+            r = ((X - ax) * (bx - ax) + (Y - ay) * (by - ay)) / len2
+            sv = ((ay - Y) * (bx - ax) - (ax - X) * (by - ay)) / len2
+            dA, dB = _norm(X - ax, Y - ay), _norm(X - bx, Y - by)
+            dseg = np.where((ax == bx) & (ay == by), dA, np.where(r <= 0.0, dA, np.where(r >= 1.0, dB,
+                                                                                       np.abs(sv) * np.sqrt(len2))))
+            f = np.where((X == ax) & (Y == ay), 0.0, np.where((X == bx) & (Y == by), 1.0, r))
+        segv = k < self.wp_cnt[..., None]
+        ks = np.argmin(np.where(segv, dseg, np.inf), -1)[..., None]
+        pick = lambda a: np.take_along_axis(a, ks, -1)[..., 0]   # noqa: E731
+        fs, Ax, Ay, Bx, By = pick(f), pick(ax), pick(ay), pick(bx), pick(by)
+        inside = (fs > 0) & (fs < 1)
+        d0, d1 = _norm(Ax - px, Ay - py), _norm(Bx - px, By - py)
+        qx = np.where(inside, Ax + fs * (Bx - Ax), np.where(d0 < d1, Ax, Bx))
+        qy = np.where(inside, Ay + fs * (By - Ay), np.where(d0 < d1, Ay, By))
+        cross = _norm(px - qx, py - qy)
+        dref = np.where(cross <= PB, 3 * (((0 - 1) / (PB - 0)) * cross + 1), -3 * 1)
+        thr = 2 * PB
+        ssp = 3 * ((thr - np.clip(_norm(v[..., 0], v[..., 1]), 0, thr)) * (1.0 / thr))
+        rmin = self.radar64.min(-1)
+        nbp = np.where((rmin >= PB) & (rmin <= 5), 3 * (((0 - 1) / (5 - PB)) * rmin + 2), 0.0)
+        bnd = self._bound_crash()
+        crash = (((((0.0 + dref) - 5) + dtg) - ssp) + 0.0) - nbp
+        normal = (((((np.where(flag & (nrem > 1), 3.0, 0.0) + dref) + dtg) - ssp) + 0.0) - nbp) + 0.0
+        r = np.where(bnd | (building != 0), crash, np.where(goal, (0.0 + 5) + 0.0, normal))
+        done = bnd | (building != 0)
+        cg = ~done & goal
+        self.reach |= cg
+        mask = (bnd.astype(np.uint8) | (ncoll > 0) << 1 | goal << 2 | (building != 0) << 3 | flag << 4
+                | cg.astype(np.uint8) << 5)
+        bbc = np.zeros((E, 4), np.uint8)
+        bbc[:, 0] = bnd.any(1)
+        bbc[:, 1] = (~bnd & (building != 0)).any(1)
+        self.step_count += 1
+        env_done = (self.T < self.step_count) | done.any(1) | self.reach.all(1)
+        return (r.astype(np.float32), done.astype(np.uint8), mask.astype(np.uint8), env_done.astype(np.uint8), bbc)

@@ -276,6 +276,71 @@ def ray_hline_crossing(cx, cy, ex, ey, ly):
 
 
 # ---------------------------------------------------------------------------
+# point -> LineString nearest point (shapely.ops.nearest_points, GEOS DistanceOp)
+# WGRU/env:2621-2632 cross_track_error; WGRU/env:1882 (the reference path of reset_world :343)
+# ---------------------------------------------------------------------------
+
+def point_to_segment(px, py, ax, ay, bx, by):
+    """GEOS 3.11 algorithm::Distance::pointToSegment."""
+    if ax == bx and ay == by:
+        return point_dist(px, py, ax, ay)
+    len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay)
+    r = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2
+    if r <= 0.0:
+        return point_dist(px, py, ax, ay)
+    if r >= 1.0:
+        return point_dist(px, py, bx, by)
+    s = ((ay - py) * (bx - ax) - (ax - px) * (by - ay)) / len2
+    return abs(s) * math.sqrt(len2)
+
+
+def _projection_factor(px, py, ax, ay, bx, by):
+    """GEOS LineSegment::projectionFactor."""
+    if px == ax and py == ay:
+        return 0.0
+    if px == bx and py == by:
+        return 1.0
+    dx, dy = bx - ax, by - ay
+    len2 = dx * dx + dy * dy
+    if len2 == 0.0:                     # C++ division: NaN (or +-inf); never > 0 and < 1 below
+        return math.nan
+    return ((px - ax) * dx + (py - ay) * dy) / len2
+
+
+def segment_closest_point(px, py, ax, ay, bx, by):
+    """GEOS LineSegment::closestPoint (project() inside the open segment, else the nearer end)."""
+    f = _projection_factor(px, py, ax, ay, bx, by)
+    if f > 0 and f < 1:
+        if (px == ax and py == ay) or (px == bx and py == by):
+            return px, py
+        return ax + f * (bx - ax), ay + f * (by - ay)
+    d0 = point_dist(ax, ay, px, py)
+    d1 = point_dist(bx, by, px, py)
+    return (ax, ay) if d0 < d1 else (bx, by)
+
+
+def nearest_point_on_linestring(px, py, pts):
+    """DistanceOp::computeMinDistance(line, point): the first segment with the strictly smallest
+    pointToSegment distance gives the nearest point; stops at distance 0 (terminateDistance)."""
+    best, loc = math.inf, None
+    for k in range(len(pts) - 1):
+        (ax, ay), (bx, by) = pts[k], pts[k + 1]
+        d = point_to_segment(px, py, ax, ay, bx, by)
+        if d < best:
+            best = d
+            loc = segment_closest_point(px, py, ax, ay, bx, by)
+        if best <= 0.0:
+            break
+    return loc
+
+
+def cross_track_distance(px, py, pts):
+    """cross_track_error(...)[0] (WGRU/env:2621-2632): point.distance(nearest_points(point, line)[1])."""
+    nx, ny = nearest_point_on_linestring(px, py, pts)
+    return point_dist(px, py, nx, ny)
+
+
+# ---------------------------------------------------------------------------
 # independent exact formulations (tests only): rational arithmetic on the
 # actual floating-point vertices GEOS would produce.
 # ---------------------------------------------------------------------------
@@ -399,3 +464,24 @@ def segment_hits_polygon_exact(p, q, poly):
     # no boundary contact: inside iff P is inside (convex ring, either orientation)
     s = [orient(V[k], V[(k + 1) % n], P) for k in range(n)]
     return all(x >= 0 for x in s) or all(x <= 0 for x in s)
+
+
+def point_polyline_distance_exact(p, pts):
+    """Exact squared Euclidean distance from p to the polyline (Fractions): the real-arithmetic value
+    the GEOS cross-track distance approximates."""
+    P = _fr(p)
+    best = None
+    for k in range(len(pts) - 1):
+        A, B = _fr(pts[k]), _fr(pts[k + 1])
+        dx, dy = B[0] - A[0], B[1] - A[1]
+        l2 = dx * dx + dy * dy
+        if l2 == 0:
+            q = A
+        else:
+            t = ((P[0] - A[0]) * dx + (P[1] - A[1]) * dy) / l2
+            t = min(max(t, Fraction(0)), Fraction(1))
+            q = (A[0] + t * dx, A[1] + t * dy)
+        d2 = (P[0] - q[0]) ** 2 + (P[1] - q[1]) ** 2
+        if best is None or d2 < best:
+            best = d2
+    return best

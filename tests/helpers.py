@@ -96,3 +96,18 @@ def uam_oracle_steps(pre, acts, N):
         res = o.full_step(acts[e])
         out.append(tuple(res) + (U.state_of(o),))
     return out
+
+
+def wgru_targets(wp, wp_rm, wp_cnt):
+    """First remaining waypoint of every agent of the WGRU variant (wp_rm: removal bit mask)."""
+    W = wp.shape[2]
+    k = np.arange(W)
+    valid = (k < np.asarray(wp_cnt)[..., None]) & (((np.asarray(wp_rm, np.int64)[..., None] >> k) & 1) == 0)
+    first = np.argmax(valid, -1)
+    return np.take_along_axis(wp, first[..., None, None].repeat(2, -1), 2)[:, :, 0]
+
+
+def steer(pos, vel, target, rng, noise=0.3, gain=0.15, damp=0.4):
+    """Actions in [-1, 1] that fly toward ``target`` with noise (exercises waypoint / goal events)."""
+    a = gain * (target - pos) - damp * vel + noise * rng.standard_normal(pos.shape)
+    return np.clip(a, -1, 1).astype(np.float32)
