@@ -57,6 +57,16 @@ const char *aac_fused_last_error(void);
 
 /* n <= AAC_GEMM_MAX products in one launch. */
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream);
+/* The launch plan of aac_gemm_batch without launching (host only): per product 0 (register
+ * fragments, 32x32 wave tiles) or 1 + cfg (LDS-staged workgroup tile: cfg >> 2 = 64x64 / 64x32 /
+ * 32x64 / 32x32, cfg & 3 = operand layouts); *workgroups = the grid (may be NULL). */
+int aac_gemm_plan(const aac_gemm_prob *probs, int32_t n, int32_t *lds_cfg, int32_t *workgroups);
+/* Process-wide tile policy (default from AAC_GEMM_LDS_MIN_WG = 512, AAC_GEMM_LDS_SMALL = 0): an
+ * eligible product takes the largest LDS workgroup tile (64x64, then 64x32 / 32x64) that gives at
+ * least min_workgroups workgroups, else the register path; small_tiles != 0 falls back to 32x32 LDS
+ * tiles instead; min_workgroups = -1 - c forces tile c (0 64x64, 1 64x32, 2 32x64, 3 32x32) on every
+ * eligible product.  For tests and measurement tools; plans built afterwards use it. */
+void aac_gemm_set_lds_policy(int32_t min_workgroups, int32_t small_tiles);
 
 /* Diagnostic builds only (-DAAC_GEMM_STAMPS): per-workgroup stamps of the last gemm launch,
  * 5 uint64 per workgroup [memrealtime entry, memtime entry, memtime after MFMA loop, memtime exit,

@@ -59,6 +59,8 @@ struct GProb {
     int wide;                  // one tile per wave, four adjacent tiles per workgroup
     int vec;                   // the epilogue may read / write 4 columns at once (16-B aligned rows)
     int tiles_n, w_begin;      // first workgroup of this product
+    int lds;                   // 0: register fragments; 1 + cfg: LDS-staged workgroup tile (gemm_lds)
+    int xcd;                   // LDS tile: XCD-aware workgroup order
 };
 
 struct GBatch {
@@ -391,11 +393,238 @@ __device__ __forceinline__ void gemm_tile(const GProb &P, int local, f4 (*red)[4
     }
 }
 
+// ---------------------------------------------------------------- LDS-staged workgroup tiles
+// Products whose operands load as 16-B segments take (32 TI) x (32 TJ) workgroup tiles: 2 x 2 waves
+// of (16 TI) x (16 TJ).  K goes in chunks of LBK = 32 through an S-stage LDS ring filled by LDS-DMA
+// (buffer_load_dwordx4 ... lds: no VGPRs, no ds_write): S - 1 chunks are in flight while one is
+// multiplied, one barrier per chunk, counted vmcnt waits.  Every operand byte crosses L2 once per
+// workgroup tile instead of once per wave tile.  A DMA instruction fills 64 consecutive 16-B slots
+// (lane-linear), so the swizzles live in the per-lane source addresses:
+//   K-contiguous operand ([row][k]): slot = row * 8 + (k/4 ^ (row & 7)); one ds_read_b128 per
+//     fragment, conflict-free for the lane groups of ds_read_b128; a DMA instruction reads 8 whole
+//     128-B row lines
+//   row-contiguous operand ([k][row]): slot = k * rows/4 + (row/4 ^ 4 ((k/4) & 1)); four ds_read_b32
+//     per fragment, the 32 lanes of each on distinct banks; a DMA instruction reads 4 (8) whole rows
+// (tools enumerate both: tests/test_fused_gpu.py covers every layout.)  Lane (lr, lk) multiplies
+// k = 16 h + 4 lk + t at step (h, t) -- one permutation of the chunk for both operands.  The ones
+// column of op(B) (bias gradient) reads as 0 from its out-of-range segment and is set to 1 in the
+// fragment of the lane that holds it.
+constexpr int LBK = 32;
+typedef __attribute__((address_space(3))) void *lds_vp;
 
-template <int DEPTH>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc_of(const float *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), (short)0, OOB, 0x00020000);
+}
+
+template <int TI, int TJ>
+struct LCfg {
+    static constexpr int BM = 32 * TI, BN = 32 * TJ;
+    static constexpr int STAGE = (BM + BN) * LBK;                     // floats per ring stage
+#ifdef AAC_LDS_STAGES
+    static constexpr int S = AAC_LDS_STAGES;
+#else
+    // ring stages: 2 (32 / 24 / 24 / 16 KB) -- more workgroups per CU beat a deeper ring on every
+    // learner shape (3 / 4 stages: +3 / +6 % over the large shapes, tools/mb_lds.py)
+    static constexpr int S = 2;
+#endif
+    static constexpr int PW = (BM + BN) / 32;                         // DMA instructions per wave per chunk
+    static constexpr int BYTES = S * STAGE * 4;
+};
+
+// one operand image (ROWS rows x LBK k) per chunk: ROWS / 8 DMA instructions, wave w issues w,
+// w + 4, ...  The per-lane source offsets are set up once (LDma::init); a chunk adds a uniform
+// step and checks the K bound (the last chunk may be partial)
+template <int ROWS, bool KC>
+struct LDma {
+    static constexpr int NI = ROWS / 32;      // instructions per wave
+    int base[NI];                             // byte offset at chunk 0, or OOB (row out of range)
+    int kx[NI];                               // the lane's k within a chunk (its segment's first k)
+    __device__ __forceinline__ void init(int ld, int rows, int row0, int w, int lane) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int sl = 64 * (w + 4 * i) + lane;
+            if (KC) {
+                const int row = sl >> 3, seg = (sl & 7) ^ (row & 7);
+                const int gr = row0 + row;
+                base[i] = gr < rows ? (gr * ld + 4 * seg) * 4 : OOB;
+                kx[i] = 4 * seg;
+            } else {
+                const int k = sl / (ROWS / 4), seg = (sl % (ROWS / 4)) ^ (((k >> 2) & 1) << 2);
+                const int gr = row0 + 4 * seg;
+                base[i] = gr < rows ? (k * ld + gr) * 4 : OOB;
+                kx[i] = k;
+            }
+        }
+    }
+    __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t X, int ld, int K, int kc, float *img, int w) const {
+        const int step = KC ? kc * 4 : kc * ld * 4;        // uniform
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int off = (base[i] != OOB && kx[i] < K - kc) ? base[i] + step : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(X, (lds_vp)(img + 256 * (w + 4 * i)), 16, off, 0, 0, 0);
+        }
+    }
+};
+
+template <int ROWS, bool KC, int T>
+__device__ __forceinline__ void lds_frag(const float *img, int rbase, int h, int lr, int lk, float (&f)[T][4]) {
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+        const int row = rbase + 16 * i + lr;
+        if (KC) {
+            const int seg = 4 * h + lk;
+            const f4 v = *reinterpret_cast<const f4 *>(img + 4 * (row * 8 + (seg ^ (row & 7))));
+            f[i][0] = v.x;
+            f[i][1] = v.y;
+            f[i][2] = v.z;
+            f[i][3] = v.w;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int k = 16 * h + 4 * lk + t;
+                f[i][t] = img[4 * (k * (ROWS / 4) + ((row >> 2) ^ (((k >> 2) & 1) << 2))) + (row & 3)];
+            }
+        }
+    }
+}
+
+// s_waitcnt vmcnt(n) for a small run-time n (the immediate must be a constant)
+__device__ __forceinline__ void vm_wait(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    }
+}
+
+template <int TI, int TJ, bool AK, bool BKC>
+__device__ __forceinline__ void gemm_lds(const GProb &P, int local, float *smem) {
+    using L = LCfg<TI, TJ>;
+    constexpr int BM = L::BM, BN = L::BN, S = L::S, ST = L::STAGE, SA = BM * LBK;
+    static_assert((S - 2) * L::PW <= 12, "vm_wait range");
+    if (P.xcd) {
+        // XCD-aware order: workgroup b runs on XCD b % 8 (round-robin dispatch), so hand each XCD a
+        // contiguous range of tiles -- the column tiles of a row block then share that XCD's L2
+        // (bijective also when the count is not a multiple of 8)
+        const int n = P.tiles_n * ((P.M + BM - 1) / BM) * P.ks;
+        const int q = n / 8, r = n % 8, x = local % 8, o = local / 8;
+        local = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+    }
+    const int s = local % P.ks, tile = local / P.ks;
+    const int m0 = (tile / P.tiles_n) * BM, n0 = (tile % P.tiles_n) * BN;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int wm = (w >> 1) * 16 * TI, wn = (w & 1) * 16 * TJ;
+    const int nreal = P.N - P.ones;
+    const int nch = (P.K + LBK - 1) / LBK, per = (nch + P.ks - 1) / P.ks;
+    const int c0 = s * per, c1 = min(nch, c0 + per);
+    const __amdgpu_buffer_rsrc_t ra = brsrc_of(P.A), rb = brsrc_of(P.B);
+    const int one_col = (P.ones && nreal >= n0 && nreal < n0 + BN) ? nreal - n0 : -1;
+    LDma<BM, AK> da;
+    LDma<BN, BKC> db;
+    da.init(P.lda, P.M, m0, w, lane);
+    db.init(P.ldb, nreal, n0, w, lane);
+    auto issue = [&](int c) {
+        float *img = smem + ((c - c0) % S) * ST;
+        da.issue(ra, P.lda, P.K, c * LBK, img, w);
+        db.issue(rb, P.ldb, P.K, c * LBK, img + SA, w);
+    };
+    f4 acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < S - 1; ++q)
+        if (c0 + q < c1) issue(c0 + q);
+    for (int c = c0; c < c1; ++c) {
+        // this wave's DMAs of chunk c have landed (the younger ones may still fly), then every
+        // wave's have, and every wave is done with chunk c - 1, whose stage chunk c + S - 1 reuses
+        vm_wait(min(S - 2, c1 - 1 - c) * L::PW);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");      // no LDS access moves above the barrier
+        const float *cur = smem + ((c - c0) % S) * ST;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float fa[TI][4], fb[TJ][4];
+            lds_frag<BM, AK, TI>(cur, wm, h, lr, lk, fa);
+            lds_frag<BN, BKC, TJ>(cur + SA, wn, h, lr, lk, fb);
+            // the next DMA behind the first fragment reads (their latency covers its issue)
+            if (h == 0 && c + S - 1 < c1) issue(c + S - 1);
+            if (one_col >= 0) {
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) fb[j][t] = wn + 16 * j + lr == one_col ? 1.0f : fb[j][t];
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+        }
+    }
+    GSTAMP(2, __builtin_amdgcn_s_memtime());
+    // every wave is done reading the ring: the tile through LDS (rows of BN + 4 floats) for 16-B
+    // row segments in the epilogue
+    aacw::lds_barrier();
+    float *ct = smem;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ct[(wm + 16 * i + 4 * lk + r) * (BN + 4) + wn + 16 * j + lr] = acc[i][j][r];
+    aacw::lds_barrier();
+    float *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
+    float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
+#pragma unroll
+    for (int q = threadIdx.x; q < BM * BN / 4; q += 256) {
+        const int rr = q / (BN / 4), c4 = (q % (BN / 4)) * 4;
+        const f4 x = *reinterpret_cast<const f4 *>(ct + rr * (BN + 4) + c4);
+        const float v[4] = {x.x, x.y, x.z, x.w};
+        epilogue4(P, C, cx, m0 + rr, n0 + c4, v);
+    }
+}
+
+static_assert(LCfg<2, 2>::BYTES >= 64 * 68 * 4 && LCfg<2, 1>::BYTES >= 64 * 36 * 4 && LCfg<1, 2>::BYTES >= 32 * 68 * 4 &&
+                  LCfg<1, 1>::BYTES >= 32 * 36 * 4,
+              "the epilogue tile fits the ring");
+constexpr int REG_LDS_BYTES = 4 * 4 * 64 * 16 + 32 * 32 * 4;    // the register path's reduction buffers
+
+template <int TI, int TJ>
+__device__ __forceinline__ void gemm_lds_layout(const GProb &P, int local, float *smem, int lay) {
+    switch (lay) {
+        case 0: gemm_lds<TI, TJ, true, true>(P, local, smem); break;
+        case 1: gemm_lds<TI, TJ, true, false>(P, local, smem); break;
+        case 2: gemm_lds<TI, TJ, false, true>(P, local, smem); break;
+        default: gemm_lds<TI, TJ, false, false>(P, local, smem); break;
+    }
+}
+
+extern __shared__ float4 g_dyn_lds[];
+
+template <int DEPTH, bool LDST>
 __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
-    __shared__ f4 red[4][4][64];       // [wave][block of the round][lane]
-    __shared__ float tile[32 * 32];    // the reduced 32x32 tile, row-major, for 16-B stores
+    // LDST: the launch holds LDS-tile products: ONE dynamic LDS array (sized for the launch's largest
+    // ring; a second __shared__ object would make the compiler drain the DMAs before every ds_read),
+    // the register path's buffers alias it
+    __shared__ float4 smem_static[LDST ? 1 : REG_LDS_BYTES / 16];
+    float *smem = reinterpret_cast<float *>(LDST ? g_dyn_lds : smem_static);
+    f4 (*red)[4][64] = reinterpret_cast<f4 (*)[4][64]>(smem);     // [wave][block of the round][lane]
+    float *tile = smem + 4 * 4 * 64 * 4;                             // the reduced 32x32 tile
 #ifdef AAC_DBG_EMPTY                   // timing probes only: the launch floor of this grid
     if (g.n > 0) return;
 #endif
@@ -407,8 +636,19 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     int pi = 0;
 #pragma unroll
     for (int k = 1; k < AAC_GEMM_MAX; ++k) pi += wg >= g.wb[k] ? 1 : 0;
-    const GProb &P = g.p[pi];
-    gemm_tile<2, DEPTH>(P, wg - P.w_begin, red, tile);
+    if (LDST && g.p[pi].lds) {
+        const GProb P = g.p[pi];       // by value: a reference would make the compiler copy g to scratch
+        const int cfg = P.lds - 1, lay = cfg & 3;
+        switch (cfg >> 2) {      // (TI, TJ): 64x64, 64x32, 32x64, 32x32 workgroup tiles
+            case 0: gemm_lds_layout<2, 2>(P, wg - P.w_begin, smem, lay); break;
+            case 1: gemm_lds_layout<2, 1>(P, wg - P.w_begin, smem, lay); break;
+            case 2: gemm_lds_layout<1, 2>(P, wg - P.w_begin, smem, lay); break;
+            default: gemm_lds_layout<1, 1>(P, wg - P.w_begin, smem, lay); break;
+        }
+    } else {
+        const GProb &P = g.p[pi];
+        gemm_tile<2, DEPTH>(P, wg - P.w_begin, red, tile);
+    }
     GSTAMP(3, __builtin_amdgcn_s_memtime());
     GSTAMP(4, __builtin_amdgcn_s_memrealtime());
 }
@@ -1341,6 +1581,12 @@ const int g_wide_kch = env_int("AAC_GEMM_WIDE_KCH", 0);
 const int g_wide_kch_tiles = env_int("AAC_GEMM_WIDE_KCH_TILES", 512);
 const int g_lw = env_int("AAC_GEMM_LW", 1);                  // row-contiguous operands by 4T-B loads
 const int g_vec = env_int("AAC_GEMM_VEC", 1);                // 16-B epilogue rows
+const int g_lds = env_int("AAC_GEMM_LDS", 1);                // LDS-staged workgroup tiles
+const int g_lds_min_k = env_int("AAC_GEMM_LDS_MIN_K", 64);   // ... for products with K >= this
+int g_lds_min_wg = env_int("AAC_GEMM_LDS_MIN_WG", 512);  // tile choice: largest tile with this many workgroups
+const long g_lds_min_mn = env_int("AAC_GEMM_LDS_MIN_MN", 64 * 64);
+int g_lds_small = env_int("AAC_GEMM_LDS_SMALL", 0);         // allow 32x32 LDS workgroup tiles
+const int g_xcd = env_int("AAC_GEMM_XCD", 0);                // XCD-aware order of the LDS tiles
 int g_dump = env_int("AAC_GEMM_DUMP", 0);      // print the plans of the first g_dump launches
 
 int plan(const aac_gemm_prob *in, int n, GBatch &g) {
@@ -1398,6 +1644,45 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         }
         d.w_begin = waves;          // in workgroups
         g.wb[i] = waves;
+        // LDS-staged workgroup tiles where both operands load as 16-B segments
+        const bool a16 = s.lda % 4 == 0 && aligned16(s.A) && (s.ta ? s.M % 4 == 0 : s.K % 4 == 0);
+        const bool b16 = s.ldb % 4 == 0 && aligned16(s.B) && (s.tb ? (s.K % 4 == 0 && !s.ones) : (s.N - s.ones) % 4 == 0);
+        d.lds = 0;
+        int pick = -1;
+        // candidates, largest first; 32x64 before 64x32 on every learner shape (tools/mb_lds.py:
+        // 5120x256x640 25.5 vs 27.1 us); forced tiles (g_lds_min_wg < 0) index cand_force
+        static const int cand_pref[4][2] = {{2, 2}, {1, 2}, {2, 1}, {1, 1}};
+        static const int cand_force[4][2] = {{2, 2}, {2, 1}, {1, 2}, {1, 1}};
+        const int(*cand)[2] = cand_pref;
+        if (g_lds && a16 && b16 && s.K >= g_lds_min_k && (long)s.M * s.N >= g_lds_min_mn && s.M >= 32 &&
+            s.N - s.ones >= 32) {
+            // 32x32 workgroup tiles re-read the operands 2x more than 64-wide ones and lose to the
+            // register path's split-K waves on these shapes (tools/mb_lds.py): only with the knob
+            // g_lds_min_wg < 0 forces tile -1 - g_lds_min_wg of cand_tall (tests)
+            if (g_lds_min_wg < 0) cand = cand_force;
+            for (int c = 0; c < (g_lds_min_wg < 0 ? 0 : (g_lds_small ? 4 : 3)); ++c) {
+                const long nt = (long)((s.M + 32 * cand[c][0] - 1) / (32 * cand[c][0])) *
+                                ((s.N + 32 * cand[c][1] - 1) / (32 * cand[c][1])) * ks;
+                if (nt >= g_lds_min_wg) {
+                    pick = c;
+                    break;
+                }
+            }
+            if (pick < 0 && g_lds_small) pick = 3;
+            if (g_lds_min_wg < 0) pick = std::min(3, -1 - g_lds_min_wg);
+        }
+        if (pick >= 0) {
+            const int TI = cand[pick][0], TJ = cand[pick][1];
+            const int cfg = (TI == 2 && TJ == 2) ? 0 : (TI == 2 ? 1 : (TJ == 2 ? 2 : 3));
+            const int lay = (s.ta ? 2 : 0) + (s.tb ? 0 : 1);       // bit 1: A row-contiguous, bit 0: B row-contiguous
+            d.lds = 1 + cfg * 4 + lay;
+            d.xcd = g_xcd;
+            d.wide = 0;
+            d.deep = 0;
+            d.tiles_n = (s.N + 32 * TJ - 1) / (32 * TJ);
+            waves += ((s.M + 32 * TI - 1) / (32 * TI)) * d.tiles_n * ks;
+            continue;
+        }
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
     }
     g.waves = waves;
@@ -1407,8 +1692,8 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         fprintf(stderr, "gemm_batch n=%d wg=%d\n", n, waves);
         for (int i = 0; i < n; ++i) {
             const GProb &d = g.p[i];
-            fprintf(stderr, "  M=%d N=%d K=%d ta=%d tb=%d ones=%d ks=%d amode=%d bmode=%d wide=%d deep=%d act=%d mact=%d add=%d\n",
-                    d.M, d.N, d.K, d.ta, d.tb, d.ones, d.ks, d.amode, d.bmode, d.wide, d.deep, d.act, d.mact,
+            fprintf(stderr, "  M=%d N=%d K=%d ta=%d tb=%d ones=%d ks=%d amode=%d bmode=%d wide=%d deep=%d lds=%d act=%d mact=%d add=%d\n",
+                    d.M, d.N, d.K, d.ta, d.tb, d.ones, d.ks, d.amode, d.bmode, d.wide, d.deep, d.lds, d.act, d.mact,
                     d.addend != nullptr);
         }
     }
@@ -1435,15 +1720,41 @@ int aac_gemm_stamps(unsigned long long *out, int32_t n_wg) {
 #endif
 }
 
+void aac_gemm_set_lds_policy(int32_t min_workgroups, int32_t small_tiles) {
+    g_lds_min_wg = min_workgroups;
+    g_lds_small = small_tiles;
+}
+
+int aac_gemm_plan(const aac_gemm_prob *probs, int32_t n, int32_t *lds_cfg, int32_t *workgroups) {
+    GBatch g{};
+    if (plan(probs, n, g)) return -1;
+    for (int i = 0; i < g.n; ++i) lds_cfg[i] = g.p[i].lds;
+    if (workgroups) *workgroups = g.waves;
+    return 0;
+}
+
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
     GBatch g{};
     if (plan(probs, n, g)) return -1;
-    bool deep = false;
-    for (int i = 0; i < g.n; ++i) deep |= g.p[i].deep != 0;
+    bool deep = false, lds = false;
+    for (int i = 0; i < g.n; ++i) {
+        deep |= g.p[i].deep != 0;
+        lds |= g.p[i].lds != 0;
+    }
     const dim3 grid(g.waves), block(256);
     hipStream_t st = (hipStream_t)stream;
-    if (deep && g_depth == 2) hipLaunchKernelGGL(gemm_kernel<2>, grid, block, 0, st, g);
-    else hipLaunchKernelGGL(gemm_kernel<1>, grid, block, 0, st, g);
+    if (lds) {
+        // the launch's LDS: the largest ring among its LDS-tile products (>= the register path's buffers)
+        static const int ring_bytes[4] = {LCfg<2, 2>::BYTES, LCfg<2, 1>::BYTES, LCfg<1, 2>::BYTES, LCfg<1, 1>::BYTES};
+        size_t bytes = REG_LDS_BYTES;
+        for (int i = 0; i < g.n; ++i)
+            if (g.p[i].lds) bytes = std::max(bytes, (size_t)ring_bytes[(g.p[i].lds - 1) >> 2]);
+        if (deep && g_depth == 2) hipLaunchKernelGGL((gemm_kernel<2, true>), grid, block, bytes, st, g);
+        else hipLaunchKernelGGL((gemm_kernel<1, true>), grid, block, bytes, st, g);
+    } else {
+        if (deep && g_depth == 2) hipLaunchKernelGGL((gemm_kernel<2, false>), grid, block, 0, st, g);
+        else hipLaunchKernelGGL((gemm_kernel<1, false>), grid, block, 0, st, g);
+    }
     FHIP(hipGetLastError());
     return 0;
 }

@@ -53,6 +53,8 @@ def lib():
         L = _native.lib()
         L.aac_fused_last_error.restype = ctypes.c_char_p
         L.aac_gemm_batch.argtypes = [ctypes.POINTER(GemmProb), i32, vp]
+        L.aac_gemm_plan.argtypes = [ctypes.POINTER(GemmProb), i32, vp, vp]
+        L.aac_gemm_set_lds_policy.argtypes = [i32, i32]
         L.aac_adam_flat_sum.argtypes = [vp, vp, i32, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         L.aac_sum_partials.argtypes = [vp, vp, i32, i64, vp]
         L.aac_critic_head.argtypes = [vp, i32, i32, vp, vp, i32, vp, vp, vp, i32, i32, f32, vp, vp, vp, vp, vp]
@@ -110,6 +112,18 @@ class GemmLaunch:
 
     def __call__(self):
         _chk(lib().aac_gemm_batch(self.arr, self.n, _stream()), "aac_gemm_batch")
+
+    def plan(self):
+        """(per-product tile mode: 0 register fragments / 1 + cfg LDS workgroup tile, grid size)."""
+        cfg = (ctypes.c_int32 * self.n)()
+        wg = ctypes.c_int32()
+        _chk(lib().aac_gemm_plan(self.arr, self.n, cfg, ctypes.byref(wg)), "aac_gemm_plan")
+        return list(cfg), wg.value
+
+
+def set_lds_policy(min_workgroups=512, small_tiles=False):
+    """Tile policy of the plans built from now on (include/aac_fused.h aac_gemm_set_lds_policy)."""
+    lib().aac_gemm_set_lds_policy(int(min_workgroups), int(bool(small_tiles)))
 
 
 def gemm_launches(probs):

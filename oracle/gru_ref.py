@@ -106,11 +106,12 @@ def ref_gru_act(actors, own, radar, h, d_own):
     return torch.stack(outs, 1), torch.stack(hs, 1)
 
 
-def random_gru_transitions(E, N, seed, H=64):
+def random_gru_transitions(E, N, seed, H=64, D0=None):
     """Synthetic transitions of the GRU learner: the ATT env's fields plus the actor hidden
-    states before (h_cur) and after (h_next) the step."""
+    states before (h_cur) and after (h_next) the step.  D0: own-row width (default the ATT env's
+    6 + 4 (N - 1); 6 for the WGRU env variant)."""
     g = torch.Generator().manual_seed(seed)
-    D0, K = 6 + 4 * (N - 1), N - 1
+    D0, K = D0 or 6 + 4 * (N - 1), N - 1
 
     def r(*s):
         return torch.randn(*s, generator=g)

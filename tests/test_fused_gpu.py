@@ -29,11 +29,32 @@ CASES = [  # M, N, K, ta, tb, ones, act, mact, addend
     (25600, 256, 192, 0, 1, 0, 1, 0, True),      # >= 2048 tiles: one tile per wave (wide), 16-B epilogue
     (20480, 130, 64, 0, 1, 0, 2, 1, False),      # wide, unaligned rows: element-wise epilogue
     (20480, 100, 64, 0, 1, 0, 1, 0, True),       # wide, 16-B rows with a ragged last column group
+    # LDS-staged workgroup tiles, every operand layout, ragged edges, the ones column
+    (256, 640, 1024, 1, 0, 1, 0, 0, False),      # weight gradient: A and B row-contiguous, ones column
+    (96, 100, 100, 1, 1, 0, 1, 0, True),         # A row-contiguous, B K-contiguous, ragged K chunk
+    (200, 132, 68, 1, 0, 0, 2, 2, True),
+    (1000, 36, 260, 0, 0, 0, 1, 1, True),        # ragged rows
+    (256, 300, 64, 0, 1, 0, 0, 0, False),
+    (192, 64, 96, 1, 1, 0, 1, 0, True),
+    (32, 200, 128, 0, 0, 0, 0, 1, False),
+    (5120, 256, 640, 0, 1, 0, 1, 0, True),
 ]
+LDS_CASES = {(1024, 640, 256), (5120, 64, 64), (25600, 256, 192), (20480, 130, 64), (20480, 100, 64), (256, 640, 1024),
+             (96, 100, 100), (200, 132, 68), (1000, 36, 260), (5120, 256, 640), (130, 70, 300),
+             (256, 300, 64), (192, 64, 96), (32, 200, 128)}
+
+
+@pytest.fixture(params=[0, 1, 2, 3], ids=["t64x64", "t64x32", "t32x64", "t32x32"])
+def lds_everywhere(request):
+    """Every eligible product on the given LDS workgroup tile, whatever its size."""
+    from multi_agent_aac_amd import fused
+    fused.set_lds_policy(-1 - request.param)
+    yield request.param
+    fused.set_lds_policy()
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_gemm_batch_epilogues(native_lib, case):
+def test_gemm_batch_epilogues(native_lib, lds_everywhere, case):
     from multi_agent_aac_amd import fused
     M, N, K, ta, tb, ones, act, mact, add = case
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
@@ -49,6 +70,9 @@ def test_gemm_batch_epilogues(native_lib, case):
                    bias=fused.ptr(bias), act=act, addend=fused.ptr(addend), ldadd=N, mask=fused.ptr(mask), ldmask=N,
                    mact=mact, ones=ones, cextra=fused.ptr(cextra))
     launch = fused.GemmLaunch([p])
+    cfg = launch.plan()[0][0]
+    assert (cfg > 0) == ((M, N, K) in LDS_CASES), launch.plan()
+    assert cfg == 0 or (cfg - 1) >> 2 == lds_everywhere
     launch()
     prod = _op(A.double(), ta) @ _op(B.double(), tb)
     want = prod.clone()
@@ -92,17 +116,21 @@ def test_gemm_batch_grouped(native_lib):
                                    rtol=1e-5)
 
 
-def test_gemm_split_copies(native_lib):
-    """ksplit > 1 writes per-split partial products that sum to the full product."""
+@pytest.mark.parametrize("N", [23, 64])
+def test_gemm_split_copies(native_lib, lds_everywhere, N):
+    """ksplit > 1 writes per-split partial products that sum to the full product (N = 64: the LDS
+    workgroup tile, whose B image carries the ones column)."""
     from multi_agent_aac_amd import fused
     torch.manual_seed(1)
-    M, N, K, S = 64, 23, 5120, 16
+    M, K, S = 64, 5120, 16
     G = torch.randn(K, M, device=DEV)          # stored rows x outputs, op(A) = G^T
     X = torch.randn(K, N, device=DEV)
     stride = M * N + M + 7
     part = torch.full((S, stride), 3.0, device=DEV)
-    fused.GemmLaunch([fused.prob(fused.ptr(G), fused.ptr(X), fused.ptr(part), M, N, K, M, N, N, ta=1, ones=1,
-                                 cextra=fused.ptr(part, M * N), ksplit=S, split_stride=stride)])()
+    launch = fused.GemmLaunch([fused.prob(fused.ptr(G), fused.ptr(X), fused.ptr(part), M, N, K, M, N, N, ta=1, ones=1,
+                                          cextra=fused.ptr(part, M * N), ksplit=S, split_stride=stride)])
+    assert (launch.plan()[0][0] > 0) == (N % 4 == 0)
+    launch()
     tot = part.double().sum(0)
     np.testing.assert_allclose(tot[:M * N].reshape(M, N).cpu(), (G.double().t() @ X.double()).cpu(), atol=2e-4)
     np.testing.assert_allclose(tot[M * N:M * N + M].cpu(), G.double().sum(0).cpu(), atol=2e-4)

@@ -90,9 +90,10 @@ def test_gru_cell_modes(native_lib, mode):
     np.testing.assert_allclose(hout.cpu().double(), hp.detach(), atol=2e-6)
 
 
-def _model(N, B, E, seed=0, d_own=6):
+def _model(N, B, E, seed=0, d_own=6, own_width=None):
     from multi_agent_aac_amd.gru import MADDPG
-    m = MADDPG([d_own, 18, 6], [d_own, 18, 6], 2, 64, 10, n_agents=N, device=DEV, seed=seed, batch_size=B)
+    m = MADDPG([d_own, 18, 6], [d_own, 18, 6], 2, 64, 10, n_agents=N, device=DEV, seed=seed, batch_size=B,
+               own_width=own_width)
     rep = m.attach_replay(4 * E, seed=seed + 3)
     return m, rep
 
@@ -111,14 +112,16 @@ def _ref_nets(m):
 KEYS = ("s_own", "s_radar", "s_nei", "act", "rew", "done", "n_own", "n_radar", "n_nei", "h_cur", "h_next")
 
 
-@pytest.mark.parametrize("N,B", [(3, 64), (8, 256)])
-def test_gru_update_matches_cpu_restatement(native_lib, N, B):
+@pytest.mark.parametrize("N,B,own_width", [(3, 64, None), (8, 256, None), (8, 256, 6)])
+def test_gru_update_matches_cpu_restatement(native_lib, N, B, own_width):
+    """own_width 6: the replay rows of the WGRU env variant (config 4, 6-wide own observation)."""
     E = 96
-    m, rep = _model(N, B, E, seed=N)
+    m, rep = _model(N, B, E, seed=N, own_width=own_width)
+    assert m.D0 == (own_width or 6 + 4 * (N - 1))
     actors, critics, actors_t, critics_t = _ref_nets(m)
     host = {k: [] for k in KEYS}
     for p in range(3):
-        tr = gru_ref.random_gru_transitions(E, N, 10 * N + p)
+        tr = gru_ref.random_gru_transitions(E, N, 10 * N + p, D0=own_width)
         rep.push_batch(*[tr[k].to(DEV).contiguous() for k in KEYS])
         for k in KEYS:
             host[k].append(tr[k])

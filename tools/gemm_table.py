@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--model", default="att")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--split", action="store_true", help="also time each product of a launch alone")
     a = ap.parse_args()
     from multi_agent_aac_amd.fused import GemmLaunch
     N, B = a.agents, a.batch
@@ -49,9 +50,8 @@ def main():
     torch.cuda.synchronize()
     tot_t, tot_f = 0.0, 0.0
     rows = []
-    for k, op in enumerate(ops):
-        if not isinstance(op, GemmLaunch):
-            continue
+
+    def timed(op):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         op()
         g = torch.cuda.CUDAGraph()        # device time, no host launch cost (as in the bench's replay)
@@ -64,12 +64,25 @@ def main():
         g.replay()
         e1.record()
         torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / a.reps * 1e3
-        shapes = " ".join(f"{p.M}x{p.N - p.ones}{'+1' if p.ones else ''}x{p.K}{'/' + str(p.ksplit) if p.ksplit > 1 else ''}"
-                          f"{'T' if p.ta else ''}{'t' if p.tb else ''}" for p in op.arr)
-        rows.append((us, op.flops, k, shapes))
+        return e0.elapsed_time(e1) / a.reps * 1e3
+
+    def shape(p, cfg):
+        mode = "" if not cfg else f"[L{(cfg - 1) >> 2}{(cfg - 1) & 3}]"
+        return (f"{p.M}x{p.N - p.ones}{'+1' if p.ones else ''}x{p.K}{'/' + str(p.ksplit) if p.ksplit > 1 else ''}"
+                f"{'T' if p.ta else ''}{'t' if p.tb else ''}{mode}")
+    for k, op in enumerate(ops):
+        if not isinstance(op, GemmLaunch):
+            continue
+        us = timed(op)
+        cfgs, wg = op.plan()
+        shapes = " ".join(shape(p, c) for p, c in zip(op.arr, cfgs))
+        rows.append((us, op.flops, k, shapes + f"  ({wg} wg)"))
         tot_t += us
         tot_f += op.flops
+        if a.split and op.n > 1:
+            for p in op.arr:
+                one = GemmLaunch([p])
+                print(f"      {k:3d} alone {timed(one):7.1f} us {one.flops / 1e9:6.3f} GF  {shape(p, one.plan()[0][0])}")
     for us, fl, k, shapes in rows:
         print(f"{k:3d} {us:7.1f} us {fl / 1e9:6.3f} GF {fl / us / 1e6:6.1f} TF/s  {shapes}")
     print(f"total {tot_t:.1f} us over {len(rows)} launches, {tot_f / 1e9:.2f} GF, {tot_f / tot_t / 1e6:.1f} TF/s")
