@@ -77,41 +77,43 @@ def update_flops(N, D0, B):
     return 2.0 * (4 * A + 7 * C) * B * N
 
 
-def run_timed(ops):
-    """Run a launch list eagerly with a HIP event pair around every grouped-GEMM launch (on the
-    launching stream); [(algorithmic FLOPs, event pair)]."""
-    from multi_agent_aac_amd.fused import GemmLaunch
-    rec = []
-    for op in ops:
-        if isinstance(op, GemmLaunch):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            op()
-            e1.record()
-            rec.append((op.flops, e0, e1))
-        else:
-            op()
-    return rec
-
-
-def gemm_roofline(model, B, updates=4):
+def gemm_roofline(model, B, reps=10):
     """Roofline of the dominant kernel, the grouped fp32 MFMA GEMM (gemm_kernel) of the fused
-    learner: algorithmic FLOPs of each launch / its HIP-event duration, over ``updates`` eager
-    update_myown-equivalents run right after the timed region (same launches as the captured
-    graph; the rocprof kernel stats under profiles/ give the same per-launch durations)."""
+    learner, after the timed region: one eager update_myown-equivalent, then every grouped-GEMM
+    launch of it replayed ``reps`` times back to back from a captured HIP graph between a HIP event
+    pair on the replay stream -- the launch's device duration without host launch gaps, as the
+    rocprof kernel trace reports it (profiles/).  achieved = algorithmic FLOPs of the launches /
+    the sum of their durations."""
+    from multi_agent_aac_amd.fused import GemmLaunch
     fu = model._fused_plan(B) if hasattr(model, "_fused_plan") else model._plan(B)
-    rec = []
-    for _ in range(updates):
-        rec += run_timed(fu.ops())
+    ops = fu.ops()
+    for op in ops:
+        op()
     torch.cuda.synchronize()
-    flops = sum(r[0] for r in rec)
-    ms = sum(r[1].elapsed_time(r[2]) for r in rec)
-    n = len(rec)
-    achieved = flops / (ms * 1e-3) / 1e12
+    flops, us = 0.0, 0.0
+    n = 0
+    for op in ops:
+        if not isinstance(op, GemmLaunch):
+            continue
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                op()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        us += e0.elapsed_time(e1) / reps * 1e3
+        flops += op.flops
+        n += 1
+    achieved = flops / (us * 1e-6) / 1e12
     return {"kernel": "gemm_kernel (grouped fp32 MFMA GEMM of the fused learner)", "bound": "mfma",
             "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-            "flop_per_launch": flops / n, "avg_launch_ms": ms / n, "launches_per_update": n // updates,
-            "gemm_ms_per_update": ms / updates}
+            "flop_per_launch": flops / n, "avg_launch_ms": us / n / 1e3, "launches_per_update": n,
+            "gemm_ms_per_update": us / 1e3, "timing": f"graph replay x{reps} per launch, HIP events"}
 
 
 def parse():
@@ -225,13 +227,47 @@ class Trainer:
             gru.reset_hidden(self.h, n.env_done)     # a new episode starts from zeros (WGRU/ma_main:476-478)
         else:
             self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
-        self.env.auto_reset(n.env_done, out=n)
         self.cur, self.nxt = n, c
-        if update and len(self.replay) > self.B:
+        run_update = update and len(self.replay) > self.B
+        # the auto-reset writes env state and the next observation rows, which the update never reads:
+        # it runs on a side stream beside the update (the next act waits for both)
+        with side_stream(self, run_update):
+            self.env.auto_reset(n.env_done, out=n)
+        if run_update:
             self.model.update(self.B, use_graph=not NO_GRAPH, want_stats=False)
+        join_side(self)
 
 
 NO_GRAPH = False
+OVERLAP_RESET = os.environ.get("AAC_OVERLAP_RESET", "0") == "1"   # measured slower: 1.241 vs 1.164 ms
+
+
+class side_stream:
+    """Run the block on the trainer's side stream, ordered after the main stream's work so far (a
+    no-op context when off)."""
+
+    def __init__(self, tr, on):
+        self.tr, self.on = tr, on and OVERLAP_RESET
+
+    def __enter__(self):
+        if not self.on:
+            return
+        if getattr(self.tr, "_side", None) is None:
+            self.tr._side = torch.cuda.Stream()
+        self.tr._side.wait_stream(torch.cuda.current_stream())
+        self._ctx = torch.cuda.stream(self.tr._side)
+        self._ctx.__enter__()
+        self.tr._side_used = True
+
+    def __exit__(self, *a):
+        if self.on:
+            self._ctx.__exit__(*a)
+
+
+def join_side(tr):
+    if getattr(tr, "_side_used", False):
+        torch.cuda.current_stream().wait_stream(tr._side)
+        tr._side_used = False
 
 
 class UamTrainer:
@@ -267,10 +303,13 @@ class UamTrainer:
             ev1.record()
             self.env_events.append((ev0, ev1))
         self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
-        self.env.auto_reset(n.env_done, out=n)
         self.cur, self.nxt = n, c
-        if update and len(self.replay) > self.B:
+        run_update = update and len(self.replay) > self.B
+        with side_stream(self, run_update):
+            self.env.auto_reset(n.env_done, out=n)
+        if run_update:
             self.model.update(self.B, use_graph=not NO_GRAPH)
+        join_side(self)
 
 
 def cpu_baseline_uam(E, N, B, seconds):

@@ -78,9 +78,15 @@ int aac_gemm_stamps(unsigned long long *out, int32_t n_wg);
 int aac_adam_flat_sum(float *param, const float *gpart, int32_t nsplit, float *grad_out, float *exp_avg,
                       float *exp_avg_sq, int64_t n, float lr, float beta1, float beta2, float eps,
                       const int32_t *step, int32_t step_add, void *stream);
+/* The same with the partial copies gstride floats apart (>= n; the learners pad it to a multiple of
+ * 4 so that the copy-parallel kernel's 16-B loads stay aligned). */
+int aac_adam_flat_sum_strided(float *p, const float *gpart, int32_t ns, int64_t gstride, float *gout, float *m,
+                              float *v, int64_t n, float lr, float b1, float b2, float eps, const int32_t *step,
+                              int32_t step_add, void *stream);
 
 /* out[i] = sum_{s < nsplit} gpart[s*n + i] in split order (before a gradient all-reduce). */
 int aac_sum_partials(float *out, const float *gpart, int32_t nsplit, int64_t n, void *stream);
+int aac_sum_partials_strided(float *out, const float *gpart, int32_t nsplit, int64_t gstride, int64_t n, void *stream);
 
 /* Critic output layer + loss gradient, rows of 256 features h[r*ldh + j]:
  *   q[r] = h[r] . w + b[0]

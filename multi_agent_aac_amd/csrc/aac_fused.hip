@@ -671,8 +671,8 @@ __device__ __forceinline__ float sum_copies(const float *__restrict__ gpart, int
     return gi;
 }
 
-__global__ void adam_sum_kernel(float *p, const float *__restrict__ gpart, int ns, float *gout, float *m, float *v,
-                                int64_t n, float lr, float b1, float b2, float eps, const int32_t *step, int step_add) {
+__global__ void adam_sum_kernel(float *p, const float *__restrict__ gpart, int ns, int64_t gs, float *gout, float *m,
+                                float *v, int64_t n, float lr, float b1, float b2, float eps, const int32_t *step, int step_add) {
     const int t = *step + step_add;
     const double bc1 = 1.0 - pow((double)b1, (double)t);
     const double bc2 = 1.0 - pow((double)b2, (double)t);
@@ -680,7 +680,7 @@ __global__ void adam_sum_kernel(float *p, const float *__restrict__ gpart, int n
     const float bc2s = (float)sqrt(bc2);
     const float w1 = (float)(1.0 - (double)b1), w2 = (float)(1.0 - (double)b2);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = sum_copies(gpart, ns, n, i);
+        const float gi = sum_copies(gpart, ns, gs, i);
         if (gout) gout[i] = gi;
         float mi = m[i];
         mi = mi + w1 * (gi - mi);               // exp_avg.lerp_(grad, 1 - beta1)
@@ -693,9 +693,86 @@ __global__ void adam_sum_kernel(float *p, const float *__restrict__ gpart, int n
     }
 }
 
-__global__ void sum_partials_kernel(float *out, const float *__restrict__ gpart, int ns, int64_t n) {
+// Copy-parallel form (copy stride gs % 4 == 0 -- the learners pad it -- and 16-B aligned copies): a
+// wave takes 64 consecutive elements; lane
+// (g = lane / 16, e4 = lane % 16) sums copies g, g + 4, g + 8, ... of elements 4 e4 .. 4 e4 + 3 with
+// 16-B loads (each copy's 64 elements are one 256-B line; up to eight loads in flight per lane), the
+// four copy groups combine in a fixed order ((g0 + g1) + (g2 + g3)) -- deterministic -- and lane
+// (g, e4) updates element 4 e4 + g.  The split-K copies of one network are 8-32 x its size, so this
+// kernel is bound by how many of their loads are in flight (2048 x 256 threads vs one element per
+// thread and a dependent batch chain in adam_sum_kernel)
+// the four-group copy sum of adam_sum4_kernel / sum_partials4_kernel (one order for both, so a
+// world > 1 update -- sum, all-reduce, Adam on the sum -- is bit-equal to one rank's fused step)
+__device__ __forceinline__ f4 copy_sum4(const float *__restrict__ gpart, int ns, int64_t gs, int64_t ii, int g) {
+    f4 acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int s0 = g; s0 < ns; s0 += 32) {
+        // unconditional loads (clamped copy index), selected afterwards: a select around each
+        // load would make the compiler branch and drain per load
+        f4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int sc = s0 + 4 * u;
+            x[u] = *reinterpret_cast<const f4 *>(gpart + (int64_t)(sc < ns ? sc : 0) * gs + ii);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (s0 + 4 * u < ns) acc += x[u];
+    }
+#pragma unroll
+    for (int d = 16; d <= 32; d <<= 1) {
+        acc.x += __shfl_xor(acc.x, d, 64);
+        acc.y += __shfl_xor(acc.y, d, 64);
+        acc.z += __shfl_xor(acc.z, d, 64);
+        acc.w += __shfl_xor(acc.w, d, 64);
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(256) adam_sum4_kernel(float *p, const float *__restrict__ gpart, int ns, int64_t gs,
+                                                        float *gout, float *m, float *v, int64_t n, float lr, float b1,
+                                                        float b2, float eps, const int32_t *step, int step_add) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, e4 = lane & 15;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (int64_t)gridDim.x * 4;
+    const int t = *step + step_add;
+    const double bc1 = 1.0 - pow((double)b1, (double)t);
+    const double bc2 = 1.0 - pow((double)b2, (double)t);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - (double)b1), w2 = (float)(1.0 - (double)b2);
+    for (int64_t base = wave * 64; base < n; base += nwaves * 64) {
+        const int64_t i = base + 4 * e4;
+        const f4 acc = copy_sum4(gpart, ns, gs, i < n ? i : 0, g);
+        const int64_t k = i + g;
+        if (k < n) {
+            const float gi = g == 0 ? acc.x : (g == 1 ? acc.y : (g == 2 ? acc.z : acc.w));
+            if (gout) gout[k] = gi;
+            float mi = m[k];
+            mi = mi + w1 * (gi - mi);
+            float vi = v[k] * b2;
+            vi = vi + w2 * (gi * gi);
+            const float den = sqrtf(vi) / bc2s + eps;
+            p[k] = p[k] + (-step_size) * (mi / den);
+            m[k] = mi;
+            v[k] = vi;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) sum_partials4_kernel(float *out, const float *__restrict__ gpart, int ns,
+                                                            int64_t gs, int64_t n) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, e4 = lane & 15;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (int64_t)gridDim.x * 4;
+    for (int64_t base = wave * 64; base < n; base += nwaves * 64) {
+        const int64_t i = base + 4 * e4;
+        const f4 acc = copy_sum4(gpart, ns, gs, i < n ? i : 0, g);
+        const int64_t k = i + g;
+        if (k < n) out[k] = g == 0 ? acc.x : (g == 1 ? acc.y : (g == 2 ? acc.z : acc.w));
+    }
+}
+
+__global__ void sum_partials_kernel(float *out, const float *__restrict__ gpart, int ns, int64_t gs, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = sum_copies(gpart, ns, n, i);
+        out[i] = sum_copies(gpart, ns, gs, i);
 }
 
 // ------------------------------------------------------------------------------ critic head
@@ -1587,6 +1664,7 @@ int g_lds_min_wg = env_int("AAC_GEMM_LDS_MIN_WG", 512);  // tile choice: largest
 const long g_lds_min_mn = env_int("AAC_GEMM_LDS_MIN_MN", 64 * 64);
 int g_lds_small = env_int("AAC_GEMM_LDS_SMALL", 0);         // allow 32x32 LDS workgroup tiles
 const int g_xcd = env_int("AAC_GEMM_XCD", 0);                // XCD-aware order of the LDS tiles
+const int g_adam4 = env_int("AAC_ADAM4", 1);                 // copy-parallel Adam over split-K copies
 int g_dump = env_int("AAC_GEMM_DUMP", 0);      // print the plans of the first g_dump launches
 
 int plan(const aac_gemm_prob *in, int n, GBatch &g) {
@@ -1764,18 +1842,48 @@ static int grid_for(int64_t n) {
     return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
 }
 
+// the copy-parallel sum (adam_sum4_kernel, sum_partials4_kernel) when the copies allow 16-B loads;
+// both entry points pick by the same rule, so their sums are the same bits
+static bool use_sum4(const float *gpart, int ns, int64_t gstride) {
+    return g_adam4 && gstride % 4 == 0 && aligned16(gpart) && ns > 1;
+}
+
+static int sum4_grid(int64_t n) { return (int)std::min<int64_t>(((n + 63) / 64 + 3) / 4, 8192); }
+
 int aac_adam_flat_sum(float *p, const float *gpart, int32_t ns, float *gout, float *m, float *v, int64_t n, float lr,
                       float b1, float b2, float eps, const int32_t *step, int32_t step_add, void *stream) {
+    return aac_adam_flat_sum_strided(p, gpart, ns, n, gout, m, v, n, lr, b1, b2, eps, step, step_add, stream);
+}
+
+int aac_adam_flat_sum_strided(float *p, const float *gpart, int32_t ns, int64_t gstride, float *gout, float *m, float *v,
+                              int64_t n, float lr, float b1, float b2, float eps, const int32_t *step, int32_t step_add,
+                              void *stream) {
     if (ns < 1) return ffail("adam_flat_sum: nsplit >= 1");
-    hipLaunchKernelGGL(adam_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, gpart, ns, gout, m,
-                       v, n, lr, b1, b2, eps, step, step_add);
+    if (gstride < n) return ffail("adam_flat_sum: copy stride < n");
+    if (use_sum4(gpart, ns, gstride)) {
+        hipLaunchKernelGGL(adam_sum4_kernel, dim3(sum4_grid(n)), dim3(256), 0, (hipStream_t)stream, p, gpart, ns, gstride,
+                           gout, m, v, n, lr, b1, b2, eps, step, step_add);
+    } else {
+        hipLaunchKernelGGL(adam_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, gpart, ns, gstride, gout,
+                           m, v, n, lr, b1, b2, eps, step, step_add);
+    }
     FHIP(hipGetLastError());
     return 0;
 }
 
 int aac_sum_partials(float *out, const float *gpart, int32_t ns, int64_t n, void *stream) {
+    return aac_sum_partials_strided(out, gpart, ns, n, n, stream);
+}
+
+int aac_sum_partials_strided(float *out, const float *gpart, int32_t ns, int64_t gstride, int64_t n, void *stream) {
     if (ns < 1) return ffail("sum_partials: nsplit >= 1");
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, gpart, ns, n);
+    if (gstride < n) return ffail("sum_partials: copy stride < n");
+    if (use_sum4(gpart, ns, gstride))
+        hipLaunchKernelGGL(sum_partials4_kernel, dim3(sum4_grid(n)), dim3(256), 0, (hipStream_t)stream, out, gpart, ns,
+                           gstride, n);
+    else
+        hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, gpart, ns,
+                           gstride, n);
     FHIP(hipGetLastError());
     return 0;
 }

@@ -57,6 +57,8 @@ def lib():
         L.aac_gemm_set_lds_policy.argtypes = [i32, i32]
         L.aac_adam_flat_sum.argtypes = [vp, vp, i32, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         L.aac_sum_partials.argtypes = [vp, vp, i32, i64, vp]
+        L.aac_sum_partials_strided.argtypes = [vp, vp, i32, i64, i64, vp]
+        L.aac_adam_flat_sum_strided.argtypes = [vp, vp, i32, i64, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         L.aac_critic_head.argtypes = [vp, i32, i32, vp, vp, i32, vp, vp, vp, i32, i32, f32, vp, vp, vp, vp, vp]
         L.aac_replay_gather_strided.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp]
         L.aac_attn_block.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
@@ -151,17 +153,23 @@ def gather_strided(ring, idx, dsts, widths, chunks, dstrides, dsts2=None):
 
 
 def adam_sum(opt, gpart, nsplit, step_add, grad_out=None):
-    """Adam step whose gradient is the sum of ``nsplit`` partial copies in ``gpart``."""
-    _chk(lib().aac_adam_flat_sum(vp(opt.flat.data.data_ptr()), vp(gpart.data_ptr()), nsplit,
-                                 vp(grad_out.data_ptr()) if grad_out is not None else None,
-                                 vp(opt.exp_avg.data_ptr()), vp(opt.exp_avg_sq.data_ptr()), opt.flat.data.numel(),
-                                 opt.lr, opt.betas[0], opt.betas[1], opt.eps, vp(opt.step_t.data_ptr()), step_add,
-                                 _stream()), "aac_adam_flat_sum")
+    """Adam step whose gradient is the sum of ``nsplit`` partial copies in ``gpart`` ([nsplit][stride],
+    stride >= the parameter count)."""
+    _chk(lib().aac_adam_flat_sum_strided(vp(opt.flat.data.data_ptr()), vp(gpart.data_ptr()), nsplit, gpart.shape[-1],
+                                         vp(grad_out.data_ptr()) if grad_out is not None else None,
+                                         vp(opt.exp_avg.data_ptr()), vp(opt.exp_avg_sq.data_ptr()),
+                                         opt.flat.data.numel(), opt.lr, opt.betas[0], opt.betas[1], opt.eps,
+                                         vp(opt.step_t.data_ptr()), step_add, _stream()), "aac_adam_flat_sum")
 
 
 def sum_partials(out, gpart, nsplit):
-    _chk(lib().aac_sum_partials(vp(out.data_ptr()), vp(gpart.data_ptr()), nsplit, out.numel(), _stream()),
-         "aac_sum_partials")
+    _chk(lib().aac_sum_partials_strided(vp(out.data_ptr()), vp(gpart.data_ptr()), nsplit, gpart.shape[-1],
+                                        out.numel(), _stream()), "aac_sum_partials")
+
+
+def padded(n, q=4):
+    """The copy stride of split-K partial gradients: a multiple of 4 floats (16-B aligned copies)."""
+    return (n + q - 1) // q * q
 
 
 def adam_at(opt, step_add):
@@ -375,8 +383,8 @@ class FusedUpdate:
         self.dcat_o, self.dcat_g, self.dv = z(R, 64), z(R, 64), z(R, 64)
         self.dqa, self.dqk, self.deo, self.dxn = z(R, 64), z(R, 64), z(R, 64), z(R * K, 64)
         # weight-gradient partial copies (summed by the Adam kernel)
-        self.ga = torch.zeros(self.SPLIT_ACTOR, model.fa.numel, device=dev)
-        self.gc = torch.zeros(self.SPLIT_CRITIC, model.fc.numel, device=dev)
+        self.ga = torch.zeros(self.SPLIT_ACTOR, padded(model.fa.numel), device=dev)
+        self.gc = torch.zeros(self.SPLIT_CRITIC, padded(model.fc.numel), device=dev)
         self._build()
 
     # ------------------------------------------------------------------ plan
@@ -518,7 +526,7 @@ class FusedUpdate:
         which depends only on the actor weights, changed after the critic step -- shares the
         critic step's launches; the policy actions land in X2 (own columns gathered there too)."""
         m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
-        SC, nC = self.SPLIT_CRITIC, m.fc.numel
+        SC, nC = self.SPLIT_CRITIC, self.gc.shape[1]     # copy stride
         gC = CriticParams(m.critics, m.fc, self.gc.data_ptr())
         X, _, _, _, y = self._batch_ptrs(i)
         f, h, dq, dh, df = cb
@@ -549,7 +557,7 @@ class FusedUpdate:
         gradient partials: critic on the policy actions, backward into the actor."""
         m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
         R = B * N
-        SA, nA = self.SPLIT_ACTOR, m.fa.numel
+        SA, nA = self.SPLIT_ACTOR, self.ga.shape[1]
         gA = ActorParams(m.actors, m.fa, self.ga.data_ptr())
         _, X, radar, nei, _ = self._batch_ptrs(i)
         f, h, dq, dh, df = self.cbuf[0]

@@ -323,3 +323,50 @@ def test_attn_train_fwd_bwd_matches_autograd(native_lib, K):
     np.testing.assert_allclose(dxn.cpu().double().reshape(R, K, 64), x_r.grad * (d(x) > 0), atol=2e-5, rtol=1e-5)
     np.testing.assert_allclose(dq.cpu().double(), q_r.grad, atol=2e-5, rtol=1e-5)
     np.testing.assert_allclose(deo.cpu().double(), eo_r.grad * (d(eo) > 0), atol=2e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("n,ns,pad", [(65536, 32, 0), (180228, 8, 0), (4100, 40, 0), (1001, 8, 0), (1001, 8, 1),
+                                      (4098, 16, 1), (4096, 3, 0), (256, 1, 0)])
+def test_adam_sum_matches_torch(native_lib, n, ns, pad):
+    """aac_adam_flat_sum (the copy-parallel kernel when the copy stride % 4 == 0, else the element
+    kernel): the summed split-K gradient and torch.optim.Adam's arithmetic, two steps,
+    deterministic; copies padded to a multiple of 4 floats as the learners lay them out
+    (``pad``); aac_sum_partials gives the same bits as the Adam kernel's sum (the world > 1 path)."""
+    from types import SimpleNamespace
+
+    from multi_agent_aac_amd import fused
+    g = torch.Generator(device=DEV).manual_seed(n + ns)
+    p0 = torch.randn(n, device=DEV, generator=g)
+    w = fused.padded(n) if pad else n
+    parts = [torch.randn(ns, w, device=DEV, generator=g) * 1e-3 for _ in range(2)]
+    runs = []
+    for _ in range(2):
+        flat = SimpleNamespace(data=p0.clone())
+        opt = SimpleNamespace(flat=flat, exp_avg=torch.zeros(n, device=DEV), exp_avg_sq=torch.zeros(n, device=DEV),
+                              lr=1e-3, betas=(0.9, 0.999), eps=1e-3, step_t=torch.zeros(1, dtype=torch.int32, device=DEV))
+        gout = torch.empty(n, device=DEV)
+        for k in range(2):
+            fused.adam_sum(opt, parts[k], ns, k + 1, grad_out=gout)
+        torch.cuda.synchronize()
+        runs.append((flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), gout.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)                     # deterministic
+    ref = p0.double().clone().requires_grad_(False)
+    m = torch.zeros(n, dtype=torch.float64, device=DEV)
+    v = torch.zeros(n, dtype=torch.float64, device=DEV)
+    for k in range(2):
+        gk = parts[k][:, :n].double().sum(0)
+        t = k + 1
+        m = 0.9 * m + 0.1 * gk
+        v = 0.999 * v + 0.001 * gk * gk
+        # eps 1e-3: the step is continuous in the gradient (at 1e-8 a summed gradient at rounding level
+        # moves a weight by +-lr whatever its size, so fp32 vs fp64 summation could flip it)
+        ref = ref - 1e-3 / (1 - 0.9 ** t) * m / (v.sqrt() / np.sqrt(1 - 0.999 ** t) + 1e-3)
+    p, mm, vv, gg = runs[0]
+    summed = torch.empty(n, device=DEV)
+    fused.sum_partials(summed, parts[1], ns)
+    torch.cuda.synchronize()
+    assert torch.equal(summed, gg)
+    np.testing.assert_allclose(gg.cpu().double(), parts[1][:, :n].double().sum(0).cpu(), rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(mm.cpu().double(), m.cpu(), rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(p.cpu().double(), ref.cpu(), rtol=0, atol=1e-6)
