@@ -103,6 +103,11 @@ __device__ bool building_hit(double px, double py, double cx, double cy, double 
     return true;
 }
 
+// occupied cells that can meet the segment c -> e (a bit per cell of the bounding box, bit
+// (i - i0) * 8 + (j - j0)), then the exact entry into each.  Collecting first keeps the wave's
+// lanes together: the per-cell loop ran the slab test whenever any lane of the wave had a
+// candidate in that cell slot, the candidate loop runs it max-popcount times.  The minimum does
+// not depend on the order (OM/env:1089-1141 takes the nearest intersection).
 __device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, double cy, double ex, double ey,
                                   double len) {
     double mind = len, d;
@@ -113,20 +118,41 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, 
     j0 = j0 < 0 ? 0 : j0;
     i1 = i1 > A.gw - 1 ? A.gw - 1 : i1;
     j1 = j1 > A.gh - 1 ? A.gh - 1 : j1;
-    // a square can only meet the segment if its centre is within its circumradius 5 sqrt(2) of
-    // the segment's line and of its extent along the line (exact: the slab test decides the rest)
+    // a square of half-size 5 centred at q meets the segment only if q lies within its support
+    // half-width 5 (|ux| + |uy|) of the segment's line and of its extent along the line (u the
+    // unit direction; everything below is scaled by L: no division).  A conservative pre-filter
+    // (relative margin 1e-9, far above the rounding of these few products): the slab test decides.
     const double ddx = ex - cx, ddy = ey - cy;
-    const double L = sqrt(ddx * ddx + ddy * ddy);
-    const double reach = 5.0 * 1.4142135623730951 * (1.0 + 1e-9) * L;   // scaled by L: no division
-    for (int i = i0; i <= i1; ++i)
-        for (int j = j0; j <= j1; ++j) {
-            if (!occ[i * A.gh + j]) continue;
-            double qx = A.gx0 + 10.0 * i, qy = A.gy0 + 10.0 * j;
-            const double wx = qx - cx, wy = qy - cy;
-            const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
-            if (fabs(cr) > reach || al < -reach || al > L * L + reach) continue;
+    const double L2 = ddx * ddx + ddy * ddy;
+    const double reach = 5.0 * (fabs(ddx) + fabs(ddy)) * (1.0 + 1e-9) + 1e-12;
+    if (i1 - i0 < 8 && j1 - j0 < 8) {
+        unsigned long long cand = 0;
+        for (int i = i0; i <= i1; ++i) {
+            const double wx = A.gx0 + 10.0 * i - cx;
+            for (int j = j0; j <= j1; ++j) {
+                const double wy = A.gy0 + 10.0 * j - cy;
+                const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
+                const bool near = fabs(cr) <= reach && al >= -reach && al <= L2 + reach;
+                if (near && occ[i * A.gh + j]) cand |= 1ull << ((i - i0) * 8 + (j - j0));
+            }
+        }
+        while (cand) {
+            const int b = __builtin_ctzll(cand);
+            cand &= cand - 1;
+            const double qx = A.gx0 + 10.0 * (i0 + (b >> 3)), qy = A.gy0 + 10.0 * (j0 + (b & 7));
             if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
         }
+    } else {      // a radar longer than the 8 x 8-cell mask covers
+        for (int i = i0; i <= i1; ++i)
+            for (int j = j0; j <= j1; ++j) {
+                if (!occ[i * A.gh + j]) continue;
+                const double qx = A.gx0 + 10.0 * i, qy = A.gy0 + 10.0 * j;
+                const double wx = qx - cx, wy = qy - cy;
+                const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
+                if (fabs(cr) > reach || al < -reach || al > L2 + reach) continue;
+                if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
+            }
+    }
     if (ray_vline(cx, cy, ex, ey, A.bound[0], d) && d < mind) mind = d;
     if (ray_vline(cx, cy, ex, ey, A.bound[1], d) && d < mind) mind = d;
     if (ray_hline(cx, cy, ex, ey, A.bound[2], d) && d < mind) mind = d;
@@ -233,28 +259,36 @@ __device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base,
     const double len = gdist(ex, ey, px, py);
     double dd = len, dob = len;
     if (A.radar_mode != AAC_RADAR_OBSTACLES) {
+        // neighbours whose 64-gon can meet the segment (closest point within pb: the GEOS 64-gon
+        // lies inside the circle of radius pb (+1e-15)), collected per 64 as a mask, then the
+        // exact entry for each candidate (same lane-compaction argument as radar_obstacles)
         const double reach2 = (pb + 1e-6) * (pb + 1e-6);
-        double shortest = INFINITY;
         const double ddx = ex - px, ddy = ey - py;
         const double inv = 1.0 / (ddx * ddx + ddy * ddy);
-        for (int j = 0; j < N; ++j) {
-            if (j == i) continue;
-            const double2 q = S.pos[base + j];
-            // exact pre-filter: the GEOS 64-gon lies inside the circle of radius pb (+1e-15)
-            double wx = q.x - px, wy = q.y - py;
-            double tt = (wx * ddx + wy * ddy) * inv;
-            tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
-            double qx = tt * ddx - wx, qy = tt * ddy - wy;
-            if (qx * qx + qy * qy > reach2) continue;
-            double t;
-            if (!ray_poly_entry(px, py, ex, ey, q.x, q.y, pb, t)) continue;
-            double ix = px + t * (ex - px), iy = py + t * (ey - py);
-            double d = gdist(ix, iy, px, py);
-            if (d < shortest) {
-                shortest = d;
-                dd = d;
+        double shortest = INFINITY;       // the nearest hit replaces len (even a rounding above it)
+        for (int j0 = 0; j0 < N; j0 += 64) {
+            const int jn = N - j0 < 64 ? N - j0 : 64;
+            unsigned long long cand = 0;
+            for (int jj = 0; jj < jn; ++jj) {
+                const double2 q = S.pos[base + j0 + jj];
+                const double wx = q.x - px, wy = q.y - py;
+                double tt = (wx * ddx + wy * ddy) * inv;
+                tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
+                const double qx = tt * ddx - wx, qy = tt * ddy - wy;
+                if (j0 + jj != i && qx * qx + qy * qy <= reach2) cand |= 1ull << jj;
+            }
+            while (cand) {
+                const int j = j0 + __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const double2 q = S.pos[base + j];
+                double t;
+                if (!ray_poly_entry(px, py, ex, ey, q.x, q.y, pb, t)) continue;
+                const double ix = px + t * (ex - px), iy = py + t * (ey - py);
+                const double d = gdist(ix, iy, px, py);
+                shortest = d < shortest ? d : shortest;
             }
         }
+        if (shortest < INFINITY) dd = shortest;
     }
     if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, px, py, ex, ey, len);
     return A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));

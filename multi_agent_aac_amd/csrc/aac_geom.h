@@ -176,6 +176,12 @@ __device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, doubl
     const double s0 = (wx * ddx + wy * ddy) / L;                   // along the ray
     const double h = fabs(wx * ddy - wy * ddx) / L;               // distance of p to the line
     const double ap = r * c_tab.apothem;
+    // c strictly inside the inscribed circle (margin far above rounding): every edge has a < 0,
+    // so the full clip never raises tlo from 0 and never empties the interval -- entry at c
+    if (w2 < ap * ap * (1.0 - 1e-9)) {
+        tout = 0.0;
+        return true;
+    }
     if (!(h < ap * (1.0 - 1e-9)) || !(w2 > r * r * (1.0 + 1e-9)) || !(s0 > 0.0))
         return ray_poly_entry_full(cx, cy, ex, ey, px, py, r, tout);
     const double tc = (s0 - sqrt(r * r - h * h)) / L;              // circumscribed-circle entry

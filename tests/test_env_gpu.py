@@ -80,6 +80,44 @@ def test_step_injected_parity(native_lib, occ, mode, N):
     assert seen & 0b11 or mode == 0 or True   # coverage is asserted in test_event_coverage
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_radar_crowded_bit_exact(native_lib, occ, mode):
+    """The radar (fp32) bit-identical to the C oracle on injected crowded states: agents inside
+    each other's 64-gon, in contact, on cell edges and on / beyond the bounds -- the cases the
+    kernel's candidate masks and the inside fast path of the drone clip must get exactly right."""
+    from oracle.consts import BOUND
+    E, N = 512, 8
+    st, wps, cnt = random_od(occ, E, N, seed=77)
+    env = _env(E, N, occ, mode)
+    co = c_oracle.BatchedOracle(E, N, occ, W=W_DEFAULT, radar_mode=mode)
+    env.reset(st, wps, cnt)
+    co.reset(st, wps, cnt)
+    rng = np.random.default_rng(40 + mode)
+    centre = np.stack([rng.uniform(BOUND[0] - 5, BOUND[1] + 5, E), rng.uniform(BOUND[2] - 5, BOUND[3] + 5, E)], -1)
+    pos = centre[:, None, :] + rng.normal(scale=3.0, size=(E, N, 2))
+    pos[::4, 1] = pos[::4, 0] + rng.uniform(-1, 1, size=(len(pos[::4]), 2))       # deep overlaps
+    edge = rng.integers(0, 22, size=(E // 4, N, 2))
+    pos[1::4] = np.stack([455.0 + 10 * edge[..., 0], 255.0 + 10 * np.minimum(edge[..., 1], 13)], -1)  # cell corners
+    pos[1::4, :, 1] += rng.integers(0, 2, size=(E // 4, N)) * rng.uniform(0, 10, size=(E // 4, N))  # on x edges
+    pos[2::8, 0, 0] = BOUND[0]                                                       # on the bound lines
+    pos[3::8, 0, 1] = BOUND[3]
+    z = np.zeros_like(pos)
+    env.set_state(pos=pos, pre_pos=pos, vel=z, pre_vel=z)
+    _state_to_oracle(env, co)
+    act = np.zeros((E, N, 2), np.float32)                                             # stay put
+    env.step(torch.from_numpy(act).cuda())
+    co.step(act)
+    torch.cuda.synchronize()
+    assert np.array_equal(env.bufs.radar.cpu().numpy(), co.radar)
+    s = env.get_state()
+    assert np.array_equal(s["pos"].cpu().numpy(), pos)
+    _cmp_step(env.bufs, co, f"crowded mode{mode}")
+    d = np.linalg.norm(pos[:, :, None] - pos[:, None], axis=-1) + np.eye(N) * 99
+    assert (d < 2.5 * np.cos(np.pi / 64)).any()                                       # the inside case occurs
+    if mode != 1:
+        assert (co.radar == 0).any()
+
+
 def test_free_running_trajectory(native_lib, occ):
     """No re-injection: 51 steps, trajectories may drift by libm ulps only."""
     E, N = 256, 5
