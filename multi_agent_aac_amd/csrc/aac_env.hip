@@ -49,6 +49,7 @@ struct Args {
     int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx;   // variant 1: wp_cur = removed-waypoint bits
     uint8_t *reach;
     const uint8_t *occ;  // n_maps * gw * gh
+    const unsigned long long *occ_rows;   // n_maps * gw row bit masks (bit j = cell (i, j)); gh <= 64
     float *own, *radar, *nei, *reward;
     uint8_t *done, *mask, *env_done, *bbc;
     double *tcpa, *dcpa;
@@ -108,12 +109,14 @@ __device__ bool building_hit(double px, double py, double cx, double cy, double 
 // lanes together: the per-cell loop ran the slab test whenever any lane of the wave had a
 // candidate in that cell slot, the candidate loop runs it max-popcount times.  The minimum does
 // not depend on the order (OM/env:1089-1141 takes the nearest intersection).
-__device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, double cy, double ex, double ey,
-                                  double len) {
+__device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsigned long long *rows, double cx,
+                                  double cy, double ex, double ey, double len) {
     double mind = len, d;
-    // only cells whose square meets the segment's bounding box can meet the segment
-    int i0 = (int)floor((fmin(cx, ex) - 5.0 - A.gx0) / 10.0), i1 = (int)ceil((fmax(cx, ex) + 5.0 - A.gx0) / 10.0);
-    int j0 = (int)floor((fmin(cy, ey) - 5.0 - A.gy0) / 10.0), j1 = (int)ceil((fmax(cy, ey) + 5.0 - A.gy0) / 10.0);
+    // only cells whose square meets the segment's bounding box can meet the segment (index range
+    // by a product with 0.1: it rounds within an ulp of the quotient, and floor / ceil of it still
+    // bracket the cells ceil((lo - 5) / 10) .. floor((hi + 5) / 10) that can touch the box)
+    int i0 = (int)floor((fmin(cx, ex) - 5.0 - A.gx0) * 0.1), i1 = (int)ceil((fmax(cx, ex) + 5.0 - A.gx0) * 0.1);
+    int j0 = (int)floor((fmin(cy, ey) - 5.0 - A.gy0) * 0.1), j1 = (int)ceil((fmax(cy, ey) + 5.0 - A.gy0) * 0.1);
     i0 = i0 < 0 ? 0 : i0;
     j0 = j0 < 0 ? 0 : j0;
     i1 = i1 > A.gw - 1 ? A.gw - 1 : i1;
@@ -125,15 +128,26 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, 
     const double ddx = ex - cx, ddy = ey - cy;
     const double L2 = ddx * ddx + ddy * ddy;
     const double reach = 5.0 * (fabs(ddx) + fabs(ddy)) * (1.0 + 1e-9) + 1e-12;
-    if (i1 - i0 < 8 && j1 - j0 < 8) {
+    if (i1 < i0 || j1 < j0) {
+        // the box lies off the grid: no cell
+    } else if (rows && i1 - i0 < 8 && j1 - j0 < 8) {
+        // the box's occupied cells from the row masks (one 8-B LDS read per row, all issued
+        // up front), the line filter on those only
+        const unsigned long long span = (2ull << (j1 - j0)) - 1;
+        unsigned long long rb[8];
+#pragma unroll
+        for (int di = 0; di < 8; ++di) rb[di] = rows[i0 + di <= i1 ? i0 + di : 0];
         unsigned long long cand = 0;
-        for (int i = i0; i <= i1; ++i) {
-            const double wx = A.gx0 + 10.0 * i - cx;
-            for (int j = j0; j <= j1; ++j) {
-                const double wy = A.gy0 + 10.0 * j - cy;
+#pragma unroll
+        for (int di = 0; di < 8; ++di) {
+            unsigned long long row = i0 + di <= i1 ? (rb[di] >> j0) & span : 0ull;
+            const double wx = A.gx0 + 10.0 * (i0 + di) - cx;
+            while (row) {
+                const int b = __builtin_ctzll(row);
+                row &= row - 1;
+                const double wy = A.gy0 + 10.0 * (j0 + b) - cy;
                 const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
-                const bool near = fabs(cr) <= reach && al >= -reach && al <= L2 + reach;
-                if (near && occ[i * A.gh + j]) cand |= 1ull << ((i - i0) * 8 + (j - j0));
+                if (fabs(cr) <= reach && al >= -reach && al <= L2 + reach) cand |= 1ull << (di * 8 + b);
             }
         }
         while (cand) {
@@ -142,7 +156,7 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, double cx, 
             const double qx = A.gx0 + 10.0 * (i0 + (b >> 3)), qy = A.gy0 + 10.0 * (j0 + (b & 7));
             if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
         }
-    } else {      // a radar longer than the 8 x 8-cell mask covers
+    } else {      // a radar longer than the 8 x 8-cell mask covers, or maps taller than 64 cells
         for (int i = i0; i <= i1; ++i)
             for (int j = j0; j <= j1; ++j) {
                 if (!occ[i * A.gh + j]) continue;
@@ -170,8 +184,15 @@ struct Lds {
     unsigned long long rmin[BLOCK];   // variant 1: per agent, the smallest radar distance (float64 bits)
     alignas(16) float obs[OBS_STAGE_FLOATS];   // the workgroup's own | nei rows (step kernel, when they fit)
 };
-// the occupancy maps follow the static LDS image as dynamic LDS (n_maps * gw * gh bytes)
+// the occupancy maps follow the static LDS image as dynamic LDS: n_maps * gw * gh bytes, then
+// (8-B aligned) the n_maps * gw row masks when the handle has them
 extern __shared__ uint8_t s_maps[];
+
+__device__ inline int rows_off(const Args &A) { return (A.n_maps * A.gw * A.gh + 7) & ~7; }
+
+__device__ inline const unsigned long long *map_rows(const Args &A, int m) {
+    return A.occ_rows ? reinterpret_cast<const unsigned long long *>(s_maps + rows_off(A)) + m * A.gw : nullptr;
+}
 
 // own + neighbour observation and tdCPA of agent i of env e (ATT/env:1285-1469)
 __device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int base, float *own = nullptr,
@@ -250,7 +271,8 @@ __device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int bas
 }
 
 // one radar ray r of agent i (ATT/env:1089-1164 drones, OM/env:1089-1141 obstacles)
-__device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ) {
+__device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ,
+                            const unsigned long long *rows) {
     const int N = A.N;
     const double pb = A.pb;
     const double2 p = S.pos[base + i];
@@ -290,13 +312,17 @@ __device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base,
         }
         if (shortest < INFINITY) dd = shortest;
     }
-    if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, px, py, ex, ey, len);
+    if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, rows, px, py, ex, ey, len);
     return A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
 }
 
 __device__ inline void load_maps(const Args &A) {
     const int bytes = A.n_maps * A.gw * A.gh;
     for (int k = threadIdx.x; k < bytes; k += BLOCK) s_maps[k] = A.occ[k];
+    if (A.occ_rows) {
+        unsigned long long *r = reinterpret_cast<unsigned long long *>(s_maps + rows_off(A));
+        for (int k = threadIdx.x; k < A.n_maps * A.gw; k += BLOCK) r[k] = A.occ_rows[k];
+    }
 }
 
 // all radar rays of the workgroup's (active) agents: one work item per (agent, ray); rmin (variant
@@ -309,8 +335,9 @@ __device__ inline void radar_phase(const Args &A, Lds &S, int e0, int nagents, b
         const int e = emap ? emap[le] : e0 + le;
         if (e >= A.E) continue;
         if (check_active && !S.active[le]) continue;
-        const uint8_t *occ = s_maps + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
-        const double d = radar_ray(A, S, i, r, le * A.N, occ);
+        const int mi = A.map_idx ? A.map_idx[e] : 0;
+        const uint8_t *occ = s_maps + mi * A.gw * A.gh;
+        const double d = radar_ray(A, S, i, r, le * A.N, occ, map_rows(A, mi));
         A.radar[((size_t)e * A.N + i) * NRAY + r] = (float)d;
         if (rmin) atomicMin(&S.rmin[la], (unsigned long long)__double_as_longlong(d));
     }
@@ -818,6 +845,7 @@ struct aac_env {
     int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx, *episode;
     int32_t *episode_own;     // the handle's own counter buffer (episode may be a caller's buffer)
     uint8_t *reach, *occ;
+    unsigned long long *occ_rows;    // row bit masks of occ (grid_h <= 64), else null
     double2 *bank_start, *bank_wp;
     int32_t *bank_cnt, *bank_off;
     int32_t bank_n, bank_maps;
@@ -825,8 +853,11 @@ struct aac_env {
     int32_t *rlist;           // [1 + E]: packed resetting envs of the last auto-reset
 };
 
-// dynamic LDS of the step / reset kernels: the handle's occupancy maps
-static size_t map_bytes(const aac_env *h) { return (size_t)h->cfg.n_maps * h->cfg.grid_w * h->cfg.grid_h; }
+// dynamic LDS of the step / reset kernels: the handle's occupancy maps and their row masks
+static size_t map_bytes(const aac_env *h) {
+    const size_t b = (size_t)h->cfg.n_maps * h->cfg.grid_w * h->cfg.grid_h;
+    return h->occ_rows ? ((b + 7) & ~(size_t)7) + 8 * (size_t)h->cfg.n_maps * h->cfg.grid_w : b;
+}
 
 static Args make_args(const aac_env *h, const aac_step_out *o) {
     Args A;
@@ -869,6 +900,7 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
     A.map_idx = h->map_idx;
     A.reach = h->reach;
     A.occ = h->occ;
+    A.occ_rows = h->occ_rows;
     A.own = o->own;
     A.radar = o->radar;
     A.nei = o->nei;
@@ -896,7 +928,8 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     if (c.radar_mode < 0 || c.radar_mode > 2) return fail(AAC_E_INVALID, "bad radar_mode");
     if (c.max_wp < 1) return fail(AAC_E_INVALID, "max_wp must be >= 1");
     if (c.n_maps < 1 || !c.occ || c.grid_w < 1 || c.grid_h < 1) return fail(AAC_E_INVALID, "bad occupancy maps");
-    if ((size_t)c.n_maps * c.grid_w * c.grid_h > MAX_MAP_BYTES) return fail(AAC_E_INVALID, "maps exceed LDS budget");
+    if ((size_t)c.n_maps * c.grid_w * (c.grid_h + 8) + 8 > MAX_MAP_BYTES)
+        return fail(AAC_E_INVALID, "maps exceed LDS budget");
     if (c.cell != 10.0) return fail(AAC_E_INVALID, "cell must be 10 m (grid geometry of ATT/grid:138)");
     if (c.variant < 0 || c.variant > 1) return fail(AAC_E_INVALID, "variant: 0 one_model_att, 1 randomOD_Wgru_radar");
     if (c.variant == 1 && (c.radar_mode != AAC_RADAR_OBSTACLES || c.team_reward || c.max_wp > 32))
@@ -925,6 +958,15 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
 #undef ALLOC
     if (st == hipSuccess) st = hipMemcpy(h->occ, c.occ, (size_t)c.n_maps * c.grid_w * c.grid_h, hipMemcpyHostToDevice);
+    if (st == hipSuccess && c.grid_h <= 64) {      // row masks for the radar's cell enumeration
+        std::vector<unsigned long long> rows((size_t)c.n_maps * c.grid_w, 0ull);
+        for (size_t r = 0; r < rows.size(); ++r)
+            for (int j = 0; j < c.grid_h; ++j)
+                if (c.occ[r * c.grid_h + j]) rows[r] |= 1ull << j;
+        st = hipMalloc((void **)&h->occ_rows, rows.size() * sizeof(unsigned long long));
+        if (st == hipSuccess)
+            st = hipMemcpy(h->occ_rows, rows.data(), rows.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+    }
     if (st == hipSuccess) {
         Tab t;
         fill_tables(t);
@@ -942,7 +984,7 @@ void aac_env_destroy(aac_env *h) {
     if (!h) return;
     void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->start, h->wp, h->wp_cur, h->wp_cnt, h->wall,
                     h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt,
-                    h->bank_off, h->rlist};
+                    h->bank_off, h->rlist, h->occ_rows};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;

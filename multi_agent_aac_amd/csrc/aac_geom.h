@@ -54,15 +54,35 @@ __device__ inline void upd(double x, double y, double &mnx, double &mxx, double 
     mxy = y > mxy ? y : mxy;
 }
 
-__device__ void fillet_ext(double px, double py, double start, double end, double r, double &mnx, double &mxx,
-                           double &mny, double &mxy) {
-    double total = fabs(start - end);
-    int nseg = (int)(total / c_tab.quantum + 0.5);
-    double inc = total / nseg;
-    for (int i = 1; i < nseg; ++i) {  // i = 0 is redundant with the offset point (GEOS isRedundant)
-        double a = start + (double)(-1 * i) * inc;
-        upd(px + r * cos(a), py + r * sin(a), mnx, mxx, mny, mxy);
+// One extreme (axis ax = 0 x / 1 y; the max when mx, else the min) over the vertices i = 1 .. nseg-1
+// that GEOS's fillet (OffsetSegmentGenerator::addDirectedFillet, oracle/aac_oracle.c fillet_ext) has: p + r (cos a_i, sin a_i), a_i = start - i inc.  The extreme of cos(a - theta)
+// over equally spaced angles sits at the vertex nearest theta (theta = 0, pi, pi/2, -pi/2), or at an
+// arc end when theta is off the arc; neighbours of the winner are smaller by >= r inc^2 (~0.02 at
+// r = 2.5), far above rounding.  So the three vertices around theta plus the two arc ends hold
+// the extreme of the computed values: the same number as the full loop with 5 instead of 31
+// fp64 cos/sin pairs per fillet.
+__device__ double fillet_extreme(double px, double py, double start, double end, double r, int ax, bool mx) {
+    const double total = fabs(start - end);
+    const int nseg = (int)(total / c_tab.quantum + 0.5);
+    double best = mx ? -INFINITY : INFINITY;
+    if (nseg < 2) return best;
+    const double inc = total / nseg;
+    const double theta = ax == 0 ? (mx ? 0.0 : PI_GEOS) : (mx ? PI_GEOS / 2.0 : -PI_GEOS / 2.0);
+    const double per = 2.0 * PI_GEOS / inc;                  // vertices per turn
+    double k = (start - theta) / inc;                         // a_i = theta at i = k (mod per)
+    k -= per * floor(k / per);
+    const int kn = (int)floor(k + 0.5), iper = (int)floor(per + 0.5);
+    const int cand[5] = {1, nseg - 1, kn - 1, kn, kn + 1};
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        int i = cand[q] % iper;
+        i = i < 0 ? i + iper : i;
+        if (i < 1 || i > nseg - 1) continue;
+        const double a = start + (double)(-1 * i) * inc;
+        const double v = ax == 0 ? px + r * cos(a) : py + r * sin(a);
+        best = mx ? (v > best ? v : best) : (v < best ? v : best);
     }
+    return best;
 }
 
 // LineString([p0,p1]).buffer(r, round caps) meets one of the 4 infinite lines x = b[0], x = b[1],
@@ -76,38 +96,53 @@ __device__ bool capsule_crash(double r, const double *b, double x0, double y0, d
     // extreme endpoint has a vertex within half a fillet step (<= quantum) of each axis
     // direction, so min x lies in [lx - r, lx - r cos(quantum)] (likewise the other sides).  A
     // line outside [min, max] of those bands is decided without building the capsule.
-    {
-        const double lo = r + 1e-9, hi = r * c_tab.cos_quantum - 1e-9;
-        const double mn_lo[2] = {lx - lo, ly - lo}, mn_hi[2] = {lx - hi, ly - hi};
-        const double mx_lo[2] = {hx + hi, hy + hi}, mx_hi[2] = {hx + lo, hy + lo};
-        bool certain = true;
-        for (int q = 0; q < 4; ++q) {
-            const int ax = q >> 1;
-            const double v = b[q];
-            if (v < mn_lo[ax] || v > mx_hi[ax]) continue;                  // certainly outside
-            if (v >= mn_hi[ax] && v <= mx_lo[ax]) return true;             // certainly inside
-            certain = false;
-        }
-        if (certain) return false;
+    const double lo = r + 1e-9, hi = r * c_tab.cos_quantum - 1e-9;
+    const double mn_lo[2] = {lx - lo, ly - lo}, mn_hi[2] = {lx - hi, ly - hi};
+    const double mx_lo[2] = {hx + hi, hy + hi}, mx_hi[2] = {hx + lo, hy + lo};
+    int need = 0;             // bit 2q: line q needs the min of its axis, bit 2q+1: the max
+    for (int q = 0; q < 4; ++q) {
+        const int ax = q >> 1;
+        const double v = b[q];
+        if (v < mn_lo[ax] || v > mx_hi[ax]) continue;                  // certainly outside
+        if (v >= mn_hi[ax] && v <= mx_lo[ax]) return true;             // certainly inside
+        // uncertain: v lies in the min band (then v <= max is certain) or in the max band
+        need |= (v < mn_hi[ax] ? 1 : 2) << (2 * q);
     }
-    double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
+    if (!need) return false;
     if (x0 == x1 && y0 == y1) {
+        double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
         for (int i = 0; i < 64; ++i) upd(x0 + r * c_tab.circ_c[i], y0 + r * c_tab.circ_s[i], mnx, mxx, mny, mxy);
-    } else {
-        double dx = x1 - x0, dy = y1 - y0;
-        double len = sqrt(dx * dx + dy * dy);
-        double ux = 1 * r * dx / len, uy = 1 * r * dy / len;
+        return (mnx <= b[0] && b[0] <= mxx) || (mnx <= b[1] && b[1] <= mxx) || (mny <= b[2] && b[2] <= mxy) ||
+               (mny <= b[3] && b[3] <= mxy);
+    }
+    // the offset-segment vertices, then per uncertain line only the extreme it needs from the two
+    // fillets (fillet_extreme): the full construction's vertex set restricted to its argmax
+    double ox[2], oy[2];                 // (min, max) over the four offset points
+    const double dx = x1 - x0, dy = y1 - y0;
+    const double len = sqrt(dx * dx + dy * dy);
+    const double ux = 1 * r * dx / len, uy = 1 * r * dy / len;
+    {
+        double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
         upd(x1 - uy, y1 + ux, mnx, mxx, mny, mxy);
         upd(x1 + uy, y1 - ux, mnx, mxx, mny, mxy);
         upd(x0 + uy, y0 - ux, mnx, mxx, mny, mxy);
         upd(x0 - uy, y0 + ux, mnx, mxx, mny, mxy);
-        double a1 = atan2(dy, dx);
-        fillet_ext(x1, y1, a1 + PI_GEOS / 2.0, a1 - PI_GEOS / 2.0, r, mnx, mxx, mny, mxy);
-        double a0 = atan2(y0 - y1, x0 - x1);
-        fillet_ext(x0, y0, a0 + PI_GEOS / 2.0, a0 - PI_GEOS / 2.0, r, mnx, mxx, mny, mxy);
+        ox[0] = mnx; ox[1] = mxx; oy[0] = mny; oy[1] = mxy;
     }
-    return (mnx <= b[0] && b[0] <= mxx) || (mnx <= b[1] && b[1] <= mxx) || (mny <= b[2] && b[2] <= mxy) ||
-           (mny <= b[3] && b[3] <= mxy);
+    const double a1 = atan2(dy, dx);
+    const double a0 = atan2(y0 - y1, x0 - x1);
+    for (int q = 0; q < 4; ++q) {
+        const int w = (need >> (2 * q)) & 3;
+        if (!w) continue;
+        const int ax = q >> 1;
+        const bool mx = w == 2;
+        double e = ax == 0 ? ox[mx] : oy[mx];
+        const double f1 = fillet_extreme(x1, y1, a1 + PI_GEOS / 2.0, a1 - PI_GEOS / 2.0, r, ax, mx);
+        const double f0 = fillet_extreme(x0, y0, a0 + PI_GEOS / 2.0, a0 - PI_GEOS / 2.0, r, ax, mx);
+        e = mx ? fmax(e, fmax(f1, f0)) : fmin(e, fmin(f1, f0));
+        if (mx ? b[q] <= e : e <= b[q]) return true;
+    }
+    return false;
 }
 
 // GEOS 64-gon(p, r0) vs 64-gon(q, r1), d = q - p: both share the vertex angles k pi/32, so the

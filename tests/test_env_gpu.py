@@ -118,6 +118,47 @@ def test_radar_crowded_bit_exact(native_lib, occ, mode):
         assert (co.radar == 0).any()
 
 
+def test_bound_capsule_band_bit_exact(native_lib, occ):
+    """Bound crash with the step's capsule inside the band where the certain-band test cannot
+    decide (its extreme within r (1 - cos(pi/32)) of the line): the kernel's per-line fillet
+    extremes against the oracle's full GEOS vertex loop, every line and direction, moving and
+    stationary agents; both outcomes must occur."""
+    from oracle.consts import BOUND, PB
+    E, N = 512, 5
+    st, wps, cnt = random_od(occ, E, N, seed=78)
+    env = _env(E, N, occ, 2)
+    co = c_oracle.BatchedOracle(E, N, occ, W=W_DEFAULT, radar_mode=2)
+    env.reset(st, wps, cnt)
+    co.reset(st, wps, cnt)
+    rng = np.random.default_rng(9)
+    M = E * N
+    vel = rng.uniform(-3, 3, size=(M, 2))
+    vel[::7] = 0.0                                         # stationary: the 64-gon branch
+    vel[1::7, 0] = 0.0                                     # axis-parallel moves
+    vel[2::7, 1] = 0.0
+    u = rng.uniform(np.cos(np.pi / 32) - 2e-3, 1 + 2e-3, size=M)
+    line = rng.integers(0, 4, size=M)
+    pos = np.stack([rng.uniform(BOUND[0] + 20, BOUND[1] - 20, M), rng.uniform(BOUND[2] + 20, BOUND[3] - 20, M)], -1)
+    step = 0.5 * vel                                       # dt = 0.5, zero action keeps the velocity
+    for q in range(4):
+        sel = line == q
+        ax = q >> 1
+        if q % 2 == 0:      # low line: the capsule's min coordinate lands r u above it
+            pos[sel, ax] = BOUND[q] + PB * u[sel] - np.minimum(0, step[sel, ax])
+        else:
+            pos[sel, ax] = BOUND[q] - PB * u[sel] - np.maximum(0, step[sel, ax])
+    pos, vel = pos.reshape(E, N, 2), vel.reshape(E, N, 2)
+    env.set_state(pos=pos, pre_pos=pos, vel=vel, pre_vel=vel)
+    _state_to_oracle(env, co)
+    act = np.zeros((E, N, 2), np.float32)
+    env.step(torch.from_numpy(act).cuda())
+    co.step(act)
+    torch.cuda.synchronize()
+    _cmp_step(env.bufs, co, "capsule band")
+    hit = co.mask & 1
+    assert 0.05 < hit.mean() < 0.95, hit.mean()
+
+
 def test_free_running_trajectory(native_lib, occ):
     """No re-injection: 51 steps, trajectories may drift by libm ulps only."""
     E, N = 256, 5
