@@ -150,6 +150,10 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
                 if (fabs(cr) <= reach && al >= -reach && al <= L2 + reach) cand |= 1ull << (di * 8 + b);
             }
         }
+#ifdef AAC_DBG_NO_SQUARE      // timing experiments only
+        mind -= (double)__popcll(cand) * 1e-30;
+        cand = 0;
+#endif
         while (cand) {
             const int b = __builtin_ctzll(cand);
             cand &= cand - 1;
@@ -167,6 +171,9 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
                 if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
             }
     }
+#ifdef AAC_DBG_NO_LINES
+    return mind;
+#endif
     if (ray_vline(cx, cy, ex, ey, A.bound[0], d) && d < mind) mind = d;
     if (ray_vline(cx, cy, ex, ey, A.bound[1], d) && d < mind) mind = d;
     if (ray_hline(cx, cy, ex, ey, A.bound[2], d) && d < mind) mind = d;
@@ -498,6 +505,8 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args A, 
     const int N = A.N;
     const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
+    // one thread per agent slot, slots packed into the first wave(s): spreading a workgroup's 20-odd
+    // agents over its four waves (slot = 4 lane + wave) measured slower, 52 -> 65 us at 4096 x 5
     const int t = threadIdx.x;
     const int le = t / N, i = t - le * N;
     const int e = e0 + le;
