@@ -90,7 +90,7 @@ def gemm_roofline(model, B, reps=10):
     for op in ops:
         op()
     torch.cuda.synchronize()
-    flops, us = 0.0, 0.0
+    flops, us, nbytes = 0.0, 0.0, 0.0
     n = 0
     for op in ops:
         if not isinstance(op, GemmLaunch):
@@ -108,11 +108,13 @@ def gemm_roofline(model, B, reps=10):
         torch.cuda.synchronize()
         us += e0.elapsed_time(e1) / reps * 1e3
         flops += op.flops
+        nbytes += op.bytes
         n += 1
     achieved = flops / (us * 1e-6) / 1e12
     return {"kernel": "gemm_kernel (grouped fp32 MFMA GEMM of the fused learner)", "bound": "mfma",
             "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-            "flop_per_launch": flops / n, "avg_launch_ms": us / n / 1e3, "launches_per_update": n,
+            "flop_per_launch": flops / n, "algorithmic_bytes_per_launch": nbytes / n,
+            "avg_launch_ms": us / n / 1e3, "launches_per_update": n,
             "gemm_ms_per_update": us / 1e3, "timing": f"graph replay x{reps} per launch, HIP events"}
 
 
@@ -138,7 +140,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "env_step_pmc.json"))
-    p.add_argument("--gemm-traffic", default=os.path.join(ROOT, "profiles", "gemm_pmc.json"))
+    p.add_argument("--gemm-traffic", default=None,
+                   help="GEMM PMC file (default profiles/gemm_pmc.json; config 4: profiles/gemm_pmc_gru.json)")
     a = p.parse_args()
     if a.agents is None:
         a.agents = {"gru": 8, "uam": 16}.get(a.model, 5)
@@ -148,6 +151,8 @@ def parse():
         a.envs = 8192 if a.model == "uam" else 4096
     if a.memory is None:
         a.memory = (1 << 20) if a.model == "uam" else 100000
+    if a.gemm_traffic is None:
+        a.gemm_traffic = os.path.join(ROOT, "profiles", "gemm_pmc_gru.json" if a.model == "gru" else "gemm_pmc.json")
     return a
 
 
@@ -691,6 +696,7 @@ def main():
                     t.get("model", "att") == a.model:
                 rf["traffic"] = t.get("hbm_bytes_per_launch")
                 rf["traffic_source"] = os.path.relpath(a.gemm_traffic, ROOT)
+                rf["traffic_over_algorithmic"] = rf["traffic"] / rf["algorithmic_bytes_per_launch"]
         out["roofline"] = rf
     else:
         out["roofline"] = out["env_roofline"]

@@ -43,7 +43,8 @@ int aac_replay_push(float *ring, int32_t row_width, int64_t capacity, int64_t *m
                     const void *const *srcs, const int32_t *widths, const int32_t *dtypes, int32_t E, void *stream);
 /* n_batches independent batches of B distinct indices uniform in [0, meta[1]) (B <= 4096,
  * meta[1] >= B) into idx[n_batches][B]; deterministic in (seed, *counter); *counter (device
- * uint64) is advanced by one per call. */
+ * uint64, < 2^32; its high half counts arriving workgroups inside the launch) is advanced by one per
+ * call in the same launch. */
 int aac_replay_sample(const int64_t *meta, int32_t B, int32_t n_batches, uint64_t seed, uint64_t *counter,
                       int32_t *idx, void *stream);
 /* dsts[f][b][widths[f]] = ring[idx[b]][field f]. */
@@ -64,6 +65,10 @@ int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *st
  * advanced once per captured update after every Adam step that reads it; NULL: no counter). */
 int aac_polyak_flat_step(float *tgt, const float *src, int64_t n, float tau, int32_t *step, int32_t step_add,
                          void *stream);
+/* Both networks' soft updates (critic, actor: ATT/maddpg:436-438) and their step counters in one
+ * launch; the same arithmetic per element as two aac_polyak_flat_step calls. */
+int aac_polyak_flat2(float *tgt1, const float *src1, int64_t n1, int32_t *step1, float *tgt2, const float *src2,
+                     int64_t n2, int32_t *step2, float tau, int32_t step_add, void *stream);
 
 /* Fused activation backward + bias gradient of y = act(x W^T + b) (nn.Linear + ReLU/Tanh of
  * ATT/nets:180-184, ATT/nets:699-701): gm = gy * act'(y) (rows of O at the given strides; gm may
@@ -80,7 +85,9 @@ int aac_bias_act(float *y, const float *b, int64_t M, int32_t O, int32_t act, vo
 /* act [E*N][2] += (float)(randn * var_e); clamp to [-1, 1]; var_e from episode[e] (device):
  * var = noise_start + ((noise_end - noise_start)/(eps_end - 1)) * (ep - 1) if ep <= eps_end else
  * noise_end (get_custom_linear_scaling_factor: end_scale 0 in ATT/maddpg:563-570, 0.03 in
- * MADDPG_ownENV_randomOD_Wgru_radar/maddpg_agent_randomOD_Wgru_radar.py:432-439). */
+ * MADDPG_ownENV_randomOD_Wgru_radar/maddpg_agent_randomOD_Wgru_radar.py:432-439).  Deterministic in
+ * (seed, *counter); *counter (device uint64 < 2^32, as for aac_replay_sample) advances by one per call
+ * in the same launch. */
 int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, int32_t eps_end, float noise_start,
                     float noise_end, uint64_t seed, uint64_t *counter, float *noise_out, void *stream);
 

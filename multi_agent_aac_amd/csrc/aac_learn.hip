@@ -137,6 +137,22 @@ struct Fields {
     int n;
 };
 
+// A launch-wide counter advanced by the launch itself (no one-thread follow-up kernel): word =
+// epoch (low 32 bits) | arrivals (high 32 bits, 0 between launches).  Thread 0 of every workgroup
+// takes the epoch with one atomic add to the arrivals; the last workgroup to arrive has seen every
+// other one take it and stores epoch + 1 with arrivals 0.  Returns the epoch to the whole group.
+__device__ inline uint64_t take_epoch(uint64_t *word) {
+    __shared__ uint64_t ep;
+    if (threadIdx.x == 0) {
+        const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long *>(word), 1ull << 32);
+        ep = old & 0xffffffffull;
+        if ((old >> 32) == (uint64_t)(gridDim.x * gridDim.y * gridDim.z) - 1)
+            atomicExch(reinterpret_cast<unsigned long long *>(word), (unsigned long long)(ep + 1));
+    }
+    __syncthreads();
+    return ep;
+}
+
 __global__ void __launch_bounds__(LEARN_BLOCK) push_kernel(float *ring, int rw, int64_t cap, const int64_t *meta,
                                                           Fields F) {
     const int e = blockIdx.x;
@@ -153,13 +169,6 @@ __global__ void __launch_bounds__(LEARN_BLOCK) push_kernel(float *ring, int rw, 
     }
 }
 
-__global__ void meta_kernel(int64_t *meta, int64_t cap, int E) {
-    meta[0] = (meta[0] + E) % cap;
-    const int64_t s = meta[1] + E;
-    meta[1] = s < cap ? s : cap;
-}
-
-__global__ void counter_kernel(uint64_t *counter) { *counter += 1; }
 
 constexpr int TBL = 8192;
 
@@ -168,15 +177,23 @@ __device__ inline int64_t draw(uint64_t seed, uint64_t ctr, int idx, int att, in
     return (int64_t)(h % (uint64_t)size);
 }
 
+// (an in-kernel advance of meta by the last of the push's E workgroups to arrive measured ~90 us
+// slower per step than this one-thread launch: E same-address atomics)
+__global__ void meta_kernel(int64_t *meta, int64_t cap, int E) {
+    meta[0] = (meta[0] + E) % cap;
+    const int64_t s = meta[1] + E;
+    meta[1] = s < cap ? s : cap;
+}
+
 __global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B, uint64_t seed,
-                                                     const uint64_t *counter, int32_t *out_all) {
+                                                     uint64_t *counter, int32_t *out_all) {
     int32_t *out = out_all + (size_t)blockIdx.x * B;   // one workgroup per batch
     __shared__ int keys[TBL];
     __shared__ int owner[TBL];
     // an empty ring still yields in-range rows (row 0): the host refuses to sample fewer rows than
     // B (DeviceReplay.sample_batch / the learners' plans), this only keeps a bad call in bounds
     const int64_t size = meta[1] > 0 ? meta[1] : 1;
-    const uint64_t ctr = *counter;
+    const uint64_t ctr = take_epoch(counter);     // the counter advances once per launch
     if (size < 2 * (int64_t)B) {
         // few spare rows (size < 2B <= 8192, the first updates after the len(memory) > B guard): a
         // redraw then hits a free row with probability (size - B) / size per round, so draw exactly
@@ -280,6 +297,24 @@ __global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_
 
 // step (optional): the optimiser's device step counter, advanced by step_add in the same launch
 // (the Polyak step is the last reader-free point of an update, ATT/maddpg:436-438)
+// two networks in one launch: workgroups [0, g1) take (tgt1, src1), the rest (tgt2, src2)
+__global__ void polyak2_kernel(float *tgt1, const float *src1, int64_t n1, int32_t *step1, float *tgt2,
+                               const float *src2, int64_t n2, int32_t *step2, int g1, float keep, float tau,
+                               int32_t step_add) {
+    const bool first = (int)blockIdx.x < g1;
+    float *tgt = first ? tgt1 : tgt2;
+    const float *src = first ? src1 : src2;
+    const int64_t n = first ? n1 : n2;
+    int32_t *step = first ? step1 : step2;
+    const int b = first ? blockIdx.x : blockIdx.x - g1, nb = first ? g1 : gridDim.x - g1;
+    if (step && b == 0 && threadIdx.x == 0) step[0] += step_add;
+    for (int64_t i = (int64_t)b * blockDim.x + threadIdx.x; i < n; i += (int64_t)nb * blockDim.x) {
+        const float a = keep * tgt[i];
+        const float c = tau * src[i];
+        tgt[i] = a + c;
+    }
+}
+
 __global__ void polyak_kernel(float *tgt, const float *src, int64_t n, float keep, float tau, int32_t *step,
                               int32_t step_add) {
     if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += step_add;
@@ -366,7 +401,7 @@ __global__ void bias_act_kernel(float *y, const float *__restrict__ b, int64_t n
 __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, int eps_end, float noise_start,
                              float noise_end, uint64_t seed, uint64_t *counter, float *noise_out) {
     const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t ctr = *counter;
+    const uint64_t ctr = take_epoch(counter);     // the counter advances once per launch
     if (row < (int64_t)E * N) {
         const int e = (int)(row / N);
         const int ep = episode ? episode[e] : 1;
@@ -477,7 +512,6 @@ int aac_replay_sample(const int64_t *meta, int32_t B, int32_t nb, uint64_t seed,
     if (B < 1 || B > 4096) return lfail("replay: 1 <= B <= 4096");
     if (nb < 1) return lfail("replay: n_batches >= 1");
     hipLaunchKernelGGL(sample_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, meta, B, seed, counter, idx);
-    hipLaunchKernelGGL(counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
     LHIP(hipGetLastError());
     return 0;
 }
@@ -518,6 +552,17 @@ int aac_polyak_flat_step(float *tgt, const float *src, int64_t n, float tau, int
     return 0;
 }
 
+int aac_polyak_flat2(float *tgt1, const float *src1, int64_t n1, int32_t *step1, float *tgt2, const float *src2,
+                     int64_t n2, int32_t *step2, float tau, int32_t step_add, void *stream) {
+    if (n1 < 1 || n2 < 1) return lfail("polyak_flat2: both networks non-empty");
+    const float keep = (float)(1.0 - (double)tau);
+    const int g1 = grid_for(n1), g2 = grid_for(n2);
+    hipLaunchKernelGGL(polyak2_kernel, dim3(g1 + g2), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, tgt1, src1, n1, step1,
+                       tgt2, src2, n2, step2, g1, keep, tau, step_add);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
 int aac_act_bgrad(const float *gy, int32_t gys, const float *y, int32_t ys, float *gm, int32_t gms, float *db,
                   int32_t M, int32_t O, int32_t act, float *ws, uint32_t *tickets, void *stream) {
     if (M <= 0 || O <= 0) return 0;
@@ -552,7 +597,6 @@ int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, in
     hipLaunchKernelGGL(noise_kernel, dim3((unsigned)((rows + LEARN_BLOCK - 1) / LEARN_BLOCK)), dim3(LEARN_BLOCK), 0,
                        (hipStream_t)stream, act, E, N, episode, eps_end, noise_start, noise_end, seed, counter,
                        noise_out);
-    hipLaunchKernelGGL(counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
     LHIP(hipGetLastError());
     return 0;
 }

@@ -111,6 +111,10 @@ class GemmLaunch:
         self.arr = (GemmProb * self.n)(*probs)
         # algorithmic FLOPs (2 M N K per product; the virtual ones column is the bias gradient)
         self.flops = sum(2.0 * p.M * p.N * p.K for p in probs)
+        # algorithmic HBM bytes: every operand read once, every output (each split-K copy) written once
+        self.bytes = sum(4.0 * (p.M * p.K + p.K * (p.N - p.ones) + max(1, p.ksplit) * p.M * p.N
+                                + (p.M * p.N if p.addend else 0) + (p.M * (p.N - p.ones) if p.mask else 0)
+                                + (p.N if p.bias else 0)) for p in probs)
 
     def __call__(self):
         _chk(lib().aac_gemm_batch(self.arr, self.n, _stream()), "aac_gemm_batch")
@@ -421,8 +425,8 @@ class FusedUpdate:
                           + self._adam(m.actor_optimizer, m.fa, self.ga, self.SPLIT_ACTOR, i + 1)
                           for i in range(N)]
         # the Polyak launches also advance the optimisers' step counters (no separate add kernels)
-        self.post = [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau, m.critic_optimizer.step_t, N),
-                     lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau, m.actor_optimizer.step_t, N)]
+        self.post = [lambda: ops.polyak_flat2(m.fc_t.data, m.fc.data, m.critic_optimizer.step_t, m.fa_t.data,
+                                              m.fa.data, m.actor_optimizer.step_t, m.tau, N)]
         self.n_launches = len(self.pre) + sum(len(it) for it in self.iters) + len(self.post)
 
     def _adam(self, opt, flat, gpart, ns, step_add):

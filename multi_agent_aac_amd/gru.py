@@ -326,8 +326,8 @@ class GruUpdate:
         L += self._adam(m.actor_optimizer, m.fa)
         # ---------------- soft update of every target (WGRU/maddpg:318-322)
         # (the Polyak launches also advance the optimisers' step counters)
-        L += [lambda: ops.polyak_flat(m.fc_t.data, m.fc.data, m.tau, m.critic_optimizer.step_t, 1),
-              lambda: ops.polyak_flat(m.fa_t.data, m.fa.data, m.tau, m.actor_optimizer.step_t, 1)]
+        L += [lambda: ops.polyak_flat2(m.fc_t.data, m.fc.data, m.critic_optimizer.step_t, m.fa_t.data, m.fa.data,
+                                       m.actor_optimizer.step_t, m.tau, 1)]
         self.L = L
 
     def ops(self):

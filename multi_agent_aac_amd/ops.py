@@ -31,6 +31,7 @@ def lib():
         L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
         L.aac_polyak_flat.argtypes = [vp, vp, i64, f32, vp]
         L.aac_polyak_flat_step.argtypes = [vp, vp, i64, f32, vp, i32, vp]
+        L.aac_polyak_flat2.argtypes = [vp, vp, i64, vp, vp, vp, i64, vp, f32, i32, vp]
         L.aac_noise_clamp.argtypes = [vp, i32, i32, vp, i32, f32, f32, u64, vp, vp, vp]
         L.aac_act_bgrad.argtypes = [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, vp]
         L.aac_bias_act.argtypes = [vp, vp, i64, i32, i32, vp]
@@ -118,6 +119,12 @@ def bias_act(y, b, act):
 def adam_flat(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     _chk(lib().aac_adam_flat(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), lr, beta1, beta2,
                              eps, _p(step), _s()), "aac_adam_flat")
+
+
+def polyak_flat2(t1, s1, step1, t2, s2, step2, tau, step_add):
+    """Both networks' soft updates and step counters in one launch (aac_polyak_flat2)."""
+    _chk(lib().aac_polyak_flat2(_p(t1), _p(s1), t1.numel(), _p(step1), _p(t2), _p(s2), t2.numel(), _p(step2), tau,
+                                step_add, _s()), "aac_polyak_flat2")
 
 
 def polyak_flat(target, source, tau, step=None, step_add=0):

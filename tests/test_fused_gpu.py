@@ -43,12 +43,12 @@ LDS_CASES = {(1024, 640, 256), (5120, 64, 64), (25600, 256, 192), (20480, 130, 6
              (96, 100, 100), (200, 132, 68), (1000, 36, 260), (5120, 256, 640), (130, 70, 300),
              (256, 300, 64), (192, 64, 96), (32, 200, 128)}
 
-
-@pytest.fixture(params=[0, 1, 2, 3], ids=["t64x64", "t64x32", "t32x64", "t32x32"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["t64x64", "t64x32", "t32x64", "t32x32", "registers"])
 def lds_everywhere(request):
-    """Every eligible product on the given LDS workgroup tile, whatever its size."""
+    """Every eligible product on the given LDS workgroup tile, whatever its size; or ("registers")
+    none, so every product takes the register path."""
     from multi_agent_aac_amd import fused
-    fused.set_lds_policy(-1 - request.param)
+    fused.set_lds_policy(-1 - request.param if request.param < 4 else 1 << 30)
     yield request.param
     fused.set_lds_policy()
 
@@ -71,8 +71,11 @@ def test_gemm_batch_epilogues(native_lib, lds_everywhere, case):
                    mact=mact, ones=ones, cextra=fused.ptr(cextra))
     launch = fused.GemmLaunch([p])
     cfg = launch.plan()[0][0]
-    assert (cfg > 0) == ((M, N, K) in LDS_CASES), launch.plan()
-    assert cfg == 0 or (cfg - 1) >> 2 == lds_everywhere
+    if lds_everywhere < 4:
+        assert (cfg > 0) == ((M, N, K) in LDS_CASES), launch.plan()
+        assert cfg == 0 or (cfg - 1) >> 2 == lds_everywhere
+    else:
+        assert cfg == 0
     launch()
     prod = _op(A.double(), ta) @ _op(B.double(), tb)
     want = prod.clone()
@@ -129,7 +132,7 @@ def test_gemm_split_copies(native_lib, lds_everywhere, N):
     part = torch.full((S, stride), 3.0, device=DEV)
     launch = fused.GemmLaunch([fused.prob(fused.ptr(G), fused.ptr(X), fused.ptr(part), M, N, K, M, N, N, ta=1, ones=1,
                                           cextra=fused.ptr(part, M * N), ksplit=S, split_stride=stride)])
-    assert (launch.plan()[0][0] > 0) == (N % 4 == 0)
+    assert (launch.plan()[0][0] > 0) == (N % 4 == 0 and lds_everywhere < 4)
     launch()
     tot = part.double().sum(0)
     np.testing.assert_allclose(tot[:M * N].reshape(M, N).cpu(), (G.double().t() @ X.double()).cpu(), atol=2e-4)

@@ -136,6 +136,14 @@ def test_adam_polyak_flat(native_lib):
     td2 = tgt.to(DEV)
     ops.polyak_flat(td2, src.to(DEV), 0.01, step, 5)
     assert torch.equal(td2, td) and int(step.item()) == 10
+    # both networks in one launch: bit-equal to two single-network launches, both counters advanced
+    t1, s1, t2, s2 = (torch.randn(k, device=DEV) for k in (n, n, 3 * n + 7, 3 * n + 7))
+    w1, w2 = t1.clone(), t2.clone()
+    st1, st2 = torch.zeros(1, dtype=torch.int32, device=DEV), torch.full((1,), 3, dtype=torch.int32, device=DEV)
+    ops.polyak_flat(w1, s1, 0.01)
+    ops.polyak_flat(w2, s2, 0.01)
+    ops.polyak_flat2(t1, s1, st1, t2, s2, st2, 0.01, 5)
+    assert torch.equal(t1, w1) and torch.equal(t2, w2) and int(st1.item()) == 5 and int(st2.item()) == 8
 
 
 def test_noise_clamp_schedule(native_lib):
