@@ -84,6 +84,24 @@ int aac_adam_flat_sum_strided(float *p, const float *gpart, int32_t ns, int64_t 
                               float *v, int64_t n, float lr, float b1, float b2, float eps, const int32_t *step,
                               int32_t step_add, void *stream);
 
+/* One network's Adam job for aac_adam_flat_sum_pair (arguments as aac_adam_flat_sum_strided). */
+typedef struct aac_adam_job {
+    float *param;
+    const float *gpart;
+    int32_t nsplit;
+    int64_t gstride;
+    float *grad_out;
+    float *exp_avg, *exp_avg_sq;
+    int64_t n;
+    float lr, beta1, beta2, eps;
+    const int32_t *step;
+    int32_t step_add;
+} aac_adam_job;
+/* Two networks' Adam steps over split-K copies in one launch (the copy-parallel kernel for both:
+ * nsplit >= 2, gstride % 4 == 0, 16-B aligned copies; AAC_ADAM4 on); each job's arithmetic is
+ * that of aac_adam_flat_sum_strided. */
+int aac_adam_flat_sum_pair(const aac_adam_job *a, const aac_adam_job *b, void *stream);
+
 /* out[i] = sum_{s < nsplit} gpart[s*n + i] in split order (before a gradient all-reduce). */
 int aac_sum_partials(float *out, const float *gpart, int32_t nsplit, int64_t n, void *stream);
 int aac_sum_partials_strided(float *out, const float *gpart, int32_t nsplit, int64_t gstride, int64_t n, void *stream);

@@ -728,34 +728,53 @@ __device__ __forceinline__ f4 copy_sum4(const float *__restrict__ gpart, int ns,
     return acc;
 }
 
-__global__ void __launch_bounds__(256) adam_sum4_kernel(float *p, const float *__restrict__ gpart, int ns, int64_t gs,
-                                                        float *gout, float *m, float *v, int64_t n, float lr, float b1,
-                                                        float b2, float eps, const int32_t *step, int step_add) {
+struct Adam4 {         // one network's Adam over its split-K copies (copy stride gs % 4 == 0)
+    float *p;
+    const float *gpart;
+    float *gout, *m, *v;
+    const int32_t *step;
+    int64_t gs, n;
+    float lr, b1, b2, eps;
+    int ns, step_add;
+};
+
+// the copy-parallel Adam of one network by workgroups blk = 0 .. nblk-1
+__device__ __forceinline__ void adam4_body(const Adam4 &P, int64_t blk, int64_t nblk) {
     const int lane = threadIdx.x & 63, g = lane >> 4, e4 = lane & 15;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (int64_t)gridDim.x * 4;
-    const int t = *step + step_add;
-    const double bc1 = 1.0 - pow((double)b1, (double)t);
-    const double bc2 = 1.0 - pow((double)b2, (double)t);
-    const float step_size = (float)((double)lr / bc1);
+    const int64_t wave = blk * 4 + (threadIdx.x >> 6), nwaves = nblk * 4;
+    const int t = *P.step + P.step_add;
+    const double bc1 = 1.0 - pow((double)P.b1, (double)t);
+    const double bc2 = 1.0 - pow((double)P.b2, (double)t);
+    const float step_size = (float)((double)P.lr / bc1);
     const float bc2s = (float)sqrt(bc2);
-    const float w1 = (float)(1.0 - (double)b1), w2 = (float)(1.0 - (double)b2);
-    for (int64_t base = wave * 64; base < n; base += nwaves * 64) {
+    const float w1 = (float)(1.0 - (double)P.b1), w2 = (float)(1.0 - (double)P.b2);
+    const float b2 = P.b2, eps = P.eps;
+    for (int64_t base = wave * 64; base < P.n; base += nwaves * 64) {
         const int64_t i = base + 4 * e4;
-        const f4 acc = copy_sum4(gpart, ns, gs, i < n ? i : 0, g);
+        const f4 acc = copy_sum4(P.gpart, P.ns, P.gs, i < P.n ? i : 0, g);
         const int64_t k = i + g;
-        if (k < n) {
+        if (k < P.n) {
             const float gi = g == 0 ? acc.x : (g == 1 ? acc.y : (g == 2 ? acc.z : acc.w));
-            if (gout) gout[k] = gi;
-            float mi = m[k];
+            if (P.gout) P.gout[k] = gi;
+            float mi = P.m[k];
             mi = mi + w1 * (gi - mi);
-            float vi = v[k] * b2;
+            float vi = P.v[k] * b2;
             vi = vi + w2 * (gi * gi);
             const float den = sqrtf(vi) / bc2s + eps;
-            p[k] = p[k] + (-step_size) * (mi / den);
-            m[k] = mi;
-            v[k] = vi;
+            P.p[k] = P.p[k] + (-step_size) * (mi / den);
+            P.m[k] = mi;
+            P.v[k] = vi;
         }
     }
+}
+
+__global__ void __launch_bounds__(256) adam_sum4_kernel(Adam4 P) { adam4_body(P, blockIdx.x, gridDim.x); }
+
+// two networks in one launch (the critic step of iteration i+1 and the actor step of iteration i
+// end together): workgroups [0, g1) take the first, the rest the second
+__global__ void __launch_bounds__(256) adam_sum4_pair_kernel(Adam4 P0, Adam4 P1, int g1) {
+    if ((int)blockIdx.x < g1) adam4_body(P0, blockIdx.x, g1);
+    else adam4_body(P1, blockIdx.x - g1, gridDim.x - g1);
 }
 
 __global__ void __launch_bounds__(256) sum_partials4_kernel(float *out, const float *__restrict__ gpart, int ns,
@@ -1861,12 +1880,30 @@ int aac_adam_flat_sum_strided(float *p, const float *gpart, int32_t ns, int64_t 
     if (ns < 1) return ffail("adam_flat_sum: nsplit >= 1");
     if (gstride < n) return ffail("adam_flat_sum: copy stride < n");
     if (use_sum4(gpart, ns, gstride)) {
-        hipLaunchKernelGGL(adam_sum4_kernel, dim3(sum4_grid(n)), dim3(256), 0, (hipStream_t)stream, p, gpart, ns, gstride,
-                           gout, m, v, n, lr, b1, b2, eps, step, step_add);
+        const Adam4 P{p, gpart, gout, m, v, step, gstride, n, lr, b1, b2, eps, ns, step_add};
+        hipLaunchKernelGGL(adam_sum4_kernel, dim3(sum4_grid(n)), dim3(256), 0, (hipStream_t)stream, P);
     } else {
         hipLaunchKernelGGL(adam_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, gpart, ns, gstride, gout,
                            m, v, n, lr, b1, b2, eps, step, step_add);
     }
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_adam_flat_sum_pair(const aac_adam_job *a, const aac_adam_job *b, void *stream) {
+    if (!a || !b) return ffail("adam_flat_sum_pair: two jobs");
+    const aac_adam_job *jj[2] = {a, b};
+    Adam4 P[2];
+    for (int q = 0; q < 2; ++q) {
+        const aac_adam_job &j = *jj[q];
+        if (j.nsplit < 2 || j.gstride < j.n || !use_sum4(j.gpart, j.nsplit, j.gstride) || j.n < 1)
+            return ffail("adam_flat_sum_pair: each job needs >= 2 copies at a 16-B aligned stride >= n "
+                         "(else two aac_adam_flat_sum_strided calls)");
+        P[q] = Adam4{j.param, j.gpart, j.grad_out, j.exp_avg, j.exp_avg_sq, j.step, j.gstride, j.n, j.lr, j.beta1,
+                     j.beta2, j.eps, j.nsplit, j.step_add};
+    }
+    const int g1 = sum4_grid(a->n), g2 = sum4_grid(b->n);
+    hipLaunchKernelGGL(adam_sum4_pair_kernel, dim3(g1 + g2), dim3(256), 0, (hipStream_t)stream, P[0], P[1], g1);
     FHIP(hipGetLastError());
     return 0;
 }

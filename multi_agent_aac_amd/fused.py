@@ -58,6 +58,7 @@ def lib():
         L.aac_adam_flat_sum.argtypes = [vp, vp, i32, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         L.aac_sum_partials.argtypes = [vp, vp, i32, i64, vp]
         L.aac_sum_partials_strided.argtypes = [vp, vp, i32, i64, i64, vp]
+        L.aac_adam_flat_sum_pair.argtypes = [ctypes.POINTER(AdamJob), ctypes.POINTER(AdamJob), vp]
         L.aac_adam_flat_sum_strided.argtypes = [vp, vp, i32, i64, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         L.aac_critic_head.argtypes = [vp, i32, i32, vp, vp, i32, vp, vp, vp, i32, i32, f32, vp, vp, vp, vp, vp]
         L.aac_replay_gather_strided.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp]
@@ -164,6 +165,32 @@ def adam_sum(opt, gpart, nsplit, step_add, grad_out=None):
                                          vp(opt.exp_avg.data_ptr()), vp(opt.exp_avg_sq.data_ptr()),
                                          opt.flat.data.numel(), opt.lr, opt.betas[0], opt.betas[1], opt.eps,
                                          vp(opt.step_t.data_ptr()), step_add, _stream()), "aac_adam_flat_sum")
+
+
+class AdamJob(ctypes.Structure):
+    _fields_ = [("param", vp), ("gpart", vp), ("nsplit", i32), ("gstride", i64), ("grad_out", vp), ("exp_avg", vp),
+                ("exp_avg_sq", vp), ("n", i64), ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32),
+                ("step", vp), ("step_add", i32)]
+
+
+def _adam_job(opt, gpart, nsplit, step_add, grad_out):
+    return AdamJob(vp(opt.flat.data.data_ptr()), vp(gpart.data_ptr()), nsplit, gpart.shape[-1],
+                   vp(grad_out.data_ptr()) if grad_out is not None else None, vp(opt.exp_avg.data_ptr()),
+                   vp(opt.exp_avg_sq.data_ptr()), opt.flat.data.numel(), opt.lr, opt.betas[0], opt.betas[1], opt.eps,
+                   vp(opt.step_t.data_ptr()), step_add)
+
+
+def adam_pair_ok(*gparts):
+    """aac_adam_flat_sum_pair's conditions: the copy-parallel Adam (AAC_ADAM4) over >= 2 copies at
+    a 16-B aligned stride."""
+    return os.environ.get("AAC_ADAM4", "1") != "0" and all(
+        g.shape[0] >= 2 and g.shape[-1] % 4 == 0 and g.data_ptr() % 16 == 0 for g in gparts)
+
+
+def adam_sum_pair(a, b):
+    """Two networks' adam_sum steps in one launch; a, b = (opt, gpart, nsplit, step_add, grad_out)."""
+    ja, jb = _adam_job(*a), _adam_job(*b)
+    _chk(lib().aac_adam_flat_sum_pair(ctypes.byref(ja), ctypes.byref(jb), _stream()), "aac_adam_flat_sum_pair")
 
 
 def sum_partials(out, gpart, nsplit):
@@ -350,6 +377,10 @@ class FusedUpdate:
     # world == 1: run the critic step of iteration i+1 beside the actor step of iteration i on a
     # second stream of the captured graph (AAC_OVERLAP=1; measured slower, off: DESIGN section 4)
     OVERLAP = os.environ.get("AAC_OVERLAP", "0") == "1"
+    # world == 1: the same independence used to merge launches instead -- the critic step of
+    # iteration i+1 zipped stage by stage with the actor forward + step of iteration i in shared
+    # grouped-GEMM launches, both Adam steps in one launch (AAC_MERGED=0: the serial order)
+    MERGED = os.environ.get("AAC_MERGED", "1") == "1"
 
     def __init__(self, model, replay, B):
         self.m, self.rep, self.B = model, replay, B
@@ -380,7 +411,7 @@ class FusedUpdate:
         # critic-step activation sets [f, h, dq, dh, df]: [0] is shared with the actor step; world > 1
         # runs the critic step of iteration i+1 beside the actor step of i, in set [1]
         self.cbuf = [(self.f, self.h, self.dq, self.dh, self.df)]
-        if model.world > 1 or self.OVERLAP:
+        if model.world > 1 or self.OVERLAP or self.MERGED:
             self.cbuf.append((z(B, 128 * N), z(B, 256), z(B), z(B, 256), z(B, 128 * N)))
         R = B * N
         self.dout, self.dha = z(R, 2), z(R, 256)
@@ -418,6 +449,8 @@ class FusedUpdate:
         elif self.OVERLAP:
             self.segs = self._overlapped(A, C)
             self.iters = [a + b + j for a, b, j in self.segs]
+        elif self.MERGED:
+            self.iters = self._merged(A, C)
         else:
             self.iters = [self._critic_step(i, A, C, self.cbuf[0], fuse_actor_fwd=True)
                           + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, i + 1)
@@ -432,6 +465,60 @@ class FusedUpdate:
     def _adam(self, opt, flat, gpart, ns, step_add):
         """world == 1: the Adam step sums the split-K partial copies itself."""
         return [lambda: adam_sum(opt, gpart, ns, step_add, grad_out=flat.grad)]
+
+    def _adam_pair(self, i_critic, i_actor):
+        """Critic Adam step i_critic + 1 and actor Adam step i_actor + 1 as one launch (or two)."""
+        m = self.m
+        ca = (m.critic_optimizer, self.gc, self.SPLIT_CRITIC, i_critic + 1, m.fc.grad)
+        aa = (m.actor_optimizer, self.ga, self.SPLIT_ACTOR, i_actor + 1, m.fa.grad)
+        if adam_pair_ok(self.gc, self.ga):
+            return [lambda: adam_sum_pair(ca, aa)]
+        return [lambda: adam_sum(*ca[:4], grad_out=ca[4]), lambda: adam_sum(*aa[:4], grad_out=aa[4])]
+
+    def _merged(self, A, C):
+        """world == 1: fewer, fuller launches.  The critic step of iteration i+1 reads the critic
+        weights after critic Adam step i (and the fixed targets) -- exactly what the actor step of
+        iteration i reads -- and neither reads the other's result (as in ``_pipelined``).  So
+        segment i+1 zips the actor forward + actor step of iteration i with the critic step of
+        iteration i+1 (activation set 1) stage by stage into shared grouped-GEMM launches and ends
+        with both Adam steps in one launch.  Every product's arithmetic is unchanged, so the
+        update is bit-identical to the serial order (tests/test_fused_gpu.py)."""
+        m, N = self.m, self.N
+        segs = [self._critic_step(0, A, C, self.cbuf[1], fuse_actor_fwd=True)
+                + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, 1)]
+        for i in range(N):
+            cs = self._critic_stages(i + 1, C, self.cbuf[1]) if i + 1 < N else None
+            ac = self._actor_stages(i, A, C)
+            if i > 0:
+                a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+            else:     # iteration 0's actor forward ran inside the critic step 0 launches
+                a_enc, a_attn, a_merge, a_out = [], None, [], []
+            L = []
+            if cs is None:
+                L += gemm_launches(a_enc) + ([a_attn] if a_attn else []) + gemm_launches(a_merge)
+                L += gemm_launches(a_out)
+                L += gemm_launches(ac["cenc"]) + gemm_launches(ac["ccomb"])
+            else:
+                L += gemm_launches(a_enc + cs["enc"])
+                if a_attn:
+                    L.append(a_attn)
+                L += gemm_launches(a_merge + cs["comb"])
+                L.append(cs["head"])
+                L += gemm_launches(a_out + cs["grad"])
+                L += gemm_launches(ac["cenc"] + cs["encw"])
+                L += gemm_launches(ac["ccomb"])
+            L.append(ac["head"])
+            L += gemm_launches(ac["dcomb"])
+            L.append(ac["aob"])
+            L += gemm_launches(ac["wgrad1"])
+            L.append(ac["attn_bwd"])
+            L += gemm_launches(ac["wgrad2"])
+            if cs is not None:
+                L += self._adam_pair(i + 1, i)
+            else:
+                L += self._adam(m.actor_optimizer, m.fa, self.ga, self.SPLIT_ACTOR, i + 1)
+            segs.append(L)
+        return segs
 
     def _overlapped(self, A, C):
         """world == 1: the update as segments (branch A, branch B, join).  The critic step of
@@ -529,36 +616,60 @@ class FusedUpdate:
         With ``fuse_actor_fwd`` the actor forward of the same iteration (ATT/maddpg:389-392) --
         which depends only on the actor weights, changed after the critic step -- shares the
         critic step's launches; the policy actions land in X2 (own columns gathered there too)."""
-        m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
-        SC, nC = self.SPLIT_CRITIC, self.gc.shape[1]     # copy stride
-        gC = CriticParams(m.critics, m.fc, self.gc.data_ptr())
-        X, _, _, _, y = self._batch_ptrs(i)
-        f, h, dq, dh, df = cb
         if fuse_actor_fwd:
             a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
         else:
             a_enc, a_attn, a_merge, a_out = [], None, [], []
-        c_enc, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
-        L = gemm_launches(c_enc + a_enc)
+        cs = self._critic_stages(i, C, cb)
+        L = gemm_launches(cs["enc"] + a_enc)
         if a_attn is not None:
             L.append(a_attn)
-        L += gemm_launches(c_comb)
-        L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh)))
-        L += gemm_launches([
+        L += gemm_launches(cs["comb"])
+        L.append(cs["head"])
+        L += gemm_launches(cs["grad"] + a_merge)
+        L += gemm_launches(cs["encw"] + a_out)
+        return L
+
+    def _critic_stages(self, i, C, cb):
+        """The critic step of iteration i as dependent stages: product lists enc, comb, grad
+        (weight gradients of the head and combine, data gradient of the combine), encw (encoder
+        weight gradients) and the head callable (mse gradient) between comb and grad."""
+        m, B, N, Din = self.m, self.B, self.N, self.Din
+        SC, nC = self.SPLIT_CRITIC, self.gc.shape[1]     # copy stride
+        gC = CriticParams(m.critics, m.fc, self.gc.data_ptr())
+        X, _, _, _, y = self._batch_ptrs(i)
+        f, h, dq, dh, df = cb
+        c_enc, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
+        head = lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq),  # noqa: E731
+                                   dh=ptr(dh))
+        grad = [
             prob(ptr(dq), ptr(h), gC.Wq, 1, 256, B, 1, 256, 256, ta=1, ones=1, cextra=gC.bq, ksplit=SC,
                  split_stride=nC),
             prob(ptr(dh), ptr(f), gC.Wc, 256, 128 * N, B, 256, 128 * N, 128 * N, ta=1, ones=1, cextra=gC.bc,
                  ksplit=SC, split_stride=nC),
             prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f), ldmask=128 * N,
-                 mact=RELU)] + a_merge)
-        L += gemm_launches([prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din,
-                                 Din, ta=1, ones=1, cextra=gC.enc_b[n], ksplit=SC, split_stride=nC)
-                            for n in range(N)] + a_out)
-        return L
+                 mact=RELU)]
+        encw = [prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din, Din, ta=1, ones=1,
+                     cextra=gC.enc_b[n], ksplit=SC, split_stride=nC) for n in range(N)]
+        return {"enc": c_enc, "comb": c_comb, "head": head, "grad": grad, "encw": encw}
 
     def _actor_step(self, i, A, C):
         """Actor step of iteration i (ATT/maddpg:389-425) after its forward, up to the weight-
         gradient partials: critic on the policy actions, backward into the actor."""
+        st = self._actor_stages(i, A, C)
+        L = gemm_launches(st["cenc"]) + gemm_launches(st["ccomb"])
+        L.append(st["head"])
+        L += gemm_launches(st["dcomb"])
+        L.append(st["aob"])
+        L += gemm_launches(st["wgrad1"])
+        L.append(st["attn_bwd"])
+        L += gemm_launches(st["wgrad2"])
+        return L
+
+    def _actor_stages(self, i, A, C):
+        """The actor step of iteration i after its forward, as dependent stages: cenc, ccomb
+        (critic on the policy actions), head (-mean Q gradient), dcomb, aob (actor output
+        backward), wgrad1, attn_bwd, wgrad2."""
         m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
         R = B * N
         SA, nA = self.SPLIT_ACTOR, self.ga.shape[1]
@@ -566,14 +677,15 @@ class FusedUpdate:
         _, X, radar, nei, _ = self._batch_ptrs(i)
         f, h, dq, dh, df = self.cbuf[0]
         c = self.acts
-        L = critic_forward(C, X, B, N, Din, f, h)
-        L.append(lambda: critic_head(ptr(h), B, C.Wq, C.bq, 1, q=ptr(self.q_a, i * B), dh=ptr(dh)))
-        L += gemm_launches([prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f),
-                                 ldmask=128 * N, mact=RELU)])
+        st = {}
+        st["cenc"], st["ccomb"] = critic_forward_stages(C, X, B, N, Din, f, h)
+        st["head"] = lambda: critic_head(ptr(h), B, C.Wq, C.bq, 1, q=ptr(self.q_a, i * B), dh=ptr(dh))
+        st["dcomb"] = [prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f),
+                            ldmask=128 * N, mact=RELU)]
         # da_n = df_n . W_enc_n[:, D0:D0+2]; dout = da * (1 - a^2); dh_a = (dout Wa) * (h_a > 0)
-        L.append(lambda: actor_out_bwd(ptr(df), 128 * N, C.enc_w[0], Din, D0, X, A.Wa, ptr(c.ha), N, R,
-                                       ptr(self.dout), ptr(self.dha)))
-        L += gemm_launches([
+        st["aob"] = lambda: actor_out_bwd(ptr(df), 128 * N, C.enc_w[0], Din, D0, X, A.Wa, ptr(c.ha), N, R,  # noqa: E731
+                                          ptr(self.dout), ptr(self.dha))
+        st["wgrad1"] = [
             prob(ptr(self.dout), ptr(c.ha), gA.Wa, 2, 256, R, 2, 256, 256, ta=1, ones=1, cextra=gA.ba, ksplit=SA,
                  split_stride=nA),
             prob(ptr(self.dha), ptr(c.cat), gA.Wm, 256, 192, R, 256, 192, 192, ta=1, ones=1, cextra=gA.bm,
@@ -581,11 +693,11 @@ class FusedUpdate:
             prob(ptr(self.dha), A.Wm, ptr(self.dcat_o), R, 64, 256, 256, 192, 64),
             prob(ptr(self.dha), A.Wm + 4 * 64, ptr(self.dcat_g), R, 64, 256, 256, 192, 64, mask=ptr(c.cat, 64),
                  ldmask=192, mact=RELU),
-            prob(ptr(self.dha), A.Wm + 4 * 128, ptr(self.dv), R, 64, 256, 256, 192, 64)])
-        L.append(lambda: attn_train_bwd(ptr(self.dv), 64, ptr(c.xn), ptr(c.alpha), ptr(c.qk), ptr(c.cat), 192,
-                                        ptr(self.dcat_o), 64, A.Wq, A.Wkv, A.Wkv + 4 * 64 * 64, ptr(self.dxn),
-                                        ptr(self.dqk), ptr(self.dqa), ptr(self.deo), R, K))
-        L += gemm_launches([
+            prob(ptr(self.dha), A.Wm + 4 * 128, ptr(self.dv), R, 64, 256, 256, 192, 64)]
+        st["attn_bwd"] = lambda: attn_train_bwd(  # noqa: E731
+            ptr(self.dv), 64, ptr(c.xn), ptr(c.alpha), ptr(c.qk), ptr(c.cat), 192, ptr(self.dcat_o), 64, A.Wq, A.Wkv,
+            A.Wkv + 4 * 64 * 64, ptr(self.dxn), ptr(self.dqk), ptr(self.dqa), ptr(self.deo), R, K)
+        st["wgrad2"] = [
             prob(ptr(self.dv), ptr(c.xb), gA.Wkv + 4 * 64 * 64, 64, 64, R, 64, 64, 64, ta=1, ksplit=SA,
                  split_stride=nA),                                                         # dWv
             prob(ptr(c.qa), ptr(self.dqk), gA.Wkv, 64, 64, R, 64, 64, 64, ta=1, ksplit=SA, split_stride=nA),  # dWk
@@ -595,8 +707,8 @@ class FusedUpdate:
             prob(ptr(self.deo), X, gA.Wo, 64, D0, R, 64, Din, D0, ta=1, ones=1, cextra=gA.bo, ksplit=SA,
                  split_stride=nA),
             prob(ptr(self.dcat_g), radar, gA.Wg, 64, 18, R, 64, 18, 18, ta=1, ones=1, cextra=gA.bg, ksplit=SA,
-                 split_stride=nA)])
-        return L
+                 split_stride=nA)]
+        return st
 
     # ------------------------------------------------------------------ run
     def ops(self):
