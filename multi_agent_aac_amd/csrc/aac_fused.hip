@@ -590,9 +590,54 @@ __device__ __forceinline__ void gemm_lds(const GProb &P, int local, float *smem)
     aacw::lds_barrier();
     float *C = P.C ? P.C + (int64_t)s * P.sstride : nullptr;
     float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
+    constexpr int RPI = 256 / (BN / 4);          // rows per pass; a thread keeps its 4 columns
+    const int c4 = (threadIdx.x % (BN / 4)) * 4, r0 = threadIdx.x / (BN / 4);
+    if (P.vec && m0 + BM <= P.M && n0 + BN <= nreal) {
+        // interior tile, 16-B rows: the bias once, every pass's addend / mask loads issued before
+        // the first store (element-by-element the loop waited on each load in turn)
+        f4 bias = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (P.bias) bias = *reinterpret_cast<const f4 *>(P.bias + n0 + c4);
+        f4 add[BM / RPI], msk[BM / RPI];
 #pragma unroll
-    for (int q = threadIdx.x; q < BM * BN / 4; q += 256) {
-        const int rr = q / (BN / 4), c4 = (q % (BN / 4)) * 4;
+        for (int it = 0; it < BM / RPI; ++it) {
+            const int m = m0 + r0 + RPI * it;
+            add[it] = P.addend ? *reinterpret_cast<const f4 *>(P.addend + (size_t)m * P.ldadd + n0 + c4)
+                               : f4{0.0f, 0.0f, 0.0f, 0.0f};
+            msk[it] = P.mact ? *reinterpret_cast<const f4 *>(P.mask + (size_t)m * P.ldmask + n0 + c4)
+                             : f4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int it = 0; it < BM / RPI; ++it) {
+            const int rr = r0 + RPI * it;
+            f4 x = *reinterpret_cast<const f4 *>(ct + rr * (BN + 4) + c4);
+            // the operation order of epilogue(): addend, then bias, then the activations
+            if (P.addend) x += add[it];
+            if (P.bias) x += bias;
+            if (P.act == 1) {
+                x.x = x.x > 0.0f ? x.x : 0.0f;
+                x.y = x.y > 0.0f ? x.y : 0.0f;
+                x.z = x.z > 0.0f ? x.z : 0.0f;
+                x.w = x.w > 0.0f ? x.w : 0.0f;
+            } else if (P.act == 2) {
+                x = f4{tanhf(x.x), tanhf(x.y), tanhf(x.z), tanhf(x.w)};
+            }
+            const f4 t = msk[it];
+            if (P.mact == 1) {
+                x.x = t.x > 0.0f ? x.x : 0.0f;
+                x.y = t.y > 0.0f ? x.y : 0.0f;
+                x.z = t.z > 0.0f ? x.z : 0.0f;
+                x.w = t.w > 0.0f ? x.w : 0.0f;
+            } else if (P.mact == 2) {
+                x = f4{x.x * (1.0f - t.x * t.x), x.y * (1.0f - t.y * t.y), x.z * (1.0f - t.z * t.z),
+                       x.w * (1.0f - t.w * t.w)};
+            }
+            *reinterpret_cast<f4 *>(C + (size_t)(m0 + rr) * P.ldc + n0 + c4) = x;
+        }
+        return;
+    }
+#pragma unroll
+    for (int it = 0; it < BM / RPI; ++it) {
+        const int rr = r0 + RPI * it;
         const f4 x = *reinterpret_cast<const f4 *>(ct + rr * (BN + 4) + c4);
         const float v[4] = {x.x, x.y, x.z, x.w};
         epilogue4(P, C, cx, m0 + rr, n0 + c4, v);
