@@ -25,3 +25,17 @@ def native_lib():
 def occ():
     from multi_agent_aac_amd import world
     return world.synthetic_map(2026)
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _drain_device_between_modules():
+    """After each GPU test module: finish the device's queued work, then collect the module's
+    native handles and captured graphs, so that no finaliser (env destroy, graph release) runs at
+    an arbitrary garbage-collection point while launches that use their memory are in flight."""
+    yield
+    import gc
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        gc.collect()
+        torch.cuda.synchronize()
