@@ -96,6 +96,9 @@ __device__ bool building_hit(double px, double py, double cx, double cy, double 
         if (dist > pb * (1.0 + 1e-12) + 1e-12) return false;
         if (dist < pb * c_tab.apothem * (1.0 - 1e-12) - 1e-12) return true;
     }
+    // not unrolled: unrolled, the compiler hoisted the 32 loop-invariant limits out of the caller's
+    // cell loop and kept them live across the whole agent phase (64 VGPRs, spilled to scratch)
+#pragma unroll 1
     for (int k = 0; k < 32; ++k) {
         double proj = fabs(dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k]);
         double lim = 5.0 * (fabs(c_tab.nrm_c[k]) + fabs(c_tab.nrm_s[k])) + pb * c_tab.apothem;
@@ -500,7 +503,14 @@ __device__ inline void store_rows(float *dst, const float *src, int n) {
 // Phases: (1) kinematics, one thread per agent; (2) radar, one work item per (agent, ray) over
 // all 256 threads; (3) observation + ss_reward predicates, one thread per agent; (4) team reward
 // and episode termination, one thread per env.
-__global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args A, const float2 *__restrict__ act) {
+// One instantiation per (env variant, radar mode): the other variant's reward code and the unused
+// radar path are compiled out, which keeps the kernel inside its 128-VGPR budget (the run-time
+// branches cost ~66 spilled VGPRs / 240 B of scratch per lane).
+template <int VAR, int RM>
+__global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain, const float2 *__restrict__ act) {
+    Args A = Ain;
+    A.variant = VAR;
+    A.radar_mode = RM;
     __shared__ Lds S;
     const int N = A.N;
     const int nag = A.epb * N;
@@ -1012,8 +1022,14 @@ int aac_env_step(aac_env *h, const float *actions, const aac_step_out *o, void *
     if (rc) return rc;
     if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return fail(AAC_E_INVALID, "step outputs");
     Args A = make_args(h, o);
-    hipLaunchKernelGGL(step_kernel, dim3(h->blocks), dim3(BLOCK), map_bytes(h), (hipStream_t)stream, A,
-                       reinterpret_cast<const float2 *>(actions));
+    const dim3 grid(h->blocks), block(BLOCK);
+    const size_t lds = map_bytes(h);
+    const hipStream_t st = (hipStream_t)stream;
+    const float2 *a2 = reinterpret_cast<const float2 *>(actions);
+    if (A.variant) hipLaunchKernelGGL((step_kernel<1, AAC_RADAR_OBSTACLES>), grid, block, lds, st, A, a2);
+    else if (A.radar_mode == AAC_RADAR_DRONES) hipLaunchKernelGGL((step_kernel<0, AAC_RADAR_DRONES>), grid, block, lds, st, A, a2);
+    else if (A.radar_mode == AAC_RADAR_OBSTACLES) hipLaunchKernelGGL((step_kernel<0, AAC_RADAR_OBSTACLES>), grid, block, lds, st, A, a2);
+    else hipLaunchKernelGGL((step_kernel<0, AAC_RADAR_COMBINED>), grid, block, lds, st, A, a2);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
