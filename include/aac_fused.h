@@ -51,12 +51,37 @@ typedef struct {
     int32_t M, N, K;
     int32_t lda, ldb, ldc, ldadd, ldmask;
     int32_t ta, tb, act, mact, ones, ksplit;
+    /* dual output (may be NULL): C2[m*ldc + n] = C[m][n] > 0 ? dscale * dvec[n] : 0 -- the critic
+     * head's actor-loss gradient dh = dq w (h > 0) with the constant dq = -1/B (ATT/maddpg:424)
+     * written by the combine layer's epilogue; needs ksplit <= 1 and no ones column */
+    const float *dvec;
+    float *C2;
+    float dscale;
 } aac_gemm_prob;
+
+/* A critic-head job (the arguments of aac_critic_head) that runs inside a grouped GEMM launch,
+ * beside products it does not depend on (aac_gemm_batch_heads). */
+typedef struct {
+    const float *h;
+    int32_t ldh, M;
+    const float *w, *b;
+    int32_t mode;
+    const float *y, *rew, *done;
+    int32_t B, N;
+    float gamma;
+    float *q, *dq, *dh, *yout;
+} aac_head_job;
+
+#define AAC_HEAD_MAX 2
 
 const char *aac_fused_last_error(void);
 
 /* n <= AAC_GEMM_MAX products in one launch. */
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream);
+/* The same launch with nh <= AAC_HEAD_MAX critic-head jobs appended as extra workgroups (four rows
+ * each; the arithmetic of aac_critic_head).  The jobs must not read what the products write, nor
+ * the products what the jobs write: one launch, no ordering between them.  n may be 0. */
+int aac_gemm_batch_heads(const aac_gemm_prob *probs, int32_t n, const aac_head_job *heads, int32_t nh, void *stream);
 /* The launch plan of aac_gemm_batch without launching (host only): per product 0 (register
  * fragments, 32x32 wave tiles) or 1 + cfg (LDS-staged workgroup tile: cfg >> 2 = 64x64 / 64x32 /
  * 32x64 / 32x32, cfg & 3 = operand layouts); *workgroups = the grid (may be NULL). */

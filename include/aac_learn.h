@@ -41,6 +41,13 @@ int aac_attn_bwd(const float *q, const float *k, const float *v, int32_t kv_stri
  * meta (device int64[2]) = {next write position, current size}; updated on the device. */
 int aac_replay_push(float *ring, int32_t row_width, int64_t capacity, int64_t *meta, int32_t n_fields,
                     const void *const *srcs, const int32_t *widths, const int32_t *dtypes, int32_t E, void *stream);
+/* The same push with the ring position and size known to the caller (pushes are host-initiated,
+ * so the host mirrors them): rows (pos + e) % capacity, then meta = {(pos + E) % capacity,
+ * min(size + E, capacity)} stored by the launch itself (one launch instead of two).  ring 16-B
+ * aligned. */
+int aac_replay_push_at(float *ring, int32_t row_width, int64_t capacity, int64_t *meta, int64_t pos, int64_t size,
+                       int32_t n_fields, const void *const *srcs, const int32_t *widths, const int32_t *dtypes,
+                       int32_t E, void *stream);
 /* n_batches independent batches of B distinct indices uniform in [0, meta[1]) (B <= 4096,
  * meta[1] >= B) into idx[n_batches][B]; deterministic in (seed, *counter); *counter (device
  * uint64, < 2^32; its high half counts arriving workgroups inside the launch) is advanced by one per
@@ -90,6 +97,13 @@ int aac_bias_act(float *y, const float *b, int64_t M, int32_t O, int32_t act, vo
  * in the same launch. */
 int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, int32_t eps_end, float noise_start,
                     float noise_end, uint64_t seed, uint64_t *counter, float *noise_out, void *stream);
+/* The actor's output layer fused with that noise: act[r] = tanh(wa . ha[r] + ba) for R = E*N agent
+ * rows of 256 features (wa = the [2][256] act_out weight, ATT/nets:213), then, with noisy != 0, the
+ * noise and clamp of aac_noise_clamp (the same per-row draw; the counter advances by one per call).
+ * ha and wa 16-B aligned. */
+int aac_actor_out_noise(const float *ha, int64_t R, const float *wa, const float *ba, float *act, int32_t N,
+                        const int32_t *episode, int32_t eps_end, float noise_start, float noise_end, uint64_t seed,
+                        uint64_t *counter, int32_t noisy, float *noise_out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -61,13 +61,59 @@ struct GProb {
     int tiles_n, w_begin;      // first workgroup of this product
     int lds;                   // 0: register fragments; 1 + cfg: LDS-staged workgroup tile (gemm_lds)
     int xcd;                   // LDS tile: XCD-aware workgroup order
+    const float *dvec;         // dual output: C2[m][n] = C[m][n] > 0 ? dscale * dvec[n] : 0
+    float *C2;
+    float dscale;
 };
+
+using aacw::wsum;
+
+struct HeadJob {          // aac_critic_head arguments (one wave per row, four rows per workgroup)
+    const float *h, *w, *b, *y, *rew, *done;
+    float *q, *dq, *dh, *yout;
+    int ldh, M, mode, B, N;
+    float gamma;
+};
+
+__device__ __forceinline__ void head_rows(const HeadJob &J, int blk) {
+    const int r = blk * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= J.M) return;
+    float hv[4], wv[4];
+    float part = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        hv[j] = J.h[(size_t)r * J.ldh + lane + 64 * j];
+        wv[j] = J.w[lane + 64 * j];
+        part = fmaf(hv[j], wv[j], part);
+    }
+    const float qv = wsum(part) + J.b[0];
+    if (J.q && lane == 0) J.q[r] = qv;
+    if (J.mode == 2) {
+        if (lane == 0) {
+            const int it = r / J.B;
+            bool any = false;
+            for (int n = 0; n < J.N; ++n) any |= J.done[(size_t)r * J.N + n] == 1.0f;
+            J.yout[r] = J.rew[(size_t)r * J.N + it] + (J.gamma * qv) * (1.0f - (any ? 1.0f : 0.0f));
+        }
+        return;
+    }
+    const float g = J.mode == 0 ? (2.0f / (float)J.M) * (qv - J.y[r]) : -(1.0f / (float)J.M);
+    if (J.dq && lane == 0) J.dq[r] = g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) J.dh[(size_t)r * 256 + lane + 64 * j] = hv[j] > 0.0f ? g * wv[j] : 0.0f;
+}
+
+constexpr int HEAD_MAX = 2;   // critic-head row jobs that may ride along in one GEMM launch
 
 struct GBatch {
     int wb[AAC_GEMM_MAX];      // first workgroup of each product (INT_MAX past n): the product
                                // select reads these 64 B with independent scalar loads
     int n, waves;
+    int hb[HEAD_MAX + 1];      // head jobs: workgroups [hb[j], hb[j + 1]) (hb[0] = waves of the products)
+    int nh;
     GProb p[AAC_GEMM_MAX];
+    HeadJob h[HEAD_MAX];
 };
 
 #ifdef AAC_GEMM_STAMPS
@@ -104,6 +150,7 @@ __device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, in
         v = v * (1.0f - t * t);
     }
     C[(size_t)m * P.ldc + n] = v;
+    if (P.C2) P.C2[(size_t)m * P.ldc + n] = v > 0.0f ? P.dscale * P.dvec[n] : 0.0f;
 }
 
 // Four adjacent columns n..n+3 of row m (n % 4 == 0): one 16-B load of the addend / mask / bias
@@ -142,6 +189,13 @@ __device__ __forceinline__ void epilogue4(const GProb &P, float *C, float *cx, i
         }
     }
     *reinterpret_cast<f4 *>(C + (size_t)m * P.ldc + n) = x;
+    if (P.C2) {      // the critic head's actor-loss gradient (dq = -1/B constant): dh = dq w (h > 0)
+        const f4 w = *reinterpret_cast<const f4 *>(P.dvec + n);
+        const float g = P.dscale;
+        *reinterpret_cast<f4 *>(P.C2 + (size_t)m * P.ldc + n) =
+            f4{x.x > 0.0f ? g * w.x : 0.0f, x.y > 0.0f ? g * w.y : 0.0f, x.z > 0.0f ? g * w.z : 0.0f,
+               x.w > 0.0f ? g * w.w : 0.0f};
+    }
 }
 
 // Fragment load modes of an operand whose rows are the MFMA row index (m for A, n for B):
@@ -592,7 +646,7 @@ __device__ __forceinline__ void gemm_lds(const GProb &P, int local, float *smem)
     float *cx = P.cextra ? P.cextra + (int64_t)s * P.sstride : nullptr;
     constexpr int RPI = 256 / (BN / 4);          // rows per pass; a thread keeps its 4 columns
     const int c4 = (threadIdx.x % (BN / 4)) * 4, r0 = threadIdx.x / (BN / 4);
-    if (P.vec && m0 + BM <= P.M && n0 + BN <= nreal) {
+    if (P.vec && !P.C2 && m0 + BM <= P.M && n0 + BN <= nreal) {
         // interior tile, 16-B rows: the bias once, every pass's addend / mask loads issued before
         // the first store (element-by-element the loop waited on each load in turn)
         f4 bias = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -676,6 +730,11 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
     GSTAMP(0, __builtin_amdgcn_s_memrealtime());
     GSTAMP(1, __builtin_amdgcn_s_memtime());
     const int wg = blockIdx.x;
+    if (wg >= g.hb[0]) {       // a critic-head job riding along (independent of the products)
+        const int j = (g.nh > 1 && wg >= g.hb[1]) ? 1 : 0;
+        head_rows(g.h[j], wg - g.hb[j]);
+        return;
+    }
     // product of this workgroup: count the products that start at or before it (wb is ascending,
     // wb[0] = 0); independent loads instead of a dependent scan of the kernel arguments
     int pi = 0;
@@ -844,38 +903,7 @@ using aacw::wsum;
 using aacw::wsum_n;
 
 
-__global__ void __launch_bounds__(256) head_kernel(const float *__restrict__ h, int ldh, int M,
-                                                   const float *__restrict__ w, const float *__restrict__ b, int mode,
-                                                   const float *__restrict__ y, const float *__restrict__ rew,
-                                                   const float *__restrict__ done, int B, int N, float gamma, float *q,
-                                                   float *dq, float *dh, float *yout) {
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (r >= M) return;
-    float hv[4], wv[4];
-    float part = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        hv[j] = h[(size_t)r * ldh + lane + 64 * j];
-        wv[j] = w[lane + 64 * j];
-        part = fmaf(hv[j], wv[j], part);
-    }
-    const float qv = wsum(part) + b[0];
-    if (q && lane == 0) q[r] = qv;
-    if (mode == 2) {
-        if (lane == 0) {
-            const int it = r / B;
-            bool any = false;
-            for (int n = 0; n < N; ++n) any |= done[(size_t)r * N + n] == 1.0f;
-            yout[r] = rew[(size_t)r * N + it] + (gamma * qv) * (1.0f - (any ? 1.0f : 0.0f));
-        }
-        return;
-    }
-    const float g = mode == 0 ? (2.0f / (float)M) * (qv - y[r]) : -(1.0f / (float)M);
-    if (dq && lane == 0) dq[r] = g;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dh[(size_t)r * 256 + lane + 64 * j] = hv[j] > 0.0f ? g * wv[j] : 0.0f;
-}
+__global__ void __launch_bounds__(256) head_kernel(HeadJob J) { head_rows(J, blockIdx.x); }
 
 // ------------------------------------------------------------------------------ actor output backward
 // Gradient through the critic's action inputs into the actor's tanh output layer, one wave per
@@ -1683,20 +1711,36 @@ struct SFields {
     int n;
 };
 
-__global__ void __launch_bounds__(256) gather_strided_kernel(const float *ring, int rw, const int32_t *idx,
+// GR sampled rows per workgroup: a thread's columns map to the same (field, destination offset)
+// in every row, so the field search and the index arithmetic run once per column, and the GR
+// row loads of a column are in flight together (one workgroup per row issued one load per thread)
+constexpr int GR = 8;
+
+__global__ void __launch_bounds__(256) gather_strided_kernel(const float *ring, int rw, const int32_t *idx, int B,
                                                              SFields F) {
-    const int b = blockIdx.x;
-    const float *src = ring + (int64_t)idx[b] * rw;
+    const int b0 = blockIdx.x * GR;
+    const int nb = min(GR, B - b0);
+    int64_t src[GR];
+#pragma unroll
+    for (int r = 0; r < GR; ++r) src[r] = (int64_t)idx[b0 + (r < nb ? r : 0)] * rw;
     for (int c = threadIdx.x; c < F.offset[F.n]; c += 256) {
         int f = 0;
         while (c >= F.offset[f + 1]) ++f;
         const int cc = c - F.offset[f];
         const int ch = F.chunk[f], ds = F.dstride[f];
-        const int64_t row0 = (int64_t)b * (F.width[f] / ch) * ds;
-        const int64_t o = row0 + (int64_t)(cc / ch) * ds + cc % ch;
-        const float v = src[c];
-        F.dst[f][o] = v;
-        if (F.dst2[f]) F.dst2[f][o] = v;
+        const int64_t per = (int64_t)(F.width[f] / ch) * ds;      // destination floats per sampled row
+        const int64_t rel = (int64_t)(cc / ch) * ds + cc % ch;
+        float v[GR];
+#pragma unroll
+        for (int r = 0; r < GR; ++r) v[r] = ring[src[r] + c];
+        float *d1 = F.dst[f], *d2 = F.dst2[f];
+#pragma unroll
+        for (int r = 0; r < GR; ++r) {
+            if (r >= nb) break;
+            const int64_t o = (int64_t)(b0 + r) * per + rel;
+            d1[o] = v[r];
+            if (d2) d2[o] = v[r];
+        }
     }
 }
 
@@ -1731,8 +1775,8 @@ const int g_xcd = env_int("AAC_GEMM_XCD", 0);                // XCD-aware order 
 const int g_adam4 = env_int("AAC_ADAM4", 1);                 // copy-parallel Adam over split-K copies
 int g_dump = env_int("AAC_GEMM_DUMP", 0);      // print the plans of the first g_dump launches
 
-int plan(const aac_gemm_prob *in, int n, GBatch &g) {
-    if (n < 1 || n > AAC_GEMM_MAX) return ffail("gemm_batch: 1 <= n <= AAC_GEMM_MAX");
+int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
+    if (n < (allow_empty ? 0 : 1) || n > AAC_GEMM_MAX) return ffail("gemm_batch: 1 <= n <= AAC_GEMM_MAX");
     g.n = n;
     int waves = 0;
     for (int i = 0; i < n; ++i) {
@@ -1745,11 +1789,15 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         if (s.N - s.ones > 0 && !s.C) return ffail(who + "NULL C");
         if (s.mact && !s.mask) return ffail(who + "mact needs mask");
         if (s.act < 0 || s.act > 2 || s.mact < 0 || s.mact > 2) return ffail(who + "bad act/mact");
+        if (s.C2 && (!s.dvec || s.ksplit > 1 || s.ones || !s.C)) return ffail(who + "dual output needs dvec, C, no split / ones");
         const int ks = s.ksplit > 1 ? s.ksplit : 1;
         if (ks > 1 && (s.split_stride <= 0 || s.addend || s.bias || s.act || s.mact))
             return ffail(who + "ksplit > 1 needs split_stride and a plain epilogue");
         d.A = s.A; d.B = s.B; d.C = s.C; d.bias = s.bias; d.addend = s.addend; d.mask = s.mask;
         d.cextra = s.cextra;
+        d.dvec = s.dvec;
+        d.C2 = s.C2;
+        d.dscale = s.dscale;
         d.sstride = s.split_stride;
         d.M = s.M; d.N = s.N; d.K = s.K;
         d.lda = s.lda; d.ldb = s.ldb; d.ldc = s.ldc; d.ldadd = s.ldadd; d.ldmask = s.ldmask;
@@ -1771,7 +1819,7 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         d.tiles_n = tn;
         d.vec = g_vec && (!s.C || (aligned16(s.C) && s.ldc % 4 == 0)) && (!s.addend || (aligned16(s.addend) && s.ldadd % 4 == 0)) &&
                 (!s.mask || (aligned16(s.mask) && s.ldmask % 4 == 0)) && (!s.bias || aligned16(s.bias)) &&
-                (ks <= 1 || (s.split_stride % 4 == 0));
+                (ks <= 1 || (s.split_stride % 4 == 0)) && (!s.C2 || (aligned16(s.C2) && aligned16(s.dvec)));
         // large products need no K cut inside a workgroup: one tile per wave; nor do short chains
         // (<= g_wide_kch chunks), where splitting K leaves waves idle and adds the LDS reduction
         const int nch_all = (s.K + KC - 1) / KC;
@@ -1796,7 +1844,7 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         static const int cand_pref[4][2] = {{2, 2}, {1, 2}, {2, 1}, {1, 1}};
         static const int cand_force[4][2] = {{2, 2}, {2, 1}, {1, 2}, {1, 1}};
         const int(*cand)[2] = cand_pref;
-        if (g_lds && a16 && b16 && s.K >= g_lds_min_k && (long)s.M * s.N >= g_lds_min_mn && s.M >= 32 &&
+        if (g_lds && !s.C2 && a16 && b16 && s.K >= g_lds_min_k && (long)s.M * s.N >= g_lds_min_mn && s.M >= 32 &&
             s.N - s.ones >= 32) {
             // 32x32 workgroup tiles re-read the operands 2x more than 64-wide ones and lose to the
             // register path's split-K waves on these shapes (tools/mb_lds.py): only with the knob
@@ -1828,6 +1876,8 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g) {
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
     }
     g.waves = waves;
+    g.nh = 0;
+    g.hb[0] = g.hb[1] = g.hb[2] = waves;
     for (int i = n; i < AAC_GEMM_MAX; ++i) g.wb[i] = 0x7fffffff;
     if (g_dump > 0) {
         --g_dump;
@@ -1875,16 +1925,58 @@ int aac_gemm_plan(const aac_gemm_prob *probs, int32_t n, int32_t *lds_cfg, int32
     return 0;
 }
 
+static int head_check(const aac_head_job &j) {
+    if (j.mode < 0 || j.mode > 2) return ffail("critic_head: mode 0, 1 or 2");
+    if (j.mode == 0 && !j.y) return ffail("critic_head: mode 0 needs y");
+    if (j.mode < 2 && !j.dh) return ffail("critic_head: modes 0/1 need dh");
+    if (j.mode == 2 && (!j.rew || !j.done || !j.yout || j.B <= 0 || j.N <= 0))
+        return ffail("critic_head: mode 2 needs rew/done/yout");
+    if (!j.h || !j.w || !j.b) return ffail("critic_head: NULL h / w / b");
+    return 0;
+}
+
+static HeadJob head_job(const aac_head_job &j) {
+    HeadJob J;
+    J.h = j.h; J.w = j.w; J.b = j.b; J.y = j.y; J.rew = j.rew; J.done = j.done;
+    J.q = j.q; J.dq = j.dq; J.dh = j.dh; J.yout = j.yout;
+    J.ldh = j.ldh; J.M = j.M; J.mode = j.mode; J.B = j.B; J.N = j.N; J.gamma = j.gamma;
+    return J;
+}
+
+static int launch_batch(GBatch &g, hipStream_t st);
+
+int aac_gemm_batch_heads(const aac_gemm_prob *probs, int32_t n, const aac_head_job *heads, int32_t nh, void *stream) {
+    if (nh < 0 || nh > HEAD_MAX || (nh > 0 && !heads)) return ffail("gemm_batch_heads: 0 <= nh <= AAC_HEAD_MAX");
+    if (n + nh < 1) return ffail("gemm_batch_heads: nothing to launch");
+    GBatch g{};
+    if (plan(probs, n, g, true)) return -1;
+    int wb = g.waves;
+    for (int j = 0; j < nh; ++j) {
+        if (head_check(heads[j])) return -1;
+        g.h[j] = head_job(heads[j]);
+        g.hb[j] = wb;
+        wb += (std::max(heads[j].M, 0) + 3) / 4;
+    }
+    for (int j = nh; j <= HEAD_MAX; ++j) g.hb[j] = wb;
+    g.nh = nh;
+    g.waves = wb;
+    if (wb == 0) return 0;
+    return launch_batch(g, (hipStream_t)stream);
+}
+
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
     GBatch g{};
     if (plan(probs, n, g)) return -1;
+    return launch_batch(g, (hipStream_t)stream);
+}
+
+static int launch_batch(GBatch &g, hipStream_t st) {
     bool deep = false, lds = false;
     for (int i = 0; i < g.n; ++i) {
         deep |= g.p[i].deep != 0;
         lds |= g.p[i].lds != 0;
     }
     const dim3 grid(g.waves), block(256);
-    hipStream_t st = (hipStream_t)stream;
     if (lds) {
         // the launch's LDS: the largest ring among its LDS-tile products (>= the register path's buffers)
         static const int ring_bytes[4] = {LCfg<2, 2>::BYTES, LCfg<2, 1>::BYTES, LCfg<1, 2>::BYTES, LCfg<1, 1>::BYTES};
@@ -1978,8 +2070,9 @@ int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, cons
     if (mode == 0 && !y) return ffail("critic_head: mode 0 needs y");
     if (mode < 2 && !dh) return ffail("critic_head: modes 0/1 need dh");
     if (mode == 2 && (!rew || !done || !yout || B <= 0 || N <= 0)) return ffail("critic_head: mode 2 needs rew/done/yout");
-    hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, M, w, b, mode, y, rew,
-                       done, B, N, gamma, q, dq, dh, yout);
+    const aac_head_job j{h, ldh, M, w, b, mode, y, rew, done, B, N, gamma, q, dq, dh, yout};
+    if (head_check(j)) return -1;
+    hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, head_job(j));
     FHIP(hipGetLastError());
     return 0;
 }
@@ -2117,7 +2210,7 @@ int aac_replay_gather_strided(const float *ring, int32_t rw, const int32_t *idx,
     }
     if (F.offset[n] > rw) return ffail("gather_strided: fields wider than the ring row");
     if (B <= 0) return 0;
-    hipLaunchKernelGGL(gather_strided_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, ring, rw, idx, F);
+    hipLaunchKernelGGL(gather_strided_kernel, dim3((B + GR - 1) / GR), dim3(256), 0, (hipStream_t)stream, ring, rw, idx, B, F);
     FHIP(hipGetLastError());
     return 0;
 }

@@ -10,12 +10,14 @@
 // adam/polyak: elementwise over one flat fp32 buffer (all parameters of a network).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdint>
 #include <string>
 
 #include "../../include/aac_learn.h"
+#include "aac_wave.h"
 
 namespace {
 
@@ -169,6 +171,48 @@ __global__ void __launch_bounds__(LEARN_BLOCK) push_kernel(float *ring, int rw, 
     }
 }
 
+// Push with the ring position known on the host (pushes are host-initiated, so the host mirrors
+// [pos, size]): a workgroup assembles PT consecutive transitions' rows in LDS from coalesced reads
+// of every field ([E][w] sources: PT*w contiguous elements each) and writes them as whole rows with
+// 16-B stores; workgroup 0 stores the advanced [pos, size] for the sampler.  No read of meta, so no
+// one-thread follow-up launch.
+extern __shared__ float4 push_lds[];
+
+__global__ void __launch_bounds__(LEARN_BLOCK) push_rows_kernel(float *ring, int rw, int64_t cap, int64_t pos,
+                                                                int64_t *meta, int64_t new_pos, int64_t new_size,
+                                                                int E, int PT, Fields F) {
+    float *rows = reinterpret_cast<float *>(push_lds);
+    const int e0 = blockIdx.x * PT;
+    const int pt = min(PT, E - e0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        meta[0] = new_pos;
+        meta[1] = new_size;
+    }
+    for (int f = 0; f < F.n; ++f) {
+        const int w = F.width[f], off = F.offset[f], n = pt * w;
+        if (F.dtype[f] == 1) {
+            const uint8_t *src = reinterpret_cast<const uint8_t *>(F.src[f]) + (size_t)e0 * w;
+            for (int k = threadIdx.x; k < n; k += LEARN_BLOCK) rows[(k / w) * rw + off + k % w] = (float)src[k];
+        } else {
+            const float *src = reinterpret_cast<const float *>(F.src[f]) + (size_t)e0 * w;
+            for (int k = threadIdx.x; k < n; k += LEARN_BLOCK) rows[(k / w) * rw + off + k % w] = src[k];
+        }
+    }
+    __syncthreads();
+    if ((rw & 3) == 0) {
+        const int r4 = rw >> 2;
+        for (int j = threadIdx.x; j < pt * r4; j += LEARN_BLOCK) {
+            const int r = j / r4, c4 = j - r * r4;
+            const int64_t row = (pos + e0 + r) % cap;
+            reinterpret_cast<float4 *>(ring + row * rw)[c4] = push_lds[r * r4 + c4];
+        }
+    } else {
+        for (int j = threadIdx.x; j < pt * rw; j += LEARN_BLOCK) {
+            const int r = j / rw, c = j - r * rw;
+            ring[((pos + e0 + r) % cap) * rw + c] = rows[j];
+        }
+    }
+}
 
 constexpr int TBL = 8192;
 
@@ -398,27 +442,36 @@ __global__ void bias_act_kernel(float *y, const float *__restrict__ b, int64_t n
 }
 
 // ------------------------------------------------------------------------------ noise
+// the exploration noise of agent row `row` (env row / N): var from the env's episode (linear
+// schedule to eps_end, then noise_end), Box-Muller pair from the hash of (seed, epoch, row)
+__device__ __forceinline__ void row_noise(int64_t row, int N, const int32_t *episode, int eps_end, float noise_start,
+                                          float noise_end, uint64_t seed, uint64_t ctr, float &n0, float &n1) {
+    const int e = (int)(row / N);
+    const int ep = episode ? episode[e] : 1;
+    double var;
+    if (ep <= eps_end) {
+        const double slope = ((double)noise_end - (double)noise_start) / (double)(eps_end - 1);
+        var = (double)noise_start + slope * (double)(ep - 1);
+    } else {
+        var = (double)noise_end;
+    }
+    const uint64_t h1 = mix64(mix64(mix64(seed) ^ ctr) ^ (uint64_t)(2 * row));
+    const uint64_t h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
+    const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
+    const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+    const double rr = sqrt(-2.0 * log(u1));
+    const double z0 = rr * cos(6.283185307179586 * u2), z1 = rr * sin(6.283185307179586 * u2);
+    n0 = (float)(z0 * var);
+    n1 = (float)(z1 * var);
+}
+
 __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, int eps_end, float noise_start,
                              float noise_end, uint64_t seed, uint64_t *counter, float *noise_out) {
     const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t ctr = take_epoch(counter);     // the counter advances once per launch
     if (row < (int64_t)E * N) {
-        const int e = (int)(row / N);
-        const int ep = episode ? episode[e] : 1;
-        double var;
-        if (ep <= eps_end) {
-            const double slope = ((double)noise_end - (double)noise_start) / (double)(eps_end - 1);
-            var = (double)noise_start + slope * (double)(ep - 1);
-        } else {
-            var = (double)noise_end;
-        }
-        const uint64_t h1 = mix64(mix64(mix64(seed) ^ ctr) ^ (uint64_t)(2 * row));
-        const uint64_t h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
-        const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
-        const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
-        const double rr = sqrt(-2.0 * log(u1));
-        const double z0 = rr * cos(6.283185307179586 * u2), z1 = rr * sin(6.283185307179586 * u2);
-        const float n0 = (float)(z0 * var), n1 = (float)(z1 * var);
+        float n0, n1;
+        row_noise(row, N, episode, eps_end, noise_start, noise_end, seed, ctr, n0, n1);
         float a0 = act[2 * row] + n0, a1 = act[2 * row + 1] + n1;
         a0 = fminf(fmaxf(a0, -1.0f), 1.0f);
         a1 = fminf(fmaxf(a1, -1.0f), 1.0f);
@@ -431,6 +484,70 @@ __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, i
     }
 }
 
+// The actor's output layer a = tanh(Wa h_a + ba) (ATT/nets:213, 256 -> 2) fused with the exploration
+// noise and clamp of choose_action (ATT/maddpg:476-500).  A wave owns AON_RW = 16 consecutive agent
+// rows: it issues the loads of all 16 rows (16 lanes per row, 16 features per lane: 1 KB row reads,
+// coalesced), computes lane j's float64 Box-Muller noise for row j while they fly, then the dot
+// pairs (sums over the 16-lane DPP rows) go through LDS to lane j, which finishes row j (tanh,
+// noise, clamp).  One noise epoch per launch (take_epoch, one atomic per workgroup).  Replaces a
+// grouped-GEMM launch with a 2-column output plus the noise launch.
+constexpr int AON_RW = 16;
+
+__global__ void __launch_bounds__(LEARN_BLOCK) actor_out_noise_kernel(const float *__restrict__ ha, int64_t R,
+                                                                      const float *__restrict__ wa,
+                                                                      const float *__restrict__ ba, float *act, int N,
+                                                                      const int32_t *episode, int eps_end,
+                                                                      float noise_start, float noise_end,
+                                                                      uint64_t seed, uint64_t *counter, int noisy,
+                                                                      float *noise_out) {
+    __shared__ float2 xs[LEARN_BLOCK / 64][AON_RW];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int q = lane >> 4, l16 = lane & 15;
+    const int64_t base = ((int64_t)blockIdx.x * (LEARN_BLOCK / 64) + w) * AON_RW;
+    float4 h[AON_RW / 4][4];
+#pragma unroll
+    for (int it = 0; it < AON_RW / 4; ++it) {
+        const int64_t row = base + 4 * it + q;
+        const float4 *hr = reinterpret_cast<const float4 *>(ha + (row < R ? row : 0) * 256) + l16 * 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) h[it][u] = hr[u];
+    }
+    const uint64_t ctr = noisy ? take_epoch(counter) : 0;      // the row loads fly across its barrier
+    float4 w0[4], w1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        w0[u] = reinterpret_cast<const float4 *>(wa)[l16 * 4 + u];
+        w1[u] = reinterpret_cast<const float4 *>(wa + 256)[l16 * 4 + u];
+    }
+    const int64_t myrow = base + lane;
+    const bool mine = lane < AON_RW && myrow < R;
+    float n0 = 0.0f, n1 = 0.0f;
+    if (noisy && mine) row_noise(myrow, N, episode, eps_end, noise_start, noise_end, seed, ctr, n0, n1);
+#pragma unroll
+    for (int it = 0; it < AON_RW / 4; ++it) {
+        float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4 x = h[it][u];
+            p0 = fmaf(x.w, w0[u].w, fmaf(x.z, w0[u].z, fmaf(x.y, w0[u].y, fmaf(x.x, w0[u].x, p0))));
+            p1 = fmaf(x.w, w1[u].w, fmaf(x.z, w1[u].z, fmaf(x.y, w1[u].y, fmaf(x.x, w1[u].x, p1))));
+        }
+        p0 = aacw::rsum16(p0);
+        p1 = aacw::rsum16(p1);
+        if (l16 == 0) xs[w][4 * it + q] = make_float2(p0, p1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");       // one wave's LDS operations run in order
+    if (!mine) return;
+    const float2 x = xs[w][lane];
+    float a0 = tanhf(x.x + ba[0]), a1 = tanhf(x.y + ba[1]);
+    if (noisy) {
+        a0 = fminf(fmaxf(a0 + n0, -1.0f), 1.0f);
+        a1 = fminf(fmaxf(a1 + n1, -1.0f), 1.0f);
+        if (noise_out) reinterpret_cast<float2 *>(noise_out)[myrow] = make_float2(n0, n1);
+    }
+    reinterpret_cast<float2 *>(act)[myrow] = make_float2(a0, a1);
+}
 
 #define LHIP(x)                                                                                  \
     do {                                                                                         \
@@ -503,6 +620,29 @@ int aac_replay_push(float *ring, int32_t rw, int64_t cap, int64_t *meta, int32_t
     }
     hipLaunchKernelGGL(push_kernel, dim3(E), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, ring, rw, cap, meta, F);
     hipLaunchKernelGGL(meta_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, meta, cap, E);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_replay_push_at(float *ring, int32_t rw, int64_t cap, int64_t *meta, int64_t pos, int64_t size, int32_t n,
+                       const void *const *srcs, const int32_t *widths, const int32_t *dtypes, int32_t E,
+                       void *stream) {
+    Fields F{};
+    if (make_fields(F, n, widths, rw)) return -1;
+    if (E < 1 || E > cap) return lfail("replay: need 1 <= E <= capacity");
+    if (pos < 0 || pos >= cap || size < 0 || size > cap) return lfail("replay: need 0 <= pos < capacity, size <= capacity");
+    if ((reinterpret_cast<uintptr_t>(ring) & 15) != 0) return lfail("replay: ring must be 16-B aligned");
+    for (int f = 0; f < n; ++f) {
+        F.src[f] = srcs[f];
+        F.dtype[f] = dtypes ? dtypes[f] : 0;
+    }
+    // transitions per workgroup: 4 (16 left one workgroup per CU: 14.2 us at E = 4096), rows within
+    // 64 KB of LDS
+    const int PT = std::max(1, std::min(4, (int)(65536 / (4 * (int64_t)rw))));
+    const size_t lds = (size_t)PT * rw * 4;
+    const int64_t np = (pos + E) % cap, ns = std::min<int64_t>(size + E, cap);
+    hipLaunchKernelGGL(push_rows_kernel, dim3((E + PT - 1) / PT), dim3(LEARN_BLOCK), lds, (hipStream_t)stream, ring, rw,
+                       cap, pos, meta, np, ns, E, PT, F);
     LHIP(hipGetLastError());
     return 0;
 }
@@ -597,6 +737,22 @@ int aac_noise_clamp(float *act, int32_t E, int32_t N, const int32_t *episode, in
     hipLaunchKernelGGL(noise_kernel, dim3((unsigned)((rows + LEARN_BLOCK - 1) / LEARN_BLOCK)), dim3(LEARN_BLOCK), 0,
                        (hipStream_t)stream, act, E, N, episode, eps_end, noise_start, noise_end, seed, counter,
                        noise_out);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_actor_out_noise(const float *ha, int64_t R, const float *wa, const float *ba, float *act, int32_t N,
+                        const int32_t *episode, int32_t eps_end, float noise_start, float noise_end, uint64_t seed,
+                        uint64_t *counter, int32_t noisy, float *noise_out, void *stream) {
+    if (R <= 0) return 0;
+    if (N <= 0 || R % N) return lfail("actor_out_noise: R must be a multiple of N > 0");
+    if (((reinterpret_cast<uintptr_t>(ha) | reinterpret_cast<uintptr_t>(wa)) & 15) != 0 ||
+        (reinterpret_cast<uintptr_t>(act) & 7) != 0 || (reinterpret_cast<uintptr_t>(noise_out) & 7) != 0)
+        return lfail("actor_out_noise: ha / wa 16-B, act / noise_out 8-B aligned");
+    if (noisy && !counter) return lfail("actor_out_noise: noisy needs the counter");
+    const int64_t wg = (R + 4 * AON_RW - 1) / (4 * AON_RW);
+    hipLaunchKernelGGL(actor_out_noise_kernel, dim3((unsigned)wg), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, ha, R, wa,
+                       ba, act, N, episode, eps_end, noise_start, noise_end, seed, counter, noisy, noise_out);
     LHIP(hipGetLastError());
     return 0;
 }

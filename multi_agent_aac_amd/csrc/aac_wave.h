@@ -20,6 +20,15 @@ __device__ __forceinline__ float wsum(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
 
+// sum over the lane's 16-lane DPP row (the first four steps of wsum): every lane of the row holds it
+__device__ __forceinline__ float rsum16(float x) {
+    DPP_STEP(x, 0xb1);
+    DPP_STEP(x, 0x4e);
+    DPP_STEP(x, 0x124);
+    DPP_STEP(x, 0x128);
+    return x;
+}
+
 // N independent wave sums with each DPP step applied to all N values before the next: the same
 // per-value order as wsum (bit-identical results), with the step latencies overlapped
 template <int N>

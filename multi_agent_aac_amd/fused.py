@@ -24,6 +24,7 @@ networks' flat gradient buffers, so there is no zero_grad.
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 from . import _native, ops
@@ -40,10 +41,17 @@ class GemmProb(ctypes.Structure):
     _fields_ = [("A", vp), ("B", vp), ("C", vp), ("bias", vp), ("addend", vp), ("mask", vp), ("cextra", vp),
                 ("split_stride", i64), ("M", i32), ("N", i32), ("K", i32), ("lda", i32), ("ldb", i32), ("ldc", i32), ("ldadd", i32),
                 ("ldmask", i32), ("ta", i32), ("tb", i32), ("act", i32), ("mact", i32), ("ones", i32),
-                ("ksplit", i32)]
+                ("ksplit", i32), ("dvec", vp), ("C2", vp), ("dscale", f32)]
+
+
+class HeadJob(ctypes.Structure):
+    """aac_head_job: a critic-head row job riding along in a grouped GEMM launch."""
+    _fields_ = [("h", vp), ("ldh", i32), ("M", i32), ("w", vp), ("b", vp), ("mode", i32), ("y", vp), ("rew", vp),
+                ("done", vp), ("B", i32), ("N", i32), ("gamma", f32), ("q", vp), ("dq", vp), ("dh", vp), ("yout", vp)]
 
 
 GEMM_MAX = 16
+HEAD_MAX = 2
 _L = None
 
 
@@ -53,6 +61,7 @@ def lib():
         L = _native.lib()
         L.aac_fused_last_error.restype = ctypes.c_char_p
         L.aac_gemm_batch.argtypes = [ctypes.POINTER(GemmProb), i32, vp]
+        L.aac_gemm_batch_heads.argtypes = [ctypes.POINTER(GemmProb), i32, ctypes.POINTER(HeadJob), i32, vp]
         L.aac_gemm_plan.argtypes = [ctypes.POINTER(GemmProb), i32, vp, vp]
         L.aac_gemm_set_lds_policy.argtypes = [i32, i32]
         L.aac_adam_flat_sum.argtypes = [vp, vp, i32, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
@@ -87,10 +96,17 @@ def ptr(t, off=0):
 
 
 def prob(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=NONE, addend=None, ldadd=0, mask=None,
-         ldmask=0, mact=NONE, ones=0, cextra=None, ksplit=1, split_stride=0):
-    """C[M][N] = mact(act(op(A) op(B) + addend + bias)); pointers are ints (see ``ptr``)."""
+         ldmask=0, mact=NONE, ones=0, cextra=None, ksplit=1, split_stride=0, dvec=None, C2=None, dscale=0.0):
+    """C[M][N] = mact(act(op(A) op(B) + addend + bias)); pointers are ints (see ``ptr``).  With C2:
+    also C2[m][n] = C[m][n] > 0 ? dscale * dvec[n] : 0 (the actor-loss critic head's dh)."""
     return GemmProb(A, B, C, bias, addend, mask, cextra, split_stride, M, N + ones, K, lda, ldb, ldc, ldadd, ldmask,
-                    ta, tb, act, mact, ones, ksplit)
+                    ta, tb, act, mact, ones, ksplit, dvec, C2, dscale)
+
+
+def head_job(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0.0, q=None, dq=None, dh=None,
+             yout=None):
+    """aac_critic_head's arguments as a job for a grouped GEMM launch (``GemmLaunch(heads=...)``)."""
+    return HeadJob(h, 256, M, w, b, mode, y, rew, done, B, N, gamma, q, dq, dh, yout)
 
 
 class Collective:
@@ -104,24 +120,35 @@ class Collective:
 
 
 class GemmLaunch:
-    """One aac_gemm_batch launch with a fixed problem list (validated when built)."""
+    """One aac_gemm_batch launch with a fixed problem list (validated when built), plus up to
+    HEAD_MAX critic-head jobs that do not depend on the products (aac_gemm_batch_heads)."""
 
-    def __init__(self, probs):
-        assert 1 <= len(probs) <= GEMM_MAX
+    def __init__(self, probs, heads=()):
+        assert 0 <= len(probs) <= GEMM_MAX and len(heads) <= HEAD_MAX and len(probs) + len(heads) >= 1
         self.n = len(probs)
-        self.arr = (GemmProb * self.n)(*probs)
-        # algorithmic FLOPs (2 M N K per product; the virtual ones column is the bias gradient)
-        self.flops = sum(2.0 * p.M * p.N * p.K for p in probs)
+        self.arr = (GemmProb * max(self.n, 1))(*probs)
+        self.nh = len(heads)
+        self.heads = (HeadJob * self.nh)(*heads) if heads else None
+        # algorithmic FLOPs (2 M N K per product; the virtual ones column is the bias gradient; a head
+        # job's 256-wide dot per row)
+        self.flops = sum(2.0 * p.M * p.N * p.K for p in probs) + sum(2.0 * 256 * h.M for h in heads)
         # algorithmic HBM bytes: every operand read once, every output (each split-K copy) written once
         self.bytes = sum(4.0 * (p.M * p.K + p.K * (p.N - p.ones) + max(1, p.ksplit) * p.M * p.N
                                 + (p.M * p.N if p.addend else 0) + (p.M * (p.N - p.ones) if p.mask else 0)
-                                + (p.N if p.bias else 0)) for p in probs)
+                                + (p.N if p.bias else 0) + (p.M * p.N if p.C2 else 0)) for p in probs)
+        # head job: h read, dh written (modes 0 / 1)
+        self.bytes += sum(4.0 * 256 * h.M * (1 if h.mode == 2 else 2) for h in heads)
 
     def __call__(self):
-        _chk(lib().aac_gemm_batch(self.arr, self.n, _stream()), "aac_gemm_batch")
+        if self.nh:
+            _chk(lib().aac_gemm_batch_heads(self.arr, self.n, self.heads, self.nh, _stream()), "aac_gemm_batch_heads")
+        else:
+            _chk(lib().aac_gemm_batch(self.arr, self.n, _stream()), "aac_gemm_batch")
 
     def plan(self):
         """(per-product tile mode: 0 register fragments / 1 + cfg LDS workgroup tile, grid size)."""
+        if self.n == 0:
+            return [], 0
         cfg = (ctypes.c_int32 * self.n)()
         wg = ctypes.c_int32()
         _chk(lib().aac_gemm_plan(self.arr, self.n, cfg, ctypes.byref(wg)), "aac_gemm_plan")
@@ -133,9 +160,11 @@ def set_lds_policy(min_workgroups=512, small_tiles=False):
     lib().aac_gemm_set_lds_policy(int(min_workgroups), int(bool(small_tiles)))
 
 
-def gemm_launches(probs):
-    """Split a product list into launches of at most GEMM_MAX."""
-    return [GemmLaunch(probs[i:i + GEMM_MAX]) for i in range(0, len(probs), GEMM_MAX)]
+def gemm_launches(probs, heads=()):
+    """Split a product list into launches of at most GEMM_MAX (head jobs ride in the first)."""
+    if not probs:
+        return [GemmLaunch([], heads)] if heads else []
+    return [GemmLaunch(probs[i:i + GEMM_MAX], heads if i == 0 else ()) for i in range(0, len(probs), GEMM_MAX)]
 
 
 def critic_head(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0.0, q=None, dq=None, dh=None,
@@ -311,20 +340,26 @@ class ActorInferActs:
         self.wqk = torch.empty(64, 64, dtype=torch.float32, device=dev)
 
 
+def actor_infer_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
+    """ActorNetwork_ATT_TwoPortion.forward for inference as dependent stages [encoders + Wqk =
+    Wk^T Wq, attention block (callable, aac_attn_block), merge, out]; GEMM stages are product lists
+    so that independent work can share their launches."""
+    c = acts
+    enc = [prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
+           prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
+           prob(ap.Wkv, ap.Wq, ptr(c.wqk), 64, 64, 64, 64, 64, 64, ta=1)]           # Wk^T Wq
+    attn = lambda: attn_block(ptr(c.cat), 192, nei, ap.Wn, ap.bn, ptr(c.wqk), ap.Wkv + 4 * 64 * 64,  # noqa: E731
+                              ptr(c.cat, 128), 192, R, K)
+    merge = [prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm, act=RELU)]
+    outp = [prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)]
+    return enc, attn, merge, outp
+
+
 def actor_forward_infer(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
     """Inference launch list of ActorNetwork_ATT_TwoPortion.forward: the own / radar encoders and
     Wqk = Wk^T Wq in one grouped launch, the fused attention block (aac_attn_block), merge, out."""
-    c = acts
-    L = gemm_launches([
-        prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
-        prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
-        prob(ap.Wkv, ap.Wq, ptr(c.wqk), 64, 64, 64, 64, 64, 64, ta=1)])           # Wk^T Wq
-    L.append(lambda: attn_block(ptr(c.cat), 192, nei, ap.Wn, ap.bn, ptr(c.wqk), ap.Wkv + 4 * 64 * 64,
-                                ptr(c.cat, 128), 192, R, K))
-    L += gemm_launches([prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm,
-                             act=RELU)])
-    L += gemm_launches([prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)])
-    return L
+    enc, attn, merge, outp = actor_infer_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
+    return gemm_launches(enc) + [attn] + gemm_launches(merge) + gemm_launches(outp)
 
 
 def critic_forward_stages(cp, X, rows, N, Din, f, h):
@@ -350,7 +385,10 @@ class ActorInfer:
         self.N, self.D0, self.K, self.dev = N, D0, N - 1, dev
         self.plans = {}
 
-    def __call__(self, own, radar, nei):
+    def __call__(self, own, radar, nei, noise=None):
+        """tanh actions [R][2]; with ``noise`` = (episode, eps_end, noise_start, noise_end, seed,
+        counter, noise_out) the output layer, the exploration noise and the clamp run as one
+        aac_actor_out_noise launch instead of a grouped-GEMM launch + aac_noise_clamp."""
         R = own.numel() // self.D0
         key = (own.data_ptr(), radar.data_ptr(), nei.data_ptr(), R)
         if key not in self.plans:
@@ -358,12 +396,20 @@ class ActorInfer:
                 assert t.is_contiguous() and t.device == self.dev and t.dtype == torch.float32
             acts = ActorInferActs(R, self.dev)
             out = torch.empty(R, 2, dtype=torch.float32, device=self.dev)
-            L = actor_forward_infer(self.ap, acts, ptr(own), self.D0, ptr(radar), ptr(nei), R, self.K, self.D0,
-                                    ptr(out), 2)
-            self.plans[key] = (L, acts, out, (own, radar, nei))
-        L, _, out, _ = self.plans[key]
+            enc, attn, merge, outp = actor_infer_stages(self.ap, acts, ptr(own), self.D0, ptr(radar), ptr(nei), R,
+                                                        self.K, self.D0, ptr(out), 2)
+            L = gemm_launches(enc) + [attn] + gemm_launches(merge)
+            self.plans[key] = (L, gemm_launches(outp), acts, out, (own, radar, nei))
+        L, Lout, acts, out, _ = self.plans[key]
         for op in L:
             op()
+        if noise is None:
+            for op in Lout:
+                op()
+        else:
+            episode, eps_end, noise_start, noise_end, seed, counter, noise_out = noise
+            ops.actor_out_noise(acts.ha, self.ap.Wa, self.ap.ba, out, self.N, episode, eps_end, noise_start,
+                                noise_end, seed, counter, noise_out)
         return out
 
 
@@ -438,19 +484,32 @@ class FusedUpdate:
         dsts2 = [ptr(self.X2)] + [None] * 8
         self.pre.append(lambda: gather_strided(rep.ring, self.idx, dsts, w, chunks, strides, dsts2=dsts2))
         Bt = nb * B
-        self.pre += actor_forward_infer(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar), ptr(self.nnei),
-                                        Bt * N, K, D0, ptr(self.Xt, D0), Din)
-        self.pre += critic_forward(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
-        self.pre.append(lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),
-                                            done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y)))
+        t_enc, t_attn, t_merge, t_out = actor_infer_stages(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar),
+                                                           ptr(self.nnei), Bt * N, K, D0, ptr(self.Xt, D0), Din)
+        t_cenc, t_comb = critic_forward_stages(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
+        t_head = lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),  # noqa: E731
+                                     done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y))
         self.segs = None
+        zip0 = m.world == 1 and not self.OVERLAP and self.MERGED
+        if zip0:
+            # the TD-target chain reads only the target networks and the gathered batches: the critic
+            # step 0's forward and the actor forward 0 (current weights, their own buffers) share its
+            # launches up to the point where the critic step needs the targets y
+            cs0 = self._critic_stages(0, C, self.cbuf[1])
+            a0_enc, a0_attn, a0_merge, a0_out = self._actor_fwd_stages(0, A)
+            self.pre += gemm_launches(t_enc + cs0["enc"] + a0_enc) + [t_attn, a0_attn]
+            self.pre += gemm_launches(t_merge + cs0["comb"] + a0_merge) + gemm_launches(t_out + a0_out)
+            self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [t_head]
+        else:
+            self.pre += gemm_launches(t_enc) + [t_attn] + gemm_launches(t_merge) + gemm_launches(t_out)
+            self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [t_head]
         if m.world > 1:
             self.iters = self._pipelined(A, C)
         elif self.OVERLAP:
             self.segs = self._overlapped(A, C)
             self.iters = [a + b + j for a, b, j in self.segs]
         elif self.MERGED:
-            self.iters = self._merged(A, C)
+            self.iters = self._merged(A, C, cs0)
         else:
             self.iters = [self._critic_step(i, A, C, self.cbuf[0], fuse_actor_fwd=True)
                           + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, i + 1)
@@ -475,39 +534,45 @@ class FusedUpdate:
             return [lambda: adam_sum_pair(ca, aa)]
         return [lambda: adam_sum(*ca[:4], grad_out=ca[4]), lambda: adam_sum(*aa[:4], grad_out=aa[4])]
 
-    def _merged(self, A, C):
+    def _merged(self, A, C, cs0):
         """world == 1: fewer, fuller launches.  The critic step of iteration i+1 reads the critic
         weights after critic Adam step i (and the fixed targets) -- exactly what the actor step of
         iteration i reads -- and neither reads the other's result (as in ``_pipelined``).  So
         segment i+1 zips the actor forward + actor step of iteration i with the critic step of
-        iteration i+1 (activation set 1) stage by stage into shared grouped-GEMM launches and ends
-        with both Adam steps in one launch.  Every product's arithmetic is unchanged, so the
-        update is bit-identical to the serial order (tests/test_fused_gpu.py)."""
+        iteration i+1 (activation set 1) stage by stage into shared grouped-GEMM launches (the
+        critic head riding along as a head job) and ends with both Adam steps in one launch.  The
+        forward half of critic step 0 and the actor forward 0 ran inside the TD-target launches
+        (``pre``).  Every product's arithmetic is unchanged, so the update is bit-identical to the
+        serial order (tests/test_fused_gpu.py)."""
         m, N = self.m, self.N
-        segs = [self._critic_step(0, A, C, self.cbuf[1], fuse_actor_fwd=True)
+        segs = [[cs0["head"]] + gemm_launches(cs0["grad"]) + gemm_launches(cs0["encw"])
                 + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, 1)]
         for i in range(N):
             cs = self._critic_stages(i + 1, C, self.cbuf[1]) if i + 1 < N else None
             ac = self._actor_stages(i, A, C)
+            L = []
+            if i == 0 and cs is not None:
+                # iteration 0's actor forward ran in pre: critic step 1 rides on the actor step's stages
+                L += gemm_launches(ac["cenc"] + cs["enc"]) + gemm_launches(ac["ccomb"] + cs["comb"])
+                L += gemm_launches(ac["dcomb"], heads=[cs["head_job"]])
+                L.append(ac["aob"])
+                L += gemm_launches(ac["wgrad1"] + cs["grad"])
+                L.append(ac["attn_bwd"])
+                L += gemm_launches(ac["wgrad2"] + cs["encw"])
+                L += self._adam_pair(i + 1, i)
+                segs.append(L)
+                continue
             if i > 0:
                 a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
-            else:     # iteration 0's actor forward ran inside the critic step 0 launches
-                a_enc, a_attn, a_merge, a_out = [], None, [], []
-            L = []
+                if cs is None:
+                    L += gemm_launches(a_enc) + [a_attn] + gemm_launches(a_merge) + gemm_launches(a_out)
+                else:
+                    L += gemm_launches(a_enc + cs["enc"]) + [a_attn] + gemm_launches(a_merge + cs["comb"])
+                    L += gemm_launches(a_out, heads=[cs["head_job"]])
             if cs is None:
-                L += gemm_launches(a_enc) + ([a_attn] if a_attn else []) + gemm_launches(a_merge)
-                L += gemm_launches(a_out)
                 L += gemm_launches(ac["cenc"]) + gemm_launches(ac["ccomb"])
             else:
-                L += gemm_launches(a_enc + cs["enc"])
-                if a_attn:
-                    L.append(a_attn)
-                L += gemm_launches(a_merge + cs["comb"])
-                L.append(cs["head"])
-                L += gemm_launches(a_out + cs["grad"])
-                L += gemm_launches(ac["cenc"] + cs["encw"])
-                L += gemm_launches(ac["ccomb"])
-            L.append(ac["head"])
+                L += gemm_launches(ac["cenc"] + cs["grad"]) + gemm_launches(ac["ccomb"] + cs["encw"])
             L += gemm_launches(ac["dcomb"])
             L.append(ac["aob"])
             L += gemm_launches(ac["wgrad1"])
@@ -640,6 +705,7 @@ class FusedUpdate:
         X, _, _, _, y = self._batch_ptrs(i)
         f, h, dq, dh, df = cb
         c_enc, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
+        hj = head_job(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh))
         head = lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq),  # noqa: E731
                                    dh=ptr(dh))
         grad = [
@@ -651,14 +717,13 @@ class FusedUpdate:
                  mact=RELU)]
         encw = [prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din, Din, ta=1, ones=1,
                      cextra=gC.enc_b[n], ksplit=SC, split_stride=nC) for n in range(N)]
-        return {"enc": c_enc, "comb": c_comb, "head": head, "grad": grad, "encw": encw}
+        return {"enc": c_enc, "comb": c_comb, "head": head, "head_job": hj, "grad": grad, "encw": encw}
 
     def _actor_step(self, i, A, C):
         """Actor step of iteration i (ATT/maddpg:389-425) after its forward, up to the weight-
         gradient partials: critic on the policy actions, backward into the actor."""
         st = self._actor_stages(i, A, C)
         L = gemm_launches(st["cenc"]) + gemm_launches(st["ccomb"])
-        L.append(st["head"])
         L += gemm_launches(st["dcomb"])
         L.append(st["aob"])
         L += gemm_launches(st["wgrad1"])
@@ -678,10 +743,15 @@ class FusedUpdate:
         f, h, dq, dh, df = self.cbuf[0]
         c = self.acts
         st = {}
-        st["cenc"], st["ccomb"] = critic_forward_stages(C, X, B, N, Din, f, h)
-        st["head"] = lambda: critic_head(ptr(h), B, C.Wq, C.bq, 1, q=ptr(self.q_a, i * B), dh=ptr(dh))
+        st["cenc"], _ = critic_forward_stages(C, X, B, N, Din, f, h)
+        # the actor loss -mean Q has the constant gradient dq = -1/B (ATT/maddpg:424), so the head's
+        # dh = dq Wo (h > 0) is a second output of the combine layer's epilogue, and Q itself (stats
+        # only) is an N = 1 product beside the combine's data gradient: no head launch on this chain
+        st["ccomb"] = [prob(ptr(f), C.Wc, ptr(h), B, 256, 128 * N, 128 * N, 128 * N, 256, tb=1, bias=C.bc, act=RELU,
+                            dvec=C.Wq, C2=ptr(dh), dscale=-float(np.float32(1.0) / np.float32(B)))]
         st["dcomb"] = [prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f),
-                            ldmask=128 * N, mact=RELU)]
+                            ldmask=128 * N, mact=RELU),
+                       prob(ptr(h), C.Wq, ptr(self.q_a, i * B), B, 1, 256, 256, 256, 1, tb=1, bias=C.bq)]
         # da_n = df_n . W_enc_n[:, D0:D0+2]; dout = da * (1 - a^2); dh_a = (dout Wa) * (h_a > 0)
         st["aob"] = lambda: actor_out_bwd(ptr(df), 128 * N, C.enc_w[0], Din, D0, X, A.Wa, ptr(c.ha), N, R,  # noqa: E731
                                           ptr(self.dout), ptr(self.dha))

@@ -121,9 +121,10 @@ class MADDPG:
         if self.fused:
             if self._infer is None:
                 self._infer = fused.ActorInfer(self.actors, self.n_agents, self.D0, self.device)
-            a = self._infer(own, radar, nei).view(*own.shape[:-1], 2)
-        else:
-            a = self.actors([own, radar, nei]).contiguous()
+            # noisy: the output layer, noise and clamp in one launch (aac_actor_out_noise)
+            nz = (episode, eps_end, noise_start, 0.0, self.noise_seed, self.noise_counter, noise_out) if noisy else None
+            return self._infer(own, radar, nei, noise=nz).view(*own.shape[:-1], 2)
+        a = self.actors([own, radar, nei]).contiguous()
         if noisy:
             ops.noise_clamp(a, episode, eps_end, noise_start, self.noise_seed, self.noise_counter, noise_out)
         return a

@@ -49,6 +49,7 @@ class DeviceReplay:
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)    # sampler RNG counter
         self.seed = int(seed)
         self.size = 0          # host mirror of meta[1] (pushes are host-initiated, so no sync needed)
+        self.pos = 0           # host mirror of meta[0]
         self._batch = {}
 
     def __len__(self):
@@ -62,7 +63,8 @@ class DeviceReplay:
         E = s_own.shape[0]
         for t in srcs:
             assert t.is_contiguous() and t.device == self.device and t.shape[0] == E
-        ops.replay_push(self.ring, self.meta, srcs, self.widths, self.dtypes, E)
+        ops.replay_push_at(self.ring, self.meta, self.pos, self.size, srcs, self.widths, self.dtypes, E)
+        self.pos = (self.pos + E) % self.capacity
         self.size = min(self.size + E, self.capacity)
 
     def check_sample(self, B):

@@ -26,6 +26,8 @@ def lib():
         L.aac_attn_fwd.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp]
         L.aac_attn_bwd.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, i32, i32, vp]
         L.aac_replay_push.argtypes = [vp, i32, i64, vp, i32, vp, vp, vp, i32, vp]
+        L.aac_actor_out_noise.argtypes = [vp, i64, vp, vp, vp, i32, vp, i32, f32, f32, u64, vp, i32, vp, vp]
+        L.aac_replay_push_at.argtypes = [vp, i32, i64, vp, i64, i64, i32, vp, vp, vp, i32, vp]
         L.aac_replay_sample.argtypes = [vp, i32, i32, u64, vp, vp, vp]
         L.aac_replay_gather.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp]
         L.aac_adam_flat.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp]
@@ -136,6 +138,14 @@ def polyak_flat(target, source, tau, step=None, step_add=0):
              "aac_polyak_flat_step")
 
 
+def actor_out_noise(ha, wa, ba, act, N, episode, eps_end, noise_start, noise_end, seed, counter, noise_out=None,
+                    noisy=True):
+    """act[R][2] = clamp(tanh(wa ha + ba) + noise) (aac_actor_out_noise; wa / ba device addresses)."""
+    R = ha.shape[0]
+    _chk(lib().aac_actor_out_noise(_p(ha), R, vp(wa), vp(ba), _p(act), N, _p(episode), eps_end, noise_start, noise_end,
+                                   u64(seed), _p(counter), int(noisy), _p(noise_out), _s()), "aac_actor_out_noise")
+
+
 def noise_clamp(act, episode, eps_end, noise_start, seed, counter, noise_out=None, noise_end=0.0):
     E, N = act.shape[0], act.shape[1]
     _chk(lib().aac_noise_clamp(_p(act), E, N, _p(episode), eps_end, noise_start, noise_end, u64(seed), _p(counter),
@@ -150,6 +160,16 @@ def replay_push(ring, meta, srcs, widths, dtypes, E):
     d = (i32 * n)(*dtypes)
     _chk(lib().aac_replay_push(_p(ring), ring.shape[1], ring.shape[0], _p(meta), n, arr, w, d, E, _s()),
          "aac_replay_push")
+
+
+def replay_push_at(ring, meta, pos, size, srcs, widths, dtypes, E):
+    """replay_push with the host's [pos, size] mirror (aac_replay_push_at: one launch)."""
+    n = len(srcs)
+    arr = (vp * n)(*[s.data_ptr() for s in srcs])
+    w = (i32 * n)(*widths)
+    d = (i32 * n)(*dtypes)
+    _chk(lib().aac_replay_push_at(_p(ring), ring.shape[1], ring.shape[0], _p(meta), pos, size, n, arr, w, d, E, _s()),
+         "aac_replay_push_at")
 
 
 def replay_sample(meta, B, seed, counter, idx_out):

@@ -189,7 +189,7 @@ def _learn_lib():
         L = uam.lib()
         vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
         L.aac_uam_learn_last_error.restype = ctypes.c_char_p
-        L.aac_gemm64_batch.argtypes = [ctypes.POINTER(fused.GemmProb), i32, vp]
+        L.aac_gemm64_batch.argtypes = [ctypes.POINTER(Gemm64Prob), i32, vp]
         L.aac_uam_gather.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.aac_uam_head.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, i32, dbl, vp, vp, vp, vp]
         L.aac_adam64_sum.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, vp]
@@ -210,11 +210,18 @@ def p64(t, off=0):
     return None if t is None else t.data_ptr() + 8 * off
 
 
+class Gemm64Prob(ctypes.Structure):
+    """aac_gemm64_prob (include/aac_uam_learn.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("A", "B", "C", "bias", "addend", "mask", "cextra")] + \
+        [("split_stride", ctypes.c_int64)] + \
+        [(n, ctypes.c_int32) for n in ("M", "N", "K", "lda", "ldb", "ldc", "ldadd", "ldmask", "ta", "tb", "act", "mact",
+                                       "ones", "ksplit")]
+
+
 def prob64(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=0, mask=None, ldmask=0, mact=0, ones=0,
            cextra=None, ksplit=1, split_stride=0):
     """One float64 product C[M][N] = mact(act(op(A) op(B) + bias)) (aac_gemm64_prob; addresses as ints)."""
-    from . import fused
-    return fused.GemmProb(A, B, C, bias, None, mask, cextra, split_stride, M, N + ones, K, lda, ldb, ldc, 0, ldmask,
+    return Gemm64Prob(A, B, C, bias, None, mask, cextra, split_stride, M, N + ones, K, lda, ldb, ldc, 0, ldmask,
                           ta, tb, act, mact, ones, ksplit)
 
 
@@ -302,7 +309,7 @@ class FusedUamUpdate:
             return prob64(dY, X, Cw, M, N, B, lddy, ldx, N, ta=1, ones=1, cextra=Cb, ksplit=KS, split_stride=stride)
 
         def gemm(probs):
-            arr = (fused.GemmProb * len(probs))(*probs)
+            arr = (Gemm64Prob * len(probs))(*probs)
             n = len(probs)
             return lambda: _ok(L.aac_gemm64_batch(arr, n, fused._stream()), "aac_gemm64_batch")
 

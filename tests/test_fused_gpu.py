@@ -179,6 +179,59 @@ def test_critic_head(native_lib, mode):
     np.testing.assert_allclose(dh.cpu(), (g[:, None] * w[None] * (h > 0)).cpu(), atol=1e-6, rtol=1e-6)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("with_product", [False, True])
+def test_head_job_in_gemm_launch(native_lib, mode, with_product):
+    """A critic-head job riding along in a grouped GEMM launch (aac_gemm_batch_heads) computes
+    exactly what the standalone aac_critic_head launch computes (same device code), and the
+    products of the launch are unaffected."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(10 + mode)
+    M, B, N = 2 * 512 + 3, 512, 2
+    P = fused.ptr
+    h = torch.relu(torch.randn(M, 256, device=DEV))
+    w, b = torch.randn(256, device=DEV), torch.randn(1, device=DEV)
+    y, rew = torch.randn(M, device=DEV), torch.randn(M, N, device=DEV)
+    done = (torch.rand(M, N, device=DEV) < 0.2).float()
+    outs = [[torch.full((M,), 7.0, device=DEV), torch.full((M,), 7.0, device=DEV),
+             torch.full((M, 256), 7.0, device=DEV), torch.full((M,), 7.0, device=DEV)] for _ in range(2)]
+    kw = dict(y=P(y), rew=P(rew), done=P(done), B=B, N=N, gamma=0.95)
+    q, dq, dh, yout = outs[0]
+    fused.critic_head(P(h), M, P(w), P(b), mode, q=P(q), dq=P(dq), dh=P(dh), yout=P(yout), **kw)
+    q, dq, dh, yout = outs[1]
+    job = fused.head_job(P(h), M, P(w), P(b), mode, q=P(q), dq=P(dq), dh=P(dh), yout=P(yout), **kw)
+    A, W = torch.randn(300, 40, device=DEV), torch.randn(72, 40, device=DEV)
+    C = torch.zeros(300, 72, device=DEV)
+    probs = [fused.prob(P(A), P(W), P(C), 300, 72, 40, 40, 40, 72, tb=1, act=fused.RELU)] if with_product else []
+    fused.GemmLaunch(probs, heads=[job])()
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    if with_product:
+        torch.testing.assert_close(C, torch.relu(A @ W.T), rtol=1e-5, atol=1e-5)
+
+
+def test_dual_output_is_actor_loss_head(native_lib):
+    """The combine layer's dual output C2 = (C > 0) dscale w equals aac_critic_head mode 1's dh
+    (dq = -1/B) bit for bit, on the register path with ragged tiles."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(3)
+    B, K = 1000, 640
+    P = fused.ptr
+    f = torch.relu(torch.randn(B, K, device=DEV))
+    Wc, bc = torch.randn(256, K, device=DEV) * 0.05, torch.randn(256, device=DEV) * 0.1
+    wq, bq = torch.randn(256, device=DEV), torch.randn(1, device=DEV)
+    h, dh = torch.empty(B, 256, device=DEV), torch.empty(B, 256, device=DEV)
+    scale = -float(np.float32(1.0) / np.float32(B))
+    fused.GemmLaunch([fused.prob(P(f), P(Wc), P(h), B, 256, K, K, K, 256, tb=1, bias=P(bc), act=fused.RELU,
+                                 dvec=P(wq), C2=P(dh), dscale=scale)])()
+    dh_ref = torch.empty(B, 256, device=DEV)
+    fused.critic_head(P(h), B, P(wq), P(bq), 1, dh=P(dh_ref))
+    torch.cuda.synchronize()
+    assert torch.equal(dh, dh_ref)
+    torch.testing.assert_close(h, torch.relu(f @ Wc.T + bc), rtol=1e-4, atol=1e-4)
+
+
 def test_gather_strided(native_lib):
     from multi_agent_aac_amd import fused
     rw, B = 50, 33
@@ -281,6 +334,20 @@ def test_fused_act_matches_ref_actor(native_lib):
     with torch.no_grad():
         want = learner_ref.actor_rows(ref, own, radar, nei)
     np.testing.assert_allclose(got.cpu(), want, atol=1e-5, rtol=1e-5)
+    # noisy: the output layer + noise + clamp launch (aac_actor_out_noise) = clamp(tanh + noise), with
+    # the noise of the standalone noise kernel (same draw from the same counter epoch)
+    from multi_agent_aac_amd import ops
+    ep = torch.randint(1, 9000, (E,), dtype=torch.int32, device=DEV)
+    noise = torch.empty(E, N, 2, device=DEV)
+    c0 = m.noise_counter.clone()
+    noisy = m.act(own.to(DEV), radar.to(DEV), nei.to(DEV), episode=ep, noise_out=noise).clone()
+    assert int(m.noise_counter) == int(c0) + 1
+    np.testing.assert_allclose(noisy.cpu(), torch.clamp(torch.as_tensor(want) + noise.cpu(), -1, 1), atol=1e-5,
+                               rtol=1e-5)
+    a2, n2 = got.clone(), torch.empty_like(noise)
+    ops.noise_clamp(a2, ep, 8000, 1.0, m.noise_seed, c0, n2)
+    assert torch.equal(n2, noise)
+    assert float(noise.abs().max()) > 0.1
 
 
 @pytest.mark.parametrize("K", [1, 4, 7, 12])       # K <= 8: MFMA kernels; 12: per-row kernels

@@ -151,7 +151,7 @@ def test_gemm64_products(native_lib, case):
         elif mact == 2:
             want = want * (1 - mask * mask)
         checks.append((C, M, N, ks, stride, ones, want, opA.sum(1)))
-    arr = (fused.GemmProb * len(probs))(*probs)
+    arr = (L.Gemm64Prob * len(probs))(*probs)
     L._ok(L._learn_lib().aac_gemm64_batch(arr, len(probs), fused._stream()), "gemm64")
     torch.cuda.synchronize()
     for C, M, N, ks, stride, ones, want, rowsum in checks:
