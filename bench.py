@@ -194,7 +194,10 @@ class Trainer:
             # WGRU/ma_main:380-389: actor_dim = critic_dim = [6, 18, 6], 64 hidden units
             self.model = gru.MADDPG([6, 18, 6], [6, 18, 6], 2, 64, 10, n_agents=N, seed=777, batch_size=B,
                                     memory_length=memory, process_group=pg, own_width=self.env.D0)
-            self.h = torch.zeros(E, N, 64, device="cuda")
+            # hidden states as a ping-pong pair: act reads h[k] and writes the next hidden into h[1 - k]
+            # (one act plan per buffer set, no copies)
+            self.hp = [torch.zeros(E, N, 64, device="cuda"), torch.zeros(E, N, 64, device="cuda")]
+            self.h = self.hp[0]
         else:
             self.model = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, seed=777, batch_size=B,
                                 memory_length=memory, process_group=pg)
@@ -214,7 +217,8 @@ class Trainer:
     def step(self, update=True, time_env=False):
         c, n = self.cur, self.nxt
         if self.gru:
-            act, hn = self.model.act(c.own, c.radar, self.h, self.episode, noisy=True)
+            hn_buf = self.hp[1] if self.h is self.hp[0] else self.hp[0]
+            act, hn = self.model.act(c.own, c.radar, self.h, self.episode, noisy=True, h_out=hn_buf)
         else:
             act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
         if time_env:
@@ -227,7 +231,7 @@ class Trainer:
             self.env_events.append((ev0, ev1))
         if self.gru:     # rows keep (cur_hidden, next_hidden) as WGRU/ma_main:636
             self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, self.h, hn)
-            self.h.copy_(hn)
+            self.h = hn
             from multi_agent_aac_amd import gru
             gru.reset_hidden(self.h, n.env_done)     # a new episode starts from zeros (WGRU/ma_main:476-478)
         else:

@@ -32,6 +32,10 @@
 #define KMAX (MAXA - 1)
 #define NONE8 255
 
+#ifndef AAC_UAM_MIN_WAVES     // waves per SIMD the step kernel is compiled for: 4 (<= 128 VGPRs) instead
+#define AAC_UAM_MIN_WAVES 4   // of the 130-VGPR / 3-wave build
+#endif
+
 namespace {
 
 // ------------------------------------------------------------------------ UAM world constants
@@ -377,7 +381,7 @@ __device__ inline void lds_agent(Lds &S, int la, double2 pos, double2 vel, doubl
 }
 
 // ------------------------------------------------------------------------------- step
-__global__ void __launch_bounds__(BLOCK) uam_step_kernel(UArgs A, const double2 *__restrict__ act) {
+__global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArgs A, const double2 *__restrict__ act) {
     __shared__ Lds S;
     const int N = A.N, K = A.K;
     const int nag = A.epb * N;

@@ -364,27 +364,30 @@ class GruUpdate:
 
 
 class _ActPlan:
-    """Batched choose_action for E envs: enc | gates | GRU fwd (actions, next hidden)."""
+    """Batched choose_action for E envs: enc | gates | GRU fwd (actions, next hidden).  Built for
+    fixed input / output buffers (no copies): own, radar, h as given, the next hidden into h_out (a
+    plan-owned buffer when None)."""
 
-    def __init__(self, m, E):
+    def __init__(self, m, own, radar, h, h_out=None):
         N, dev = m.n_agents, m.device
+        E = own.shape[0]
         self.E = E
-        self.own = torch.zeros(E, N, m.D0, device=dev)
-        self.radar = torch.zeros(E, N, 18, device=dev)
-        self.h = torch.zeros(E, N, H, device=dev)
+        for t in (own, radar, h):
+            assert t.is_contiguous() and t.device == dev and t.dtype == torch.float32 and t.shape[0] == E
+        self.inputs = (own, radar, h)            # kept alive with the plan
+        D0 = own.shape[-1]
         self.cat, self.gi, self.gh = (torch.empty(E, N, w, device=dev) for w in (128, 192, 192))
-        self.a, self.hn = torch.empty(E, N, 2, device=dev), torch.empty(E, N, H, device=dev)
+        self.a = torch.empty(E, N, 2, device=dev)
+        self.hn = h_out if h_out is not None else torch.empty(E, N, H, device=dev)
+        assert self.hn.is_contiguous() and self.hn.shape == (E, N, H)
         A = stack_addrs(m.actors, ACTOR_PARAMS, m.fa)
-        self.L = gemm_launches(enc2_probs(A, "Wo", "bo", "Wg", "bg", ptr(self.own), m.D0, m.d_own, ptr(self.radar),
-                                          18, 18, ptr(self.cat), E, N))
-        self.L += gemm_launches(gate_probs(A, ptr(self.cat), ptr(self.h), ptr(self.gi), ptr(self.gh), E, N))
-        self.L.append(gru_cell(A, "Wout", "bout", m.fa.numel // N, 2, TANH, ptr(self.gi), ptr(self.gh), ptr(self.h),
+        self.L = gemm_launches(enc2_probs(A, "Wo", "bo", "Wg", "bg", ptr(own), D0, m.d_own, ptr(radar), 18, 18,
+                                          ptr(self.cat), E, N))
+        self.L += gemm_launches(gate_probs(A, ptr(self.cat), ptr(h), ptr(self.gi), ptr(self.gh), E, N))
+        self.L.append(gru_cell(A, "Wout", "bout", m.fa.numel // N, 2, TANH, ptr(self.gi), ptr(self.gh), ptr(h),
                                E, N, FWD, hout=ptr(self.hn), ldho=H, y=ptr(self.a), ldy=2))
 
-    def __call__(self, own, radar, h):
-        for dst, src in ((self.own, own), (self.radar, radar), (self.h, h)):
-            if src.data_ptr() != dst.data_ptr():
-                dst.copy_(src)
+    def __call__(self):
         for op in self.L:
             op()
         return self.a, self.hn
@@ -453,15 +456,21 @@ class MADDPG:
 
     @torch.no_grad()
     def act(self, own, radar, h, episode=None, noisy=True, eps_end=8000, noise_start=1.0, noise_end=0.03,
-            noise_out=None):
+            noise_out=None, h_out=None):
         """Batched choose_action (WGRU/maddpg:336-428): (tanh actions + noise, clamped; next hidden).
-        own (E, N, >= d_own), radar (E, N, 18), h (E, N, 64).  The returned tensors are the plan's
-        static buffers (valid until the next call with the same E)."""
-        E = own.shape[0]
-        plan = self._acts.get(E)
+        own (E, N, >= d_own), radar (E, N, 18), h (E, N, 64) contiguous on the device.  The next hidden
+        goes to ``h_out`` when given (e.g. the other half of a ping-pong pair), else to a buffer of
+        the plan; the actions are a plan buffer (valid until the next call on the same inputs).  One
+        plan per input / output buffer set, so no copies."""
+        own, radar, h = own.contiguous(), radar.contiguous(), h.contiguous()
+        key = (own.data_ptr(), radar.data_ptr(), h.data_ptr(), None if h_out is None else h_out.data_ptr(),
+               tuple(own.shape))
+        plan = self._acts.get(key)
         if plan is None:
-            plan = self._acts[E] = _ActPlan(self, E)
-        a, hn = plan(own, radar, h)
+            if len(self._acts) > 8:       # callers with fresh tensors every step: do not grow without bound
+                self._acts.clear()
+            plan = self._acts[key] = _ActPlan(self, own, radar, h, h_out)
+        a, hn = plan()
         if noisy:
             ops.noise_clamp(a, episode, eps_end, noise_start, self.noise_seed, self.noise_counter, noise_out,
                             noise_end=noise_end)

@@ -1,7 +1,7 @@
 export TMPDIR=/tmp
-T="rocprofv3 --kernel-trace --output-format csv"
-SHORT="--steps 10 --warmup 3 --no-cpu-baseline --env-micro 0"
 bash tools/gpu_job.sh \
-  "learn:::500:::python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_learner_gpu.py tests/test_fused_gpu.py tests/test_facade_gpu.py tests/test_gru_gpu.py" \
-  "b3:::200:::python bench.py --no-cpu-baseline --steps 50" \
-  "prof3:::240:::$T --stats -d gpurun_out/prof3 -o run -- python3 bench.py $SHORT"
+  "tests:::500:::python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gru_gpu.py tests/test_uam_gpu.py tests/test_uam_learner_gpu.py tests/test_parallel_gpu.py" \
+  "b4:::200:::python bench.py --model gru --no-cpu-baseline --steps 50" \
+  "b5:::200:::python bench.py --model uam --no-cpu-baseline --steps 50" \
+  "b5v:::200:::AAC_LIB=$PWD/tools/variants/lib_uamw1.so python bench.py --model uam --no-cpu-baseline --steps 50" \
+  "b5b:::200:::python bench.py --model uam --no-cpu-baseline --steps 50"
