@@ -27,5 +27,8 @@ elif [ "$1" = pmc ]; then
     "w4:::90:::timeout -s KILL 80 $T --pmc WRITE_SIZE -d gpurun_out/pmc4w -o run -- python3 bench.py --model gru $SHORT" \
     "fe:::90:::timeout -s KILL 80 $T --pmc FETCH_SIZE -d gpurun_out/pmcef -o run -- $ENV" \
     "we:::90:::timeout -s KILL 80 $T --pmc WRITE_SIZE -d gpurun_out/pmcew -o run -- $ENV" \
-    "sq:::90:::timeout -s KILL 80 $T --pmc $SQ -d gpurun_out/pmcsq -o run -- $ENV"
+    "sq:::90:::timeout -s KILL 80 $T --pmc $SQ -d gpurun_out/pmcsq -o run -- $ENV" \
+    "f5:::90:::timeout -s KILL 80 $T --pmc FETCH_SIZE -d gpurun_out/pmc5f -o run -- python3 bench.py --model uam $SHORT" \
+    "w5:::90:::timeout -s KILL 80 $T --pmc WRITE_SIZE -d gpurun_out/pmc5w -o run -- python3 bench.py --model uam $SHORT" \
+    "gt:::200:::python tools/gemm_table.py"
 fi

@@ -73,7 +73,7 @@ def main():
             with open(os.path.join(PROF, name), "w") as fh:
                 json.dump(d, fh, indent=1)
             print(name, d["value"], d["ms_per_step"], d["roofline"].get("frac"))
-        for d, name, marker in (("prof3", "train_step", "::step_kernel("), ("prof4", "gru_step", "::step_kernel("),
+        for d, name, marker in (("prof3", "train_step", "::step_kernel"), ("prof4", "gru_step", "::step_kernel"),
                                 ("prof5", "uam_step", "uam_step_kernel")):
             txt = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_window.py"), trace_csv(d), "5",
                                   marker], capture_output=True, text=True, check=True).stdout
@@ -95,17 +95,25 @@ def main():
                 (b3, "pmc3f", "pmc3w", ["r02_env_step_pmc.json", "env_step_pmc.json"], "att", "combined"),
                 (b4, "pmc4f", "pmc4w", ["r02_env_step_pmc_n8.json", "env_step_pmc_n8.json"], "wgru", "obstacles")):
             c, er = b["config"], b["env_roofline"]
-            traffic(fd, wd, "::step_kernel(", "median",
+            traffic(fd, wd, "::step_kernel", "median",
                     {"envs": c["envs_per_gpu"] if "envs_per_gpu" in c else c.get("envs"), "agents": c.get("agents"),
                      "radar": radar, "variant": variant, "maps": c.get("maps", 1),
                      "algorithmic_bytes_per_launch": int(er["bytes_per_agent_step"] * er["agents_per_launch"])},
                     names)
         from bench import env_bytes_per_agent_step     # noqa: E402  (ATT env, N = 5)
-        traffic("pmcef", "pmcew", "::step_kernel(", "median",
+        traffic("pmcef", "pmcew", "::step_kernel", "median",
                 {"envs": 262144, "agents": 5, "radar": "combined", "variant": "att",
                  "algorithmic_bytes_per_launch": int(env_bytes_per_agent_step(5) * 262144 * 5)},
                 ["r02_env_step_pmc_262144.json"])
-        rows = [r for r in csv.DictReader(open(counter_csv("pmcsq"))) if "::step_kernel(" in r["Kernel_Name"]]
+        b5 = json.load(open(os.path.join(PROF, "r02_bench_uam.json")))
+        c5 = b5["config"]
+        traffic("pmc5f", "pmc5w", "uam_step_kernel", "median",
+                {"envs": c5["envs_per_gpu"], "agents": c5["agents"], "tdcpa": bool(c5.get("tdcpa")),
+                 "algorithmic_bytes_per_launch": int(b5["env_roofline"]["bytes_per_agent_step"] *
+                                                     b5["env_roofline"]["agents_per_launch"])},
+                ["r02_uam_env_pmc.json", "uam_env_pmc.json"])
+        shutil.copy(os.path.join(OUT, "gt.log"), os.path.join(PROF, "r02_gemm_table.txt"))
+        rows = [r for r in csv.DictReader(open(counter_csv("pmcsq"))) if "::step_kernel" in r["Kernel_Name"]]
         by = {}
         for r in rows:
             by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
