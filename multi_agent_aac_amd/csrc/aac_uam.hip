@@ -155,16 +155,21 @@ __device__ bool ray_gon_boundary_full(double cx, double cy, double ex, double ey
 //    circumscribed circle, so the six edges around that angle hold the minimum: same vertices, same
 //    arithmetic as the full clip, whose value it returns.
 //  * anything else (c in the thin annulus between the circles): the full clip.
-__device__ bool ray_gon_boundary(double cx, double cy, double ex, double ey, double px, double py, double r,
-                                 double inv_l2, double &tout) {
+__device__ inline bool ray_gon_candidate(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                         double inv_l2) {
     const double ddx = ex - cx, ddy = ey - cy;
     const double wx = px - cx, wy = py - cy;
-    {
-        double tt = (wx * ddx + wy * ddy) * inv_l2;
-        tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
-        const double qx = tt * ddx - wx, qy = tt * ddy - wy;
-        if (qx * qx + qy * qy > (r + 1e-6) * (r + 1e-6)) return false;
-    }
+    double tt = (wx * ddx + wy * ddy) * inv_l2;
+    tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
+    const double qx = tt * ddx - wx, qy = tt * ddy - wy;
+    return qx * qx + qy * qy <= (r + 1e-6) * (r + 1e-6);
+}
+
+// ray_gon_boundary past its pre-filter (the caller has established ray_gon_candidate)
+__device__ bool ray_gon_boundary_cand(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                      double &tout) {
+    const double ddx = ex - cx, ddy = ey - cy;
+    const double wx = px - cx, wy = py - cy;
     const double w2 = wx * wx + wy * wy;
     if (w2 > r * r * (1.0 + 1e-9)) return ray_poly_entry(cx, cy, ex, ey, px, py, r, tout);
     const double ap = r * c_tab.apothem;
@@ -195,6 +200,12 @@ __device__ bool ray_gon_boundary(double cx, double cy, double ex, double ey, dou
         return true;
     }
     return ray_gon_boundary_full(cx, cy, ex, ey, px, py, r, tout);
+}
+
+__device__ inline bool ray_gon_boundary(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                        double inv_l2, double &tout) {
+    return ray_gon_candidate(cx, cy, ex, ey, px, py, r, inv_l2) &&
+           ray_gon_boundary_cand(cx, cy, ex, ey, px, py, r, tout);
 }
 
 // segment c->e vs the finite bound segment x = lx, y in [y0, y1] (UAM/env:1413-1427)
@@ -289,12 +300,24 @@ __device__ double radar_ray(const UArgs &A, const Lds &S, int le, int base, int 
             if (d < best) best = d;
         }
     }
-    for (int j = 0; j < A.N; ++j) {
-        if (j == i) continue;
-        const double2 q = S.pos[base + j];
-        if (ray_gon_boundary(cx, cy, ex, ey, q.x, q.y, A.pb, inv_l2, t)) {
-            d = gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy);
-            if (d < best) best = d;
+    // the other aircraft: candidates (the cheap pre-filter) collected as a lane mask first, then the
+    // clips for the candidates only -- a wave runs max-popcount clip iterations instead of one per
+    // neighbour slot that any of its lanes needs (the minimum does not depend on the order)
+    for (int j0 = 0; j0 < A.N; j0 += 64) {
+        const int jn = A.N - j0 < 64 ? A.N - j0 : 64;
+        unsigned long long cand = 0;
+        for (int jj = 0; jj < jn; ++jj) {
+            const double2 q = S.pos[base + j0 + jj];
+            if (j0 + jj != i && ray_gon_candidate(cx, cy, ex, ey, q.x, q.y, A.pb, inv_l2)) cand |= 1ull << jj;
+        }
+        while (cand) {
+            const int j = j0 + __builtin_ctzll(cand);
+            cand &= cand - 1;
+            const double2 q = S.pos[base + j];
+            if (ray_gon_boundary_cand(cx, cy, ex, ey, q.x, q.y, A.pb, t)) {
+                d = gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy);
+                if (d < best) best = d;
+            }
         }
     }
     return best;
