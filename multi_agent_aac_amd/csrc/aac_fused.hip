@@ -110,6 +110,7 @@ struct GBatch {
     int wb[AAC_GEMM_MAX];      // first workgroup of each product (INT_MAX past n): the product
                                // select reads these 64 B with independent scalar loads
     int n, waves;
+    int xcd_all;               // launch-wide XCD-aware workgroup order (AAC_GEMM_XCD_ALL)
     int hb[HEAD_MAX + 1];      // head jobs: workgroups [hb[j], hb[j + 1]) (hb[0] = waves of the products)
     int nh;
     GProb p[AAC_GEMM_MAX];
@@ -729,7 +730,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
 #endif
     GSTAMP(0, __builtin_amdgcn_s_memrealtime());
     GSTAMP(1, __builtin_amdgcn_s_memtime());
-    const int wg = blockIdx.x;
+    int wg = blockIdx.x;
+    if (g.xcd_all) {
+        // workgroup b is dispatched to XCD b % 8: give each XCD a contiguous range of the launch's
+        // workgroups, so that the tiles of one product share an XCD's L2 (bijective for any count)
+        const int n = gridDim.x, q = n / 8, r = n % 8, x = wg % 8, o = wg / 8;
+        wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+    }
     if (wg >= g.hb[0]) {       // a critic-head job riding along (independent of the products)
         const int j = (g.nh > 1 && wg >= g.hb[1]) ? 1 : 0;
         head_rows(g.h[j], wg - g.hb[j]);
@@ -1772,6 +1779,7 @@ int g_lds_min_wg = env_int("AAC_GEMM_LDS_MIN_WG", 512);  // tile choice: largest
 const long g_lds_min_mn = env_int("AAC_GEMM_LDS_MIN_MN", 64 * 64);
 int g_lds_small = env_int("AAC_GEMM_LDS_SMALL", 0);         // allow 32x32 LDS workgroup tiles
 const int g_xcd = env_int("AAC_GEMM_XCD", 0);                // XCD-aware order of the LDS tiles
+const int g_xcd_all = env_int("AAC_GEMM_XCD_ALL", 0);        // ... of every workgroup of a launch
 const int g_adam4 = env_int("AAC_ADAM4", 1);                 // copy-parallel Adam over split-K copies
 int g_dump = env_int("AAC_GEMM_DUMP", 0);      // print the plans of the first g_dump launches
 
@@ -1876,6 +1884,7 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
     }
     g.waves = waves;
+    g.xcd_all = g_xcd_all;
     g.nh = 0;
     g.hb[0] = g.hb[1] = g.hb[2] = waves;
     for (int i = n; i < AAC_GEMM_MAX; ++i) g.wb[i] = 0x7fffffff;
