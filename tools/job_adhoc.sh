@@ -1,7 +1,4 @@
 export TMPDIR=/tmp
-for m in gru att; do
-for kv in AAC_NONE=1 AAC_GEMM_XCD_ALL=1 AAC_NONE=2 AAC_GEMM_XCD_ALL=2; do
-  env $kv timeout -k 10 120 python bench.py --model $m --steps 40 --warmup 5 --no-cpu-baseline --env-micro 0 > gpurun_out/ab.json 2>/dev/null || exit 1
-  python -c "import json,sys; d=json.loads([l for l in open('gpurun_out/ab.json') if l.startswith('{')][-1]); print('$m $kv', round(d['ms_per_step'],4), round(d['roofline']['frac'],4), round(d['roofline']['gemm_ms_per_update'],4))" | tee -a gpurun_out/ab.txt
-done
-done
+bash tools/gpu_job.sh \
+  "all:::1100:::python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/" \
+  "smoke:::200:::python -c 'import __graft_entry__ as g; g.smoke()'"
