@@ -962,7 +962,13 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     h->K = c.N - 1;
     h->D0 = c.variant ? 6 : 6 + 4 * h->K;
     h->W = c.max_wp;
-    h->epb = c.N > 24 ? 1 : 24 / c.N;   // ~24 agents x 18 rays of radar work per 256-thread workgroup
+    // ~24 agents x 18 rays of radar work per 256-thread workgroup (AAC_ENV_AGENTS_PER_WG: tuning)
+    static const int apw = [] {
+        const char *v = getenv("AAC_ENV_AGENTS_PER_WG");
+        const int k = v ? atoi(v) : 24;
+        return k < 1 ? 1 : (k > BLOCK ? BLOCK : k);
+    }();
+    h->epb = c.N > apw ? 1 : apw / c.N;
     h->blocks = (c.E + h->epb - 1) / h->epb;
     const size_t EN = (size_t)c.E * c.N;
     hipError_t st = hipSuccess;
