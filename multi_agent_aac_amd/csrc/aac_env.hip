@@ -962,13 +962,18 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     h->K = c.N - 1;
     h->D0 = c.variant ? 6 : 6 + 4 * h->K;
     h->W = c.max_wp;
-    // ~24 agents x 18 rays of radar work per 256-thread workgroup (AAC_ENV_AGENTS_PER_WG: tuning)
-    static const int apw = [] {
+    // agents per 256-thread workgroup: ~24 (x 18 rays of radar work) while that leaves fewer than
+    // 1024 workgroups (4 per CU, all resident: 46 vs 51-58 us per step at 4096 x 5 for 35 / 50 / 15
+    // agents); ~50 once the grid stays >= 1024 workgroups with them (262 144 x 5: 1.66 -> 1.16 ms).
+    // AAC_ENV_AGENTS_PER_WG forces a value (tuning).
+    static const int apw_env = [] {
         const char *v = getenv("AAC_ENV_AGENTS_PER_WG");
-        const int k = v ? atoi(v) : 24;
-        return k < 1 ? 1 : (k > BLOCK ? BLOCK : k);
+        const int k = v ? atoi(v) : 0;
+        return k < 0 ? 0 : (k > BLOCK ? BLOCK : k);
     }();
-    h->epb = c.N > apw ? 1 : apw / c.N;
+    auto epb_for = [&](int apw) { return c.N > apw ? 1 : apw / c.N; };
+    if (apw_env) h->epb = epb_for(apw_env);
+    else h->epb = (c.E / epb_for(50) >= 1024) ? epb_for(50) : epb_for(24);
     h->blocks = (c.E + h->epb - 1) / h->epb;
     const size_t EN = (size_t)c.E * c.N;
     hipError_t st = hipSuccess;

@@ -71,13 +71,14 @@ def _state_to_oracle(env, co):
     co.reach[:] = s["reach"]; co.wall[:] = s["wall"]; co.step_count[:] = s["step"]
 
 
-def test_env_n8_e4096_combined(native_lib, occ):
+@pytest.mark.parametrize("E,N", [(4096, 8), (12288, 5)])
+def test_env_n8_e4096_combined(native_lib, occ, E, N):
     """Config 4's env shape: E = 4096, N = 8, combined radar, 10 steps from identical injected state
     with OD-bank auto-reset: masks / done / bbc / env_done bit-exact, obs / radar / reward 1e-5,
-    positions 1e-12."""
+    positions 1e-12.  E = 12288, N = 5: a grid large enough for the 50-agent workgroups (10 envs
+    per workgroup, aac_env.hip's epb choice) of the step and reset kernels."""
     from multi_agent_aac_amd import world
     from multi_agent_aac_amd.env import BatchedEnv
-    E, N = 4096, 8
     bank = world.ODBank(occ, n_pairs=65536, seed=2026, max_wp=W_DEFAULT)
     st, wps, cnt = bank.sample_env_od(E, N, np.random.default_rng(8))
     env = BatchedEnv(E, N, occ, radar_mode="combined", max_wp=W_DEFAULT)

@@ -1,4 +1,4 @@
 export TMPDIR=/tmp
 bash tools/gpu_job.sh \
-  "all:::1100:::python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/" \
-  "smoke:::200:::python -c 'import __graft_entry__ as g; g.smoke()'"
+  "tests:::600:::python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_env_gpu.py tests/test_config_size_gpu.py -k 'env or Env' tests/test_wgru_gpu.py tests/test_multimap_gpu.py" \
+  "b3:::200:::python bench.py --no-cpu-baseline --steps 50"
