@@ -70,16 +70,23 @@ typedef struct {
     int32_t B, N;
     float gamma;
     float *q, *dq, *dh, *yout;
+    /* mode 2 only (M2 > 0): the critic step's mse head (mode 0 with M = M2) on rows r < M2 of h2
+     * (w2, b2: the current critic's output layer; q2, dq2, dh2 as q, dq, dh), chained on the TD
+     * target just computed for row r -- the TD target of update_myown's first batch and its critic
+     * loss gradient in one pass */
+    const float *h2, *w2, *b2;
+    float *q2, *dq2, *dh2;
+    int32_t M2;
 } aac_head_job;
 
-#define AAC_HEAD_MAX 2
+#define AAC_HEAD_MAX 1
 
 const char *aac_fused_last_error(void);
 
 /* n <= AAC_GEMM_MAX products in one launch. */
 int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream);
-/* The same launch with nh <= AAC_HEAD_MAX critic-head jobs appended as extra workgroups (four rows
- * each; the arithmetic of aac_critic_head).  The jobs must not read what the products write, nor
+/* The same launch with nh <= AAC_HEAD_MAX critic-head jobs (without a chained head) appended as
+ * extra workgroups (four rows each; the arithmetic of aac_critic_head).  The jobs must not read what the products write, nor
  * the products what the jobs write: one launch, no ordering between them.  n may be 0. */
 int aac_gemm_batch_heads(const aac_gemm_prob *probs, int32_t n, const aac_head_job *heads, int32_t nh, void *stream);
 /* The launch plan of aac_gemm_batch without launching (host only): per product 0 (register
@@ -140,6 +147,10 @@ int aac_sum_partials_strided(float *out, const float *gpart, int32_t nsplit, int
 int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, const float *b, int32_t mode,
                     const float *y, const float *rew, const float *done, int32_t B, int32_t N, float gamma, float *q,
                     float *dq, float *dh, float *yout, void *stream);
+
+/* One head job as its own launch (the arithmetic of aac_critic_head; with M2 > 0 the chained mse
+ * head of the job's mode 2, which aac_gemm_batch_heads does not take). */
+int aac_critic_head_job(const aac_head_job *job, void *stream);
 
 /* Backward of the critic's action inputs into the actor's output layer, one row r = b*N + n per
  * actor row (R = B*N): da_j = df[b][n*128 .. +128] . W_enc_n[:, d0 + j] (wenc = N stacked

@@ -73,8 +73,35 @@ struct HeadJob {          // aac_critic_head arguments (one wave per row, four r
     float *q, *dq, *dh, *yout;
     int ldh, M, mode, B, N;
     float gamma;
+    // mode 2 only: the critic step's mse head (mode 0) on rows r < M2 of h2, chained on the TD
+    // target just computed for row r (the critic step 0 of update_myown needs exactly y[0, B))
+    const float *h2, *w2, *b2;
+    float *q2, *dq2, *dh2;
+    int M2;
 };
 
+__device__ __forceinline__ void mse_head_row(const float *h, int ldh, const float *w, const float *b, int M, int r,
+                                             float y, float *q, float *dq, float *dh) {
+    const int lane = threadIdx.x & 63;
+    float hv[4], wv[4];
+    float part = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        hv[j] = h[(size_t)r * ldh + lane + 64 * j];
+        wv[j] = w[lane + 64 * j];
+        part = fmaf(hv[j], wv[j], part);
+    }
+    const float qv = wsum(part) + b[0];
+    if (q && lane == 0) q[r] = qv;
+    const float g = (2.0f / (float)M) * (qv - y);
+    if (dq && lane == 0) dq[r] = g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dh[(size_t)r * 256 + lane + 64 * j] = hv[j] > 0.0f ? g * wv[j] : 0.0f;
+}
+
+// CHAIN: the mode-2 job's chained mse head is compiled in (the standalone head kernel only; inside
+// gemm_kernel the extra code made the compiler keep the by-value GBatch in scratch, 3.2 KB per lane)
+template <bool CHAIN>
 __device__ __forceinline__ void head_rows(const HeadJob &J, int blk) {
     const int r = blk * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -90,12 +117,12 @@ __device__ __forceinline__ void head_rows(const HeadJob &J, int blk) {
     const float qv = wsum(part) + J.b[0];
     if (J.q && lane == 0) J.q[r] = qv;
     if (J.mode == 2) {
-        if (lane == 0) {
-            const int it = r / J.B;
-            bool any = false;
-            for (int n = 0; n < J.N; ++n) any |= J.done[(size_t)r * J.N + n] == 1.0f;
-            J.yout[r] = J.rew[(size_t)r * J.N + it] + (J.gamma * qv) * (1.0f - (any ? 1.0f : 0.0f));
-        }
+        const int it = r / J.B;
+        bool any = false;
+        for (int n = 0; n < J.N; ++n) any |= J.done[(size_t)r * J.N + n] == 1.0f;
+        const float yv = J.rew[(size_t)r * J.N + it] + (J.gamma * qv) * (1.0f - (any ? 1.0f : 0.0f));
+        if (lane == 0) J.yout[r] = yv;
+        if (CHAIN && r < J.M2) mse_head_row(J.h2, J.ldh, J.w2, J.b2, J.M2, r, yv, J.q2, J.dq2, J.dh2);
         return;
     }
     const float g = J.mode == 0 ? (2.0f / (float)J.M) * (qv - J.y[r]) : -(1.0f / (float)J.M);
@@ -104,7 +131,7 @@ __device__ __forceinline__ void head_rows(const HeadJob &J, int blk) {
     for (int j = 0; j < 4; ++j) J.dh[(size_t)r * 256 + lane + 64 * j] = hv[j] > 0.0f ? g * wv[j] : 0.0f;
 }
 
-constexpr int HEAD_MAX = 2;   // critic-head row jobs that may ride along in one GEMM launch
+constexpr int HEAD_MAX = 1;   // critic-head row jobs that may ride along in one GEMM launch
 
 struct GBatch {
     int wb[AAC_GEMM_MAX];      // first workgroup of each product (INT_MAX past n): the product
@@ -738,8 +765,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(GBatch g) {
         wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
     }
     if (wg >= g.hb[0]) {       // a critic-head job riding along (independent of the products)
-        const int j = (g.nh > 1 && wg >= g.hb[1]) ? 1 : 0;
-        head_rows(g.h[j], wg - g.hb[j]);
+        // static indices, copied by value: a dynamically indexed reference into the by-value
+        // kernel argument made the compiler copy the whole GBatch to scratch (3.4 KB per lane)
+        const HeadJob J = g.h[0];
+        head_rows<false>(J, wg - g.hb[0]);
         return;
     }
     // product of this workgroup: count the products that start at or before it (wb is ascending,
@@ -910,7 +939,7 @@ using aacw::wsum;
 using aacw::wsum_n;
 
 
-__global__ void __launch_bounds__(256) head_kernel(HeadJob J) { head_rows(J, blockIdx.x); }
+__global__ void __launch_bounds__(256) head_kernel(HeadJob J) { head_rows<true>(J, blockIdx.x); }
 
 // ------------------------------------------------------------------------------ actor output backward
 // Gradient through the critic's action inputs into the actor's tanh output layer, one wave per
@@ -1891,7 +1920,7 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
     g.waves = waves;
     g.xcd_all = g_xcd_all;
     g.nh = 0;
-    g.hb[0] = g.hb[1] = g.hb[2] = waves;
+    g.hb[0] = g.hb[1] = waves;
     for (int i = n; i < AAC_GEMM_MAX; ++i) g.wb[i] = 0x7fffffff;
     if (g_dump > 0) {
         --g_dump;
@@ -1946,6 +1975,8 @@ static int head_check(const aac_head_job &j) {
     if (j.mode == 2 && (!j.rew || !j.done || !j.yout || j.B <= 0 || j.N <= 0))
         return ffail("critic_head: mode 2 needs rew/done/yout");
     if (!j.h || !j.w || !j.b) return ffail("critic_head: NULL h / w / b");
+    if (j.M2 > 0 && (j.mode != 2 || !j.h2 || !j.w2 || !j.b2 || !j.dh2 || j.M2 > j.M))
+        return ffail("critic_head: a chained mse head needs mode 2, h2 / w2 / b2 / dh2 and M2 <= M");
     return 0;
 }
 
@@ -1954,6 +1985,7 @@ static HeadJob head_job(const aac_head_job &j) {
     J.h = j.h; J.w = j.w; J.b = j.b; J.y = j.y; J.rew = j.rew; J.done = j.done;
     J.q = j.q; J.dq = j.dq; J.dh = j.dh; J.yout = j.yout;
     J.ldh = j.ldh; J.M = j.M; J.mode = j.mode; J.B = j.B; J.N = j.N; J.gamma = j.gamma;
+    J.h2 = j.h2; J.w2 = j.w2; J.b2 = j.b2; J.q2 = j.q2; J.dq2 = j.dq2; J.dh2 = j.dh2; J.M2 = j.M2 > 0 ? j.M2 : 0;
     return J;
 }
 
@@ -1967,6 +1999,7 @@ int aac_gemm_batch_heads(const aac_gemm_prob *probs, int32_t n, const aac_head_j
     int wb = g.waves;
     for (int j = 0; j < nh; ++j) {
         if (head_check(heads[j])) return -1;
+        if (heads[j].M2 > 0) return ffail("gemm_batch_heads: a chained head job runs alone (aac_critic_head_job)");
         g.h[j] = head_job(heads[j]);
         g.hb[j] = wb;
         wb += (std::max(heads[j].M, 0) + 3) / 4;
@@ -2084,9 +2117,19 @@ int aac_critic_head(const float *h, int32_t ldh, int32_t M, const float *w, cons
     if (mode == 0 && !y) return ffail("critic_head: mode 0 needs y");
     if (mode < 2 && !dh) return ffail("critic_head: modes 0/1 need dh");
     if (mode == 2 && (!rew || !done || !yout || B <= 0 || N <= 0)) return ffail("critic_head: mode 2 needs rew/done/yout");
-    const aac_head_job j{h, ldh, M, w, b, mode, y, rew, done, B, N, gamma, q, dq, dh, yout};
+    const aac_head_job j{h, ldh, M, w, b, mode, y, rew, done, B, N, gamma, q, dq, dh, yout,
+                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
     if (head_check(j)) return -1;
     hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, head_job(j));
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_critic_head_job(const aac_head_job *job, void *stream) {
+    if (!job) return ffail("critic_head_job: NULL job");
+    if (job->M <= 0) return 0;
+    if (head_check(*job)) return -1;
+    hipLaunchKernelGGL(head_kernel, dim3((job->M + 3) / 4), dim3(256), 0, (hipStream_t)stream, head_job(*job));
     FHIP(hipGetLastError());
     return 0;
 }

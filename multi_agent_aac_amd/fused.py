@@ -47,11 +47,12 @@ class GemmProb(ctypes.Structure):
 class HeadJob(ctypes.Structure):
     """aac_head_job: a critic-head row job riding along in a grouped GEMM launch."""
     _fields_ = [("h", vp), ("ldh", i32), ("M", i32), ("w", vp), ("b", vp), ("mode", i32), ("y", vp), ("rew", vp),
-                ("done", vp), ("B", i32), ("N", i32), ("gamma", f32), ("q", vp), ("dq", vp), ("dh", vp), ("yout", vp)]
+                ("done", vp), ("B", i32), ("N", i32), ("gamma", f32), ("q", vp), ("dq", vp), ("dh", vp), ("yout", vp),
+                ("h2", vp), ("w2", vp), ("b2", vp), ("q2", vp), ("dq2", vp), ("dh2", vp), ("M2", i32)]
 
 
 GEMM_MAX = 16
-HEAD_MAX = 2
+HEAD_MAX = 1
 _L = None
 
 
@@ -62,6 +63,7 @@ def lib():
         L.aac_fused_last_error.restype = ctypes.c_char_p
         L.aac_gemm_batch.argtypes = [ctypes.POINTER(GemmProb), i32, vp]
         L.aac_gemm_batch_heads.argtypes = [ctypes.POINTER(GemmProb), i32, ctypes.POINTER(HeadJob), i32, vp]
+        L.aac_critic_head_job.argtypes = [ctypes.POINTER(HeadJob), vp]
         L.aac_gemm_plan.argtypes = [ctypes.POINTER(GemmProb), i32, vp, vp]
         L.aac_gemm_set_lds_policy.argtypes = [i32, i32]
         L.aac_adam_flat_sum.argtypes = [vp, vp, i32, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
@@ -104,9 +106,12 @@ def prob(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=NONE, adden
 
 
 def head_job(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0.0, q=None, dq=None, dh=None,
-             yout=None):
-    """aac_critic_head's arguments as a job for a grouped GEMM launch (``GemmLaunch(heads=...)``)."""
-    return HeadJob(h, 256, M, w, b, mode, y, rew, done, B, N, gamma, q, dq, dh, yout)
+             yout=None, chain=None):
+    """aac_critic_head's arguments as a job for a grouped GEMM launch (``GemmLaunch(heads=...)``).
+    chain (mode 2): (h2, w2, b2, q2, dq2, dh2, M2), the mse head of rows r < M2 of h2 on the TD target
+    just computed for row r."""
+    c = chain if chain is not None else (None, None, None, None, None, None, 0)
+    return HeadJob(h, 256, M, w, b, mode, y, rew, done, B, N, gamma, q, dq, dh, yout, *c)
 
 
 class Collective:
@@ -131,13 +136,13 @@ class GemmLaunch:
         self.heads = (HeadJob * self.nh)(*heads) if heads else None
         # algorithmic FLOPs (2 M N K per product; the virtual ones column is the bias gradient; a head
         # job's 256-wide dot per row)
-        self.flops = sum(2.0 * p.M * p.N * p.K for p in probs) + sum(2.0 * 256 * h.M for h in heads)
+        self.flops = sum(2.0 * p.M * p.N * p.K for p in probs) + sum(2.0 * 256 * (h.M + h.M2) for h in heads)
         # algorithmic HBM bytes: every operand read once, every output (each split-K copy) written once
         self.bytes = sum(4.0 * (p.M * p.K + p.K * (p.N - p.ones) + max(1, p.ksplit) * p.M * p.N
                                 + (p.M * p.N if p.addend else 0) + (p.M * (p.N - p.ones) if p.mask else 0)
                                 + (p.N if p.bias else 0) + (p.M * p.N if p.C2 else 0)) for p in probs)
         # head job: h read, dh written (modes 0 / 1)
-        self.bytes += sum(4.0 * 256 * h.M * (1 if h.mode == 2 else 2) for h in heads)
+        self.bytes += sum(4.0 * 256 * (h.M * (1 if h.mode == 2 else 2) + 2 * h.M2) for h in heads)
 
     def __call__(self):
         if self.nh:
@@ -173,6 +178,11 @@ def critic_head(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0
                                vp(done) if done else None, B, N, gamma, vp(q) if q else None,
                                vp(dq) if dq else None, vp(dh) if dh else None, vp(yout) if yout else None,
                                _stream()), "aac_critic_head")
+
+
+def critic_head_job(job):
+    """One HeadJob as its own launch (aac_critic_head_job; the chained TD + mse head)."""
+    _chk(lib().aac_critic_head_job(ctypes.byref(job), _stream()), "aac_critic_head_job")
 
 
 def gather_strided(ring, idx, dsts, widths, chunks, dstrides, dsts2=None):
@@ -499,7 +509,12 @@ class FusedUpdate:
             a0_enc, a0_attn, a0_merge, a0_out = self._actor_fwd_stages(0, A)
             self.pre += gemm_launches(t_enc + cs0["enc"] + a0_enc) + [t_attn, a0_attn]
             self.pre += gemm_launches(t_merge + cs0["comb"] + a0_merge) + gemm_launches(t_out + a0_out)
-            self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [t_head]
+            # the TD target of all batches with critic step 0's mse head chained on batch 0's rows
+            f0, h0, dq0, dh0, _ = self.cbuf[1]
+            tjob = head_job(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew), done=ptr(self.done), B=B, N=N,
+                            gamma=m.GAMMA, yout=ptr(self.y),
+                            chain=(ptr(h0), C.Wq, C.bq, ptr(self.q_c), ptr(dq0), ptr(dh0), B))
+            self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [lambda: critic_head_job(tjob)]
         else:
             self.pre += gemm_launches(t_enc) + [t_attn] + gemm_launches(t_merge) + gemm_launches(t_out)
             self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [t_head]
@@ -545,7 +560,7 @@ class FusedUpdate:
         (``pre``).  Every product's arithmetic is unchanged, so the update is bit-identical to the
         serial order (tests/test_fused_gpu.py)."""
         m, N = self.m, self.N
-        segs = [[cs0["head"]] + gemm_launches(cs0["grad"]) + gemm_launches(cs0["encw"])
+        segs = [gemm_launches(cs0["grad"]) + gemm_launches(cs0["encw"])      # its head ran chained in pre
                 + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, 1)]
         for i in range(N):
             cs = self._critic_stages(i + 1, C, self.cbuf[1]) if i + 1 < N else None

@@ -211,6 +211,36 @@ def test_head_job_in_gemm_launch(native_lib, mode, with_product):
         torch.testing.assert_close(C, torch.relu(A @ W.T), rtol=1e-5, atol=1e-5)
 
 
+def test_chained_td_and_mse_head(native_lib):
+    """A mode-2 head job with a chained mse head (critic step 0's loss on the first B rows of the TD
+    targets it has just computed; aac_critic_head_job) equals the two standalone aac_critic_head
+    launches bit for bit."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(21)
+    B, nb, N = 300, 3, 4
+    Bt = nb * B
+    P = fused.ptr
+    ht, h = torch.relu(torch.randn(Bt, 256, device=DEV)), torch.relu(torch.randn(B, 256, device=DEV))
+    wt, bt, w, b = (torch.randn(256, device=DEV), torch.randn(1, device=DEV), torch.randn(256, device=DEV),
+                    torch.randn(1, device=DEV))
+    rew = torch.randn(Bt, N, device=DEV)
+    done = (torch.rand(Bt, N, device=DEV) < 0.2).float()
+    outs = [[torch.full((Bt,), 7.0, device=DEV), torch.full((B,), 7.0, device=DEV), torch.full((B,), 7.0, device=DEV),
+             torch.full((B, 256), 7.0, device=DEV)] for _ in range(2)]
+    y, q, dq, dh = outs[0]
+    fused.critic_head(P(ht), Bt, P(wt), P(bt), 2, rew=P(rew), done=P(done), B=B, N=N, gamma=0.95, yout=P(y))
+    fused.critic_head(P(h), B, P(w), P(b), 0, y=P(y), q=P(q), dq=P(dq), dh=P(dh))
+    y, q, dq, dh = outs[1]
+    job = fused.head_job(P(ht), Bt, P(wt), P(bt), 2, rew=P(rew), done=P(done), B=B, N=N, gamma=0.95, yout=P(y),
+                         chain=(P(h), P(w), P(b), P(q), P(dq), P(dh), B))
+    fused.critic_head_job(job)
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    with pytest.raises(RuntimeError, match="chained"):
+        fused.GemmLaunch([], heads=[job])()
+
+
 def test_dual_output_is_actor_loss_head(native_lib):
     """The combine layer's dual output C2 = (C > 0) dscale w equals aac_critic_head mode 1's dh
     (dq = -1/B) bit for bit, on the register path with ragged tiles."""
