@@ -1820,7 +1820,13 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
     // launches of many independent products (the GRU learner's per-agent groups: 16 products of
     // 512 x 192) fill the chip together, so each product takes LDS tiles from 48 workgroups on
     // (config 4: 0.564 -> 0.558 ms per step; config 3's launches of <= 11 products keep 512)
-    const int min_wg = (g_lds_min_wg > 0 && g_lds_min_wg <= 512 && n >= 12) ? std::min(g_lds_min_wg, g_lds_min_wg_many) : g_lds_min_wg;
+    // (only launches without split-K products: the tile choice of a product must not depend on
+    // which other products share its launch in the ATT learner, whose merged and serial schedules
+    // group them differently and must stay bit-identical)
+    bool nosplit = true;
+    for (int i = 0; i < n; ++i) nosplit &= in[i].ksplit <= 1;
+    const int min_wg = (g_lds_min_wg > 0 && g_lds_min_wg <= 512 && n >= 12 && nosplit)
+                           ? std::min(g_lds_min_wg, g_lds_min_wg_many) : g_lds_min_wg;
     for (int i = 0; i < n; ++i) {
         const aac_gemm_prob &s = in[i];
         GProb &d = g.p[i];
