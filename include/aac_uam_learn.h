@@ -71,6 +71,12 @@ int aac_uam_head(const double *h, int32_t B, const double *w, const double *b, i
                  const double *rew, const double *done, int32_t ldr, double gamma, double *dq, double *dh,
                  double *lterm, void *stream);
 
+/* aac_uam_head mode 2 on the target critic's rows ht (TD target into y) and mode 0 on the critic's
+ * rows h chained in one launch: for each row r, y[r] = rew[r*ldr] + gamma Q'(1 - done[r*ldr]), then
+ * the mse head of Q(h[r]) against that y (dq, dh, lterm = e^2) -- the values of the two launches. */
+int aac_uam_td_mse_head(const double *ht, const double *wt, const double *bt, const double *rew, const double *done,
+                        int32_t ldr, double gamma, double *y, const double *h, const double *w, const double *b,
+                        int32_t B, double *dq, double *dh, double *lterm, void *stream);
 /* torch.optim.Adam(fused, capturable) step for float64 parameters: g = sum of nsplit partial
  * copies gpart[s*n + i] in copy order; t = *step + step_add, bias corrections in float64:
  *   m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= (lr/(1-b1^t)) m / (sqrt(v)/sqrt(1-b2^t) + eps) */

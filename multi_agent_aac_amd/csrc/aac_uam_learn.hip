@@ -214,6 +214,46 @@ __global__ void __launch_bounds__(256) uam_head_kernel(const double *__restrict_
     for (int c = 0; c < 4; ++c) dh[(size_t)r * 256 + lane + 64 * c] = hv[c] > 0.0 ? dq * w[lane + 64 * c] : 0.0;
 }
 
+// the TD target (mode 2 on the target critic's rows ht) and the critic's mse head (mode 0 on h) of
+// the same row in one pass: y[r] is computed and then used in-register (the values of the two
+// launches of uam_head_kernel, bit for bit)
+__device__ __forceinline__ double row_dot256(const double *__restrict__ hr, const double *__restrict__ w, int lane,
+                                             double (&hv)[4]) {
+    double p = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        hv[c] = hr[lane + 64 * c];
+        p = fma(hv[c], w[lane + 64 * c], p);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+    return p;
+}
+
+__global__ void __launch_bounds__(256) uam_td_mse_head_kernel(const double *__restrict__ ht,
+                                                              const double *__restrict__ wt,
+                                                              const double *__restrict__ bt,
+                                                              const double *__restrict__ rew,
+                                                              const double *__restrict__ done, int ldr, double gamma,
+                                                              double *y, const double *__restrict__ h,
+                                                              const double *__restrict__ w,
+                                                              const double *__restrict__ b, int B, double *dqo,
+                                                              double *dh, double *lterm) {
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= B) return;
+    double hv[4];
+    const double qt = row_dot256(ht + (size_t)r * 256, wt, lane, hv) + bt[0];
+    const double yv = rew[(size_t)r * ldr] + gamma * qt * (1.0 - done[(size_t)r * ldr]);
+    if (lane == 0) y[r] = yv;
+    const double q = row_dot256(h + (size_t)r * 256, w, lane, hv) + b[0];
+    const double e = q - yv;
+    const double dq = (2.0 / B) * e;
+    if (lane == 0) lterm[r] = e * e;
+    if (dqo && lane == 0) dqo[r] = dq;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dh[(size_t)r * 256 + lane + 64 * c] = hv[c] > 0.0 ? dq * w[lane + 64 * c] : 0.0;
+}
+
 __global__ void adam64_kernel(double *p, const double *__restrict__ gpart, int ns, double *m, double *v, int64_t n,
                               double lr, double b1, double b2, double eps, const int32_t *step, int step_add) {
     const int t = *step + step_add;
@@ -429,6 +469,18 @@ int aac_uam_head(const double *h, int32_t B, const double *w, const double *b, i
     if (mode < 2 && (!dh || !lterm)) return lfail("uam_head: modes 0 / 1 need dh / lterm");
     hipLaunchKernelGGL(uam_head_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, B, w, b, mode, y, rew,
                        done, ldr, gamma, dq, dh, lterm);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_uam_td_mse_head(const double *ht, const double *wt, const double *bt, const double *rew, const double *done,
+                        int32_t ldr, double gamma, double *y, const double *h, const double *w, const double *b,
+                        int32_t B, double *dq, double *dh, double *lterm, void *stream) {
+    if (B <= 0) return 0;
+    if (!ht || !wt || !bt || !rew || !done || !y || !h || !w || !b || !dh || !lterm)
+        return lfail("uam_td_mse_head: bad argument");
+    hipLaunchKernelGGL(uam_td_mse_head_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, ht, wt, bt, rew,
+                       done, ldr, gamma, y, h, w, b, B, dq, dh, lterm);
     LHIP(hipGetLastError());
     return 0;
 }

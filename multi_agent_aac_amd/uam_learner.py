@@ -192,6 +192,7 @@ def _learn_lib():
         L.aac_gemm64_batch.argtypes = [ctypes.POINTER(Gemm64Prob), i32, vp]
         L.aac_uam_gather.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.aac_uam_head.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, i32, dbl, vp, vp, vp, vp]
+        L.aac_uam_td_mse_head.argtypes = [vp, vp, vp, vp, vp, i32, dbl, vp, vp, vp, vp, i32, vp, vp, vp, vp]
         L.aac_adam64_sum.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, vp]
         L.aac_uam_polyak.argtypes = [vp, vp, i64, dbl, vp, vp, vp, i32, vp, vp]
         L.aac_uam_push.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp, i64, vp]
@@ -339,13 +340,12 @@ class FusedUamUpdate:
             gemm([lin(xt, 9, Wc(ct, "SA_fc"), Bc(ct, "SA_fc"), P(st.hc1t), 128, 9, 64, RELU)]),
             gemm([lin(P(st.hc1t), 128, Wc(ct, "merge_fc_grid"), Bc(ct, "merge_fc_grid"), P(st.hc2t), 256, 128, 256,
                       RELU)]),
-            # TD target r + gamma Q'(s', a')(1 - done) and the mse gradient (UAM/maddpg:346-380)
-            lambda: _ok(L.aac_uam_head(P(st.hc2t), B, Wc(ct, "out_feature_q"), Bc(ct, "out_feature_q"), 2, P(st.y),
-                                       P(R, 27), P(R, 28), ROW, float(m.GAMMA), None, None, None, fused._stream()),
-                        "aac_uam_head"),
-            lambda: _ok(L.aac_uam_head(P(st.hc2), B, Wc(c, "out_feature_q"), Bc(c, "out_feature_q"), 0, P(st.y),
-                                       None, None, 0, 0.0, P(st.dq), P(st.dh2), P(st.lq), fused._stream()),
-                        "aac_uam_head"),
+            # TD target r + gamma Q'(s', a')(1 - done) and the mse gradient (UAM/maddpg:346-380), one
+            # launch: the critic's head chained on each row's just-computed target
+            lambda: _ok(L.aac_uam_td_mse_head(P(st.hc2t), Wc(ct, "out_feature_q"), Bc(ct, "out_feature_q"), P(R, 27),
+                                              P(R, 28), ROW, float(m.GAMMA), P(st.y), P(st.hc2),
+                                              Wc(c, "out_feature_q"), Bc(c, "out_feature_q"), B, P(st.dq), P(st.dh2),
+                                              P(st.lq), fused._stream()), "aac_uam_td_mse_head"),
             # critic weight gradients and the backward into the merge layer's input
             gemm([wgrad(P(st.dq), 1, P(st.hc2), 256, 1, 256, gc["out_feature_q.0.weight"], gc["out_feature_q.0.bias"],
                         nC),

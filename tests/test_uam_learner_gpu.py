@@ -273,3 +273,33 @@ def test_adam_state_shared_across_plans_and_torch_path(native_lib):
     for mine, ref in ((m.actors, a), (m.critics, c), (m.actors_target, at), (m.critics_target, ct)):
         for (k, p), (_, q) in zip(mine.state_dict().items(), ref.state_dict().items()):
             np.testing.assert_allclose(p.cpu().numpy(), q.numpy(), rtol=0, atol=1e-10, err_msg=k)
+
+
+def test_td_mse_head_equals_two_heads(native_lib):
+    """aac_uam_td_mse_head (the TD target and the critic's mse head chained per row) equals the two
+    aac_uam_head launches (mode 2, then mode 0) bit for bit."""
+    from multi_agent_aac_amd import fused
+    from multi_agent_aac_amd import uam_learner as L
+    g = torch.Generator(device="cuda").manual_seed(4)
+    B, ldr = 300, 5
+    r = lambda *s: torch.rand(*s, device="cuda", dtype=torch.float64, generator=g) * 2 - 1   # noqa: E731
+    ht, h = torch.relu(r(B, 256)), torch.relu(r(B, 256))
+    wt, bt, w, b = r(256), r(1), r(256), r(1)
+    rows = r(B, ldr)
+    rows[:, 1] = (rows[:, 1] > 0.6).double()              # done flags
+    rew, done = rows[:, 0:], rows[:, 1:]
+    P = lambda t: t.data_ptr()                            # noqa: E731
+    outs = [[torch.full((B,), 7.0, device="cuda", dtype=torch.float64) for _ in range(3)] +
+            [torch.full((B, 256), 7.0, device="cuda", dtype=torch.float64)] for _ in range(2)]
+    lib = L._learn_lib()
+    y, dq, lq, dh = outs[0]
+    L._ok(lib.aac_uam_head(P(ht), B, P(wt), P(bt), 2, P(y), P(rew), P(done), ldr, 0.95, None, None, None,
+                           fused._stream()), "head2")
+    L._ok(lib.aac_uam_head(P(h), B, P(w), P(b), 0, P(y), None, None, 0, 0.0, P(dq), P(dh), P(lq), fused._stream()),
+          "head0")
+    y, dq, lq, dh = outs[1]
+    L._ok(lib.aac_uam_td_mse_head(P(ht), P(wt), P(bt), P(rew), P(done), ldr, 0.95, P(y), P(h), P(w), P(b), B, P(dq),
+                                  P(dh), P(lq), fused._stream()), "td_mse")
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
