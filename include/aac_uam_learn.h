@@ -41,6 +41,11 @@ typedef struct {
     int32_t M, N, K;
     int32_t lda, ldb, ldc, ldadd, ldmask;
     int32_t ta, tb, act, mact, ones, ksplit;
+    /* dual output (may be NULL): C2[m*ldc + n] = C[m][n] > 0 ? dscale * dvec[n] : 0 -- the actor
+     * loss's critic head dh = -1/B w (h > 0) from the merge layer's epilogue (UAM/maddpg:512) */
+    const double *dvec;
+    double *C2;
+    double dscale;
 } aac_gemm64_prob;
 
 const char *aac_uam_learn_last_error(void);

@@ -53,6 +53,9 @@ struct Q64 {
     int M, N, K, lda, ldb, ldc, ldadd, ldmask, ta, tb, act, mact, ones, ks;
     int tiles_n, w_begin;           // w_begin in waves
     int kw;                         // waves per tile: 1, or 4 (a workgroup splits K and reduces in LDS)
+    const double *dvec;             // dual output: C2[m][n] = C[m][n] > 0 ? dscale * dvec[n] : 0
+    double *C2;
+    double dscale;
 };
 
 struct Q64Batch {
@@ -158,6 +161,7 @@ __global__ void __launch_bounds__(256) gemm64_kernel(Q64Batch g) {
             v = v * (1.0 - t * t);
         }
         C[(size_t)mm * P.ldc + n] = v;
+        if (P.C2) P.C2[(size_t)mm * P.ldc + n] = v > 0.0 ? P.dscale * P.dvec[n] : 0.0;
     }
 }
 
@@ -420,6 +424,8 @@ int aac_gemm64_batch(const aac_gemm64_prob *in, int32_t n, void *stream) {
         d.M = s.M; d.N = s.N; d.K = s.K;
         d.lda = s.lda; d.ldb = s.ldb; d.ldc = s.ldc; d.ldadd = s.ldadd; d.ldmask = s.ldmask;
         d.ta = s.ta; d.tb = s.tb; d.act = s.act; d.mact = s.mact; d.ones = s.ones; d.ks = ks;
+        if (s.C2 && (!s.dvec || ks > 1 || s.ones || !s.C)) return lfail(who + "dual output needs dvec, C, no split / ones");
+        d.dvec = s.dvec; d.C2 = s.C2; d.dscale = s.dscale;
         const int tm = (s.M + 15) / 16, tn = (s.N + 15) / 16;
         d.tiles_n = tn;
         // long chains over few tiles: four waves per tile (K quarters, LDS reduction), the tile's

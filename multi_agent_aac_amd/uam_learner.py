@@ -216,14 +216,16 @@ class Gemm64Prob(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("A", "B", "C", "bias", "addend", "mask", "cextra")] + \
         [("split_stride", ctypes.c_int64)] + \
         [(n, ctypes.c_int32) for n in ("M", "N", "K", "lda", "ldb", "ldc", "ldadd", "ldmask", "ta", "tb", "act", "mact",
-                                       "ones", "ksplit")]
+                                       "ones", "ksplit")] + \
+        [("dvec", ctypes.c_void_p), ("C2", ctypes.c_void_p), ("dscale", ctypes.c_double)]
 
 
 def prob64(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=0, mask=None, ldmask=0, mact=0, ones=0,
-           cextra=None, ksplit=1, split_stride=0):
-    """One float64 product C[M][N] = mact(act(op(A) op(B) + bias)) (aac_gemm64_prob; addresses as ints)."""
+           cextra=None, ksplit=1, split_stride=0, dvec=None, C2=None, dscale=0.0):
+    """One float64 product C[M][N] = mact(act(op(A) op(B) + bias)) (aac_gemm64_prob; addresses as ints);
+    with C2 also C2 = (C > 0) dscale dvec[n] (the actor-loss head's dh)."""
     return Gemm64Prob(A, B, C, bias, None, mask, cextra, split_stride, M, N + ones, K, lda, ldb, ldc, 0, ldmask,
-                          ta, tb, act, mact, ones, ksplit)
+                      ta, tb, act, mact, ones, ksplit, dvec, C2, dscale)
 
 
 def _rebind(params, flat):
@@ -359,14 +361,16 @@ class FusedUamUpdate:
             # actor step: -mean Q(s, pi(s)) through the updated critic (UAM/maddpg:389-512)
             gemm([lin(xp, 9, Wc(c, "SA_fc"), Bc(c, "SA_fc"), P(st.hp1), 128, 9, 64, RELU),
                   lin(g, ROW, Wc(c, "SA_grid"), Bc(c, "SA_grid"), P(st.hp1, 64), 128, 18, 64, RELU)]),
-            gemm([lin(P(st.hp1), 128, Wc(c, "merge_fc_grid"), Bc(c, "merge_fc_grid"), P(st.hp2), 256, 128, 256,
-                      RELU)]),
-            lambda: _ok(L.aac_uam_head(P(st.hp2), B, Wc(c, "out_feature_q"), Bc(c, "out_feature_q"), 1, P(st.y),
-                                       None, None, 0, 0.0, None, P(st.dp2), P(st.la), fused._stream()),
-                        "aac_uam_head"),
+            # -mean Q has the constant gradient dq = -1/B (UAM/maddpg:512): the head's dh is a second
+            # output of the merge layer's epilogue, and Q itself (the actor loss) an N = 1 product
+            # beside the backward into the merge layer's input -- no head launch on this chain
+            gemm([prob64(P(st.hp1), Wc(c, "merge_fc_grid"), P(st.hp2), B, 256, 128, 128, 128, 256, tb=1,
+                         bias=Bc(c, "merge_fc_grid"), act=RELU, dvec=Wc(c, "out_feature_q"), C2=P(st.dp2),
+                         dscale=-1.0 / B)]),
             # d/d(own-encoder input) of the critic, first 64 features only (the action columns)
             gemm([prob64(P(st.dp2), Wc(c, "merge_fc_grid"), P(st.dp1), B, 64, 256, 256, 128, 64,
-                         mask=P(st.hp1), ldmask=128, mact=RELU)]),
+                         mask=P(st.hp1), ldmask=128, mact=RELU),
+                  lin(P(st.hp2), 256, Wc(c, "out_feature_q"), Bc(c, "out_feature_q"), P(st.la), 1, 256, 1, 0)]),
             # da = dx V1[:, 7:9], times tanh' of the policy action
             gemm([prob64(P(st.dp1), Wc(c, "SA_fc") + 8 * 7, P(st.dout), B, 2, 64, 64, 9, 2,
                          mask=P(st.xp, 7), ldmask=9, mact=TANH)]),
