@@ -186,7 +186,7 @@ class Trainer:
         else:
             self.occ = world.synthetic_map(2026)
             self.bank = world.ODBank(self.occ, n_pairs=65536, seed=2026 + seed, max_wp=32)
-        self.env = BatchedEnv(E, N, self.occ, radar_mode=radar, max_wp=32, variant=variant)
+        self.env = BatchedEnv(E, N, self.occ, radar_mode=None if self.gru else radar, max_wp=32, variant=variant)
         self.env.set_od_bank(self.bank, seed=1234 + seed)
         D0 = 6 + 4 * (N - 1)
         if self.gru:
@@ -546,7 +546,7 @@ def env_microbench(E, N, radar, iters=20, variant="att"):
     from multi_agent_aac_amd.env import BatchedEnv
     occ = world.synthetic_map(2026)
     bank = world.ODBank(occ, n_pairs=65536, seed=5, max_wp=32)
-    env = BatchedEnv(E, N, occ, radar_mode=radar, max_wp=32, variant=variant)
+    env = BatchedEnv(E, N, occ, radar_mode=None if variant == "wgru" else radar, max_wp=32, variant=variant)
     env.set_od_bank(bank, seed=3)
     env.auto_reset(None)
     g = torch.Generator(device="cuda").manual_seed(0)

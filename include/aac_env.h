@@ -115,14 +115,16 @@ int aac_env_stamps(unsigned long long *out, int32_t n_wg);
  * is enqueued on `stream` (ordered after the caller's pending resets and its fill of the buffer). */
 int aac_env_use_episode_buffer(aac_env *env, int32_t *episode_dev, void *stream);
 
-/* State export / import (device pointers, each may be NULL to skip). */
+/* State export / import (device pointers, each may be NULL to skip).  `start` (double2[E][N]) is
+ * the episode start: the reference-path origin of the WGRU variant's cross-track reward
+ * (WGRU/env:2621-2632, `ref_line` of reset_world); a state injected from another OD must carry it. */
 int aac_env_get_state(aac_env *env, double *pos, double *vel, double *pre_pos, double *pre_vel, double *goal,
                       double *wp, int32_t *wp_cur, int32_t *wp_cnt, uint8_t *reach, int32_t *wall, int32_t *step,
-                      int32_t *map_idx, void *stream);
+                      int32_t *map_idx, double *start, void *stream);
 int aac_env_set_state(aac_env *env, const double *pos, const double *vel, const double *pre_pos,
                       const double *pre_vel, const double *goal, const double *wp, const int32_t *wp_cur,
                       const int32_t *wp_cnt, const uint8_t *reach, const int32_t *wall, const int32_t *step,
-                      const int32_t *map_idx, void *stream);
+                      const int32_t *map_idx, const double *start, void *stream);
 
 /* Host utilities (no GPU). A* restates ATT/jps_straight.py:17-72 on a grid_w x grid_h x-major
  * grid (0 = free); writes up to max_len (x, y) cells, returns the path length or 0 if none. */

@@ -62,8 +62,8 @@ def lib():
     L.aac_env_set_reset_compact.argtypes = [ctypes.c_int32]
     L.aac_env_set_reset_compact.restype = None
     L.aac_env_use_episode_buffer.argtypes = [vp, vp, vp]
-    L.aac_env_get_state.argtypes = [vp] + [vp] * 12 + [vp]
-    L.aac_env_set_state.argtypes = [vp] + [vp] * 12 + [vp]
+    L.aac_env_get_state.argtypes = [vp] + [vp] * 13 + [vp]
+    L.aac_env_set_state.argtypes = [vp] + [vp] * 13 + [vp]
     L.aac_astar.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32]
     L.aac_od_bank_build.argtypes = [vp, i32, i32, vp, ctypes.c_double, i32, ctypes.c_uint64, i32, vp, vp, vp]
     for name in EXPORTS:

@@ -1161,9 +1161,10 @@ int aac_env_use_episode_buffer(aac_env *h, int32_t *episode_dev, void *stream) {
 
 int aac_env_get_state(aac_env *h, double *pos, double *vel, double *pre_pos, double *pre_vel, double *goal, double *wp,
                       int32_t *wp_cur, int32_t *wp_cnt, uint8_t *reach, int32_t *wall, int32_t *step,
-                      int32_t *map_idx, void *stream) {
+                      int32_t *map_idx, double *start, void *stream) {
     if (!h) return fail(AAC_E_INVALID, "null handle");
     const size_t EN = (size_t)h->cfg.E * h->cfg.N, E = h->cfg.E;
+    CPY(start, h->start, EN * 16)
     CPY(pos, h->pos, EN * 16) CPY(vel, h->vel, EN * 16) CPY(pre_pos, h->pre_pos, EN * 16)
     CPY(pre_vel, h->pre_vel, EN * 16) CPY(goal, h->goal, EN * 16) CPY(wp, h->wp, EN * h->W * 16)
     CPY(wp_cur, h->wp_cur, EN * 4) CPY(wp_cnt, h->wp_cnt, EN * 4) CPY(reach, h->reach, EN)
@@ -1174,9 +1175,10 @@ int aac_env_get_state(aac_env *h, double *pos, double *vel, double *pre_pos, dou
 int aac_env_set_state(aac_env *h, const double *pos, const double *vel, const double *pre_pos, const double *pre_vel,
                       const double *goal, const double *wp, const int32_t *wp_cur, const int32_t *wp_cnt,
                       const uint8_t *reach, const int32_t *wall, const int32_t *step, const int32_t *map_idx,
-                      void *stream) {
+                      const double *start, void *stream) {
     if (!h) return fail(AAC_E_INVALID, "null handle");
     const size_t EN = (size_t)h->cfg.E * h->cfg.N, E = h->cfg.E;
+    CPY(h->start, start, EN * 16)
     CPY(h->pos, pos, EN * 16) CPY(h->vel, vel, EN * 16) CPY(h->pre_pos, pre_pos, EN * 16)
     CPY(h->pre_vel, pre_vel, EN * 16) CPY(h->goal, goal, EN * 16) CPY(h->wp, wp, EN * h->W * 16)
     CPY(h->wp_cur, wp_cur, EN * 4) CPY(h->wp_cnt, wp_cnt, EN * 4) CPY(h->reach, reach, EN)

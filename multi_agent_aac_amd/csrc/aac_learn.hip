@@ -149,7 +149,8 @@ __device__ inline uint64_t take_epoch(uint64_t *word) {
         const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long *>(word), 1ull << 32);
         ep = old & 0xffffffffull;
         if ((old >> 32) == (uint64_t)(gridDim.x * gridDim.y * gridDim.z) - 1)
-            atomicExch(reinterpret_cast<unsigned long long *>(word), (unsigned long long)(ep + 1));
+            // low 32 bits only: the arrival field must restart at 0 even when the epoch wraps
+            atomicExch(reinterpret_cast<unsigned long long *>(word), (unsigned long long)((ep + 1) & 0xffffffffull));
     }
     __syncthreads();
     return ep;

@@ -62,9 +62,9 @@ class BatchedEnv:
     WGRU/ma_main:653-661): obstacle radar, 6-wide own rows, per-agent reward; its defaults are
     max_spd 10 (WGRU/ma_main:409) and episode_length 150 (WGRU/ma_main:1044)."""
 
-    def __init__(self, E, N, occ, radar_mode="drones", compat=True, team_reward=True, max_wp=32,
-                 episode_length=50, device=None, bound=_world.BOUND, cell=_world.CELL, tdcpa=False,
-                 dt=0.5, acc_max=8.0, vmax=5.0, pB=2.5, radar_len=15.0, variant="att"):
+    def __init__(self, E, N, occ, radar_mode=None, compat=True, team_reward=None, max_wp=32,
+                 episode_length=None, device=None, bound=_world.BOUND, cell=_world.CELL, tdcpa=False,
+                 dt=0.5, acc_max=8.0, vmax=None, pB=2.5, radar_len=15.0, variant="att"):
         if not torch.cuda.is_available():
             raise RuntimeError("BatchedEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device if device is not None else "cuda")
@@ -76,10 +76,20 @@ class BatchedEnv:
         self.occ = np.ascontiguousarray(occ)
         self.E, self.N, self.K = int(E), int(N), int(N) - 1
         self.variant = VARIANTS[variant]
+        # per-variant defaults for the arguments left at None; an explicit value is kept as given
+        # (variant 1 supports only the obstacle radar and per-agent rewards, so asking it for
+        # anything else raises instead of being overwritten)
+        d_radar, d_team, d_vmax, d_ep = (("obstacles", False, 10.0, 150) if self.variant else ("drones", True, 5.0, 50))
         if self.variant:
-            radar_mode, team_reward = "obstacles", False
-            vmax = 10.0 if vmax == 5.0 else vmax
-            episode_length = 150 if episode_length == 50 else episode_length
+            if radar_mode is not None and RADAR_MODES.get(radar_mode, radar_mode) != RADAR_MODES["obstacles"]:
+                raise ValueError("variant 'wgru' uses the obstacle radar (WGRU/env:990-1054); got radar_mode=%r"
+                                 % (radar_mode,))
+            if team_reward:
+                raise ValueError("variant 'wgru' computes per-agent rewards (WGRU/env:1800-1960); team_reward=True")
+        radar_mode = d_radar if radar_mode is None else radar_mode
+        team_reward = d_team if team_reward is None else team_reward
+        vmax = d_vmax if vmax is None else vmax
+        episode_length = d_ep if episode_length is None else episode_length
         self.D0 = 6 if self.variant else 6 + 4 * self.K
         self.W = int(max_wp)
         self.tdcpa = tdcpa
@@ -205,7 +215,7 @@ class BatchedEnv:
                  goal=torch.empty(E, N, 2, **f64), wp=torch.empty(E, N, W, 2, **f64),
                  wp_cur=torch.empty(E, N, **i32), wp_cnt=torch.empty(E, N, **i32),
                  reach=torch.empty(E, N, dtype=torch.uint8, device=d), wall=torch.empty(E, N, **i32),
-                 step=torch.empty(E, **i32), map_idx=torch.empty(E, **i32))
+                 step=torch.empty(E, **i32), map_idx=torch.empty(E, **i32), start=torch.empty(E, N, 2, **f64))
         _native.check(_native.lib().aac_env_get_state(self._h, *[_ptr(s[k]) for k in _STATE_KEYS], _stream()),
                       "aac_env_get_state")
         return s
@@ -214,7 +224,7 @@ class BatchedEnv:
         d = self.device
         dt = dict(pos=torch.float64, vel=torch.float64, pre_pos=torch.float64, pre_vel=torch.float64,
                   goal=torch.float64, wp=torch.float64, wp_cur=torch.int32, wp_cnt=torch.int32,
-                  reach=torch.uint8, wall=torch.int32, step=torch.int32, map_idx=torch.int32)
+                  reach=torch.uint8, wall=torch.int32, step=torch.int32, map_idx=torch.int32, start=torch.float64)
         t = {k: (torch.as_tensor(v, dtype=dt[k], device=d).contiguous() if v is not None else None)
              for k, v in kw.items()}
         for k in t:
@@ -226,7 +236,7 @@ class BatchedEnv:
 
 
 _STATE_KEYS = ("pos", "vel", "pre_pos", "pre_vel", "goal", "wp", "wp_cur", "wp_cnt", "reach", "wall", "step",
-               "map_idx")
+               "map_idx", "start")
 
 
 # =========================================================================== facade

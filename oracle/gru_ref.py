@@ -95,6 +95,52 @@ def ref_gru_update(actors, critics, actors_t, critics_t, b, d_own, gamma=0.95, t
     return stats, opts
 
 
+def ref_gru_update_dp(actors, critics, actors_t, critics_t, rank_b, d_own, gamma=0.95, tau=0.01, lr=1e-3,
+                      opts=None):
+    """Data-parallel update_myown: rank r holds batch rank_b[r] of its own
+    replay shard; every Adam step uses the mean over the ranks of their gradients (each rank's loss
+    of WGRU/maddpg:242-310 on its own batch, backward of loss / world accumulated).  Returns
+    stats[r] = [(loss_q, loss_a, q, target)] per agent on rank r's batch."""
+    N, ws = len(actors), len(rank_b)
+    if opts is None:
+        opts = ([torch.optim.Adam(a.parameters(), lr=lr) for a in actors],
+                [torch.optim.Adam(c.parameters(), lr=lr) for c in critics])
+    a_opts, c_opts = opts
+    stats = [[] for _ in range(ws)]
+    for i in range(N):
+        rows = []
+        for b in rank_b:
+            own, nown = b["s_own"][..., :d_own], b["n_own"][..., :d_own]
+            with torch.no_grad():
+                na = actors_t[i]([nown[:, i], b["n_radar"][:, i]], b["h_next"][:, i])[0]
+                qn = critics_t[i]([nown[:, i], b["n_radar"][:, i]], na, b["h_next"][:, i])[0].squeeze()
+                target = (b["rew"][:, i] + gamma * qn * (1 - b["done"][:, i])).unsqueeze(1)
+            rows.append((own, target))
+        c_opts[i].zero_grad()
+        lq, qs = [], []
+        for (own, target), b in zip(rows, rank_b):
+            q = critics[i]([own[:, i], b["s_radar"][:, i]], b["act"][:, i], b["h_cur"][:, i])[0]
+            loss_q = nn.MSELoss()(q, target)
+            (loss_q / ws).backward()
+            lq.append(loss_q.item())
+            qs.append(q.detach().clone())
+        c_opts[i].step()
+        a_opts[i].zero_grad()
+        la = []
+        for (own, _), b in zip(rows, rank_b):
+            a_i = actors[i]([own[:, i], b["s_radar"][:, i]], b["h_cur"][:, i])[0]
+            loss_a = 3 - critics[i]([own[:, i], b["s_radar"][:, i]], a_i, b["h_cur"][:, i])[0].mean()
+            (loss_a / ws).backward()
+            la.append(loss_a.item())
+        a_opts[i].step()
+        for r in range(ws):
+            stats[r].append((lq[r], la[r], qs[r], rows[r][1].squeeze(1).clone()))
+    for i in range(N):
+        soft_update(critics_t[i], critics[i], tau)
+        soft_update(actors_t[i], actors[i], tau)
+    return stats, opts
+
+
 def ref_gru_act(actors, own, radar, h, d_own):
     """Deterministic actions and next hidden states of all agents: own (E, N, >= d_own)."""
     outs, hs = [], []

@@ -106,6 +106,54 @@ def ref_update(actor, critic, actor_t, critic_t, batches, gamma=0.95, tau=0.01, 
     return stats, opts
 
 
+def ref_update_dp(actor, critic, actor_t, critic_t, rank_batches, gamma=0.95, tau=0.01, lr=1e-3, opts=None):
+    """One data-parallel update_myown: every rank holds its own replay
+    shard and samples its own batch i for iteration i; before each Adam step the ranks average
+    their gradients (all_reduce(SUM) / world, ATT/maddpg:375-425 per rank).  Restated literally:
+    each rank's loss on its own batch, backward of loss / world accumulated into the one set of
+    gradients, then the Adam step.  rank_batches[r] = the N batch dicts of rank r.  Returns
+    stats[r] = [(loss_q, loss_a, q, target)] per iteration on rank r's batch."""
+    ws = len(rank_batches)
+    N = len(rank_batches[0])
+    if opts is None:
+        opts = (torch.optim.Adam(actor.parameters(), lr=lr), torch.optim.Adam(critic.parameters(), lr=lr))
+    a_opt, c_opt = opts
+    stats = [[] for _ in range(ws)]
+    for agent in range(N):
+        targets = []
+        for r in range(ws):
+            b = rank_batches[r][agent]
+            with torch.no_grad():
+                na = actor_rows(actor_t, b["n_own"], b["n_radar"], b["n_nei"])
+                qn = critic_t([b["n_own"], b["n_radar"]], na).squeeze()
+                done_comb = torch.from_numpy(np.array([1 if any(torch.eq(d, 1)) else 0 for d in b["done"]]))
+                targets.append((b["rew"][:, agent] + gamma * qn * (1 - done_comb)).unsqueeze(1))
+        c_opt.zero_grad()
+        lq, qs = [], []
+        for r in range(ws):
+            b = rank_batches[r][agent]
+            q = critic([b["s_own"], b["s_radar"]], b["act"])
+            loss_q = nn.MSELoss()(q, targets[r])
+            (loss_q / ws).backward()
+            lq.append(loss_q.item())
+            qs.append(q.detach().clone())
+        c_opt.step()
+        a_opt.zero_grad()
+        la = []
+        for r in range(ws):
+            b = rank_batches[r][agent]
+            a_i = actor_rows(actor, b["s_own"], b["s_radar"], b["s_nei"])
+            loss_a = -critic([b["s_own"], b["s_radar"]], a_i).mean()
+            (loss_a / ws).backward()
+            la.append(loss_a.item())
+        a_opt.step()
+        for r in range(ws):
+            stats[r].append((lq[r], la[r], qs[r], targets[r].squeeze(1).clone()))
+    soft_update(critic_t, critic, tau)
+    soft_update(actor_t, actor, tau)
+    return stats, opts
+
+
 def random_transitions(E, N, seed, zero_nei_frac=0.1):
     g = torch.Generator().manual_seed(seed)
     D0, K = 6 + 4 * (N - 1), N - 1

@@ -66,3 +66,34 @@ def ref_update(actor, critic, actor_t, critic_t, opt_a, opt_c, b, gamma=0.95, ta
     soft_update(critic_t, critic, tau)
     soft_update(actor_t, actor, tau)
     return float(loss_Q.detach()), float(actor_loss.detach())
+
+
+def ref_update_dp(actor, critic, actor_t, critic_t, opt_a, opt_c, rank_b, gamma=0.95, tau=0.01):
+    """Data-parallel update_myown: rank r's loss of UAM/maddpg:346-512 on
+    its own batch rank_b[r]; each Adam step uses the mean of the ranks' gradients (backward of
+    loss / world accumulated).  Returns [(loss_q, loss_a)] per rank."""
+    ws = len(rank_b)
+    targets = []
+    for b in rank_b:
+        with torch.no_grad():
+            n0, n2 = b["n_own"], b["n_radar"]
+            next_q = critic_t([n0, n2], actor_t([n0, n2])).squeeze()
+            targets.append((b["rew"] + gamma * next_q * (1 - b["done"])).unsqueeze(1))
+    opt_c.zero_grad()
+    lq = []
+    for b, y in zip(rank_b, targets):
+        loss_Q = nn.MSELoss()(critic([b["own"], b["radar"]], b["act"]), y)
+        (loss_Q / ws).backward()
+        lq.append(float(loss_Q.detach()))
+    opt_c.step()
+    opt_a.zero_grad()
+    la = []
+    for b in rank_b:
+        s = [b["own"], b["radar"]]
+        actor_loss = -critic(s, actor(s)).mean()
+        (actor_loss / ws).backward()
+        la.append(float(actor_loss.detach()))
+    opt_a.step()
+    soft_update(critic_t, critic, tau)
+    soft_update(actor_t, actor, tau)
+    return list(zip(lq, la))

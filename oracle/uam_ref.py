@@ -95,6 +95,30 @@ def calculate_bearing(xh, yh, xi, yi):
     return -th if th < 0 else 360 - th
 
 
+def compute_t_cpa_d_cpa_potential_col(other_pos, host_pos, other_vel, host_vel, other_bound, host_bound,
+                                      total_possible_conf):
+    """UAM/util:916-938: time / distance of closest approach of the host to one neighbour, and the
+    running count of potential conflicts (CPA within one time unit closer than the two bounds).
+    Zero relative velocity: tcpa = -10 and d = the distance after one time unit (counted once if
+    it is inside the bounds; the [0, 1] test cannot fire for -10)."""
+    rel_dist_with_neg = -1 * (other_pos - host_pos)
+    rel_vel = other_vel - host_vel
+    sq = np.square(np.linalg.norm(rel_vel))
+    if sq == 0:
+        tcpa = -10
+        new_nei = other_pos + (other_vel * 1)
+        new_host = host_pos + (host_vel * 1)
+        d_tcpa = np.linalg.norm(new_host - new_nei)
+        if d_tcpa < (other_bound + host_bound):
+            total_possible_conf = total_possible_conf + 1
+    else:
+        tcpa = np.dot(rel_dist_with_neg, rel_vel) / sq
+        d_tcpa = np.linalg.norm(((rel_dist_with_neg * -1) + (rel_vel * tcpa)))
+    if (tcpa <= 1) and (tcpa >= 0) and (d_tcpa < (other_bound + host_bound)):
+        total_possible_conf = total_possible_conf + 1
+    return tcpa, d_tcpa, total_possible_conf
+
+
 def calculate_next_position(start, target, speed, dt):
     """UAM/util:300-318."""
     direction = target - start
@@ -456,8 +480,13 @@ class UAMEnv:
         return np.array(out)
 
     def observe(self):
-        """cur_state_norm_state_v3 (UAM/env:1294-1919): normalised (own, p2, radar, p3)."""
+        """cur_state_norm_state_v3 (UAM/env:1294-1919): normalised (own, p2, radar, p3).
+        The tdCPA values of UAM/env:1738-1745 (current state, and ``pre_pos`` / ``pre_vel``) are
+        kept in ``self.tdcpa_out`` = (tcpa[N][K], dcpa[N][K], conf_cur[N], conf_pre[N]) in the
+        sorted neighbour order; ``ss_reward`` recomputes the same values from the same state and
+        neighbour dict (UAM/env:4001-4010), so one copy serves both call sites."""
         own, p2, rad, p3 = [], [], [], []
+        tc_all, dc_all, cc_all, cp_all = [], [], [], []
         for i, ag in self.all_agents.items():
             ag.surroundingNeighbor = self.neighbours(ag)
             ag.observableSpace = self.radar(i)
@@ -466,8 +495,16 @@ class UAMEnv:
             norm_G = nmlz_pos([ag.goal[-1][0], ag.goal[-1][1]])
             o = np.append(np.concatenate([norm_pos, norm_vel, norm_G - norm_pos]), ag.heading)
             nb, n3 = [], []
+            cc = cp = 0
+            tcs, dcs = [], []
             for j, other in ag.surroundingNeighbor.items():
                 oa = self.all_agents[j]
+                tc, dc, cc = compute_t_cpa_d_cpa_potential_col(oa.pos, ag.pos, oa.vel, ag.vel,
+                                                               oa.protectiveBound, ag.protectiveBound, cc)
+                _, _, cp = compute_t_cpa_d_cpa_potential_col(oa.pre_pos, ag.pre_pos, oa.pre_vel, ag.pre_vel,
+                                                             oa.protectiveBound, ag.protectiveBound, cp)
+                tcs.append(float(tc))
+                dcs.append(float(dc))
                 norm_delta = norm_pos - nmlz_pos([oa.pos[0], oa.pos[1]])
                 nb.append(np.append(np.concatenate([norm_delta, nmlz_vel([oa.vel[0], oa.vel[1]])]), ag.heading))
                 npd = nmlz_pos_diff([other[0] - ag.pos[0], other[1] - ag.pos[1]])
@@ -478,6 +515,12 @@ class UAMEnv:
             p2.append(np.concatenate(nb))
             rad.append(ag.observableSpace.copy())
             p3.append(np.array(n3))
+            tc_all.append(tcs)
+            dc_all.append(dcs)
+            cc_all.append(cc)
+            cp_all.append(cp)
+        self.tdcpa_out = (np.array(tc_all), np.array(dc_all), np.array(cc_all, dtype=np.int32),
+                          np.array(cp_all, dtype=np.int32))
         return np.array(own), np.array(p2), np.array(rad), np.array(p3)
 
     # ------------------------------------------------------------------ reward

@@ -88,13 +88,13 @@ def bank_draw(bank_start, n_bank, seed, e, episode, N, pb=2.5, off=0):
 def uam_oracle_steps(pre, acts, N):
     """Worker for the config-5 parity test (spawned process, numpy only): one oracle/uam_ref.py
     step per env of ``pre`` (a device state dict sliced to the checked envs) from that exact
-    pre-step state.  Returns [(obs, reward, done, check_goal, bbc, mask, over, post_state)]."""
+    pre-step state.  Returns [(obs, reward, done, check_goal, bbc, mask, over, post_state, tdcpa)]."""
     from oracle import uam_ref as U
     out = []
     for e in range(len(acts)):
         o = U.env_from_state(pre, e, N)
         res = o.full_step(acts[e])
-        out.append(tuple(res) + (U.state_of(o),))
+        out.append(tuple(res) + (U.state_of(o), o.tdcpa_out))
     return out
 
 

@@ -231,6 +231,7 @@ def test_uam_n16_e8192_subset(native_lib):
     pick = np.random.default_rng(56)
     checked = 0
     seen = 0
+    conf = 0
     with cf.ProcessPoolExecutor(8, mp_context=mp.get_context("spawn")) as pool:
         for k in range(20):
             pre = {key: v.cpu().numpy() for key, v in env.get_state().items()}
@@ -240,13 +241,14 @@ def test_uam_n16_e8192_subset(native_lib):
             b = env.bufs
             post = {key: v.cpu().numpy() for key, v in env.get_state().items()}
             out = {name: getattr(b, name).cpu().numpy() for name in ("own", "radar", "nei", "nei6", "reward", "mask",
-                                                                     "done", "bbc", "env_done")}
+                                                                     "done", "bbc", "env_done", "tcpa", "dcpa",
+                                                                     "conf_cur", "conf_pre")}
             seen |= int(np.bitwise_or.reduce(out["mask"].reshape(-1)))
             envs = np.sort(pick.choice(E, S, replace=False))
             chunks = np.array_split(envs, 8)
             futs = [pool.submit(uam_oracle_steps, {key: v[c] for key, v in pre.items()}, act[c], N) for c in chunks]
             res = [r for f in futs for r in f.result()]
-            for e, (obs, r, d, cg, bbc, mk, over, ref) in zip(envs, res):
+            for e, (obs, r, d, cg, bbc, mk, over, ref, td) in zip(envs, res):
                 own, p2, rad, p3 = obs
                 w = f"step {k} env {e}"
                 np.testing.assert_allclose(out["own"][e], own, rtol=0, atol=TOL, err_msg=w)
@@ -261,9 +263,15 @@ def test_uam_n16_e8192_subset(native_lib):
                 for key in ("pos", "vel", "pre_pos", "pre_vel", "heading", "clouds"):
                     np.testing.assert_allclose(post[key][e], ref[key], rtol=0, atol=1e-12, err_msg=w + key)
                 assert np.array_equal(post["reach"][e], ref["reach"]) and np.array_equal(post["top2"][e], ref["top2"])
+                # the live tdCPA outputs (UAM/util:916-938 at UAM/env:1738-1745 / :4001-4010)
+                np.testing.assert_allclose(out["tcpa"][e], td[0], rtol=0, atol=TOL, err_msg=w + " tcpa")
+                np.testing.assert_allclose(out["dcpa"][e], td[1], rtol=0, atol=TOL, err_msg=w + " dcpa")
+                assert np.array_equal(out["conf_cur"][e], td[2]) and np.array_equal(out["conf_pre"][e], td[3]), w
+                conf += int(td[2].sum())
                 checked += 1
             env.auto_reset(b.env_done)
     assert checked == 20 * S
+    assert conf > 0                             # potential tdCPA conflicts were counted and compared
     assert seen & 0b110 == 0b110, bin(seen)     # cloud / runway conflicts and drone collisions occurred
 
 

@@ -38,6 +38,7 @@ def _state_to_oracle(env, co):
     co.pos[:] = s["pos"]; co.vel[:] = s["vel"]; co.pre_pos[:] = s["pre_pos"]; co.pre_vel[:] = s["pre_vel"]
     co.goal[:] = s["goal"]; co.wp[:] = s["wp"]; co.wp_cur[:] = s["wp_cur"]; co.wp_cnt[:] = s["wp_cnt"]
     co.reach[:] = s["reach"]; co.wall[:] = s["wall"]; co.step_count[:] = s["step"]
+    co.start[:] = s["start"]
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])

@@ -33,7 +33,7 @@ def _np_state(env):
     return {k: v.cpu().numpy() for k, v in env.get_state().items()}
 
 
-def _check_obs(b, e, obs, nei6=True):
+def _check_obs(b, e, obs, nei6=True, tdcpa=None):
     own, p2, rad, p3 = obs
     N = own.shape[0]
     np.testing.assert_allclose(b.own[e].cpu().numpy(), own, rtol=0, atol=TOL)
@@ -41,6 +41,19 @@ def _check_obs(b, e, obs, nei6=True):
     np.testing.assert_allclose(b.nei[e].cpu().numpy().reshape(N, -1), p2, rtol=0, atol=TOL)
     if nei6:
         np.testing.assert_allclose(b.nei6[e].cpu().numpy(), p3, rtol=0, atol=TOL)
+    if tdcpa is not None:
+        check_tdcpa(b, e, tdcpa)
+
+
+def check_tdcpa(b, e, tdcpa, err=""):
+    """The live tdCPA outputs (UAM/util:916-938 at UAM/env:1738-1745, :4001-4010) against the
+    oracle's ``tdcpa_out``: tcpa / dcpa in the sorted neighbour order within 1e-9, the two
+    potential-conflict counts bit-exact."""
+    tc, dc, cc, cp = tdcpa
+    np.testing.assert_allclose(b.tcpa[e].cpu().numpy(), tc, rtol=0, atol=TOL, err_msg=err + " tcpa")
+    np.testing.assert_allclose(b.dcpa[e].cpu().numpy(), dc, rtol=0, atol=TOL, err_msg=err + " dcpa")
+    assert np.array_equal(b.conf_cur[e].cpu().numpy(), cc), (err, b.conf_cur[e].cpu().numpy(), cc)
+    assert np.array_equal(b.conf_pre[e].cpu().numpy(), cp), (err, b.conf_pre[e].cpu().numpy(), cp)
 
 
 @pytest.mark.parametrize("N", [16, 5])
@@ -55,7 +68,7 @@ def test_uam_reset_matches_oracle(native_lib, N):
     for e in range(E):
         o = U.UAMEnv(N)
         obs = o.reset(st[e], go[e], cl[e, 0], cl[e, 1])
-        _check_obs(env.bufs, e, obs)
+        _check_obs(env.bufs, e, obs, tdcpa=o.tdcpa_out)
         ref = U.state_of(o)
         for k in ("pos", "vel", "pre_pos", "pre_vel", "goal", "start", "clouds"):
             np.testing.assert_array_equal(s[k][e], ref[k], err_msg=k)
@@ -74,6 +87,7 @@ def _stepped_pair(N, E, seed, steps, act_scale=1.0):
     env.reset(st, go, cl)
     rng = np.random.default_rng(seed)
     masks = []
+    conf = [0, 0]          # potential conflicts counted, zero-relative-velocity pairs seen
     for k in range(steps):
         pre = _np_state(env)
         act = rng.uniform(-act_scale, act_scale, (E, N, 2))
@@ -84,7 +98,9 @@ def _stepped_pair(N, E, seed, steps, act_scale=1.0):
         for e in range(E):
             o = U.env_from_state(pre, e, N)
             obs, r, d, cg, bbc, mk, over = o.full_step(act[e])
-            _check_obs(b, e, obs)
+            _check_obs(b, e, obs, tdcpa=o.tdcpa_out)
+            conf[0] += int(o.tdcpa_out[2].sum())
+            conf[1] += int((o.tdcpa_out[0] == -10).sum())
             np.testing.assert_allclose(b.reward[e].cpu().numpy(), r, rtol=0, atol=TOL)
             assert np.array_equal(b.mask[e].cpu().numpy(), mk), (k, e, b.mask[e].cpu().numpy(), mk)
             assert np.array_equal(b.done[e].cpu().numpy().astype(bool), d)
@@ -97,18 +113,65 @@ def _stepped_pair(N, E, seed, steps, act_scale=1.0):
             assert np.array_equal(post["top2"][e], ref["top2"])
             assert post["cloud_tgt"][e] == ref["cloud_tgt"] and post["step"][e] == ref["step"]
         masks.append(b.mask.cpu().numpy().copy())
-    return masks
+    return masks, conf
 
 
 def test_uam_step_matches_oracle_n16(native_lib):
-    masks = _stepped_pair(16, 4, 7, 6)
+    masks, conf = _stepped_pair(16, 4, 7, 6)
     assert sum(int((m & 2).any()) for m in masks) > 0      # runway / cloud conflicts happen
+    assert conf[0] > 0                                     # potential tdCPA conflicts were compared
 
 
 def test_uam_step_matches_oracle_n3_long(native_lib):
     # few aircraft, small actions: long episodes reach goals, move the go-around aircraft along
     # its loop and exercise the near-drone band
     _stepped_pair(3, 8, 11, 25, act_scale=0.6)
+
+
+@pytest.mark.parametrize("N", [16, 4])
+def test_uam_tdcpa_branches(native_lib, N):
+    """tdCPA (UAM/util:916-938) on injected states built to hit every branch: pairs flying with
+    equal velocities (zero relative velocity: tcpa = -10, conflict when the one-unit look-ahead is
+    inside the two bounds), head-on pairs closing inside one time unit (tcpa in [0, 1], d < 1) and
+    diverging pairs (tcpa < 0).  Current and ``pre_*`` counts both compared bit-exact."""
+    from multi_agent_aac_amd import uam
+    E = 8
+    st, go, cl = _episodes(E, N, 300 + N)
+    env = uam.BatchedUAM(E, N, p3=True, tdcpa=True)
+    env.reset(st, go, cl)
+    s = _np_state(env)
+    rng = np.random.default_rng(N)
+    pos, vel = s["pos"].copy(), s["vel"].copy()
+    for e in range(E):
+        for i in range(0, N - 1, 2):
+            c = np.array([12.0 + 2.5 * (i % 6), 8.0 + 4.0 * (i // 6)]) + rng.uniform(-0.2, 0.2, 2)
+            kind = (e + i // 2) % 3
+            if kind == 0:        # same velocity, 0.6 apart: zero relative velocity, conflict
+                v = rng.uniform(-0.3, 0.3, 2)
+                pos[e, i], pos[e, i + 1] = c, c + [0.6, 0.0]
+                vel[e, i] = vel[e, i + 1] = v
+            elif kind == 1:      # head-on, closing: tcpa in [0, 1], d < 1
+                pos[e, i], pos[e, i + 1] = c, c + [0.9, 0.05]
+                vel[e, i], vel[e, i + 1] = [0.4, 0.0], [-0.4, 0.0]
+            else:                # diverging: tcpa < 0
+                pos[e, i], pos[e, i + 1] = c, c + [0.9, 0.0]
+                vel[e, i], vel[e, i + 1] = [-0.4, 0.0], [0.4, 0.0]
+    env.set_state(pos=pos, vel=vel, pre_pos=pos, pre_vel=vel)
+    pre = _np_state(env)
+    act = np.zeros((E, N, 2))
+    env.step(torch.from_numpy(act).to(DEV))
+    torch.cuda.synchronize()
+    b = env.bufs
+    seen_zero = seen_conf = seen_neg = 0
+    for e in range(E):
+        o = U.env_from_state(pre, e, N)
+        obs, *_ = o.full_step(act[e])
+        _check_obs(b, e, obs, tdcpa=o.tdcpa_out)
+        tc = o.tdcpa_out[0]
+        seen_zero += int((tc == -10).sum())
+        seen_neg += int(((tc < 0) & (tc != -10)).sum())
+        seen_conf += int(o.tdcpa_out[2].sum() + o.tdcpa_out[3].sum())
+    assert seen_zero > 0 and seen_conf > 0 and seen_neg > 0, (seen_zero, seen_conf, seen_neg)
 
 
 def test_uam_event_coverage(native_lib):

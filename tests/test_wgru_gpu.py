@@ -92,12 +92,46 @@ def test_wgru_auto_reset_bank(native_lib, occ):
         _cmp_step(env.bufs, co, f"bank t{t}")
 
 
+def test_wgru_set_state_carries_reference_path(native_lib, occ):
+    """A state injected from a different OD (set_state of every key, `start` included) steps like
+    the oracle reset with that OD: the cross-track reward reads the injected reference-path origin,
+    not the one the env's own last reset wrote."""
+    E, N = 64, 8
+    st1, wps1, cnt1 = random_od(occ, E, N, seed=41)
+    st2, wps2, cnt2 = random_od(occ, E, N, seed=42)
+    env, donor = _env(E, N, occ), _env(E, N, occ)
+    env.reset(st1, wps1, cnt1)
+    donor.reset(st2, wps2, cnt2)
+    torch.cuda.synchronize()
+    s = donor.get_state()
+    assert not np.array_equal(s["start"].cpu().numpy(), env.get_state()["start"].cpu().numpy())
+    env.set_state(**s)
+    np.testing.assert_array_equal(env.get_state()["start"].cpu().numpy(), st2)
+    co = c_oracle.BatchedOracle(E, N, occ, W=W_DEFAULT, variant="wgru")
+    co.reset(st2, wps2, cnt2)
+    rng = np.random.default_rng(3)
+    for t in range(5):
+        _state_to_oracle(env, co)
+        act = steer(co.pos, co.vel, _targets(co), rng)
+        env.step(torch.from_numpy(act).cuda())
+        co.step(act)
+        torch.cuda.synchronize()
+        _cmp_step(env.bufs, co, f"injected t{t}")
+
+
 def test_wgru_config_checks(native_lib, occ):
     from multi_agent_aac_amd import _native
     from multi_agent_aac_amd.env import BatchedEnv
     env = BatchedEnv(8, 4, occ, variant="wgru")
     assert env.cfg.radar_mode == 1 and env.cfg.team_reward == 0 and env.cfg.vmax == 10.0
     assert env.cfg.episode_length == 150 and env.bufs.own.shape == (8, 4, 6)
+    # explicit values are kept (ADVICE r02: 5 / 50 used to be rewritten to the variant defaults)
+    e2 = BatchedEnv(8, 4, occ, variant="wgru", vmax=5.0, episode_length=50)
+    assert e2.cfg.vmax == 5.0 and e2.cfg.episode_length == 50
+    with pytest.raises(ValueError):
+        BatchedEnv(8, 4, occ, variant="wgru", radar_mode="drones")
+    with pytest.raises(ValueError):
+        BatchedEnv(8, 4, occ, variant="wgru", team_reward=True)
     cfg = env.cfg
     cfg.radar_mode = 0                      # variant 1 needs the obstacle radar
     import ctypes
