@@ -9,7 +9,11 @@ One timed *step* = one vectorised training iteration of ATT/main:248-447 on ever
 value = E_total * N * steps / max-over-ranks wall time.  Inputs are synthetic (seeded map, OD
 bank, random-init networks); the replay is pre-filled to 1e5 transitions before timing.
 
-python bench.py [--gpus N] [--steps K] [--warmup W]        (N > 1: launched by torch.distributed.run)
+python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1: one process per GPU under torch.distributed.run (RCCL).  When WORLD_SIZE is already set (the
+driver's ``torch.distributed.run ... bench.py --gpus N``) this process is one rank; otherwise this
+process starts the N ranks itself as a child ``torch.distributed.run`` (before touching the GPU),
+waits, and exits with its return code (rank 0 prints the line).
 
 ``--model gru`` measures config 4 instead (randomOD_gru_radar): the
 same vectorised loop with the GRU-actor MADDPG of MADDPG_ownENV_randomOD_Wgru_radar (one GRU actor
@@ -32,6 +36,8 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+from multi_agent_aac_amd import trace  # noqa: E402  (roctx ranges, off unless AAC_ROCTX=1)
 
 METRIC = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 5 agents×4096 envs"
 METRIC_GRU = "agent-env-steps/sec (whole node) + MADDPG updates/sec, 8 agents×4096 envs, GRU actor"
@@ -137,6 +143,12 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-procs", type=int, default=None,
+                   help="CPU-baseline processes (default: physical cores, capped at the GPU box's per-GPU CPU "
+                        "share of 16, AAC_CPU_SHARE)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="N > 1 plumbing check: every rank joins the process group (gloo), prints its rank and "
+                        "exits without touching the GPU")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "env_step_pmc.json"))
@@ -156,6 +168,27 @@ def parse():
     return a
 
 
+def launch_ranks(a, argv):
+    """``--gpus N`` (N > 1) outside a torch.distributed.run environment: start the N ranks as a child
+    ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1`` of this
+    script (one process per GPU, RCCL), before anything here has touched the GPU (no exec: a child
+    process).  The CPU baseline is a 1-GPU field (rank 0 at N = 1 only), so the ranks skip it.
+    Returns the child's exit code; rank 0's JSON line reaches stdout directly."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    if "--no-cpu-baseline" not in argv:
+        cmd.append("--no-cpu-baseline")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC only on this host driver (RCCL)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def setup_dist(backend):
     from multi_agent_aac_amd import parallel
     ws, rank, local, _ = parallel.init_from_env(backend)
@@ -168,7 +201,27 @@ def barrier(ws):
     torch.cuda.synchronize()
 
 
-class Trainer:
+class CheckpointMixin:
+    """Full-state checkpoint of the training loop (multi_agent_aac_amd/checkpoint.py): learner,
+    replay, env state + episode counters, and the loop's current observation rows (+ GRU hidden
+    states).  A run resumed from it continues bit-identically (tests/test_checkpoint_gpu.py)."""
+
+    def checkpoint_parts(self):
+        extra = {f"cur.{k}": v for k, v in vars(self.cur).items() if torch.is_tensor(v)}
+        if getattr(self, "gru", False):
+            extra["h"] = self.h
+        return dict(learner=self.model, replay=self.replay, env=self.env, extra=extra)
+
+    def save_checkpoint(self, path):
+        from multi_agent_aac_amd import checkpoint
+        return checkpoint.save(path, **self.checkpoint_parts())
+
+    def load_checkpoint(self, path):
+        from multi_agent_aac_amd import checkpoint
+        return checkpoint.load(path, **self.checkpoint_parts())
+
+
+class Trainer(CheckpointMixin):
     """Vectorised ma_main loop on one GPU (shared by bench.py and the examples)."""
 
     def __init__(self, E, N, B, memory, radar, seed, pg=None, model="att", maps=1):
@@ -216,34 +269,39 @@ class Trainer:
 
     def step(self, update=True, time_env=False):
         c, n = self.cur, self.nxt
-        if self.gru:
-            hn_buf = self.hp[1] if self.h is self.hp[0] else self.hp[0]
-            act, hn = self.model.act(c.own, c.radar, self.h, self.episode, noisy=True, h_out=hn_buf)
-        else:
-            act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
+        with trace.range("act"):
+            if self.gru:
+                hn_buf = self.hp[1] if self.h is self.hp[0] else self.hp[0]
+                act, hn = self.model.act(c.own, c.radar, self.h, self.episode, noisy=True, h_out=hn_buf)
+            else:
+                act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
         if time_env:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        self.env.step(act, out=n)
+        with trace.range("env_step"):
+            self.env.step(act, out=n)
         if time_env:
             ev1.record()
             self.env_events.append((ev0, ev1))
-        if self.gru:     # rows keep (cur_hidden, next_hidden) as WGRU/ma_main:636
-            self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, self.h, hn)
-            self.h = hn
-            from multi_agent_aac_amd import gru
-            gru.reset_hidden(self.h, n.env_done)     # a new episode starts from zeros (WGRU/ma_main:476-478)
-        else:
-            self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
+        with trace.range("replay_push"):
+            if self.gru:     # rows keep (cur_hidden, next_hidden) as WGRU/ma_main:636
+                self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, self.h,
+                                       hn)
+                self.h = hn
+                from multi_agent_aac_amd import gru
+                gru.reset_hidden(self.h, n.env_done)     # a new episode starts from zeros (WGRU/ma_main:476-478)
+            else:
+                self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei)
         self.cur, self.nxt = n, c
         run_update = update and len(self.replay) > self.B
         # the auto-reset writes env state and the next observation rows, which the update never reads:
         # it runs on a side stream beside the update (the next act waits for both)
-        with side_stream(self, run_update):
+        with side_stream(self, run_update), trace.range("auto_reset"):
             self.env.auto_reset(n.env_done, out=n)
         if run_update:
-            self.model.update(self.B, use_graph=not NO_GRAPH, want_stats=False)
+            with trace.range("update"):
+                self.model.update(self.B, use_graph=not NO_GRAPH, want_stats=False)
         join_side(self)
 
 
@@ -279,7 +337,7 @@ def join_side(tr):
         tr._side_used = False
 
 
-class UamTrainer:
+class UamTrainer(CheckpointMixin):
     """Vectorised UAM/main:361-640 loop on one GPU: actor + noise, env step, one replay row per
     aircraft, GPU auto-reset from the episode bank, one update_myown (one gradient iteration)."""
 
@@ -303,31 +361,34 @@ class UamTrainer:
 
     def step(self, update=True, time_env=False):
         c, n = self.cur, self.nxt
-        act = self.model.act(c.own, c.radar, self.episode, noisy=True)
+        with trace.range("act"):
+            act = self.model.act(c.own, c.radar, self.episode, noisy=True)
         if time_env:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        self.env.step(act, out=n)
+        with trace.range("env_step"):
+            self.env.step(act, out=n)
         if time_env:
             ev1.record()
             self.env_events.append((ev0, ev1))
-        self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
+        with trace.range("replay_push"):
+            self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
         self.cur, self.nxt = n, c
         run_update = update and len(self.replay) > self.B
-        with side_stream(self, run_update):
+        with side_stream(self, run_update), trace.range("auto_reset"):
             self.env.auto_reset(n.env_done, out=n)
         if run_update:
-            self.model.update(self.B, use_graph=not NO_GRAPH)
+            with trace.range("update"):
+                self.model.update(self.B, use_graph=not NO_GRAPH)
         join_side(self)
 
 
-def cpu_baseline_uam(E, N, B, seconds):
+def cpu_baseline_uam(E, N, B, seconds, procs_req=None):
     """UAM: the reference-shaped scalar oracle env step (oracle/uam_ref.py) on the host cores plus the
     CPU float64 update_myown restatement (bounded sample)."""
     import multiprocessing as mp
     from oracle import uam_learner_ref as R
-    cores = len(os.sched_getaffinity(0))
-    procs = min(cores, 16)
+    procs, phys, cores = baseline_procs(procs_req)
     ctx = mp.get_context("spawn")
     budget = seconds / 2
     with ctx.Pool(procs) as pool:
@@ -350,6 +411,8 @@ def cpu_baseline_uam(E, N, B, seconds):
     t_upd = (time.perf_counter() - t0) / n_upd
     t_iter = E * N / env_rate + t_upd
     return {"value": E * N / t_iter, "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
+            "physical_cores": phys, "affinity_cores": cores, "cpu_model": cpu_model(),
+            "per_physical_core_extrapolated": _extrapolate(env_rate, procs, phys, t_upd, E, N),
             "sample": (f"reference-shaped scalar UAM env oracle on {procs} processes x 1 env x {N} aircraft, "
                        f"{steps} env steps ({env_rate:.3g} agent-env-steps/s env-only) + CPU float64 "
                        f"update_myown restatement B={B} x {n_upd} ({t_upd * 1e3:.2f} ms each), {procs} threads; "
@@ -373,6 +436,42 @@ def _cpu_uam_worker(N, budget, wid):
             env.reset(*U.sample_episode(N, py, npr))
         steps += 1
     return steps, time.perf_counter() - t0
+
+
+def host_cores():
+    """(physical cores = lscpu 'Core(s) per socket' x 'Socket(s)', CPUs in this process's affinity)."""
+    import subprocess
+    aff = len(os.sched_getaffinity(0))
+    per, sockets = None, None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Core(s) per socket:"):
+                per = int(line.split(":", 1)[1])
+            elif line.startswith("Socket(s):"):
+                sockets = int(line.split(":", 1)[1])
+    except Exception:
+        pass
+    return (per * sockets if per and sockets else aff), aff
+
+
+def baseline_procs(requested=None):
+    """Processes of the CPU baseline: one per physical core, capped by the affinity and
+    by the GPU box's CPU share per GPU (16, AAC_CPU_SHARE): the host is shared by the jobs of its 8
+    GPUs.  Returns (procs, physical cores, affinity CPUs)."""
+    phys, aff = host_cores()
+    if requested:
+        return int(requested), phys, aff
+    return max(1, min(phys, aff, int(os.environ.get("AAC_CPU_SHARE", "16")))), phys, aff
+
+
+def _extrapolate(env_rate, procs, phys, t_upd, E, N):
+    """The same iteration with the env spread over one process per physical core: the measured
+    per-process env rate x physical cores (envs are independent and the scalar env is compute-bound:
+    no shared state), plus the measured update time."""
+    rate = env_rate / procs * phys
+    return {"value": E * N / (E * N / rate + t_upd), "env_only": rate, "cores": phys,
+            "basis": f"measured per-process env rate x {phys} physical cores + measured update time"}
 
 
 def cpu_model():
@@ -416,7 +515,7 @@ def _cpu_update_time(N, B, budget, model, threads):
     return (time.perf_counter() - t0) / n_upd, n_upd
 
 
-def cpu_baseline(E, N, B, radar, seconds, model="att"):
+def cpu_baseline(E, N, B, radar, seconds, model="att", procs_req=None):
     """BASELINE.md's CPU baseline on the host cores (bounded sample of the same workload): the env
     step timed in three forms, each combined with the torch-CPU update_myown restatement as one
     training iteration (value = E x N agent-steps / (env step + update)):
@@ -427,9 +526,8 @@ def cpu_baseline(E, N, B, radar, seconds, model="att"):
     Each env rate is agent-env-steps/s summed over the processes (envs are independent)."""
     import multiprocessing as mp
     if model == "uam":
-        return cpu_baseline_uam(E, N, B, seconds)
-    cores = len(os.sched_getaffinity(0))
-    procs = min(cores, 16)
+        return cpu_baseline_uam(E, N, B, seconds, procs_req)
+    procs, phys, cores = baseline_procs(procs_req)
     ctx = mp.get_context("spawn")
     per = max(1, E // procs)
     slot = seconds / 5
@@ -456,7 +554,8 @@ def cpu_baseline(E, N, B, radar, seconds, model="att"):
              "c_port_per_core": mode(cp, "oracle/aac_oracle.c batched C restatement, one process per core")}
     head = modes["scalar_per_core"]
     return {"value": head["value"], "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
-            "affinity_cores": cores, "cpu_model": cpu_model(),
+            "physical_cores": phys, "affinity_cores": cores, "cpu_model": cpu_model(),
+            "per_physical_core_extrapolated": _extrapolate(head["env_only"], procs, phys, t_upd, E, N),
             "sample": (f"mode 1: reference-shaped scalar env ({sref}, {radar} radar) on {procs} processes "
                        f"x 1 env x {N} agents, {sum(r[0] for r in m1)} env steps in ~{slot:.1f} s "
                        f"({head['env_only']:.3g} agent-env-steps/s env-only) + torch-CPU update_myown restatement "
@@ -595,11 +694,24 @@ def main():
     global NO_GRAPH
     a = parse()
     NO_GRAPH = a.no_graph
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
     ws0 = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and ws0 != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ws0}")
+    if a.launch_check:
+        from multi_agent_aac_amd import parallel
+        ws, rank, _, _ = parallel.init_from_env("gloo") if ws0 > 1 else (1, 0, 0, None)
+        if ws > 1:
+            dist.barrier()
+        print(json.dumps({"launch_check": True, "rank": rank, "world_size": ws, "gpus": a.gpus}), flush=True)
+        if ws > 1:
+            dist.destroy_process_group()
+        return
     cpu = None
     if ws0 == 1 and not a.no_cpu_baseline:
         # before any GPU initialisation: the pool's children must not inherit a GPU context
-        cpu = cpu_baseline(a.envs, a.agents, a.batch, a.radar, a.cpu_seconds, model=a.model)
+        cpu = cpu_baseline(a.envs, a.agents, a.batch, a.radar, a.cpu_seconds, model=a.model, procs_req=a.cpu_procs)
     ws, rank, local = setup_dist(a.backend)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(777 + rank)
@@ -616,8 +728,9 @@ def main():
     barrier(ws)
     tr.env_events.clear()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        tr.step(update=True, time_env=True)
+    with trace.range("timed_steps"):
+        for _ in range(a.steps):
+            tr.step(update=True, time_env=True)
     barrier(ws)
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], device="cuda")

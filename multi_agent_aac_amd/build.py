@@ -17,11 +17,14 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("AAC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["csrc/aac_env.hip", "csrc/aac_learn.hip", "csrc/aac_fused.hip", "csrc/aac_gru.hip", "csrc/aac_mpe.hip",
-           "csrc/aac_uam.hip", "csrc/aac_uam_actor.hip", "csrc/aac_uam_learn.hip", "csrc/aac_host.cpp"]
+           "csrc/aac_uam.hip", "csrc/aac_uam_actor.hip", "csrc/aac_uam_learn.hip", "csrc/aac_host.cpp",
+           "csrc/aac_trace.cpp"]
 HEADERS = ["include/aac_env.h", "include/aac_learn.h", "include/aac_fused.h", "include/aac_gru.h", "include/aac_mpe.h",
-           "include/aac_uam.h", "include/aac_uam_learn.h", "multi_agent_aac_amd/csrc/aac_wave.h",
+           "include/aac_uam.h", "include/aac_uam_learn.h", "include/aac_trace.h", "multi_agent_aac_amd/csrc/aac_wave.h",
            "multi_agent_aac_amd/csrc/aac_geom.h"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}"]
+# roctx ranges (include/aac_trace.h) come from rocprofiler-sdk's roctx library, found at run time by rpath
+LINK = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
 LIB = os.path.join(HERE, "libaac_env.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 
@@ -54,7 +57,7 @@ def build(force=False, verbose=False, jobs=None):
             for f in [ex.submit(_compile, s, o, verbose) for s, o in todo]:
                 f.result()
     if force or todo or _stale(LIB, objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs + LINK
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, cwd=HERE)

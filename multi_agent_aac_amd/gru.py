@@ -36,7 +36,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import fused, ops, parallel
+from . import fused, ops, parallel, trace
 from .fused import RELU, TANH, Collective, gemm_launches, prob, ptr
 from .memory import DeviceReplay, Experience, ReplayMemory
 from .networks import FlatParams
@@ -522,9 +522,11 @@ class MADDPG:
     def _replay(self):
         graphs, colls = self._graph
         for k, g in enumerate(graphs):
-            g.replay()
+            with trace.range(f"update.seg{k}"):
+                g.replay()
             if k < len(colls):
-                colls[k]()
+                with trace.range("allreduce"):
+                    colls[k]()
 
     def update(self, B=None, use_graph=True, idx=None, want_stats=True, replay=None):
         """One update_myown on the device replay (no host synchronisation); ``replay`` defaults to

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from . import fused, ops, parallel
+from . import fused, ops, parallel, trace
 from .memory import DeviceReplay, ReplayMemory
 from .networks import ActorNetwork_ATT_TwoPortion, CriticCombine, FlatParams
 
@@ -266,11 +266,14 @@ class MADDPG:
         if isinstance(self._graph, tuple):
             graphs, colls = self._graph
             for k, g in enumerate(graphs):
-                g.replay()
+                with trace.range(f"update.seg{k}"):
+                    g.replay()
                 if k < len(colls):
-                    colls[k]()
+                    with trace.range("allreduce"):
+                        colls[k]()
         else:
-            self._graph.replay()
+            with trace.range("update.graph"):
+                self._graph.replay()
 
     def update(self, B=None, use_graph=True, idx_list=None, want_stats=True, replay=None):
         """One update_myown-equivalent on the device replay (no host synchronisation).  Returns

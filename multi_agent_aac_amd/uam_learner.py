@@ -32,7 +32,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import ops, uam
+from . import ops, trace, uam
 
 F64 = torch.float64
 ROW = 7 + 18 + 2 + 1 + 1 + 7 + 18           # [own | radar | a | r | done | own' | radar']
@@ -452,9 +452,11 @@ class FusedUamUpdate:
 
     def replay(self):
         for k, g in enumerate(self.graphs):
-            g.replay()
+            with trace.range(f"update.seg{k}"):
+                g.replay()
             if k < len(self.colls):
-                self.colls[k]()
+                with trace.range("allreduce"):
+                    self.colls[k]()
 
 
 class MADDPG:

@@ -1,0 +1,72 @@
+"""Full-state checkpoint / resume (multi_agent_aac_amd/checkpoint.py): a
+training loop interrupted after a checkpoint and resumed in a fresh process state (new env, learner,
+replay, captured graphs) continues bit-identically to the uninterrupted run -- parameters, targets,
+Adam moments and steps, replay rows / position / sampler counter, env state and episode counters,
+observation rows.  ATT (config 3 shape, small), GRU (config 4 learner + WGRU env), UAM (config 5)."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(model):
+    import bench
+    if model == "uam":
+        return bench.UamTrainer(256, 6, 128, 8192, seed=1)
+    return bench.Trainer(256, 5 if model == "att" else 4, 128, 4096, "combined", seed=1, model=model)
+
+
+def _snapshot(tr):
+    from multi_agent_aac_amd import checkpoint
+    torch.cuda.synchronize()
+    out = {"L." + k: v.clone() for k, v in checkpoint.learner_tensors(tr.model).items()}
+    out.update({"R." + k: v.clone() for k, v in checkpoint.replay_tensors(tr.replay).items()})
+    out.update({"E." + k: v.clone() for k, v in checkpoint.env_tensors(tr.env).items()})
+    out.update({"X." + k: v.clone() for k, v in tr.checkpoint_parts()["extra"].items()})
+    return out
+
+
+@pytest.mark.parametrize("model", ["att", "gru", "uam"])
+def test_resume_is_bit_identical(native_lib, model, tmp_path):
+    a = _trainer(model)
+    while len(a.replay) <= a.B:
+        a.step(update=False)
+    for _ in range(3):
+        a.step(update=True)
+    path = str(tmp_path / f"{model}.ckpt")
+    a.save_checkpoint(path)
+    for _ in range(4):
+        a.step(update=True)
+    want = _snapshot(a)
+    b = _trainer(model)                  # fresh loop: its own first OD draws, random init, empty replay
+    b.load_checkpoint(path)
+    for _ in range(4):
+        b.step(update=True)
+    got = _snapshot(b)
+    assert set(want) == set(got)
+    bad = [k for k in want if not torch.equal(want[k], got[k])]
+    assert not bad, bad
+    assert len(a.replay) == len(b.replay) and a.replay.pos == b.replay.pos
+
+
+def test_checkpoint_refuses_mismatch(native_lib, tmp_path):
+    from multi_agent_aac_amd import checkpoint
+    a = _trainer("att")
+    path = str(tmp_path / "att.ckpt")
+    checkpoint.save(path, learner=a.model, replay=a.replay)
+    g = _trainer("gru")
+    with pytest.raises(ValueError):
+        checkpoint.load(path, learner=g.model)
+    with pytest.raises(KeyError):
+        checkpoint.load(path, learner=a.model, env=a.env)
+    ck = torch.load(path, weights_only=True)
+    ck["parts"]["replay"]["tensors"]["counter"].fill_(1 << 32)     # 32-bit RNG epochs only
+    torch.save(ck, path)
+    with pytest.raises(ValueError):
+        checkpoint.load(path, replay=a.replay)

@@ -13,5 +13,5 @@ objs=""
 for o in build/obj/*.o; do
   if [ "$(basename $o)" = "$base.o" ]; then objs="$objs $out/$tag.$base.o"; else objs="$objs $o"; fi
 done
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/lib_$tag.so $objs
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/lib_$tag.so $objs -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 echo $out/lib_$tag.so
