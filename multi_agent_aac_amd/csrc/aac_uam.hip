@@ -31,6 +31,7 @@
 #define MAXA 64   // aircraft per workgroup
 #define KMAX (MAXA - 1)
 #define NONE8 255
+#define CLIP_CAP 2048   // radar clip jobs per workgroup in LDS (8 KB: four workgroups per CU still fit)
 
 #ifndef AAC_UAM_MIN_WAVES     // waves per SIMD the step kernel is compiled for: 4 (<= 128 VGPRs) instead
 #define AAC_UAM_MIN_WAVES 4   // of the 130-VGPR / 3-wave build
@@ -99,6 +100,8 @@ struct Lds {
                                           // coefficient, bit2 collision bearing doubles the crash
                                           // penalty, bit3 previous-nearest-two collided
     double nd_val[MAXA], base[MAXA];      // m d + c of the near-drone band; dist_to_goal - near_building
+    unsigned nclip;                       // radar work list: (ray, polygon) clip jobs (radar_phase)
+    uint32_t clip[CLIP_CAP];
 };
 
 __device__ inline double nmlz(double v, double lo, double hi) { return 2 * ((v - lo) / (hi - lo)) - 1; }
@@ -278,60 +281,131 @@ __device__ void order_phase(const UArgs &A, Lds &S, int nag) {
     }
 }
 
-// (3) radar ray r of aircraft i (UAM/env:1360-1486): min over the runway boundary, the 4 bound
-// segments, the cloud boundaries and the other aircraft's 64-gons; default the ray's GEOS length
-__device__ double radar_ray(const UArgs &A, const Lds &S, int le, int base, int i, int r) {
+// (3) radar of aircraft i (UAM/env:1360-1486): per ray the minimum over the runway boundary, the 4
+// bound segments, the cloud boundaries and the other aircraft's 64-gons; default the ray's GEOS length.
+// The radar as a work list (the default): (3a) per (aircraft, ray) the fixed boundaries -- ray length,
+// runway, bound segments -- and the cheap exact pre-filter of the 64-gons (the env's two clouds and
+// the other aircraft), whose candidates are appended to an LDS list of (ray, polygon) clip jobs;
+// (3b) the clips of the list spread evenly over all 256 threads, each hit folded into its ray by an
+// LDS atomic min on the (non-negative) float64 bits; (3c) the rays to HBM.  The per-ray loop of
+// radar_ray ran the clips of one ray in one lane, so a wave waited for its most crowded ray (the
+// crowded start zones give rays with 5-10 candidates beside rays with none): 2/3 of the step
+// kernel's cycles.  The minimum does not depend on the order: bit-identical to radar_ray.
+// A job is (w << 8) | j: w = local aircraft * NRAY + ray, j < 64 another aircraft, 64 + k cloud k.
+// A list that would overflow CLIP_CAP leaves the lane to clip its remaining candidates itself.
+__device__ inline double ray_clip_dist(const UArgs &A, const Lds &S, int le, int base, int i, int r, int j,
+                                       bool &hit) {
     const double2 p = S.pos[base + i];
     const double cx = p.x, cy = p.y;
     const double ex = cx + A.radar_len * c_tab.ray_c[r], ey = cy + A.radar_len * c_tab.ray_s[r];
-    const double inv_l2 = 1.0 / ((ex - cx) * (ex - cx) + (ey - cy) * (ey - cy));
-    double best = gdist(ex, ey, cx, cy), d, t;
-    const double *rw = c_world.runway;
-    if (ray_square(cx, cy, ex, ey, rw[0], rw[1], rw[2], rw[3], d) && d < best) best = d;
-    const double *b = A.bound;
-    if (ray_vseg(cx, cy, ex, ey, b[0], b[2], b[3], d) && d < best) best = d;
-    if (ray_vseg(cx, cy, ex, ey, b[1], b[2], b[3], d) && d < best) best = d;
-    if (ray_hseg(cx, cy, ex, ey, b[3], b[0], b[1], d) && d < best) best = d;
-    if (ray_hseg(cx, cy, ex, ey, b[2], b[0], b[1], d) && d < best) best = d;
-    for (int k = 0; k < 2; ++k) {
-        const double2 c = S.cl[le][k];
-        if (ray_gon_boundary(cx, cy, ex, ey, c.x, c.y, c_world.radius[k], inv_l2, t)) {
-            d = gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy);
-            if (d < best) best = d;
-        }
+    double2 q;
+    double rad;
+    if (j >= 64) {
+        q = S.cl[le][j - 64];
+        rad = c_world.radius[j - 64];
+    } else {
+        q = S.pos[base + j];
+        rad = A.pb;
     }
-    // the other aircraft: candidates (the cheap pre-filter) collected as a lane mask first, then the
-    // clips for the candidates only -- a wave runs max-popcount clip iterations instead of one per
-    // neighbour slot that any of its lanes needs (the minimum does not depend on the order)
-    for (int j0 = 0; j0 < A.N; j0 += 64) {
-        const int jn = A.N - j0 < 64 ? A.N - j0 : 64;
-        unsigned long long cand = 0;
-        for (int jj = 0; jj < jn; ++jj) {
-            const double2 q = S.pos[base + j0 + jj];
-            if (j0 + jj != i && ray_gon_candidate(cx, cy, ex, ey, q.x, q.y, A.pb, inv_l2)) cand |= 1ull << jj;
-        }
-        while (cand) {
-            const int j = j0 + __builtin_ctzll(cand);
-            cand &= cand - 1;
-            const double2 q = S.pos[base + j];
-            if (ray_gon_boundary_cand(cx, cy, ex, ey, q.x, q.y, A.pb, t)) {
-                d = gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy);
-                if (d < best) best = d;
-            }
-        }
-    }
-    return best;
+    double t;
+    hit = ray_gon_boundary_cand(cx, cy, ex, ey, q.x, q.y, rad, t);
+    return hit ? gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy) : 0.0;
 }
 
 __device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag, const int32_t *emap = nullptr) {
-    for (int w = threadIdx.x; w < nag * NRAY; w += BLOCK) {
+    const int lane = threadIdx.x & 63;
+    const int total = nag * NRAY;
+    if (threadIdx.x == 0) S.nclip = 0;
+    __syncthreads();
+    // (3a) fixed boundaries + candidates; uniform trip count so that every lane joins the wave scan
+    for (int w0 = 0; w0 < total; w0 += BLOCK) {
+        const int w = w0 + threadIdx.x;
+        const int la = w / NRAY, r = w - la * NRAY;
+        const int le = la / A.N, i = la - le * A.N;
+        const bool on = w < total && S.active[le < A.epb ? le : 0] && (emap ? emap[le] : e0 + le) < A.E;
+        double best = 0.0;
+        unsigned long long cand = 0;      // other aircraft j < 64
+        int ccl = 0;                      // clouds (bits 0, 1)
+        if (on) {
+            const int base = le * A.N;
+            const double2 p = S.pos[base + i];
+            const double cx = p.x, cy = p.y;
+            const double ex = cx + A.radar_len * c_tab.ray_c[r], ey = cy + A.radar_len * c_tab.ray_s[r];
+            const double inv_l2 = 1.0 / ((ex - cx) * (ex - cx) + (ey - cy) * (ey - cy));
+            best = gdist(ex, ey, cx, cy);
+            double d;
+            const double *rw = c_world.runway;
+            if (ray_square(cx, cy, ex, ey, rw[0], rw[1], rw[2], rw[3], d) && d < best) best = d;
+            const double *b = A.bound;
+            if (ray_vseg(cx, cy, ex, ey, b[0], b[2], b[3], d) && d < best) best = d;
+            if (ray_vseg(cx, cy, ex, ey, b[1], b[2], b[3], d) && d < best) best = d;
+            if (ray_hseg(cx, cy, ex, ey, b[3], b[0], b[1], d) && d < best) best = d;
+            if (ray_hseg(cx, cy, ex, ey, b[2], b[0], b[1], d) && d < best) best = d;
+            for (int k = 0; k < 2; ++k) {
+                const double2 c = S.cl[le][k];
+                if (ray_gon_candidate(cx, cy, ex, ey, c.x, c.y, c_world.radius[k], inv_l2)) ccl |= 1 << k;
+            }
+            for (int jj = 0; jj < A.N; ++jj) {
+                const double2 q = S.pos[base + jj];
+                if (jj != i && ray_gon_candidate(cx, cy, ex, ey, q.x, q.y, A.pb, inv_l2)) cand |= 1ull << jj;
+            }
+        }
+        // slots for this lane's jobs: inclusive wave scan of the counts, one LDS atomic per wave
+        const int cnt = __popcll(cand) + __popc(ccl);
+        int incl = cnt;
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const int v = __shfl_up(incl, dd, 64);
+            if (lane >= dd) incl += v;
+        }
+        int wbase = 0;
+        if (lane == 63 && incl > 0) wbase = (int)atomicAdd(&S.nclip, (unsigned)incl);
+        wbase = __shfl(wbase, 63, 64);
+        int slot = wbase + incl - cnt;
+        if (on) {
+            const uint32_t tag = (uint32_t)w << 8;
+            while (ccl | (cand != 0)) {
+                int j;
+                if (ccl) {
+                    const int k = __builtin_ctz(ccl);
+                    ccl &= ccl - 1;
+                    j = 64 + k;
+                } else {
+                    j = __builtin_ctzll(cand);
+                    cand &= cand - 1;
+                }
+                if (slot < CLIP_CAP) {
+                    S.clip[slot] = tag | (uint32_t)j;
+                } else {          // list full: clip it here (same arithmetic, same minimum)
+                    bool hit;
+                    const double d = ray_clip_dist(A, S, le, le * A.N, i, r, j, hit);
+                    if (hit && d < best) best = d;
+                }
+                ++slot;
+            }
+            S.rad[la][r] = best;
+        }
+    }
+    __syncthreads();
+    // (3b) the clip jobs, evenly over the workgroup
+    const int nj = S.nclip < (unsigned)CLIP_CAP ? (int)S.nclip : CLIP_CAP;
+    for (int q = threadIdx.x; q < nj; q += BLOCK) {
+        const uint32_t job = S.clip[q];
+        const int w = (int)(job >> 8), j = (int)(job & 255u);
+        const int la = w / NRAY, r = w - la * NRAY;
+        const int le = la / A.N, i = la - le * A.N;
+        bool hit;
+        const double d = ray_clip_dist(A, S, le, le * A.N, i, r, j, hit);
+        if (hit) atomicMin(reinterpret_cast<unsigned long long *>(&S.rad[la][r]), (unsigned long long)__double_as_longlong(d));
+    }
+    __syncthreads();
+    // (3c) the rays to HBM
+    for (int w = threadIdx.x; w < total; w += BLOCK) {
         const int la = w / NRAY, r = w - la * NRAY;
         const int le = la / A.N, i = la - le * A.N;
         const int e = emap ? emap[le] : e0 + le;
         if (e >= A.E || !S.active[le]) continue;
-        const double v = radar_ray(A, S, le, le * A.N, i, r);
-        S.rad[la][r] = v;
-        A.radar[((size_t)e * A.N + i) * NRAY + r] = v;
+        A.radar[((size_t)e * A.N + i) * NRAY + r] = S.rad[la][r];
     }
 }
 
