@@ -109,6 +109,10 @@ void aac_env_set_reset_compact(int32_t on);
 /* Diagnostic builds only (-DAAC_ENV_STAMPS): per-workgroup phase stamps of the last step launch
  * (7 uint64 per workgroup); returns an error in a normal build. */
 int aac_env_stamps(unsigned long long *out, int32_t n_wg);
+/* The same for the reset kernel (7 uint64 per workgroup: realtime at entry, memtime at entry / after
+ * the OD draw / after the state writes / after the radar / after the observation, realtime at exit;
+ * all zero for a workgroup without a resetting env); an error in a normal build. */
+int aac_env_reset_stamps(unsigned long long *out, int32_t n_wg);
 /* From now on the per-env episode counter (int32[E], advanced by every auto-reset of an env) lives
  * in the caller's device buffer episode_dev (the current counts are copied into it); the caller
  * keeps it alive while the handle exists.  A trainer's noise schedule can read it directly.  The copy

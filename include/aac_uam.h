@@ -96,6 +96,9 @@ int aac_uam_actor(const double *own, const double *radar, int32_t R, const doubl
                   double noise_start, double noise_end, uint64_t seed, uint64_t *counter, int32_t noisy,
                   void *stream);
 const char *aac_uam_actor_last_error(void);
+/* 16-row tiles per block of aac_uam_actor (1, 2 or 4; default 4, or AAC_UAM_ACTOR_NT): the same
+ * arithmetic per row for every value (tests compare them bit for bit). */
+int aac_uam_actor_set_tiles(int32_t nt);
 
 /* Device-to-device copies of the state (NULL = skip), for tests and the reference facade. */
 int aac_uam_get_state(aac_uam *env, double *pos, double *vel, double *pre_pos, double *pre_vel, double *goal,

@@ -481,8 +481,18 @@ __device__ unsigned long long g_env_st[ESTAMP_WG][7];
     do {                                                                                               \
         if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_env_st[blockIdx.x][k] = (v);                \
     } while (0)
+// reset_kernel: [s_memrealtime at entry, s_memtime at entry / after the OD draw / after the state
+// writes / after the radar / after the observation, s_memrealtime at exit]; zero = workgroup idle
+__device__ unsigned long long g_reset_st[ESTAMP_WG][7];
+#define RSTAMP(k, v)                                                                                    \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_reset_st[blockIdx.x][k] = (v);              \
+    } while (0)
 #else
 #define ESTAMP(k, v) \
+    do {             \
+    } while (0)
+#define RSTAMP(k, v) \
     do {             \
     } while (0)
 #endif
@@ -731,7 +741,12 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     __syncthreads();
     int any = 0;
     for (int k = 0; k < A.epb; ++k) any |= S.active[k];
-    if (!any) return;
+    if (!any) {
+        RSTAMP(1, 0ull);      // stamp builds: mark the workgroup idle in this launch
+        return;
+    }
+    RSTAMP(0, __builtin_amdgcn_s_memrealtime());
+    RSTAMP(1, __builtin_amdgcn_s_memtime());
     const int le = t / N, i = t - le * N;
     const int e = emap[le < A.epb ? le : 0];
     const bool active = (t < nag) && (e < A.E) && S.active[le];
@@ -790,6 +805,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         }
     }
     __syncthreads();
+    RSTAMP(2, __builtin_amdgcn_s_memtime());
     if (active) {
         double2 st;
         int cnt;
@@ -824,8 +840,18 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         S.goal[t] = A.goal[ai];
     }
     __syncthreads();   // map_idx (explicit or drawn) written above is read by the radar phase below
+    RSTAMP(3, __builtin_amdgcn_s_memtime());
     radar_phase(A, S, e0, nag, true, emap);
+#ifdef AAC_ENV_STAMPS
+    __syncthreads();
+#endif
+    RSTAMP(4, __builtin_amdgcn_s_memtime());
     if (active) observe_agent(A, S, e, i, base);
+#ifdef AAC_ENV_STAMPS
+    __syncthreads();
+#endif
+    RSTAMP(5, __builtin_amdgcn_s_memtime());
+    RSTAMP(6, __builtin_amdgcn_s_memrealtime());
 }
 
 // ordered list of the done envs for the packed auto-reset (aacw::compact_flags)
@@ -1136,6 +1162,18 @@ int aac_env_stamps(unsigned long long *out, int32_t n_wg) {
 #ifdef AAC_ENV_STAMPS
     const size_t n = sizeof(unsigned long long) * 7 * (size_t)std::min(n_wg, ESTAMP_WG);
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_env_st), n));
+    return AAC_OK;
+#else
+    (void)out;
+    (void)n_wg;
+    return fail(AAC_E_STATE, "built without AAC_ENV_STAMPS");
+#endif
+}
+
+int aac_env_reset_stamps(unsigned long long *out, int32_t n_wg) {
+#ifdef AAC_ENV_STAMPS
+    const size_t n = sizeof(unsigned long long) * 7 * (size_t)std::min(n_wg, ESTAMP_WG);
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_reset_st), n));
     return AAC_OK;
 #else
     (void)out;

@@ -100,6 +100,7 @@ struct Lds {
                                           // coefficient, bit2 collision bearing doubles the crash
                                           // penalty, bit3 previous-nearest-two collided
     double nd_val[MAXA], base[MAXA];      // m d + c of the near-drone band; dist_to_goal - near_building
+    int ccnt[MAXA], pcnt[MAXA];           // tdCPA potential-conflict counts (current, previous state)
     unsigned nclip;                       // radar work list: (ray, polygon) clip jobs (radar_phase)
     uint32_t clip[CLIP_CAP];
 };
@@ -264,8 +265,62 @@ __device__ void dist_row(const UArgs &A, const Lds &S, int la, int base) {
 // distance, i.e. rank_j = #{k : d_k < d_j or (d_k == d_j and k < j)}.  One (aircraft, neighbour)
 // pair per work item over the whole workgroup (one thread per aircraft left three quarters of the
 // threads idle on the N^2 comparisons: ~57 k cycles per workgroup at N = 16).
+// N <= 16: one 16-lane DPP row per aircraft, lane j holding d_j; the row's 15 rotations (row_ror)
+// bring every d_k to lane j, which counts the ranks in registers (no LDS reads in the loop).  Lanes
+// j >= N and the aircraft itself hold +inf, which ranks after every real distance: the same rank as
+// the LDS loop below.
+__device__ inline double dpp_ror_f64(double x, int n) {
+    const long long b = __double_as_longlong(x);
+    int lo = (int)(b & 0xffffffffll), hi = (int)(b >> 32);
+    switch (n) {      // the DPP control must be an immediate: row_ror:n = 0x120 + n
+#define ROR(k)                                                                      \
+    case k:                                                                         \
+        lo = __builtin_amdgcn_update_dpp(0, lo, 0x120 + k, 0xf, 0xf, false);        \
+        hi = __builtin_amdgcn_update_dpp(0, hi, 0x120 + k, 0xf, 0xf, false);        \
+        break;
+        ROR(1) ROR(2) ROR(3) ROR(4) ROR(5) ROR(6) ROR(7) ROR(8) ROR(9) ROR(10) ROR(11) ROR(12) ROR(13) ROR(14)
+        ROR(15)
+#undef ROR
+    }
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ inline int dpp_ror_i32(int x, int n) {
+    switch (n) {
+#define ROR(k) \
+    case k: return __builtin_amdgcn_update_dpp(0, x, 0x120 + k, 0xf, 0xf, false);
+        ROR(1) ROR(2) ROR(3) ROR(4) ROR(5) ROR(6) ROR(7) ROR(8) ROR(9) ROR(10) ROR(11) ROR(12) ROR(13) ROR(14)
+        ROR(15)
+#undef ROR
+    }
+    return x;
+}
+
+__device__ void order_phase_rows(const UArgs &A, Lds &S, int nag) {
+    const int N = A.N;
+    const int j = threadIdx.x & 15;
+    for (int la0 = 0; la0 < nag; la0 += BLOCK / 16) {
+        const int la = la0 + (threadIdx.x >> 4);     // uniform per 16-lane row
+        const int le = la / N, i = la - le * N;
+        const bool on = la < nag && S.active[le < A.epb ? le : 0];
+        const double dj = (on && j < N && j != i) ? s_dist[(size_t)la * N + j] : INFINITY;
+        int rank = 0;
+#pragma unroll
+        for (int s = 1; s < 16; ++s) {
+            const double dk = dpp_ror_f64(dj, s);
+            const int k = dpp_ror_i32(j, s);
+            rank += (dk < dj) || (dk == dj && k < j);
+        }
+        if (on && j < N && j != i) S.order[la][rank] = (uint8_t)j;
+    }
+}
+
 __device__ void order_phase(const UArgs &A, Lds &S, int nag) {
     const int N = A.N;
+    if (N <= 16) {
+        order_phase_rows(A, S, nag);
+        return;
+    }
     for (int w = threadIdx.x; w < nag * N; w += BLOCK) {
         const int la = w / N, j = w - la * N;
         const int le = la / N, i = la - le * N;
@@ -312,70 +367,72 @@ __device__ inline double ray_clip_dist(const UArgs &A, const Lds &S, int le, int
     return hit ? gdist(cx + t * (ex - cx), cy + t * (ey - cy), cx, cy) : 0.0;
 }
 
-__device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag, const int32_t *emap = nullptr) {
+// overflow clips of the pair pass land after every ray's base value (phase 3a) has been written:
+// fold them in with the same LDS atomic min as the list's clips (non-negative float64 bits)
+__device__ inline void pending_min(Lds &S, int la, int r, double d) {
+    atomicMin(reinterpret_cast<unsigned long long *>(&S.rad[la][r]), (unsigned long long)__double_as_longlong(d));
+}
+
+// slots for a lane's cnt jobs: inclusive wave scan of the counts, one LDS atomic per wave (every
+// lane of the wave calls it)
+__device__ inline int clip_slots(Lds &S, int cnt) {
     const int lane = threadIdx.x & 63;
+    int incl = cnt;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+        const int v = __shfl_up(incl, dd, 64);
+        if (lane >= dd) incl += v;
+    }
+    int wbase = 0;
+    if (lane == 63 && incl > 0) wbase = (int)atomicAdd(&S.nclip, (unsigned)incl);
+    wbase = __shfl(wbase, 63, 64);
+    return wbase + incl - cnt;
+}
+
+__device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag, const int32_t *emap = nullptr) {
     const int total = nag * NRAY;
     if (threadIdx.x == 0) S.nclip = 0;
     __syncthreads();
-    // (3a) fixed boundaries + candidates; uniform trip count so that every lane joins the wave scan
+    // (3a) per (aircraft, ray): the fixed boundaries and the clouds' pre-filter; uniform trip count
+    // so that every lane joins the wave scan
     for (int w0 = 0; w0 < total; w0 += BLOCK) {
         const int w = w0 + threadIdx.x;
         const int la = w / NRAY, r = w - la * NRAY;
         const int le = la / A.N, i = la - le * A.N;
         const bool on = w < total && S.active[le < A.epb ? le : 0] && (emap ? emap[le] : e0 + le) < A.E;
         double best = 0.0;
-        unsigned long long cand = 0;      // other aircraft j < 64
         int ccl = 0;                      // clouds (bits 0, 1)
         if (on) {
             const int base = le * A.N;
             const double2 p = S.pos[base + i];
             const double cx = p.x, cy = p.y;
             const double ex = cx + A.radar_len * c_tab.ray_c[r], ey = cy + A.radar_len * c_tab.ray_s[r];
-            const double inv_l2 = 1.0 / ((ex - cx) * (ex - cx) + (ey - cy) * (ey - cy));
             best = gdist(ex, ey, cx, cy);
             double d;
+            // the runway's slab test (four divisions) only for segments whose bounding box comes
+            // within 1e-9 of the rectangle: farther, the exact test cannot report a hit
             const double *rw = c_world.runway;
-            if (ray_square(cx, cy, ex, ey, rw[0], rw[1], rw[2], rw[3], d) && d < best) best = d;
+            if (fmax(cx, ex) >= rw[0] - 1e-9 && fmin(cx, ex) <= rw[1] + 1e-9 && fmax(cy, ey) >= rw[2] - 1e-9 &&
+                fmin(cy, ey) <= rw[3] + 1e-9 && ray_square(cx, cy, ex, ey, rw[0], rw[1], rw[2], rw[3], d) && d < best)
+                best = d;
             const double *b = A.bound;
             if (ray_vseg(cx, cy, ex, ey, b[0], b[2], b[3], d) && d < best) best = d;
             if (ray_vseg(cx, cy, ex, ey, b[1], b[2], b[3], d) && d < best) best = d;
             if (ray_hseg(cx, cy, ex, ey, b[3], b[0], b[1], d) && d < best) best = d;
             if (ray_hseg(cx, cy, ex, ey, b[2], b[0], b[1], d) && d < best) best = d;
+            const double inv_l2 = 1.0 / ((ex - cx) * (ex - cx) + (ey - cy) * (ey - cy));
             for (int k = 0; k < 2; ++k) {
                 const double2 c = S.cl[le][k];
                 if (ray_gon_candidate(cx, cy, ex, ey, c.x, c.y, c_world.radius[k], inv_l2)) ccl |= 1 << k;
             }
-            for (int jj = 0; jj < A.N; ++jj) {
-                const double2 q = S.pos[base + jj];
-                if (jj != i && ray_gon_candidate(cx, cy, ex, ey, q.x, q.y, A.pb, inv_l2)) cand |= 1ull << jj;
-            }
         }
-        // slots for this lane's jobs: inclusive wave scan of the counts, one LDS atomic per wave
-        const int cnt = __popcll(cand) + __popc(ccl);
-        int incl = cnt;
-#pragma unroll
-        for (int dd = 1; dd < 64; dd <<= 1) {
-            const int v = __shfl_up(incl, dd, 64);
-            if (lane >= dd) incl += v;
-        }
-        int wbase = 0;
-        if (lane == 63 && incl > 0) wbase = (int)atomicAdd(&S.nclip, (unsigned)incl);
-        wbase = __shfl(wbase, 63, 64);
-        int slot = wbase + incl - cnt;
+        int slot = clip_slots(S, __popc(ccl));
         if (on) {
-            const uint32_t tag = (uint32_t)w << 8;
-            while (ccl | (cand != 0)) {
-                int j;
-                if (ccl) {
-                    const int k = __builtin_ctz(ccl);
-                    ccl &= ccl - 1;
-                    j = 64 + k;
-                } else {
-                    j = __builtin_ctzll(cand);
-                    cand &= cand - 1;
-                }
+            while (ccl) {
+                const int j = 64 + __builtin_ctz(ccl);
+                ccl &= ccl - 1;
                 if (slot < CLIP_CAP) {
-                    S.clip[slot] = tag | (uint32_t)j;
+                    S.clip[slot] = ((uint32_t)w << 8) | (uint32_t)j;
                 } else {          // list full: clip it here (same arithmetic, same minimum)
                     bool hit;
                     const double d = ray_clip_dist(A, S, le, le * A.N, i, r, j, hit);
@@ -386,7 +443,54 @@ __device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag, const int32
             S.rad[la][r] = best;
         }
     }
+    __syncthreads();     // every ray's base value is in S.rad before 3a' may fold overflow clips into it
+    // (3a') per (aircraft, other aircraft): which of the 18 rays can meet the other's 64-gon.  A
+    // float32 superset of ray_gon_candidate's test (segment-to-centre distance <= pB + 1e-6): the
+    // centre within pB + 1e-6 + 1e-3 of the ray's line and of its extent; the 1e-3 margin is far
+    // above float32 rounding at these coordinates (~1e-5), and a pair outside the exact test that
+    // gets through only costs a clip that reports no hit (the clips are exact for any segment).
+    // Per pair instead of per ray: 18 float32 tests replace 18 float64 ones, the candidates'
+    // distances come out of one subtraction.
+    const int npair = nag * A.N;
+    const float lim = (float)A.pb + 1e-6f + 1e-3f, Lf = (float)A.radar_len + lim;
+    for (int p0 = 0; p0 < npair; p0 += BLOCK) {
+        const int pr = p0 + threadIdx.x;
+        const int la = pr / A.N, j = pr - la * A.N;
+        const int le = la / A.N, i = la - le * A.N;
+        const bool on = pr < npair && j != i && S.active[le < A.epb ? le : 0] &&
+                        (emap ? emap[le] : e0 + le) < A.E;
+        unsigned rays = 0;
+        if (on) {
+            const int base = le * A.N;
+            const double2 p = S.pos[base + i], q = S.pos[base + j];
+            const float dx = (float)(q.x - p.x), dy = (float)(q.y - p.y);
+#pragma unroll
+            for (int r = 0; r < NRAY; ++r) {
+                const float c = (float)c_tab.ray_c[r], sn = (float)c_tab.ray_s[r];
+                const float perp = dx * sn - dy * c, along = dx * c + dy * sn;
+                if (fabsf(perp) <= lim && along >= -lim && along <= Lf) rays |= 1u << r;
+            }
+        }
+        int slot = clip_slots(S, __popc(rays));
+        if (on && rays) {
+            const int base = le * A.N;
+            while (rays) {
+                const int r = __builtin_ctz(rays);
+                rays &= rays - 1;
+                const int w = la * NRAY + r;
+                if (slot < CLIP_CAP) {
+                    S.clip[slot] = ((uint32_t)w << 8) | (uint32_t)j;
+                } else {          // list full: clip it now; the ray's minimum through the LDS atomic
+                    bool hit;
+                    const double d = ray_clip_dist(A, S, le, base, i, r, j, hit);
+                    if (hit) pending_min(S, la, r, d);
+                }
+                ++slot;
+            }
+        }
+    }
     __syncthreads();
+    USTAMP(7);
     // (3b) the clip jobs, evenly over the workgroup
     const int nj = S.nclip < (unsigned)CLIP_CAP ? (int)S.nclip : CLIP_CAP;
     for (int q = threadIdx.x; q < nj; q += BLOCK) {
@@ -399,6 +503,7 @@ __device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag, const int32
         if (hit) atomicMin(reinterpret_cast<unsigned long long *>(&S.rad[la][r]), (unsigned long long)__double_as_longlong(d));
     }
     __syncthreads();
+    USTAMP(8);
     // (3c) the rays to HBM
     for (int w = threadIdx.x; w < total; w += BLOCK) {
         const int la = w / NRAY, r = w - la * NRAY;
@@ -409,14 +514,16 @@ __device__ void radar_phase(const UArgs &A, Lds &S, int e0, int nag, const int32
     }
 }
 
-// (4) observation rows of aircraft i of env e (UAM/env:1616-1880) + tdCPA (UAM/env:1745-1750)
-__device__ void observe(const UArgs &A, const Lds &S, int e, int la, int base, int i) {
-    const int N = A.N, K = A.K;
-    const size_t ai = (size_t)e * N + i;
+// (4) observation rows (UAM/env:1616-1880) + tdCPA (UAM/env:1738-1745).  The own row and the two
+// nearest neighbours per aircraft; the per-neighbour rows (p2, p3, tcpa / dcpa) as work items over
+// (aircraft, neighbour slot) on all 256 threads -- one thread per aircraft ran K = 15 slots in a row
+// on a single wave -- with the two potential-conflict counts summed by LDS atomics (integer sums:
+// the order does not matter).
+__device__ void observe_own(const UArgs &A, Lds &S, int e, int la, int i) {
+    const size_t ai = (size_t)e * A.N + i;
     const double *b = A.bound;
     const double2 p = S.pos[la], v = S.vel[la], g = S.goal[la];
     const double npx = nmlz(p.x, b[0], b[1]), npy = nmlz(p.y, b[2], b[3]);
-    const double hd = S.heading[la];
     double *own = A.own + ai * 7;
     own[0] = npx;
     own[1] = npy;
@@ -424,47 +531,80 @@ __device__ void observe(const UArgs &A, const Lds &S, int e, int la, int base, i
     own[3] = v.y / A.vmax;
     own[4] = nmlz(g.x, b[0], b[1]) - npx;
     own[5] = nmlz(g.y, b[2], b[3]) - npy;
-    own[6] = hd;
-    const double dxm = b[0] - b[1], dxM = b[1] - b[0], dym = b[2] - b[3], dyM = b[3] - b[2];
-    const double2 hp = S.ppos[la], hv = S.pvel[la];
-    int cc = 0, cp = 0;
-    for (int k = 0; k < K; ++k) {
-        const int j = S.order[la][k];
-        const double2 q = S.pos[base + j], w = S.vel[base + j];
-        if (A.nei) {
-            double *nb = A.nei + (ai * K + k) * 5;
-            nb[0] = npx - nmlz(q.x, b[0], b[1]);
-            nb[1] = npy - nmlz(q.y, b[2], b[3]);
-            nb[2] = w.x / A.vmax;
-            nb[3] = w.y / A.vmax;
-            nb[4] = hd;
+    own[6] = S.heading[la];
+    A.top2[ai * 2 + 0] = A.K > 0 ? S.order[la][0] : NONE8;
+    A.top2[ai * 2 + 1] = A.K > 1 ? S.order[la][1] : NONE8;
+    S.ccnt[la] = 0;
+    S.pcnt[la] = 0;
+}
+
+__device__ void observe_slot(const UArgs &A, Lds &S, int e, int la, int base, int i, int k) {
+    const int N = A.N, K = A.K;
+    const size_t ai = (size_t)e * N + i;
+    const double *b = A.bound;
+    const double2 p = S.pos[la], v = S.vel[la];
+    const int j = S.order[la][k];
+    const double2 q = S.pos[base + j], w = S.vel[base + j];
+    if (A.nei) {
+        const double npx = nmlz(p.x, b[0], b[1]), npy = nmlz(p.y, b[2], b[3]);
+        double *nb = A.nei + (ai * K + k) * 5;
+        nb[0] = npx - nmlz(q.x, b[0], b[1]);
+        nb[1] = npy - nmlz(q.y, b[2], b[3]);
+        nb[2] = w.x / A.vmax;
+        nb[3] = w.y / A.vmax;
+        nb[4] = S.heading[la];
+    }
+    if (A.nei6) {
+        const double dxm = b[0] - b[1], dxM = b[1] - b[0], dym = b[2] - b[3], dyM = b[3] - b[2];
+        double *n6 = A.nei6 + (ai * K + k) * 6;
+        n6[0] = 2 * (((q.x - p.x) - dxm) / (dxM - dxm)) - 1;
+        n6[1] = 2 * (((q.y - p.y) - dym) / (dyM - dym)) - 1;
+        n6[2] = 2 * (((w.y - q.x) - dxm) / (dxM - dxm)) - 1;     // other_agent[-2] - other_agent[0]
+        n6[3] = 2 * (((A.pb - q.y) - dym) / (dyM - dym)) - 1;    // other_agent[-1] - other_agent[1]
+        n6[4] = w.x / A.vmax;
+        n6[5] = w.y / A.vmax;
+    }
+    if (A.tcpa || A.conf_cur) {
+        double tc, dc, t2, d2;
+        int cc = 0, cp = 0;
+        tdcpa(q.x, q.y, p.x, p.y, w.x, w.y, v.x, v.y, A.pb, tc, dc, cc);
+        const double2 hp = S.ppos[la], hv = S.pvel[la];
+        const double2 qp = S.ppos[base + j], wp = S.pvel[base + j];
+        tdcpa(qp.x, qp.y, hp.x, hp.y, wp.x, wp.y, hv.x, hv.y, A.pb, t2, d2, cp);
+        if (A.tcpa) {
+            A.tcpa[ai * K + k] = tc;
+            A.dcpa[ai * K + k] = dc;
         }
-        if (A.nei6) {
-            double *n6 = A.nei6 + (ai * K + k) * 6;
-            n6[0] = 2 * (((q.x - p.x) - dxm) / (dxM - dxm)) - 1;
-            n6[1] = 2 * (((q.y - p.y) - dym) / (dyM - dym)) - 1;
-            n6[2] = 2 * (((w.y - q.x) - dxm) / (dxM - dxm)) - 1;     // other_agent[-2] - other_agent[0]
-            n6[3] = 2 * (((A.pb - q.y) - dym) / (dyM - dym)) - 1;    // other_agent[-1] - other_agent[1]
-            n6[4] = w.x / A.vmax;
-            n6[5] = w.y / A.vmax;
-        }
-        if (A.tcpa || A.conf_cur) {
-            double tc, dc, t2, d2;
-            tdcpa(q.x, q.y, p.x, p.y, w.x, w.y, v.x, v.y, A.pb, tc, dc, cc);
-            const double2 qp = S.ppos[base + j], wp = S.pvel[base + j];
-            tdcpa(qp.x, qp.y, hp.x, hp.y, wp.x, wp.y, hv.x, hv.y, A.pb, t2, d2, cp);
-            if (A.tcpa) {
-                A.tcpa[ai * K + k] = tc;
-                A.dcpa[ai * K + k] = dc;
+        if (cc) atomicAdd(&S.ccnt[la], cc);
+        if (cp) atomicAdd(&S.pcnt[la], cp);
+    }
+}
+
+// the whole phase for the workgroup's aircraft (step and reset); ends with a barrier
+__device__ void observe_phase(const UArgs &A, Lds &S, int e0, int nag, const int32_t *emap) {
+    const int N = A.N, K = A.K;
+    for (int la = threadIdx.x; la < nag; la += BLOCK) {
+        const int le = la / N, i = la - le * N;
+        const int e = emap ? emap[le] : e0 + le;
+        if (e < A.E && S.active[le]) observe_own(A, S, e, la, i);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < nag * K; w += BLOCK) {
+        const int la = w / K, k = w - la * K;
+        const int le = la / N, i = la - le * N;
+        const int e = emap ? emap[le] : e0 + le;
+        if (e < A.E && S.active[le]) observe_slot(A, S, e, la, le * N, i, k);
+    }
+    __syncthreads();
+    if (A.conf_cur)
+        for (int la = threadIdx.x; la < nag; la += BLOCK) {
+            const int le = la / N, i = la - le * N;
+            const int e = emap ? emap[le] : e0 + le;
+            if (e < A.E && S.active[le]) {
+                A.conf_cur[(size_t)e * N + i] = S.ccnt[la];
+                A.conf_pre[(size_t)e * N + i] = S.pcnt[la];
             }
         }
-    }
-    if (A.conf_cur) {
-        A.conf_cur[ai] = cc;
-        A.conf_pre[ai] = cp;
-    }
-    A.top2[ai * 2 + 0] = K > 0 ? S.order[la][0] : NONE8;
-    A.top2[ai * 2 + 1] = K > 1 ? S.order[la][1] : NONE8;
 }
 
 __device__ inline void lds_agent(Lds &S, int la, double2 pos, double2 vel, double2 pp, double2 pv, double2 g,
@@ -565,8 +705,8 @@ __global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArg
     __syncthreads(); USTAMP(4);
 
     // ---- (4) observation; the goal touch of every aircraft first (UAM/env:3929-3936)
+    observe_phase(A, S, e0, nag, nullptr);
     if (active) {
-        observe(A, S, e, t, base, i);
         const double2 g = S.goal[t];
         if (gons_meet(g.x - np.x, g.y - np.y, A.pb + 1.0, false)) S.reach[t] = 1;
     }
@@ -647,8 +787,58 @@ __global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArg
     __syncthreads(); USTAMP(6);
 
     // ---- (6) per env, aircraft in order: the coefficient doubling persists over later aircraft
-    //      of the same call (UAM/env:4320, :4546); done, bbc, termination (UAM/main:624-637)
-    if (t < A.epb && e0 + t < A.E) {
+    //      of the same call (UAM/env:4320, :4546); done, bbc, termination (UAM/main:624-637).
+    // N <= 16: one 16-lane row per env, lane j = aircraft j.  Each doubling multiplies by 2, which is
+    // exact, so aircraft j's coefficients are 2.0 and 50.0 times 2^(doublings among aircraft 0..j):
+    // an inclusive prefix count over the row (ballot + popcount) instead of the sequential walk.
+    if (N <= 16) {
+        const int q = t >> 4, j = t & 15;
+        const int eq = e0 + q;
+        const bool on = q < A.epb && eq < A.E && j < N;     // q uniform per row
+        const int la = q * N + j;
+        uint8_t fl = 0, kind = 4, rch = 1;
+        if (on) {
+            fl = S.flag[la];
+            kind = S.kind[la];
+            rch = S.reach[la];
+        }
+        const unsigned long long dbl_nd = __ballot(on && (fl & 1) && (fl & 2));
+        const unsigned long long dbl_cr = __ballot(on && kind == 2 && (fl & 4));
+        const int sh = 16 * ((t >> 4) & 3);
+        const unsigned long long upto = ((2ull << j) - 1) << sh, row = 0xffffull << sh;
+        const double ndc = ldexp(2.0, __popcll(dbl_nd & upto));
+        const double crash = ldexp(50.0, __popcll(dbl_cr & upto));
+        int dn = 0;
+        if (on) {
+            const double nd = (fl & 1) ? ndc * S.nd_val[la] : ndc * 0;
+            double rew;
+            dn = 1;
+            if (kind == 0 || kind == 1 || kind == 2) {
+                rew = 0 - crash;
+            } else if (kind == 3) {
+                rew = 0 + 50.0 + 0;
+                dn = 0;
+            } else {
+                rew = S.base[la] - nd;
+                dn = 0;
+            }
+            const size_t aj = (size_t)eq * N + j;
+            A.reward[aj] = rew;
+            A.done[aj] = (uint8_t)dn;
+        }
+        const unsigned long long m_done = __ballot(on && dn), m_nreach = __ballot(on && !rch);
+        const unsigned long long m_k0 = __ballot(on && kind == 0), m_k1 = __ballot(on && kind == 1);
+        const unsigned long long m_k2 = __ballot(on && kind == 2), m_k3 = __ballot(on && kind == 2 && (fl & 8));
+        if (on && j == 0) {
+            A.bbc[4 * eq + 0] = (m_k0 & row) != 0;
+            A.bbc[4 * eq + 1] = (m_k1 & row) != 0;
+            A.bbc[4 * eq + 2] = (m_k2 & row) != 0;
+            A.bbc[4 * eq + 3] = (m_k3 & row) != 0;
+            const int st = A.step[eq] + 1;
+            A.step[eq] = st;
+            A.env_done[eq] = (uint8_t)((A.episode_length < st) || (m_done & row) != 0 || (m_nreach & row) == 0);
+        }
+    } else if (t < A.epb && e0 + t < A.E) {
         const int eq = e0 + t, bq = t * N;
         double crash = 50.0, ndc = 2.0;
         int any_done = 0, all_reach = 1;
@@ -776,7 +966,7 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     __syncthreads();
     radar_phase(A, S, e0, nag, emap);
     __syncthreads();
-    if (active) observe(A, S, e, t, base, i);
+    observe_phase(A, S, e0, nag, emap);
 }
 
 // ordered list of the done envs for the packed auto-reset (aacw::compact_flags)

@@ -28,6 +28,12 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int HLD = 132;     // LDS row stride (doubles) of a wave's 16 x 128 hidden slab
 
 thread_local std::string g_aerr;
+// 16-row tiles per block of the weights-stationary actor (aac_uam_actor_set_tiles; AAC_UAM_ACTOR_NT)
+int g_actor_nt = [] {
+    const char *v = getenv("AAC_UAM_ACTOR_NT");
+    const int k = v ? atoi(v) : 4;
+    return (k == 1 || k == 2 || k == 4) ? k : 4;
+}();
 
 __host__ __device__ inline uint64_t amix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -190,9 +196,16 @@ __device__ __forceinline__ double row_noise(const ActorArgs &A, int r, uint64_t 
     return rr * cos(6.283185307179586 * u2) * var;
 }
 
+// NT 16-row tiles per block (the rows of the block on the MFMA's n axis, NT independent accumulator
+// chains per weight fragment): each merge-layer weight fragment held in registers feeds NT MFMAs per
+// k step, so the block's latency chain (loads, two barriers, the 32-step merge chain, the output
+// reduction, the noise) is paid once per 16 NT rows.  NT = 1 was the first form: ~10 k cycles per
+// 16 rows at one wave per SIMD.  Every row's arithmetic is the same for any NT (bit-identical).
+template <int NT>
 __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
-    __shared__ double sH[128 * TI];          // [h_o | h_r] of the block, [feature][row]
-    __shared__ double sP[4][16][2];          // per-wave partial output dots
+    constexpr int ROWS = 16 * NT, TS = ROWS + 1;       // TS: row stride of the [feature][rows] image
+    __shared__ double sH[128 * TS];          // [h_o | h_r] of the block, [feature][row]
+    __shared__ double sP[4][ROWS][2];        // per-wave partial output dots
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
     const uint64_t ctr = A.noisy ? *A.counter : 0;
     // A fragments (lane: output row 16 t + n of the tile, k slot kq of each 4-step)
@@ -226,80 +239,93 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
         }
     }
     const double b40 = A.b4[0], b41 = A.b4[1];
-    const int nblk = (A.R + 15) / 16;
+    const int nblk = (A.R + ROWS - 1) / ROWS;
     for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        const int r0 = blk * 16, r = r0 + n;
-        const int rc = r < A.R ? r : A.R - 1;            // rows past R feed only their own column
-        double bo[2], br[5];
+        const int r0 = blk * ROWS;
+        double bo[NT][2], br[NT][5];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int k = 4 * s + kq;
-            bo[s] = A.own[(size_t)rc * 7 + (k < 7 ? k : 6)];
-        }
+        for (int q = 0; q < NT; ++q) {
+            const int r = r0 + 16 * q + n;
+            const int rc = r < A.R ? r : A.R - 1;        // rows past R feed only their own column
 #pragma unroll
-        for (int s = 0; s < 5; ++s) {
-            const int k = 4 * s + kq;
-            br[s] = A.radar[(size_t)rc * 18 + (k < 18 ? k : 17)];
+            for (int s = 0; s < 2; ++s) {
+                const int k = 4 * s + kq;
+                bo[q][s] = A.own[(size_t)rc * 7 + (k < 7 ? k : 6)];
+            }
+#pragma unroll
+            for (int s = 0; s < 5; ++s) {
+                const int k = 4 * s + kq;
+                br[q][s] = A.radar[(size_t)rc * 18 + (k < 18 ? k : 17)];
+            }
         }
         // h_o^T = relu(W1 own^T + b1), h_r^T = relu(W2 radar^T + b2): padded k slots have a zero A
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bo[s], acc, 0, 0, 0);
+        for (int q = 0; q < NT; ++q) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const double v = acc[j] + c1[j];
-            sH[(16 * w + kq + 4 * j) * TI + n] = v > 0.0 ? v : 0.0;
-        }
-        acc = d4{0.0, 0.0, 0.0, 0.0};
+            for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bo[q][s], acc, 0, 0, 0);
+            d4 acr = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int s = 0; s < 5; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], br[s], acc, 0, 0, 0);
+            for (int s = 0; s < 5; ++s) acr = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], br[q][s], acr, 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const double v = acc[j] + c2[j];
-            sH[(64 + 16 * w + kq + 4 * j) * TI + n] = v > 0.0 ? v : 0.0;
+            for (int j = 0; j < 4; ++j) {
+                const double v = acc[j] + c1[j];
+                sH[(16 * w + kq + 4 * j) * TS + 16 * q + n] = v > 0.0 ? v : 0.0;
+                const double u = acr[j] + c2[j];
+                sH[(64 + 16 * w + kq + 4 * j) * TS + 16 * q + n] = u > 0.0 ? u : 0.0;
+            }
         }
         __syncthreads();
-        // h^T = relu(W3 [h_o | h_r]^T + b3), two output tiles per wave, then this lane's share of
-        // the 128 -> 2 output layer
-        d4 h0 = {0.0, 0.0, 0.0, 0.0}, h1 = {0.0, 0.0, 0.0, 0.0};
+        // h^T = relu(W3 [h_o | h_r]^T + b3), two output tiles per wave and NT row tiles, then this
+        // lane's share of the 128 -> 2 output layer
+        d4 h0[NT], h1[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            h0[q] = d4{0.0, 0.0, 0.0, 0.0};
+            h1[q] = d4{0.0, 0.0, 0.0, 0.0};
+        }
 #pragma unroll
         for (int s = 0; s < 32; ++s) {
-            const double b = sH[(4 * s + kq) * TI + n];
-            h0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a3[0][s], b, h0, 0, 0, 0);
-            h1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a3[1][s], b, h1, 0, 0, 0);
-        }
-        double p0 = 0.0, p1 = 0.0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            double v = h0[j] + c3[0][j];
-            v = v > 0.0 ? v : 0.0;
-            p0 = fma(u0[0][j], v, p0);
-            p1 = fma(u1[0][j], v, p1);
+            for (int q = 0; q < NT; ++q) {
+                const double b = sH[(4 * s + kq) * TS + 16 * q + n];
+                h0[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a3[0][s], b, h0[q], 0, 0, 0);
+                h1[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a3[1][s], b, h1[q], 0, 0, 0);
+            }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            double v = h1[j] + c3[1][j];
-            v = v > 0.0 ? v : 0.0;
-            p0 = fma(u0[1][j], v, p0);
-            p1 = fma(u1[1][j], v, p1);
-        }
-        // sum over the four lane groups that hold row n, then over the waves in order
-        p0 += __shfl_xor(p0, 16, 64);
-        p1 += __shfl_xor(p1, 16, 64);
-        p0 += __shfl_xor(p0, 32, 64);
-        p1 += __shfl_xor(p1, 32, 64);
-        if (kq == 0) {
-            sP[w][n][0] = p0;
-            sP[w][n][1] = p1;
+        for (int q = 0; q < NT; ++q) {
+            double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double v = h0[q][j] + c3[0][j];
+                v = v > 0.0 ? v : 0.0;
+                p0 = fma(u0[0][j], v, p0);
+                p1 = fma(u1[0][j], v, p1);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double v = h1[q][j] + c3[1][j];
+                v = v > 0.0 ? v : 0.0;
+                p0 = fma(u0[1][j], v, p0);
+                p1 = fma(u1[1][j], v, p1);
+            }
+            // sum over the four lane groups that hold row n, then (below) over the waves in order
+            p0 += __shfl_xor(p0, 16, 64);
+            p1 += __shfl_xor(p1, 16, 64);
+            p0 += __shfl_xor(p0, 32, 64);
+            p1 += __shfl_xor(p1, 32, 64);
+            if (kq == 0) {
+                sP[w][16 * q + n][0] = p0;
+                sP[w][16 * q + n][1] = p1;
+            }
         }
         __syncthreads();
-        if (threadIdx.x < 16) {
-            const int rr = r0 + threadIdx.x;
+        for (int x = threadIdx.x; x < ROWS; x += 256) {
+            const int rr = r0 + x;
             if (rr < A.R) {
-                const double s0 = ((sP[0][threadIdx.x][0] + sP[1][threadIdx.x][0]) + sP[2][threadIdx.x][0]) +
-                                  sP[3][threadIdx.x][0];
-                const double s1 = ((sP[0][threadIdx.x][1] + sP[1][threadIdx.x][1]) + sP[2][threadIdx.x][1]) +
-                                  sP[3][threadIdx.x][1];
+                const double s0 = ((sP[0][x][0] + sP[1][x][0]) + sP[2][x][0]) + sP[3][x][0];
+                const double s1 = ((sP[0][x][1] + sP[1][x][1]) + sP[2][x][1]) + sP[3][x][1];
                 double x0 = tanh(s0 + b40), x1 = tanh(s1 + b41);
                 if (A.noisy) {
                     double e1;
@@ -321,6 +347,15 @@ __global__ void actor_counter_kernel(uint64_t *counter) { *counter += 1; }
 extern "C" {
 
 const char *aac_uam_actor_last_error(void) { return g_aerr.c_str(); }
+
+int aac_uam_actor_set_tiles(int32_t nt) {
+    if (nt != 1 && nt != 2 && nt != 4) {
+        g_aerr = "aac_uam_actor_set_tiles: 1, 2 or 4 row tiles per block";
+        return AAC_E_INVALID;
+    }
+    g_actor_nt = nt;
+    return 0;
+}
 
 int aac_uam_actor(const double *own, const double *radar, int32_t R, const double *w1, const double *b1,
                   const double *w2, const double *b2, const double *w3, const double *b3, const double *w4,
@@ -350,10 +385,16 @@ int aac_uam_actor(const double *own, const double *radar, int32_t R, const doubl
     } else {
         static const int cap = [] {
             const char *v = getenv("AAC_UAM_ACTOR_WGS");
-            return v ? atoi(v) : 256;     // one workgroup per CU (300 VGPRs: one wave per SIMD)
+            return v ? atoi(v) : 256;     // one workgroup per CU (> 256 VGPRs: one wave per SIMD)
         }();
-        const int wgs = nblk < cap ? nblk : cap;
-        hipLaunchKernelGGL(uam_actor_ws_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A);
+        const int nt = g_actor_nt;
+        const int nb = (R + 16 * nt - 1) / (16 * nt);
+        const int wgs = nb < cap ? nb : cap;
+        switch (nt) {
+            case 1: hipLaunchKernelGGL(uam_actor_ws_kernel<1>, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A); break;
+            case 2: hipLaunchKernelGGL(uam_actor_ws_kernel<2>, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A); break;
+            default: hipLaunchKernelGGL(uam_actor_ws_kernel<4>, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A); break;
+        }
     }
     if (noisy) hipLaunchKernelGGL(actor_counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
     const hipError_t e = hipGetLastError();

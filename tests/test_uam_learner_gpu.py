@@ -192,6 +192,32 @@ def test_actor_kernel_rows(native_lib, R):
     torch.testing.assert_close(a, ref, rtol=0, atol=1e-13)
 
 
+def test_actor_tiles_bit_identical(native_lib):
+    """aac_uam_actor with 1, 2 and 4 sixteen-row tiles per block (aac_uam_actor_set_tiles): the same
+    per-row arithmetic, so identical outputs to the bit, with and without the exploration noise."""
+    import ctypes
+    from multi_agent_aac_amd import uam
+    m, _ = _model()
+    L = uam.lib()
+    L.aac_uam_actor_set_tiles.argtypes = [ctypes.c_int32]
+    R = 4099                       # ragged: partial 64-row blocks
+    g = torch.Generator(device=DEV).manual_seed(9)
+    own = torch.rand(R, 1, 7, dtype=torch.float64, device=DEV, generator=g) * 2 - 1
+    radar = torch.rand(R, 1, 18, dtype=torch.float64, device=DEV, generator=g) * 5
+    ep = torch.randint(1, 12000, (R,), dtype=torch.int32, device=DEV, generator=g)
+    outs = []
+    try:
+        for nt in (1, 2, 4):
+            assert L.aac_uam_actor_set_tiles(nt) == 0
+            m.noise_counter.zero_()
+            outs.append((m.act(own, radar, None, noisy=False), m.act(own, radar, ep, noisy=True)))
+    finally:
+        L.aac_uam_actor_set_tiles(4)
+    for a, b in outs[1:]:
+        assert torch.equal(a, outs[0][0]) and torch.equal(b, outs[0][1])
+    assert L.aac_uam_actor_set_tiles(3) != 0
+
+
 def test_reference_surface(native_lib, tmp_path):
     from multi_agent_aac_amd import uam_learner as L
     m = L.MADDPG([7, 20, 18, 6], [7, 20, 18, 6], 2, n_agents=3, device=DEV, seed=2, batch_size=8, memory_length=64)

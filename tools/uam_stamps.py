@@ -1,7 +1,8 @@
 """Phase timestamps (s_memtime) of uam_step_kernel's first 64 workgroups at the config-5 size,
 from a probe build with -DAAC_UAM_STAMPS (multi_agent_aac_amd/libaac_probe.so via AAC_LIB).
-Phases: 1 clouds + kinematics, 2 distances, 3 neighbour order, 4 radar, 5 observation + goal
-touch, 6 ss_reward predicates, end: the per-env pass and the writes."""
+Phases: 1 clouds + kinematics, 2 distances, 3 neighbour order, radar (3a fixed boundaries +
+candidate list, 3b clip jobs, 3c stores), 5 observation + goal touch, 6 ss_reward predicates, end:
+the per-env pass and the writes."""
 import ctypes
 import os
 import sys
@@ -27,7 +28,7 @@ def main():
         torch.cuda.synchronize()
         L.aac_uam_stamps(buf)
         a = np.array(buf, dtype=np.int64).reshape(64, 16)
-        marks = [0, 1, 2, 3, 4, 5, 6, 15]
+        marks = [0, 1, 2, 3, 7, 8, 4, 5, 6, 15]     # radar = 3a (3 -> 7), 3b clips (7 -> 8), 3c stores (8 -> 4)
         d = np.diff(a[:, marks], axis=1)
         print("phase cycles (mean over 64 WGs):", [int(x) for x in d.mean(0)], "total", int((a[:, 15] - a[:, 0]).mean()))
         env.auto_reset(b.env_done)
