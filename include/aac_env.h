@@ -102,9 +102,10 @@ int aac_env_set_od_banks(aac_env *env, int32_t n_maps, const double *start, cons
 /* Re-draws the OD of every env with env_done_dev[e] != 0 from the bank (reference rule: starts
  * more than 2 pB apart, ATT/env:258-268) and overwrites those envs' rows of ``out``. */
 int aac_env_auto_reset(aac_env *env, const uint8_t *env_done_dev, const aac_step_out *out, void *stream);
-/* Process-wide: on != 0 the auto-reset first packs the done envs into an ordered list (one extra
- * launch) so that each reset workgroup holds epb of them; 0 (default, unless AAC_ENV_RESET_PACKED=1)
- * resets over contiguous env ranges.  Results are identical either way. */
+/* Process-wide: on > 0 the auto-reset first packs the done envs into an ordered list (one extra
+ * launch) so that each reset workgroup holds epb of them; 0 resets over contiguous env ranges; < 0
+ * (the default, or AAC_ENV_RESET_PACKED=0 / 1) packs for the WGRU variant only, where a large
+ * share of the envs ends every step.  Results are identical either way. */
 void aac_env_set_reset_compact(int32_t on);
 /* Diagnostic builds only (-DAAC_ENV_STAMPS): per-workgroup phase stamps of the last step launch
  * (7 uint64 per workgroup); returns an error in a normal build. */

@@ -37,6 +37,7 @@
 #endif                            // scratch on cold paths); 2 waves: 1.75x slower at 262 144 envs
 // observation rows staged in LDS for coalesced 16-B stores (floats per workgroup, else direct)
 #define OBS_STAGE_FLOATS 2560
+#define WPC 8            // variant 1: waypoints per agent kept in LDS by the step kernel
 
 namespace {
 
@@ -199,6 +200,13 @@ struct Lds {
 extern __shared__ uint8_t s_maps[];
 
 __device__ inline int rows_off(const Args &A) { return (A.n_maps * A.gw * A.gh + 7) & ~7; }
+
+// variant 1: after the maps (and row masks), 16-B aligned, the first WPC waypoints of each of the
+// workgroup's agents (wp_cache_bytes on the host side)
+__device__ inline double2 *wp_cache(const Args &A) {
+    const int end = A.occ_rows ? rows_off(A) + 8 * A.n_maps * A.gw : A.n_maps * A.gw * A.gh;
+    return reinterpret_cast<double2 *>(s_maps + ((end + 15) & ~15));
+}
 
 __device__ inline const unsigned long long *map_rows(const Args &A, int m) {
     return A.occ_rows ? reinterpret_cast<const unsigned long long *>(s_maps + rows_off(A)) + m * A.gw : nullptr;
@@ -381,10 +389,16 @@ __device__ double2 segment_closest_point(double px, double py, double ax, double
 // list = the waypoints whose bit in rm is clear), progress toward that waypoint, cross-track reward
 // against the reference path start -> waypoints (reset_world :339-343), small-step and
 // near-building penalties; per-agent reward
-__device__ double wgru_reward(const Args &A, size_t ai, double2 pp, double2 p, double2 v, uint32_t rm, int cnt,
-                              double rmin, int goal, int bnd, int building, int &flag, int &done, int &cg,
+// waypoint k of an agent: the step kernel's LDS copy of its first WPC waypoints, else HBM (the
+// searches below walk the list with a compare after every load: from HBM each step waited for its load)
+struct WpView {
+    const double2 *lds, *hbm;
+    __device__ double2 operator[](int k) const { return k < WPC ? lds[k] : hbm[k]; }
+};
+
+__device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, double2 p, double2 v, uint32_t rm,
+                              int cnt, double rmin, int goal, int bnd, int building, int &flag, int &done, int &cg,
                               uint8_t &fl) {
-    const double2 *wp = A.wp + ai * A.W;
     const double px = p.x, py = p.y, pb = A.pb;
     int nrem = cnt - __popc(rm & (cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1u)));
     double smallest = INFINITY;
@@ -572,15 +586,43 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         if (!A.variant) w0 = A.wp[(size_t)ai * A.W + cur];     // variant 1: cur is a bit mask
     }
     if (A.variant) S.rmin[t] = 0x7ff0000000000000ull;       // +inf
+    // variant 1: the first WPC waypoints of every agent of the workgroup, loaded now by all threads
+    // (one load each, in flight across the radar phase) and put in LDS after it
+    constexpr int WPI = 2;           // items per thread held across the radar (nag <= 64); the rest after it
+    double2 wpv[WPI];
+    const int wpn = A.variant ? nag * (A.W < WPC ? A.W : WPC) : 0;
+    if (A.variant) {
+#pragma unroll
+        for (int u = 0; u < WPI; ++u) {
+            const int w = t + u * BLOCK;
+            const int kmax = A.W < WPC ? A.W : WPC;
+            const int la = w / kmax, k = w - la * kmax;
+            const int eq = e0 + la / N;
+            wpv[u] = (w < wpn && eq < A.E) ? A.wp[((size_t)eq * N + la % N) * A.W + k] : make_double2(0.0, 0.0);
+        }
+    }
     aacw::lds_barrier();
     ESTAMP(2, __builtin_amdgcn_s_memtime());
 #ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
     radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0);
 #endif
+    if (A.variant) {
+        double2 *wc = wp_cache(A);
+        const int kmax = A.W < WPC ? A.W : WPC;
+#pragma unroll
+        for (int u = 0; u < WPI; ++u) {
+            const int w = t + u * BLOCK;
+            if (w < wpn) wc[(w / kmax) * WPC + w % kmax] = wpv[u];
+        }
+        for (int w = t + WPI * BLOCK; w < wpn; w += BLOCK) {
+            const int la = w / kmax, k = w - la * kmax, eq = e0 + la / N;
+            if (eq < A.E) wc[la * WPC + k] = A.wp[((size_t)eq * N + la % N) * A.W + k];
+        }
+    }
 #ifdef AAC_ENV_STAMPS
     aacw::lds_barrier();
 #else
-    if (A.variant) aacw::lds_barrier();     // the agent phase reads the radar minima (uniform branch)
+    if (A.variant) aacw::lds_barrier();     // the agent phase reads the radar minima and the waypoint cache
 #endif
     ESTAMP(3, __builtin_amdgcn_s_memtime());
     const int D0 = A.D0, K6 = A.K * 6;
@@ -641,8 +683,9 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         uint8_t fl = 0;
         double r;
         if (A.variant) {
-            r = wgru_reward(A, ai, pp, np, S.vel[t], (uint32_t)cur, wcnt, __longlong_as_double((long long)S.rmin[t]),
-                            goal, bnd, building, wpf, done, cg, fl);
+            const WpView wv{wp_cache(A) + t * WPC, A.wp + ai * A.W};
+            r = wgru_reward(A, ai, wv, pp, np, S.vel[t], (uint32_t)cur, wcnt,
+                            __longlong_as_double((long long)S.rmin[t]), goal, bnd, building, wpf, done, cg, fl);
             if (cg) {
                 reach = 1;
                 A.reach[ai] = 1;
@@ -806,22 +849,44 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     }
     __syncthreads();
     RSTAMP(2, __builtin_amdgcn_s_memtime());
+    // the waypoint lists, copied by all threads over (agent, waypoint) items: a thread copying its
+    // agent's W waypoints in a row waited for every load before the store that might alias it
+    {
+        const int nw = nag * A.W;
+        for (int w0 = 0; w0 < nw; w0 += 4 * BLOCK) {
+            double2 v[4];
+            size_t dst[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int w = w0 + u * BLOCK + t;
+                const int la = w / A.W, k = w - la * A.W, lq = la / N;
+                ok[u] = w < nw && S.active[lq < A.epb ? lq : 0] && emap[lq < A.epb ? lq : 0] < A.E;
+                const size_t aq = ok[u] ? (size_t)emap[lq] * N + (la - lq * N) : 0;
+                dst[u] = aq * A.W + k;
+                v[u] = !ok[u] ? make_double2(0.0, 0.0)
+                              : (R.mode == 1 ? R.bank_wp[(size_t)S.idx[la] * A.W + k] : R.wps[aq * A.W + k]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (ok[u]) A.wp[dst[u]] = v[u];
+        }
+    }
     if (active) {
-        double2 st;
+        double2 st, g;
         int cnt;
         if (R.mode == 1) {
             int idx = S.idx[base + i];
             st = R.bank_start[idx];
             cnt = R.bank_cnt[idx];
-            for (int k = 0; k < A.W; ++k) A.wp[ai * A.W + k] = R.bank_wp[(size_t)idx * A.W + k];
-            A.goal[ai] = R.bank_wp[(size_t)idx * A.W + cnt - 1];
+            g = R.bank_wp[(size_t)idx * A.W + cnt - 1];
         } else {
             st = R.start[ai];
             cnt = R.cnt[ai];
-            for (int k = 0; k < A.W; ++k) A.wp[ai * A.W + k] = R.wps[ai * A.W + k];
-            A.goal[ai] = R.wps[ai * A.W + cnt - 1];
+            g = R.wps[ai * A.W + cnt - 1];
             if (i == 0 && A.map_idx) A.map_idx[e] = R.map_idx ? R.map_idx[e] : 0;
         }
+        A.goal[ai] = g;
         const double2 z = make_double2(0.0, 0.0);
         A.pos[ai] = st;
         A.pre_pos[ai] = st;
@@ -837,7 +902,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
         S.ppos[t] = st;
         S.vel[t] = z;
         S.pvel[t] = z;
-        S.goal[t] = A.goal[ai];
+        S.goal[t] = g;
     }
     __syncthreads();   // map_idx (explicit or drawn) written above is read by the radar phase below
     RSTAMP(3, __builtin_amdgcn_s_memtime());
@@ -861,12 +926,15 @@ __global__ void __launch_bounds__(1024) env_compact_kernel(const uint8_t *__rest
 
 // ------------------------------------------------------------------------------ host side
 thread_local std::string g_err;
-// AAC_ENV_RESET_PACKED=1: auto-reset over the packed list of done envs.  Off by default here: few
-// envs end per step at config 3, so the reset is one workgroup's latency either way and the packing
-// launch only adds to it (kernel trace: reset 36.4 us -> 37.7 us + 4.8 us packing)
-bool g_env_no_compact = [] {
+// Auto-reset over the packed list of done envs: -1 (default) per variant -- off for the ATT env, where
+// few envs end per step at config 3, so the reset is one workgroup's latency either way and the
+// packing launch only adds to it (kernel trace: reset 36.4 us -> 37.7 us + 4.8 us packing); on for
+// the WGRU variant, where ~38 % of the envs end per step at config 4 and the contiguous ranges keep
+// ~1 000 workgroups busy (two rounds) for what fits in one.  AAC_ENV_RESET_PACKED=0 / 1 or
+// aac_env_set_reset_compact force it.
+int g_env_compact = [] {
     const char *v = getenv("AAC_ENV_RESET_PACKED");
-    return !(v && v[0] == '1');
+    return v ? (v[0] == '1' ? 1 : 0) : -1;
 }();
 
 int fail(int code, const std::string &msg) {
@@ -1060,7 +1128,8 @@ int aac_env_step(aac_env *h, const float *actions, const aac_step_out *o, void *
     if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return fail(AAC_E_INVALID, "step outputs");
     Args A = make_args(h, o);
     const dim3 grid(h->blocks), block(BLOCK);
-    const size_t lds = map_bytes(h);
+    size_t lds = map_bytes(h);
+    if (A.variant) lds = ((lds + 15) & ~(size_t)15) + sizeof(double2) * WPC * (size_t)h->epb * h->cfg.N;
     const hipStream_t st = (hipStream_t)stream;
     const float2 *a2 = reinterpret_cast<const float2 *>(actions);
     if (A.variant) hipLaunchKernelGGL((step_kernel<1, AAC_RADAR_OBSTACLES>), grid, block, lds, st, A, a2);
@@ -1145,7 +1214,8 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
     R.bank_maps = h->bank_maps;
     R.seed = h->bank_seed;
     R.episode = h->episode;
-    if (env_done && !g_env_no_compact) {
+    const bool packed = g_env_compact < 0 ? h->cfg.variant != 0 : g_env_compact != 0;
+    if (env_done && packed) {
         hipLaunchKernelGGL(env_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, env_done, h->cfg.E,
                            h->rlist);
         HIPCHK(hipGetLastError());
@@ -1156,7 +1226,7 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
     return AAC_OK;
 }
 
-void aac_env_set_reset_compact(int32_t on) { g_env_no_compact = on == 0; }
+void aac_env_set_reset_compact(int32_t on) { g_env_compact = on < 0 ? -1 : (on != 0); }
 
 int aac_env_stamps(unsigned long long *out, int32_t n_wg) {
 #ifdef AAC_ENV_STAMPS

@@ -260,7 +260,7 @@ def test_packed_auto_reset_bit_exact(native_lib, occ):
             for key in sa:
                 assert torch.equal(sa[key], sb[key]), (k, key)
     finally:
-        lib.aac_env_set_reset_compact(0)
+        lib.aac_env_set_reset_compact(-1)
     assert resets > 0
 
 

@@ -26,9 +26,26 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     L = _native.lib()
     L.aac_env_reset_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.aac_env_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     nwg = 65536
+    epb_for = lambda apw: 1 if N > apw else apw // N                      # noqa: E731  (aac_env.hip policy)
+    epb = epb_for(50) if E // epb_for(50) >= 1024 else epb_for(24)
+    swg = (E + epb - 1) // epb
     for k in range(40):
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
         env.step(torch.rand(E, N, 2, device="cuda", generator=g) * 2 - 1)
+        s1.record()
+        torch.cuda.synchronize()
+        if k >= 30 and not k % 3:
+            sb = np.zeros((swg, 7), dtype=np.uint64)
+            assert L.aac_env_stamps(sb.ctypes.data, swg) == 0
+            ss = sb.astype(np.int64)
+            sp = np.diff(ss[:, 1:6], axis=1)
+            print(f"[{kind}] step {k}: {swg} wg x {epb} envs, event {s0.elapsed_time(s1) * 1e3:.1f} us")
+            for name, col in zip(("kinematics", "radar", "agent", "final"), sp.T):
+                print(f"  {name:10s} cycles median {np.median(col):8.0f}  p90 {np.percentile(col, 90):8.0f}  "
+                      f"max {col.max():8.0f}")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         env.auto_reset(env.bufs.env_done)
