@@ -182,6 +182,33 @@ int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const flo
 int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *Wn, const float *bn,
                    const float *Wqk, const float *Wv, float *out, int32_t ldo, int32_t R, int32_t K, void *stream);
 
+/* The actor's encoders fused into its neighbour attention (ATT/nets:194-210), K <= 8:
+ *   e_o = relu(Wo own[:d_own] + bo), e_g = relu(Wg radar + bg)  -> cat[r][0:64], cat[r][64:128]
+ *   x_j = relu(Wn nei_j + bn)                                    -> xn[(r*K + j)*64] (train)
+ *   q = Wq e_o, qk = Wk^T q, alpha = masked softmax(x_j . qk / 8), xb = sum alpha_j x_j
+ *   v_att = Wv xb                                                -> cat[r][128:192]
+ * (q, qk, alpha, xb kept for aac_attn_train_bwd when xn != NULL; inference leaves them NULL).  The
+ * encoders' GEMM launch before the attention disappears.  Optional riding job in the same launch
+ * (c_rows > 0): the critic's per-agent encoders f[b][n*128 + c] = relu(W_n x_bn + b_n) (ATT/nets:
+ * 697-701, R3) of rows x_bn = cx + b*cx_ld + n*c_din, W_n = cW + n*128*c_din, b_n = cb + n*128,
+ * f = cf + b*c_n*128 + n*128 -- independent work that shares the launch; R = 0 runs it alone. */
+typedef struct {
+    const float *own; int32_t ld_own; int32_t d_own;
+    const float *radar; int32_t ld_radar;
+    const float *nei;
+    const float *Wo, *bo, *Wg, *bg, *Wn, *bn, *Wq, *Wk, *Wv;
+    float *cat; int32_t ld_cat;
+    float *xn, *q, *qk, *alpha, *xb;
+    int32_t R, K;
+    const float *cx; int32_t cx_ld; int32_t c_din;
+    const float *cW, *cb;
+    float *cf;
+    int32_t c_rows, c_n;
+} aac_attn_enc_args;
+/* nset = 1 or 2 independent argument sets in one launch (e.g. the target actor's inference pass
+ * beside a training forward; K <= 8 each). */
+int aac_attn_enc_fwd(const aac_attn_enc_args *args, int32_t nset, void *stream);
+
 /* Replay gather with interleaved destinations: element c of field f of sampled row b goes to
  * dsts[f][b*(widths[f]/chunks[f])*dstrides[f] + (c/chunks[f])*dstrides[f] + c%chunks[f]]
  * (chunks = widths, dstrides = widths gives aac_replay_gather), and to the same place in

@@ -1738,6 +1738,188 @@ __global__ void __launch_bounds__(256) attn_mfma_block_kernel(const float *__res
     }
 }
 
+// ------------------------------------------------- encoders fused into the attention (aac_attn_enc_fwd)
+// 16 x 16 tile of e^T = W x^T over K inputs (k = 4 s + h; A = W[f0 + n][k], B = x[row n][k]); lane
+// (n, h) gets the pre-activations of features f0 + 4 h .. + 3 of row n
+__device__ __forceinline__ f4 enc_mfma(const float *__restrict__ W, int K, int f0, const float *__restrict__ xrow,
+                                       int n, int h) {
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int ks = (K + 3) >> 2;
+    for (int s = 0; s < ks; ++s) {
+        const int k = 4 * s + h;
+        const float a = k < K ? W[(f0 + n) * K + k] : 0.0f;
+        const float b = k < K ? xrow[k] : 0.0f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+__device__ __forceinline__ f4 relu_bias4(f4 v, const float *__restrict__ b) {
+    f4 r;
+    r.x = v.x + b[0];
+    r.y = v.y + b[1];
+    r.z = v.z + b[2];
+    r.w = v.w + b[3];
+    r.x = r.x > 0.0f ? r.x : 0.0f;
+    r.y = r.y > 0.0f ? r.y : 0.0f;
+    r.z = r.z > 0.0f ? r.z : 0.0f;
+    r.w = r.w > 0.0f ? r.w : 0.0f;
+    return r;
+}
+
+// the riding job: the critic encoders of 16 rows of one agent (eight 16-feature tiles, two per wave)
+__device__ void critic_enc_rows(const aac_attn_enc_args &A, int job) {
+    const int nrb = (A.c_rows + 15) / 16;
+    const int ag = job / nrb, rb = job - ag * nrb;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
+    const int r = rb * 16 + n, rc = r < A.c_rows ? r : A.c_rows - 1;
+    const float *x = A.cx + (size_t)rc * A.cx_ld + (size_t)ag * A.c_din;
+    const float *W = A.cW + (size_t)ag * 128 * A.c_din, *bb = A.cb + ag * 128;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int f0 = 32 * w + 16 * t;
+        const f4 v = relu_bias4(enc_mfma(W, A.c_din, f0, x, n, h), bb + f0 + 4 * h);
+        if (r < A.c_rows) *reinterpret_cast<f4 *>(A.cf + (size_t)r * A.c_n * 128 + ag * 128 + f0 + 4 * h) = v;
+    }
+}
+
+// up to two independent sets (e.g. the target actor's inference attention and a training one) in one
+// launch; set s owns workgroups [start[s], start[s] + nattn[s]) for its attention blocks and the next
+// nride[s] for its riding critic-encoder jobs
+struct AttnEncBatch {
+    aac_attn_enc_args a[2];
+    int start[2], nattn[2], nride[2];
+    int nset;
+};
+
+template <int KM>
+__global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
+    const int s = (P.nset > 1 && (int)blockIdx.x >= P.start[1]) ? 1 : 0;
+    const aac_attn_enc_args &A = P.a[s];
+    const int nattn = P.nattn[s];
+    const int lb = blockIdx.x - P.start[s];
+    if (lb >= nattn) {
+        critic_enc_rows(A, lb - nattn);
+        return;
+    }
+    const bool train = A.xn != nullptr;       // uniform: inference leaves the backward's operands NULL
+    __shared__ float sE[64 * TS], sQ[64 * TS], sX[64 * TS];
+    __shared__ f4 sQK4[16 * QS / 4];
+    __shared__ f4 sXn4[16 * KM * QS / 4];        // x_j of the block: [(row * KM + j)][feature]
+    float *sQK = reinterpret_cast<float *>(sQK4), *sXn = reinterpret_cast<float *>(sXn4);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
+    const int fo = 16 * w + 4 * h;
+    const int R = A.R, K = A.K;
+    const int nblk = (R + 15) / 16;
+    for (int blk = lb; blk < nblk; blk += nattn) {
+        const int r0 = blk * 16, r = r0 + n;
+        const bool rin = r < R;
+        const int rc = rin ? r : R - 1;
+        // encoders: this wave's 16 features of e_o, e_g and of every x_j (transposed, rows on n)
+        const f4 eo = relu_bias4(enc_mfma(A.Wo, A.d_own, 16 * w, A.own + (size_t)rc * A.ld_own, n, h), A.bo + fo);
+        const f4 eg = relu_bias4(enc_mfma(A.Wg, 18, 16 * w, A.radar + (size_t)rc * A.ld_radar, n, h), A.bg + fo);
+        f4 xj[KM];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const int jc = j < K ? j : K - 1;
+            xj[j] = relu_bias4(enc_mfma(A.Wn, 6, 16 * w, A.nei + ((size_t)rc * K + jc) * 6, n, h), A.bn + fo);
+        }
+        float *crow = A.cat + (size_t)r * A.ld_cat;
+        if (rin) {
+            *reinterpret_cast<f4 *>(crow + fo) = eo;
+            *reinterpret_cast<f4 *>(crow + 64 + fo) = eg;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sE[(fo + j) * TS + n] = eo[j];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (train && rin && j < K) *reinterpret_cast<f4 *>(A.xn + ((size_t)r * K + j) * 64 + fo) = xj[j];
+            *reinterpret_cast<f4 *>(sXn + (n * KM + j) * QS + fo) = xj[j];
+        }
+        // the projections' weight fragments and the mask rows (slot = lane)
+        float b[16], aq[16], ak[16], av[16];
+        ld16w(A.Wq + (16 * w + n) * 64 + 16 * h, aq);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) ak[s] = A.Wk[(16 * h + s) * 64 + 16 * w + n];
+        ld16w(A.Wv + (16 * w + n) * 64 + 16 * h, av);
+        float ms[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = r0 + 4 * w + i, rr = row < R ? row : R - 1;
+            const f2 *pn = reinterpret_cast<const f2 *>(A.nei + ((size_t)rr * K + (lane < K ? lane : K - 1)) * 6);
+            const f2 n0 = pn[0], n1 = pn[1], n2 = pn[2];
+            ms[i] = ((((n0.x + n0.y) + n1.x) + n1.y) + n2.x) + n2.y;
+        }
+        __syncthreads();
+        // q^T = Wq e_o^T
+        lds_bfrag(sE, h, n, b);
+        f4 acc = mfma_k64(aq, b);
+        if (train && rin) *reinterpret_cast<f4 *>(A.q + (size_t)r * 64 + fo) = acc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sQ[(fo + j) * TS + n] = acc[j];
+        __syncthreads();
+        // qk^T = Wk^T q^T
+        lds_bfrag(sQ, h, n, b);
+        acc = mfma_k64(ak, b);
+        if (train && rin) *reinterpret_cast<f4 *>(A.qk + (size_t)r * 64 + fo) = acc;
+        *reinterpret_cast<f4 *>(sQK + n * QS + fo) = acc;
+        __syncthreads();
+        // masked softmax and xb for the wave's four rows (lane = feature), as attn_mfma_fwd_kernel
+        {
+            float p[4 * KM], x[4][KM], qk4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                qk4[i] = sQK[(4 * w + i) * QS + lane];
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    x[i][j] = j < K ? sXn[((4 * w + i) * KM + j) * QS + lane] : 0.0f;
+                    p[i * KM + j] = x[i][j] * qk4[i];
+                }
+            }
+            wsum_n(p);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int rl = 4 * w + i, row = r0 + rl;
+                float sc[KM];
+                float mx = -INFINITY;
+                unsigned valid = 0;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    sc[j] = p[i * KM + j] / 8.0f;
+                    const bool v = j < K && __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ms[i]), j)) != 0.0f;
+                    valid |= (v ? 1u : 0u) << j;
+                    mx = (v && sc[j] > mx) ? sc[j] : mx;
+                }
+                float den = 0.0f;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    const float e = (valid >> j & 1) ? __expf(sc[j] - mx) : 0.0f;
+                    sc[j] = e;
+                    den += e;
+                }
+                float xb = 0.0f, al = 0.0f;
+                const float inv = 1.0f / den;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    const float a = (valid >> j & 1) ? sc[j] * inv : 0.0f;
+                    xb = fmaf(a, x[i][j], xb);
+                    al = lane == j ? a : al;
+                }
+                if (train && row < R) {
+                    if (lane < K) A.alpha[(size_t)row * K + lane] = al;
+                    A.xb[(size_t)row * 64 + lane] = xb;
+                }
+                sX[lane * TS + rl] = xb;
+            }
+        }
+        __syncthreads();
+        // v^T = Wv xb^T -> cat[r][128:192]
+        lds_bfrag(sX, h, n, b);
+        acc = mfma_k64(av, b);
+        if (rin) *reinterpret_cast<f4 *>(crow + 128 + fo) = acc;
+    }
+}
+
 // ------------------------------------------------------------------------------ gather
 struct SFields {
     float *dst[16];
@@ -2250,6 +2432,46 @@ int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *
     else if (K <= 8) hipLaunchKernelGGL(attn_block_kernel<8>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
     else if (K <= 16) hipLaunchKernelGGL(attn_block_kernel<16>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
     else hipLaunchKernelGGL(attn_block_kernel<32>, grid, block, 0, st, eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K);
+    FHIP(hipGetLastError());
+    return 0;
+}
+
+static int attn_enc_check(const aac_attn_enc_args &A) {
+    const bool train = A.xn != nullptr;
+    if (A.R > 0) {
+        if (A.K < 1 || A.K > 8) return ffail("attn_enc_fwd: 1 <= K <= 8");
+        if (!A.own || !A.radar || !A.nei || !A.Wo || !A.bo || !A.Wg || !A.bg || !A.Wn || !A.bn || !A.Wq || !A.Wk ||
+            !A.Wv || !A.cat || A.d_own < 1)
+            return ffail("attn_enc_fwd: null operand");
+        if (!aligned16(A.cat) || A.ld_cat % 4 != 0 || (reinterpret_cast<uintptr_t>(A.nei) & 7) != 0)
+            return ffail("attn_enc_fwd: cat rows must be 16-B aligned, nei 8-B aligned");
+        if (train && (!A.q || !A.qk || !A.alpha || !A.xb || !aligned16(A.q) || !aligned16(A.qk) || !aligned16(A.xn)))
+            return ffail("attn_enc_fwd: training outputs q, qk, alpha, xb (16-B aligned q, qk, xn)");
+    }
+    if (A.c_rows > 0 && (!A.cx || !A.cW || !A.cb || !A.cf || A.c_n < 1 || A.c_din < 1 || !aligned16(A.cf)))
+        return ffail("attn_enc_fwd: critic-encoder job operands (16-B aligned cf)");
+    return 0;
+}
+
+int aac_attn_enc_fwd(const aac_attn_enc_args *args, int32_t nset, void *stream) {
+    if (!args || nset < 1 || nset > 2) return ffail("attn_enc_fwd: 1 or 2 argument sets");
+    AttnEncBatch P{};
+    P.nset = nset;
+    int total = 0, kmax = 1;
+    for (int s = 0; s < nset; ++s) {
+        if (attn_enc_check(args[s])) return -1;
+        P.a[s] = args[s];
+        P.start[s] = total;
+        P.nattn[s] = args[s].R > 0 ? mfma_attn_grid(args[s].R) : 0;
+        P.nride[s] = args[s].c_rows > 0 ? args[s].c_n * ((args[s].c_rows + 15) / 16) : 0;
+        total += P.nattn[s] + P.nride[s];
+        if (args[s].R > 0 && args[s].K > kmax) kmax = args[s].K;
+    }
+    if (total == 0) return 0;
+    const dim3 g(total), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (kmax > 4) hipLaunchKernelGGL(attn_enc_kernel<8>, g, b, 0, st, P);
+    else hipLaunchKernelGGL(attn_enc_kernel<4>, g, b, 0, st, P);
     FHIP(hipGetLastError());
     return 0;
 }

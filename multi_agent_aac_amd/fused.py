@@ -51,6 +51,16 @@ class HeadJob(ctypes.Structure):
                 ("h2", vp), ("w2", vp), ("b2", vp), ("q2", vp), ("dq2", vp), ("dh2", vp), ("M2", i32)]
 
 
+class AttnEncArgs(ctypes.Structure):
+    """aac_attn_enc_args (include/aac_fused.h): the actor's encoders + neighbour attention of R rows,
+    plus an optional riding job (the critic's per-agent encoders of c_rows samples)."""
+    _fields_ = [("own", vp), ("ld_own", i32), ("d_own", i32), ("radar", vp), ("ld_radar", i32), ("nei", vp),
+                ("Wo", vp), ("bo", vp), ("Wg", vp), ("bg", vp), ("Wn", vp), ("bn", vp), ("Wq", vp), ("Wk", vp),
+                ("Wv", vp), ("cat", vp), ("ld_cat", i32), ("xn", vp), ("q", vp), ("qk", vp), ("alpha", vp),
+                ("xb", vp), ("R", i32), ("K", i32), ("cx", vp), ("cx_ld", i32), ("c_din", i32), ("cW", vp),
+                ("cb", vp), ("cf", vp), ("c_rows", i32), ("c_n", i32)]
+
+
 GEMM_MAX = 16
 HEAD_MAX = 1
 _L = None
@@ -78,6 +88,7 @@ def lib():
         L.aac_attn_train_fwd.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
         L.aac_attn_train_bwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, i32, i32,
                                          vp]
+        L.aac_attn_enc_fwd.argtypes = [ctypes.POINTER(AttnEncArgs), i32, vp]
         L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         _L = L
     return _L
@@ -158,6 +169,55 @@ class GemmLaunch:
         wg = ctypes.c_int32()
         _chk(lib().aac_gemm_plan(self.arr, self.n, cfg, ctypes.byref(wg)), "aac_gemm_plan")
         return list(cfg), wg.value
+
+
+class AttnEnc:
+    """One aac_attn_enc_fwd launch over one or two independent argument sets (AttnEncArgs)."""
+
+    def __init__(self, *sets):
+        assert 1 <= len(sets) <= 2
+        self.n = len(sets)
+        self.arr = (AttnEncArgs * self.n)(*sets)
+
+    def __call__(self):
+        _chk(lib().aac_attn_enc_fwd(self.arr, self.n, _stream()), "aac_attn_enc_fwd")
+
+
+_RIDE = ("cx", "cx_ld", "c_din", "cW", "cb", "cf", "c_rows", "c_n")
+
+
+def attn_set(ap, own, ld_own, d_own, radar, nei, R, K, cat, acts=None, ride=None):
+    """Argument set of the actor's encoders + attention over R rows (ATT/nets:194-210): e_o, e_g and
+    v_att land in cat[r][0:192]; with ``acts`` (ActorActs) the backward's x_j, q, qk, alpha, xb are
+    kept.  ``ride``: the critic-encoder job (``critic_enc_ride``) sharing the launch."""
+    a = AttnEncArgs()
+    a.own, a.ld_own, a.d_own, a.radar, a.ld_radar, a.nei = own, ld_own, d_own, radar, 18, nei
+    a.Wo, a.bo, a.Wg, a.bg, a.Wn, a.bn = ap.Wo, ap.bo, ap.Wg, ap.bg, ap.Wn, ap.bn
+    a.Wq, a.Wk, a.Wv = ap.Wq, ap.Wkv, ap.Wkv + 4 * 64 * 64
+    a.cat, a.ld_cat, a.R, a.K = cat, 192, R, K
+    if acts is not None:
+        a.xn, a.q, a.qk, a.alpha, a.xb = ptr(acts.xn), ptr(acts.qa), ptr(acts.qk), ptr(acts.alpha), ptr(acts.xb)
+    return with_ride(a, ride)
+
+
+def with_ride(a, ride):
+    """A copy of argument set ``a`` carrying the riding critic-encoder job ``ride`` (or none)."""
+    b = AttnEncArgs.from_buffer_copy(a)
+    for k in _RIDE:
+        setattr(b, k, 0 if ride is None else ride[k])
+    return b
+
+
+def critic_enc_ride(cp, X, rows, N, Din, f):
+    """The critic's per-agent encoders f[b][n*128:(n+1)*128] = relu(enc_n X[b][n]) (ATT/nets:697-701,
+    R3) as a riding job of an aac_attn_enc_fwd launch (the per-agent weights are consecutive)."""
+    return {"cx": X, "cx_ld": N * Din, "c_din": Din, "cW": cp.enc_w[0], "cb": cp.enc_b[0], "cf": ptr(f),
+            "c_rows": rows, "c_n": N}
+
+
+def ride_only(ride):
+    """An argument set with no attention rows that runs only the riding critic-encoder job."""
+    return with_ride(AttnEncArgs(), ride)
 
 
 def set_lds_policy(min_workgroups=512, small_tiles=False):
@@ -320,24 +380,21 @@ class ActorActs:
 
 def actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
     """ActorNetwork_ATT_TwoPortion.forward (ATT/nets:194-213) over R rows as dependent stages
-    [encoders, attention (callable, aac_attn_train_fwd: q, Wk^T q, masked softmax, Wv sum a x),
-    merge, out]; GEMM stages are product lists so they can share launches with independent
-    work.  The tanh actions land at ``out`` (row stride ``ld_out``, e.g. the critic-input rows)."""
+    [encoders + attention (AttnEncArgs set of aac_attn_enc_fwd: e_o, e_g, x_j, q, Wk^T q, masked
+    softmax, Wv sum a x), merge, out]; GEMM stages are product lists and the attention set can carry
+    a riding job, so they share launches with independent work.  The tanh actions land at ``out``
+    (row stride ``ld_out``, e.g. the critic-input rows)."""
     c = acts
-    enc = [prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
-           prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
-           prob(nei, ap.Wn, ptr(c.xn), R * K, 64, 6, 6, 6, 64, tb=1, bias=ap.bn, act=RELU)]
-    attn = lambda: attn_train_fwd(ptr(c.cat), 192, ptr(c.xn), nei, ap.Wq, ap.Wkv, ap.Wkv + 4 * 64 * 64,  # noqa: E731
-                                  ptr(c.qa), ptr(c.qk), ptr(c.alpha), ptr(c.xb), ptr(c.cat, 128), 192, R, K)
+    attn = attn_set(ap, own, ld_own, D0, radar, nei, R, K, ptr(c.cat), acts=c)
     merge = [prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm, act=RELU)]
     outp = [prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)]
-    return enc, attn, merge, outp
+    return attn, merge, outp
 
 
 def actor_forward(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
     """Launch list of the training actor forward (activations kept for the backward)."""
-    enc, attn, merge, outp = actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
-    return gemm_launches(enc) + [attn] + gemm_launches(merge) + gemm_launches(outp)
+    attn, merge, outp = actor_forward_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
+    return [AttnEnc(attn)] + gemm_launches(merge) + gemm_launches(outp)
 
 
 class ActorInferActs:
@@ -347,29 +404,24 @@ class ActorInferActs:
         self.R = R
         self.cat = torch.empty(R, 192, dtype=torch.float32, device=dev)
         self.ha = torch.empty(R, 256, dtype=torch.float32, device=dev)
-        self.wqk = torch.empty(64, 64, dtype=torch.float32, device=dev)
 
 
 def actor_infer_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
-    """ActorNetwork_ATT_TwoPortion.forward for inference as dependent stages [encoders + Wqk =
-    Wk^T Wq, attention block (callable, aac_attn_block), merge, out]; GEMM stages are product lists
-    so that independent work can share their launches."""
+    """ActorNetwork_ATT_TwoPortion.forward for inference as dependent stages [encoders + attention
+    (AttnEncArgs set, nothing kept for a backward), merge, out]; GEMM stages are product lists so
+    that independent work can share their launches."""
     c = acts
-    enc = [prob(own, ap.Wo, ptr(c.cat), R, 64, D0, ld_own, D0, 192, tb=1, bias=ap.bo, act=RELU),
-           prob(radar, ap.Wg, ptr(c.cat, 64), R, 64, 18, 18, 18, 192, tb=1, bias=ap.bg, act=RELU),
-           prob(ap.Wkv, ap.Wq, ptr(c.wqk), 64, 64, 64, 64, 64, 64, ta=1)]           # Wk^T Wq
-    attn = lambda: attn_block(ptr(c.cat), 192, nei, ap.Wn, ap.bn, ptr(c.wqk), ap.Wkv + 4 * 64 * 64,  # noqa: E731
-                              ptr(c.cat, 128), 192, R, K)
+    attn = attn_set(ap, own, ld_own, D0, radar, nei, R, K, ptr(c.cat))
     merge = [prob(ptr(c.cat), ap.Wm, ptr(c.ha), R, 256, 192, 192, 192, 256, tb=1, bias=ap.bm, act=RELU)]
     outp = [prob(ptr(c.ha), ap.Wa, out, R, 2, 256, 256, 256, ld_out, tb=1, bias=ap.ba, act=TANH)]
-    return enc, attn, merge, outp
+    return attn, merge, outp
 
 
 def actor_forward_infer(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out):
-    """Inference launch list of ActorNetwork_ATT_TwoPortion.forward: the own / radar encoders and
-    Wqk = Wk^T Wq in one grouped launch, the fused attention block (aac_attn_block), merge, out."""
-    enc, attn, merge, outp = actor_infer_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
-    return gemm_launches(enc) + [attn] + gemm_launches(merge) + gemm_launches(outp)
+    """Inference launch list of ActorNetwork_ATT_TwoPortion.forward: encoders + attention in one
+    aac_attn_enc_fwd launch, merge, out."""
+    attn, merge, outp = actor_infer_stages(ap, acts, own, ld_own, radar, nei, R, K, D0, out, ld_out)
+    return [AttnEnc(attn)] + gemm_launches(merge) + gemm_launches(outp)
 
 
 def critic_forward_stages(cp, X, rows, N, Din, f, h):
@@ -406,9 +458,9 @@ class ActorInfer:
                 assert t.is_contiguous() and t.device == self.dev and t.dtype == torch.float32
             acts = ActorInferActs(R, self.dev)
             out = torch.empty(R, 2, dtype=torch.float32, device=self.dev)
-            enc, attn, merge, outp = actor_infer_stages(self.ap, acts, ptr(own), self.D0, ptr(radar), ptr(nei), R,
-                                                        self.K, self.D0, ptr(out), 2)
-            L = gemm_launches(enc) + [attn] + gemm_launches(merge)
+            attn, merge, outp = actor_infer_stages(self.ap, acts, ptr(own), self.D0, ptr(radar), ptr(nei), R,
+                                                   self.K, self.D0, ptr(out), 2)
+            L = [AttnEnc(attn)] + gemm_launches(merge)
             self.plans[key] = (L, gemm_launches(outp), acts, out, (own, radar, nei))
         L, Lout, acts, out, _ = self.plans[key]
         for op in L:
@@ -494,8 +546,8 @@ class FusedUpdate:
         dsts2 = [ptr(self.X2)] + [None] * 8
         self.pre.append(lambda: gather_strided(rep.ring, self.idx, dsts, w, chunks, strides, dsts2=dsts2))
         Bt = nb * B
-        t_enc, t_attn, t_merge, t_out = actor_infer_stages(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar),
-                                                           ptr(self.nnei), Bt * N, K, D0, ptr(self.Xt, D0), Din)
+        t_attn, t_merge, t_out = actor_infer_stages(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar),
+                                                    ptr(self.nnei), Bt * N, K, D0, ptr(self.Xt, D0), Din)
         t_cenc, t_comb = critic_forward_stages(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
         t_head = lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),  # noqa: E731
                                      done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y))
@@ -506,8 +558,8 @@ class FusedUpdate:
             # step 0's forward and the actor forward 0 (current weights, their own buffers) share its
             # launches up to the point where the critic step needs the targets y
             cs0 = self._critic_stages(0, C, self.cbuf[1])
-            a0_enc, a0_attn, a0_merge, a0_out = self._actor_fwd_stages(0, A)
-            self.pre += gemm_launches(t_enc + cs0["enc"] + a0_enc) + [t_attn, a0_attn]
+            a0_attn, a0_merge, a0_out = self._actor_fwd_stages(0, A)
+            self.pre += [AttnEnc(with_ride(t_attn, cs0["enc"]), a0_attn)]
             self.pre += gemm_launches(t_merge + cs0["comb"] + a0_merge) + gemm_launches(t_out + a0_out)
             # the TD target of all batches with critic step 0's mse head chained on batch 0's rows
             f0, h0, dq0, dh0, _ = self.cbuf[1]
@@ -516,7 +568,7 @@ class FusedUpdate:
                             chain=(ptr(h0), C.Wq, C.bq, ptr(self.q_c), ptr(dq0), ptr(dh0), B))
             self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [lambda: critic_head_job(tjob)]
         else:
-            self.pre += gemm_launches(t_enc) + [t_attn] + gemm_launches(t_merge) + gemm_launches(t_out)
+            self.pre += [AttnEnc(t_attn)] + gemm_launches(t_merge) + gemm_launches(t_out)
             self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [t_head]
         if m.world > 1:
             self.iters = self._pipelined(A, C)
@@ -568,7 +620,7 @@ class FusedUpdate:
             L = []
             if i == 0 and cs is not None:
                 # iteration 0's actor forward ran in pre: critic step 1 rides on the actor step's stages
-                L += gemm_launches(ac["cenc"] + cs["enc"]) + gemm_launches(ac["ccomb"] + cs["comb"])
+                L += [AttnEnc(ride_only(ac["cenc"]), ride_only(cs["enc"]))] + gemm_launches(ac["ccomb"] + cs["comb"])
                 L += gemm_launches(ac["dcomb"], heads=[cs["head_job"]])
                 L.append(ac["aob"])
                 L += gemm_launches(ac["wgrad1"] + cs["grad"])
@@ -578,17 +630,17 @@ class FusedUpdate:
                 segs.append(L)
                 continue
             if i > 0:
-                a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+                a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
                 if cs is None:
-                    L += gemm_launches(a_enc) + [a_attn] + gemm_launches(a_merge) + gemm_launches(a_out)
+                    L += [AttnEnc(a_attn)] + gemm_launches(a_merge) + gemm_launches(a_out)
                 else:
-                    L += gemm_launches(a_enc + cs["enc"]) + [a_attn] + gemm_launches(a_merge + cs["comb"])
+                    L += [AttnEnc(with_ride(a_attn, cs["enc"]))] + gemm_launches(a_merge + cs["comb"])
                     L += gemm_launches(a_out, heads=[cs["head_job"]])
+            L.append(AttnEnc(ride_only(ac["cenc"])))
             if cs is None:
-                L += gemm_launches(ac["cenc"]) + gemm_launches(ac["ccomb"])
+                L += gemm_launches(ac["ccomb"]) + gemm_launches(ac["dcomb"])
             else:
-                L += gemm_launches(ac["cenc"] + cs["grad"]) + gemm_launches(ac["ccomb"] + cs["encw"])
-            L += gemm_launches(ac["dcomb"])
+                L += gemm_launches(ac["ccomb"] + cs["grad"]) + gemm_launches(ac["dcomb"] + cs["encw"])
             L.append(ac["aob"])
             L += gemm_launches(ac["wgrad1"])
             L.append(ac["attn_bwd"])
@@ -688,22 +740,21 @@ class FusedUpdate:
         return actor_forward_stages(A, self.acts, X2, Din, radar, nei, B * N, K, D0, X2 + 4 * D0, Din)
 
     def _actor_fwd_launches(self, i, A):
-        a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
-        return gemm_launches(a_enc) + [a_attn] + gemm_launches(a_merge) + gemm_launches(a_out)
+        a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+        return [AttnEnc(a_attn)] + gemm_launches(a_merge) + gemm_launches(a_out)
 
     def _critic_step(self, i, A, C, cb, fuse_actor_fwd):
         """Critic step of iteration i (ATT/maddpg:375-387) up to its weight-gradient partials.
         With ``fuse_actor_fwd`` the actor forward of the same iteration (ATT/maddpg:389-392) --
         which depends only on the actor weights, changed after the critic step -- shares the
         critic step's launches; the policy actions land in X2 (own columns gathered there too)."""
-        if fuse_actor_fwd:
-            a_enc, a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
-        else:
-            a_enc, a_attn, a_merge, a_out = [], None, [], []
         cs = self._critic_stages(i, C, cb)
-        L = gemm_launches(cs["enc"] + a_enc)
-        if a_attn is not None:
-            L.append(a_attn)
+        if fuse_actor_fwd:
+            a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+            L = [AttnEnc(with_ride(a_attn, cs["enc"]))]
+        else:
+            a_merge, a_out = [], []
+            L = [AttnEnc(ride_only(cs["enc"]))]
         L += gemm_launches(cs["comb"])
         L.append(cs["head"])
         L += gemm_launches(cs["grad"] + a_merge)
@@ -711,15 +762,17 @@ class FusedUpdate:
         return L
 
     def _critic_stages(self, i, C, cb):
-        """The critic step of iteration i as dependent stages: product lists enc, comb, grad
-        (weight gradients of the head and combine, data gradient of the combine), encw (encoder
-        weight gradients) and the head callable (mse gradient) between comb and grad."""
+        """The critic step of iteration i as dependent stages: enc (the encoders as a riding job of an
+        aac_attn_enc_fwd launch), product lists comb, grad (weight gradients of the head and combine,
+        data gradient of the combine), encw (encoder weight gradients) and the head callable (mse
+        gradient) between comb and grad."""
         m, B, N, Din = self.m, self.B, self.N, self.Din
         SC, nC = self.SPLIT_CRITIC, self.gc.shape[1]     # copy stride
         gC = CriticParams(m.critics, m.fc, self.gc.data_ptr())
         X, _, _, _, y = self._batch_ptrs(i)
         f, h, dq, dh, df = cb
-        c_enc, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
+        _, c_comb = critic_forward_stages(C, X, B, N, Din, f, h)
+        c_enc = critic_enc_ride(C, X, B, N, Din, f)
         hj = head_job(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh))
         head = lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq),  # noqa: E731
                                    dh=ptr(dh))
@@ -738,7 +791,7 @@ class FusedUpdate:
         """Actor step of iteration i (ATT/maddpg:389-425) after its forward, up to the weight-
         gradient partials: critic on the policy actions, backward into the actor."""
         st = self._actor_stages(i, A, C)
-        L = gemm_launches(st["cenc"]) + gemm_launches(st["ccomb"])
+        L = [AttnEnc(ride_only(st["cenc"]))] + gemm_launches(st["ccomb"])
         L += gemm_launches(st["dcomb"])
         L.append(st["aob"])
         L += gemm_launches(st["wgrad1"])
@@ -747,7 +800,7 @@ class FusedUpdate:
         return L
 
     def _actor_stages(self, i, A, C):
-        """The actor step of iteration i after its forward, as dependent stages: cenc, ccomb
+        """The actor step of iteration i after its forward, as dependent stages: cenc (riding job), ccomb
         (critic on the policy actions), head (-mean Q gradient), dcomb, aob (actor output
         backward), wgrad1, attn_bwd, wgrad2."""
         m, B, N, D0, K, Din = self.m, self.B, self.N, self.D0, self.K, self.Din
@@ -758,7 +811,7 @@ class FusedUpdate:
         f, h, dq, dh, df = self.cbuf[0]
         c = self.acts
         st = {}
-        st["cenc"], _ = critic_forward_stages(C, X, B, N, Din, f, h)
+        st["cenc"] = critic_enc_ride(C, X, B, N, Din, f)
         # the actor loss -mean Q has the constant gradient dq = -1/B (ATT/maddpg:424), so the head's
         # dh = dq Wo (h > 0) is a second output of the combine layer's epilogue, and Q itself (stats
         # only) is an N = 1 product beside the combine's data gradient: no head launch on this chain

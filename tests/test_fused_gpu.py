@@ -425,6 +425,73 @@ def test_attn_train_fwd_bwd_matches_autograd(native_lib, K):
     np.testing.assert_allclose(deo.cpu().double(), eo_r.grad * (d(eo) > 0), atol=2e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("K", [1, 4, 7])
+def test_attn_enc_fwd_matches_reference(native_lib, K):
+    """aac_attn_enc_fwd: the actor's encoders (e_o, e_g, x_j) computed inside the attention launch
+    (ATT/nets:194-210) against fp64 torch -- training (q, qk, alpha, xb, x_j kept) and inference --
+    plus the riding critic-encoder job (ATT/nets:697-701); a two-set launch gives the same bits as
+    the sets launched alone."""
+    from types import SimpleNamespace
+
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(20 + K)
+    R, D0, Nc, Din, rows = 611, 6 + 4 * K, 5, 24, 203
+    d = lambda t: t.double().cpu()   # noqa: E731
+    r = lambda *s, sc=1.0: (torch.randn(*s, device=DEV) * sc).contiguous()   # noqa: E731
+    own = r(R, D0 + 2)                            # row stride D0 + 2 (the critic-input rows)
+    radar = torch.rand(R, 18, device=DEV) * 15
+    nei = r(R, K, 6)
+    nei[::4, 0] = 0.0
+    nei[9] = 0.0                                  # an all-masked row
+    W = {k: r(*s, sc=sc) for k, s, sc in (("Wo", (64, D0), 0.3), ("bo", (64,), 0.1), ("Wg", (64, 18), 0.1),
+                                             ("bg", (64,), 0.1), ("Wn", (64, 6), 0.4), ("bn", (64,), 0.1),
+                                             ("Wq", (64, 64), 0.125))}
+    kv = r(128, 64, sc=0.125)
+    P = fused.ptr
+    ap = SimpleNamespace(**{k: P(v) for k, v in W.items()}, Wkv=P(kv))
+    cx = r(rows, Nc, Din)
+    cw, cb = r(Nc, 128, Din, sc=0.2), r(Nc, 128, sc=0.1)
+    cp = SimpleNamespace(enc_w=[P(cw, n * 128 * Din) for n in range(Nc)], enc_b=[P(cb, n * 128) for n in range(Nc)])
+    acts = fused.ActorActs(R, K, DEV)
+    cat_t = torch.full((R, 192), 7.0, device=DEV)
+    cat_i = torch.full((R, 192), 7.0, device=DEV)
+    f1 = torch.full((rows, Nc * 128), 7.0, device=DEV)
+    tr = fused.attn_set(ap, P(own), D0 + 2, D0, P(radar), P(nei), R, K, P(cat_t), acts=acts,
+                        ride=fused.critic_enc_ride(cp, P(cx), rows, Nc, Din, f1))
+    inf = fused.attn_set(ap, P(own), D0 + 2, D0, P(radar), P(nei), R, K, P(cat_i))
+    fused.AttnEnc(tr, inf)()
+    torch.cuda.synchronize()
+    # reference (fp64)
+    eo = torch.relu(d(own)[:, :D0] @ d(W["Wo"]).t() + d(W["bo"]))
+    eg = torch.relu(d(radar) @ d(W["Wg"]).t() + d(W["bg"]))
+    x = torch.relu(d(nei) @ d(W["Wn"]).t() + d(W["bn"]))
+    q = eo @ d(W["Wq"]).t()
+    k, v = x @ d(kv[:64]).t(), x @ d(kv[64:]).t()
+    score = torch.einsum("rkc,rc->rk", k, q) / 8.0
+    mask = d(nei).mean(-1) != 0
+    a = torch.nan_to_num(torch.softmax(score.masked_fill(~mask, float("-inf")), dim=1)).masked_fill(~mask, 0.0)
+    want = torch.cat([eo, eg, torch.einsum("rk,rkc->rc", a, v)], 1)
+    for cat in (cat_t, cat_i):
+        np.testing.assert_allclose(cat.cpu().double(), want, atol=3e-5, rtol=1e-5)
+    np.testing.assert_allclose(acts.xn.cpu().double().reshape(R, K, 64), x, atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(acts.qa.cpu().double(), q, atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(acts.qk.cpu().double(), q @ d(kv[:64]), atol=3e-5, rtol=1e-5)
+    np.testing.assert_allclose(acts.alpha.cpu().double(), a, atol=1e-6)
+    np.testing.assert_allclose(acts.xb.cpu().double(), torch.einsum("rk,rkc->rc", a, x), atol=2e-5, rtol=1e-5)
+    fw = torch.relu(torch.einsum("bnd,ncd->bnc", d(cx), d(cw)) + d(cb)).reshape(rows, Nc * 128)
+    np.testing.assert_allclose(f1.cpu().double(), fw, atol=2e-5, rtol=1e-5)
+    # the sets alone, and the riding job alone: the same bits
+    cat2, cat3, f2 = torch.zeros_like(cat_t), torch.zeros_like(cat_i), torch.zeros_like(f1)
+    acts2 = fused.ActorActs(R, K, DEV)
+    fused.AttnEnc(fused.attn_set(ap, P(own), D0 + 2, D0, P(radar), P(nei), R, K, P(cat2), acts=acts2))()
+    fused.AttnEnc(fused.attn_set(ap, P(own), D0 + 2, D0, P(radar), P(nei), R, K, P(cat3)))()
+    fused.AttnEnc(fused.ride_only(fused.critic_enc_ride(cp, P(cx), rows, Nc, Din, f2)))()
+    torch.cuda.synchronize()
+    assert torch.equal(cat2, cat_t) and torch.equal(cat3, cat_i) and torch.equal(f2, f1)
+    for n in ("xn", "qa", "qk", "alpha", "xb"):
+        assert torch.equal(getattr(acts2, n), getattr(acts, n)), n
+
+
 @pytest.mark.parametrize("n,ns,pad", [(65536, 32, 0), (180228, 8, 0), (4100, 40, 0), (1001, 8, 0), (1001, 8, 1),
                                       (4098, 16, 1), (4096, 3, 0), (256, 1, 0)])
 def test_adam_sum_matches_torch(native_lib, n, ns, pad):
