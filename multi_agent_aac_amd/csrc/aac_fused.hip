@@ -1739,22 +1739,100 @@ __global__ void __launch_bounds__(256) attn_mfma_block_kernel(const float *__res
 }
 
 // ------------------------------------------------- encoders fused into the attention (aac_attn_enc_fwd)
-// 16 x 16 tile of e^T = W x^T over K inputs (k = 4 s + h; A = W[f0 + n][k], B = x[row n][k]); lane
-// (n, h) gets the pre-activations of features f0 + 4 h .. + 3 of row n
-__device__ __forceinline__ f4 enc_mfma(const float *__restrict__ W, int K, int f0, const float *__restrict__ xrow,
-                                       int n, int h) {
-    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    const int ks = (K + 3) >> 2;
-    for (int s = 0; s < ks; ++s) {
-        const int k = 4 * s + h;
-        const float a = k < K ? W[(f0 + n) * K + k] : 0.0f;
-        const float b = k < K ? xrow[k] : 0.0f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+// The encoder weights and a block's input rows are small contiguous arrays: the workgroup stages them
+// in LDS with coalesced loads (rows zero-padded to a multiple of 4), and the MFMA fragments come from
+// there.  (Fragment loads straight from global memory -- 16 rows x 4 scattered floats per lane and
+// step -- made the launch bound on vector-memory instructions, not on the arithmetic.)
+constexpr int ENC_DMAX = 40;                 // own rows / critic-input rows up to 40 floats (K <= 8)
+// LDS row strides: the fragment reads cover k < round4(K); an odd stride spreads the 16 rows of a
+// read over distinct banks (a multiple of 8 put them on 4 banks or fewer)
+__device__ __forceinline__ int enc_stride(int k) { return ((k + 3) & ~3) + 1; }
+constexpr int ENC_SMAX = ENC_DMAX + 1, ENC_SG = 21, ENC_SN = 9;       // own / critic rows, radar, neighbour
+constexpr int ENC_W_FLOATS = 64 * ENC_SMAX + 64 * ENC_SG + 64 * ENC_SN + 192;   // Wo | Wg | Wn | bo bg bn
+constexpr int ENC_OFF_WG = 64 * ENC_SMAX, ENC_OFF_WN = ENC_OFF_WG + 64 * ENC_SG, ENC_OFF_B = ENC_OFF_WN + 64 * ENC_SN;
+
+// Staging into LDS rows of stride Kp >= K (zero-padded), in two halves so that every load of several
+// blocks is in flight before the first LDS store (a loop that stored each value right after loading
+// it waited a full memory latency per iteration).  No integer divisions on the item index: a
+// contiguous [rows][K] weight matrix goes linearly (row = item * ceil(2^32 / K) >> 32, exact for
+// items < 2^16 and K <= 64), a block of 16 strided input rows as 16 threads per row.  Out-of-range
+// items load src[0].
+template <int MAXI>
+struct Stage {
+    float v[MAXI];
+};
+
+__device__ __forceinline__ uint64_t div_magic(int K) { return ((1ull << 32) + (uint64_t)K - 1) / (uint64_t)K; }
+
+template <int MAXI>
+__device__ __forceinline__ void stage_w_load(Stage<MAXI> &st, const float *__restrict__ src, int n) {
+#pragma unroll
+    for (int u = 0; u < MAXI; ++u) {
+        const int g = threadIdx.x + 256 * u;
+        const float v = src[g < n ? g : 0];
+        st.v[u] = v;
     }
+}
+
+// store the linear items of a [rows][K] matrix as LDS rows of stride Kp, and zero the pad columns
+template <int MAXI>
+__device__ __forceinline__ void stage_w_store(const Stage<MAXI> &st, float *dst, int K, int Kp, int rows) {
+    const uint64_t m = div_magic(K);
+    const int n = rows * K;
+#pragma unroll
+    for (int u = 0; u < MAXI; ++u) {
+        const int g = threadIdx.x + 256 * u;
+        const int r = (int)(((uint64_t)g * m) >> 32);
+        if (g < n) dst[r * Kp + (g - r * K)] = st.v[u];
+    }
+    for (int i = threadIdx.x; i < rows * 4; i += 256) {
+        const int r = i >> 2, c = i & 3;
+        if (K + c < Kp) dst[r * Kp + K + c] = 0.0f;
+    }
+}
+
+// 16 input rows (global row stride ld, K used columns) -> LDS rows of stride Kp; rows >= nrows zero
+template <int MAXI>
+__device__ __forceinline__ void stage_r_load(Stage<MAXI> &st, const float *__restrict__ src, int ld, int K, int nrows) {
+    const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+#pragma unroll
+    for (int u = 0; u < MAXI; ++u) {
+        const int k = c + 16 * u;
+        const bool ok = k < K && r < nrows;
+        const float v = src[ok ? (size_t)r * ld + k : 0];
+        st.v[u] = ok ? v : 0.0f;
+    }
+}
+
+template <int MAXI>
+__device__ __forceinline__ void stage_r_store(const Stage<MAXI> &st, float *dst, int Kp) {
+    const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+#pragma unroll
+    for (int u = 0; u < MAXI; ++u) {
+        const int k = c + 16 * u;
+        if (k < Kp) dst[r * Kp + k] = st.v[u];
+    }
+}
+
+// 16 x 16 tile of e^T = W x^T over K inputs from LDS (k = 4 s + h; A = W[f0 + n][k], B = x[row n][k],
+// W rows of stride Kw, x rows of stride Kx, both zero-padded past K); lane (n, h) gets the
+// pre-activations of features f0 + 4 h .. + 3 of row n.  Steps past ceil(K / 4) are skipped (uniform).
+template <int KS>
+__device__ __forceinline__ f4 enc_lds(const float *sW, int Kw, const float *sx, int Kx, int K, int f0, int n, int h) {
+    float a[KS], b[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        a[s] = 4 * s < K ? sW[(f0 + n) * Kw + 4 * s + h] : 0.0f;
+        b[s] = 4 * s < K ? sx[n * Kx + 4 * s + h] : 0.0f;
+    }
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+        if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
     return acc;
 }
 
-__device__ __forceinline__ f4 relu_bias4(f4 v, const float *__restrict__ b) {
+__device__ __forceinline__ f4 relu_bias4(f4 v, const float *b) {
     f4 r;
     r.x = v.x + b[0];
     r.y = v.y + b[1];
@@ -1767,18 +1845,28 @@ __device__ __forceinline__ f4 relu_bias4(f4 v, const float *__restrict__ b) {
     return r;
 }
 
-// the riding job: the critic encoders of 16 rows of one agent (eight 16-feature tiles, two per wave)
-__device__ void critic_enc_rows(const aac_attn_enc_args &A, int job) {
+// the riding job: the critic encoders of 16 rows of one agent (eight 16-feature tiles, two per wave),
+// W_n, b_n and the 16 input rows staged in LDS
+__device__ void critic_enc_rows(const aac_attn_enc_args &A, int job, float *smem) {
     const int nrb = (A.c_rows + 15) / 16;
     const int ag = job / nrb, rb = job - ag * nrb;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
-    const int r = rb * 16 + n, rc = r < A.c_rows ? r : A.c_rows - 1;
-    const float *x = A.cx + (size_t)rc * A.cx_ld + (size_t)ag * A.c_din;
-    const float *W = A.cW + (size_t)ag * 128 * A.c_din, *bb = A.cb + ag * 128;
+    const int Din = A.c_din, Dp = enc_stride(Din), r0 = rb * 16;
+    float *sW = smem, *sx = smem + 128 * ENC_SMAX, *sb = sx + 16 * ENC_SMAX;
+    Stage<128 * ENC_DMAX / 256> gw;
+    Stage<(ENC_SMAX + 15) / 16> gx;
+    stage_w_load(gw, A.cW + (size_t)ag * 128 * Din, 128 * Din);
+    stage_r_load(gx, A.cx + (size_t)r0 * A.cx_ld + (size_t)ag * Din, A.cx_ld, Din, A.c_rows - r0);
+    const float bias = A.cb[ag * 128 + (threadIdx.x & 127)];
+    stage_w_store(gw, sW, Din, Dp, 128);
+    stage_r_store(gx, sx, Dp);
+    if (threadIdx.x < 128) sb[threadIdx.x] = bias;
+    __syncthreads();
+    const int r = r0 + n;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int f0 = 32 * w + 16 * t;
-        const f4 v = relu_bias4(enc_mfma(W, A.c_din, f0, x, n, h), bb + f0 + 4 * h);
+        const f4 v = relu_bias4(enc_lds<ENC_DMAX / 4>(sW, Dp, sx, Dp, Din, f0, n, h), sb + f0 + 4 * h);
         if (r < A.c_rows) *reinterpret_cast<f4 *>(A.cf + (size_t)r * A.c_n * 128 + ag * 128 + f0 + 4 * h) = v;
     }
 }
@@ -1792,37 +1880,120 @@ struct AttnEncBatch {
     int nset;
 };
 
+// LDS (floats): encoder weights | region U (the block's staged input rows, later sQ + sQK) | sE (later
+// sX) | sXn
+template <int KM>
+struct AttnEncLds {
+    static constexpr int NS = 8 * KM + 1;        // staged neighbour rows: slot j at j * 8, odd row stride
+    static constexpr int IN = 16 * ENC_SMAX + 16 * ENC_SG + 16 * NS;
+    static constexpr int U = IN > 2 * 64 * TS ? IN : 2 * 64 * TS;
+    static constexpr int OFF_U = ENC_W_FLOATS, OFF_E = OFF_U + ((U + 3) & ~3), OFF_XN = OFF_E + ((64 * TS + 3) & ~3);
+    static constexpr int OFF_S = OFF_XN + 16 * KM * QS;       // scores, then alpha: [16][KM] each
+    static constexpr int TOTAL = OFF_S + 2 * 16 * KM;
+};
+static_assert(AttnEncLds<4>::TOTAL >= 128 * ENC_SMAX + 16 * ENC_SMAX + 128, "ride job fits in the attention's LDS");
+
 template <int KM>
 __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
+    using L = AttnEncLds<KM>;
+    __shared__ f4 smem4[L::TOTAL / 4];
+    float *smem = reinterpret_cast<float *>(smem4);
     const int s = (P.nset > 1 && (int)blockIdx.x >= P.start[1]) ? 1 : 0;
     const aac_attn_enc_args &A = P.a[s];
     const int nattn = P.nattn[s];
     const int lb = blockIdx.x - P.start[s];
     if (lb >= nattn) {
-        critic_enc_rows(A, lb - nattn);
+        critic_enc_rows(A, lb - nattn, smem);
         return;
     }
+    ASTAMP(0);
     const bool train = A.xn != nullptr;       // uniform: inference leaves the backward's operands NULL
-    __shared__ float sE[64 * TS], sQ[64 * TS], sX[64 * TS];
-    __shared__ f4 sQK4[16 * QS / 4];
-    __shared__ f4 sXn4[16 * KM * QS / 4];        // x_j of the block: [(row * KM + j)][feature]
-    float *sQK = reinterpret_cast<float *>(sQK4), *sXn = reinterpret_cast<float *>(sXn4);
+    float *sWo = smem, *sWg = smem + ENC_OFF_WG, *sWn = smem + ENC_OFF_WN, *sB = smem + ENC_OFF_B;
+    float *sOwn = smem + L::OFF_U, *sRad = sOwn + 16 * ENC_SMAX, *sNei = sRad + 16 * ENC_SG;
+    float *sQ = smem + L::OFF_U, *sQK = sQ + 64 * TS;          // alias the staged rows (dead by then)
+    float *sE = smem + L::OFF_E, *sX = sE;                      // sE dead after the q stage
+    float *sXn = smem + L::OFF_XN;                              // x_j of the block: [(row * KM + j)][feature]
+    float *sS = smem + L::OFF_S, *sA = sS + 16 * KM;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
     const int fo = 16 * w + 4 * h;
-    const int R = A.R, K = A.K;
+    const int R = A.R, K = A.K, Do = A.d_own, Dop = enc_stride(Do);
+    constexpr int NS = L::NS, NNEI = KM * 8 / 16;
+    // the block's input rows (own, radar: rows of the LDS images; neighbours: slot j of row r at
+    // r * NS + 8 j), all loads in flight before the stores
+    struct In {
+        Stage<(ENC_SMAX + 15) / 16> o;
+        Stage<(ENC_SG + 15) / 16> g;
+        float nv[NNEI];
+    } in;
+    auto load_in = [&](int r0) {
+        stage_r_load(in.o, A.own + (size_t)r0 * A.ld_own, A.ld_own, Do, R - r0);
+        stage_r_load(in.g, A.radar + (size_t)r0 * A.ld_radar, A.ld_radar, 18, R - r0);
+        // neighbour rows: 16 threads per row over its KM * 8 (slot, k) items
+        const int row = threadIdx.x >> 4, c = threadIdx.x & 15;
+#pragma unroll
+        for (int u = 0; u < NNEI; ++u) {
+            const int e = c + 16 * u, j = e >> 3, k = e & 7;
+            const bool ok = k < 6 && j < K && r0 + row < R;
+            const float v = A.nei[ok ? ((size_t)(r0 + row) * K + j) * 6 + k : 0];
+            in.nv[u] = ok ? v : 0.0f;
+        }
+    };
+    auto store_in = [&]() {
+        stage_r_store(in.o, sOwn, Dop);
+        stage_r_store(in.g, sRad, ENC_SG);
+        const int row = threadIdx.x >> 4, c = threadIdx.x & 15;
+#pragma unroll
+        for (int u = 0; u < NNEI; ++u) sNei[row * NS + c + 16 * u] = in.nv[u];
+    };
+    // the encoder weights, once per workgroup, loaded together with the first block's rows
+    {
+        Stage<64 * ENC_DMAX / 256> go;
+        Stage<(64 * 18 + 255) / 256> gg;
+        Stage<(64 * 6 + 255) / 256> gn;
+        stage_w_load(go, A.Wo, 64 * Do);
+        stage_w_load(gg, A.Wg, 64 * 18);
+        stage_w_load(gn, A.Wn, 64 * 6);
+        const int k = threadIdx.x;
+        const float bias = k < 64 ? A.bo[k] : (k < 128 ? A.bg[k - 64] : A.bn[k < 192 ? k - 128 : 0]);
+        load_in(lb * 16);
+        stage_w_store(go, sWo, Do, Dop, 64);
+        stage_w_store(gg, sWg, 18, ENC_SG, 64);
+        stage_w_store(gn, sWn, 6, ENC_SN, 64);
+        if (k < 192) sB[k] = bias;
+    }
     const int nblk = (R + 15) / 16;
     for (int blk = lb; blk < nblk; blk += nattn) {
         const int r0 = blk * 16, r = r0 + n;
         const bool rin = r < R;
-        const int rc = rin ? r : R - 1;
+        // (region U was last read before the previous block's final barrier)
+        if (blk != lb) load_in(r0);
+        store_in();
+        // the projections' weight fragments (in flight across the staging barrier)
+        float b[16], aq[16], ak[16], av[16];
+        ld16w(A.Wq + (16 * w + n) * 64 + 16 * h, aq);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ak[t] = A.Wk[(16 * h + t) * 64 + 16 * w + n];
+        ld16w(A.Wv + (16 * w + n) * 64 + 16 * h, av);
+        ASTAMP(1);
+        __syncthreads();
+        ASTAMP(2);
         // encoders: this wave's 16 features of e_o, e_g and of every x_j (transposed, rows on n)
-        const f4 eo = relu_bias4(enc_mfma(A.Wo, A.d_own, 16 * w, A.own + (size_t)rc * A.ld_own, n, h), A.bo + fo);
-        const f4 eg = relu_bias4(enc_mfma(A.Wg, 18, 16 * w, A.radar + (size_t)rc * A.ld_radar, n, h), A.bg + fo);
+        const f4 eo = relu_bias4(enc_lds<ENC_DMAX / 4>(sWo, Dop, sOwn, Dop, Do, 16 * w, n, h), sB + fo);
+        const f4 eg = relu_bias4(enc_lds<5>(sWg, ENC_SG, sRad, ENC_SG, 18, 16 * w, n, h), sB + 64 + fo);
         f4 xj[KM];
 #pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            const int jc = j < K ? j : K - 1;
-            xj[j] = relu_bias4(enc_mfma(A.Wn, 6, 16 * w, A.nei + ((size_t)rc * K + jc) * 6, n, h), A.bn + fo);
+        for (int j = 0; j < KM; ++j)
+            xj[j] = relu_bias4(enc_lds<2>(sWn, ENC_SN, sNei + j * 8, NS, 6, 16 * w, n, h), sB + 128 + fo);
+        // the valid-neighbour mask of row r = lane (wave 0, lanes < 16: they run the softmax), read
+        // before region U is overwritten
+        unsigned valid = 0;
+        if (w == 0 && lane < 16) {
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                const float *pn = sNei + lane * NS + j * 8;
+                const float m = ((((pn[0] + pn[1]) + pn[2]) + pn[3]) + pn[4]) + pn[5];
+                valid |= (j < K && m != 0.0f ? 1u : 0u) << j;
+            }
         }
         float *crow = A.cat + (size_t)r * A.ld_cat;
         if (rin) {
@@ -1836,21 +2007,9 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
             if (train && rin && j < K) *reinterpret_cast<f4 *>(A.xn + ((size_t)r * K + j) * 64 + fo) = xj[j];
             *reinterpret_cast<f4 *>(sXn + (n * KM + j) * QS + fo) = xj[j];
         }
-        // the projections' weight fragments and the mask rows (slot = lane)
-        float b[16], aq[16], ak[16], av[16];
-        ld16w(A.Wq + (16 * w + n) * 64 + 16 * h, aq);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) ak[s] = A.Wk[(16 * h + s) * 64 + 16 * w + n];
-        ld16w(A.Wv + (16 * w + n) * 64 + 16 * h, av);
-        float ms[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = r0 + 4 * w + i, rr = row < R ? row : R - 1;
-            const f2 *pn = reinterpret_cast<const f2 *>(A.nei + ((size_t)rr * K + (lane < K ? lane : K - 1)) * 6);
-            const f2 n0 = pn[0], n1 = pn[1], n2 = pn[2];
-            ms[i] = ((((n0.x + n0.y) + n1.x) + n1.y) + n2.x) + n2.y;
-        }
+        ASTAMP(3);
         __syncthreads();
+        ASTAMP(4);
         // q^T = Wq e_o^T
         lds_bfrag(sE, h, n, b);
         f4 acc = mfma_k64(aq, b);
@@ -1858,65 +2017,78 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) sQ[(fo + j) * TS + n] = acc[j];
         __syncthreads();
+        ASTAMP(5);
         // qk^T = Wk^T q^T
         lds_bfrag(sQ, h, n, b);
         acc = mfma_k64(ak, b);
         if (train && rin) *reinterpret_cast<f4 *>(A.qk + (size_t)r * 64 + fo) = acc;
         *reinterpret_cast<f4 *>(sQK + n * QS + fo) = acc;
         __syncthreads();
-        // masked softmax and xb for the wave's four rows (lane = feature), as attn_mfma_fwd_kernel
-        {
-            float p[4 * KM], x[4][KM], qk4[4];
+        ASTAMP(6);
+        // scores s[r][j] = x_j[r] . qk[r] on MFMA: wave w takes slots j = w (+ 4): the 16 x 16 product
+        // X_j QK^T over the 64 features (k = 16 c + 4 h + t, 16-B LDS reads), whose diagonal is the
+        // 16 scores; lane (n, h) holds rows 4 h .. 4 h + 3 of column n, so lane n, h = n / 4 has s[n][j]
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                qk4[i] = sQK[(4 * w + i) * QS + lane];
+        for (int jj = 0; jj < KM / 4; ++jj) {
+            const int j = w + 4 * jj;
+            f4 sa = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-                for (int j = 0; j < KM; ++j) {
-                    x[i][j] = j < K ? sXn[((4 * w + i) * KM + j) * QS + lane] : 0.0f;
-                    p[i * KM + j] = x[i][j] * qk4[i];
-                }
+            for (int c = 0; c < 4; ++c) {
+                const f4 xa = *reinterpret_cast<const f4 *>(sXn + (n * KM + j) * QS + 16 * c + 4 * h);
+                const f4 qb = *reinterpret_cast<const f4 *>(sQK + n * QS + 16 * c + 4 * h);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) sa = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[t], qb[t], sa, 0, 0, 0);
             }
-            wsum_n(p);
+            if ((n >> 2) == h) sS[n * KM + j] = sa[n & 3];
+        }
+        __syncthreads();
+        // masked softmax of row r = lane (wave 0, lanes < 16); alpha to LDS (and the training output)
+        if (w == 0 && lane < 16) {
+            const int row = r0 + lane;
+            float sc[KM];
+            float mx = -INFINITY;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int rl = 4 * w + i, row = r0 + rl;
-                float sc[KM];
-                float mx = -INFINITY;
-                unsigned valid = 0;
+            for (int j = 0; j < KM; ++j) {
+                sc[j] = sS[lane * KM + j] / 8.0f;
+                mx = ((valid >> j & 1) && sc[j] > mx) ? sc[j] : mx;
+            }
+            float den = 0.0f;
 #pragma unroll
-                for (int j = 0; j < KM; ++j) {
-                    sc[j] = p[i * KM + j] / 8.0f;
-                    const bool v = j < K && __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ms[i]), j)) != 0.0f;
-                    valid |= (v ? 1u : 0u) << j;
-                    mx = (v && sc[j] > mx) ? sc[j] : mx;
-                }
-                float den = 0.0f;
+            for (int j = 0; j < KM; ++j) {
+                const float e = (valid >> j & 1) ? __expf(sc[j] - mx) : 0.0f;
+                sc[j] = e;
+                den += e;
+            }
+            const float inv = 1.0f / den;
 #pragma unroll
-                for (int j = 0; j < KM; ++j) {
-                    const float e = (valid >> j & 1) ? __expf(sc[j] - mx) : 0.0f;
-                    sc[j] = e;
-                    den += e;
-                }
-                float xb = 0.0f, al = 0.0f;
-                const float inv = 1.0f / den;
-#pragma unroll
-                for (int j = 0; j < KM; ++j) {
-                    const float a = (valid >> j & 1) ? sc[j] * inv : 0.0f;
-                    xb = fmaf(a, x[i][j], xb);
-                    al = lane == j ? a : al;
-                }
-                if (train && row < R) {
-                    if (lane < K) A.alpha[(size_t)row * K + lane] = al;
-                    A.xb[(size_t)row * 64 + lane] = xb;
-                }
-                sX[lane * TS + rl] = xb;
+            for (int j = 0; j < KM; ++j) {
+                const float a = (valid >> j & 1) ? sc[j] * inv : 0.0f;
+                sA[lane * KM + j] = a;
+                if (train && row < R && j < K) A.alpha[(size_t)row * K + j] = a;
             }
         }
         __syncthreads();
+        // xb = sum_j alpha_j x_j: lane (n, h) = row n, features fo .. fo + 3 (the sX image of the v stage)
+        {
+            f4 xb = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                const float a = sA[n * KM + j];
+                const f4 xv = *reinterpret_cast<const f4 *>(sXn + (n * KM + j) * QS + fo);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xb[t] = fmaf(a, xv[t], xb[t]);
+            }
+            if (train && rin) *reinterpret_cast<f4 *>(A.xb + (size_t)r * 64 + fo) = xb;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) sX[(fo + t) * TS + n] = xb[t];
+        }
+        __syncthreads();
+        ASTAMP(7);
         // v^T = Wv xb^T -> cat[r][128:192]
         lds_bfrag(sX, h, n, b);
         acc = mfma_k64(av, b);
         if (rin) *reinterpret_cast<f4 *>(crow + 128 + fo) = acc;
+        ASTAMP(8);
     }
 }
 
@@ -2445,11 +2617,13 @@ static int attn_enc_check(const aac_attn_enc_args &A) {
             return ffail("attn_enc_fwd: null operand");
         if (!aligned16(A.cat) || A.ld_cat % 4 != 0 || (reinterpret_cast<uintptr_t>(A.nei) & 7) != 0)
             return ffail("attn_enc_fwd: cat rows must be 16-B aligned, nei 8-B aligned");
+        if (A.d_own > ENC_DMAX) return ffail("attn_enc_fwd: d_own <= 40");
         if (train && (!A.q || !A.qk || !A.alpha || !A.xb || !aligned16(A.q) || !aligned16(A.qk) || !aligned16(A.xn)))
             return ffail("attn_enc_fwd: training outputs q, qk, alpha, xb (16-B aligned q, qk, xn)");
     }
-    if (A.c_rows > 0 && (!A.cx || !A.cW || !A.cb || !A.cf || A.c_n < 1 || A.c_din < 1 || !aligned16(A.cf)))
-        return ffail("attn_enc_fwd: critic-encoder job operands (16-B aligned cf)");
+    if (A.c_rows > 0 && (!A.cx || !A.cW || !A.cb || !A.cf || A.c_n < 1 || A.c_din < 1 || A.c_din > ENC_DMAX ||
+                         !aligned16(A.cf)))
+        return ffail("attn_enc_fwd: critic-encoder job operands (c_din <= 40, 16-B aligned cf)");
     return 0;
 }
 
