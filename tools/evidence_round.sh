@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-2 evidence on the GPU box (repo root), in two calls (each fits gpurun's limit):
-#   bash tools/evidence_r02.sh bench   -> the three bench lines (with CPU baselines) + rocprofv3
+# Per-round evidence on the GPU box (repo root), in two calls (each fits gpurun's limit):
+#   bash tools/evidence_round.sh bench   -> the three bench lines (with CPU baselines) + rocprofv3
 #                                         kernel traces / stats of short config 3 / 4 / 5 runs
-#   bash tools/evidence_r02.sh pmc     -> FETCH_SIZE / WRITE_SIZE passes (config 3 and 4 benches, the
+#   bash tools/evidence_round.sh pmc     -> FETCH_SIZE / WRITE_SIZE passes (config 3 and 4 benches, the
 #                                         env at 262 144 envs) and the env's SQ counters at 262 144
 # Every step has its own time limit (tools/gpu_job.sh stops at the first crash or timeout); each
-# --pmc pass is its own run with no trace domains.  Summaries: tools/evidence_r02_summary.py.
+# --pmc pass is its own run with no trace domains.  Summaries: tools/evidence_summary.py.
 export TMPDIR=/tmp
 T="rocprofv3 --kernel-trace --output-format csv"
 SHORT="--steps 10 --warmup 3 --no-cpu-baseline --env-micro 0"

@@ -1,8 +1,8 @@
-"""Turn the gpurun_out/ results of tools/evidence_r02.sh into the committed profiles/ files:
+"""Turn the gpurun_out/ results of tools/evidence_round.sh into the committed profiles/ files:
 bench lines, per-step kernel summaries (last 5 traced steps), kernel stats, and the PMC traffic
 files the bench reads (HBM bytes per launch next to the algorithmic bytes).
 
-python tools/evidence_r02_summary.py bench | pmc
+python tools/evidence_summary.py bench | pmc  (round tag from AAC_ROUND, default r03)
 """
 import csv
 import json
@@ -14,6 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT, PROF = os.path.join(ROOT, "gpurun_out"), os.path.join(ROOT, "profiles")
+R = os.environ.get("AAC_ROUND", "r03")
 
 
 def bench_line(label):
@@ -67,8 +68,8 @@ def traffic(fdir, wdir, kernel, stat, extra, out_names):
 def main():
     what = sys.argv[1]
     if what == "bench":
-        for label, name in (("bench", "r02_bench.json"), ("bench_gru", "r02_bench_gru.json"),
-                            ("bench_uam", "r02_bench_uam.json")):
+        for label, name in (("bench", f"{R}_bench.json"), ("bench_gru", f"{R}_bench_gru.json"),
+                            ("bench_uam", f"{R}_bench_uam.json")):
             d = bench_line(label)
             with open(os.path.join(PROF, name), "w") as fh:
                 json.dump(d, fh, indent=1)
@@ -77,23 +78,23 @@ def main():
                                 ("prof5", "uam_step", "uam_step_kernel")):
             txt = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_window.py"), trace_csv(d), "5",
                                   marker], capture_output=True, text=True, check=True).stdout
-            with open(os.path.join(PROF, f"r02_{name}_summary.txt"), "w") as fh:
+            with open(os.path.join(PROF, f"{R}_{name}_summary.txt"), "w") as fh:
                 fh.write(txt)
-            shutil.copy(stats_csv(d), os.path.join(PROF, f"r02_{name}_kernel_stats.csv"))
+            shutil.copy(stats_csv(d), os.path.join(PROF, f"{R}_{name}_kernel_stats.csv"))
             print(txt.splitlines()[0])
     elif what == "pmc":
-        b3 = json.load(open(os.path.join(PROF, "r02_bench.json")))
-        b4 = json.load(open(os.path.join(PROF, "r02_bench_gru.json")))
-        for b, fd, wd, names, model in ((b3, "pmc3f", "pmc3w", ["r02_gemm_pmc.json", "gemm_pmc.json"], "att"),
-                                        (b4, "pmc4f", "pmc4w", ["r02_gemm_pmc_gru.json", "gemm_pmc_gru.json"], "gru")):
+        b3 = json.load(open(os.path.join(PROF, f"{R}_bench.json")))
+        b4 = json.load(open(os.path.join(PROF, f"{R}_bench_gru.json")))
+        for b, fd, wd, names, model in ((b3, "pmc3f", "pmc3w", [f"{R}_gemm_pmc.json", "gemm_pmc.json"], "att"),
+                                        (b4, "pmc4f", "pmc4w", [f"{R}_gemm_pmc_gru.json", "gemm_pmc_gru.json"], "gru")):
             c, rf = b["config"], b["roofline"]
             traffic(fd, wd, "gemm_kernel", "mean",
                     {"model": model, "envs": c["envs_per_gpu"] if "envs_per_gpu" in c else c.get("envs"),
                      "agents": c.get("agents"), "batch": c.get("batch"),
                      "algorithmic_bytes_per_launch": int(rf["algorithmic_bytes_per_launch"])}, names)
         for b, fd, wd, names, variant, radar in (
-                (b3, "pmc3f", "pmc3w", ["r02_env_step_pmc.json", "env_step_pmc.json"], "att", "combined"),
-                (b4, "pmc4f", "pmc4w", ["r02_env_step_pmc_n8.json", "env_step_pmc_n8.json"], "wgru", "obstacles")):
+                (b3, "pmc3f", "pmc3w", [f"{R}_env_step_pmc.json", "env_step_pmc.json"], "att", "combined"),
+                (b4, "pmc4f", "pmc4w", [f"{R}_env_step_pmc_n8.json", "env_step_pmc_n8.json"], "wgru", "obstacles")):
             c, er = b["config"], b["env_roofline"]
             traffic(fd, wd, "::step_kernel", "median",
                     {"envs": c["envs_per_gpu"] if "envs_per_gpu" in c else c.get("envs"), "agents": c.get("agents"),
@@ -104,15 +105,15 @@ def main():
         traffic("pmcef", "pmcew", "::step_kernel", "median",
                 {"envs": 262144, "agents": 5, "radar": "combined", "variant": "att",
                  "algorithmic_bytes_per_launch": int(env_bytes_per_agent_step(5) * 262144 * 5)},
-                ["r02_env_step_pmc_262144.json"])
-        b5 = json.load(open(os.path.join(PROF, "r02_bench_uam.json")))
+                [f"{R}_env_step_pmc_262144.json"])
+        b5 = json.load(open(os.path.join(PROF, f"{R}_bench_uam.json")))
         c5 = b5["config"]
         traffic("pmc5f", "pmc5w", "uam_step_kernel", "median",
                 {"envs": c5["envs_per_gpu"], "agents": c5["agents"], "tdcpa": bool(c5.get("tdcpa")),
                  "algorithmic_bytes_per_launch": int(b5["env_roofline"]["bytes_per_agent_step"] *
                                                      b5["env_roofline"]["agents_per_launch"])},
-                ["r02_uam_env_pmc.json", "uam_env_pmc.json"])
-        shutil.copy(os.path.join(OUT, "gt.log"), os.path.join(PROF, "r02_gemm_table.txt"))
+                [f"{R}_uam_env_pmc.json", "uam_env_pmc.json"])
+        shutil.copy(os.path.join(OUT, "gt.log"), os.path.join(PROF, f"{R}_gemm_table.txt"))
         rows = [r for r in csv.DictReader(open(counter_csv("pmcsq"))) if "::step_kernel" in r["Kernel_Name"]]
         by = {}
         for r in rows:
@@ -125,7 +126,7 @@ def main():
                "wait_any_frac": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
                "note": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_ANY in quad-cycles; GRBM_GUI_ACTIVE summed "
                        "over 8 XCDs; tools/env_only.py --envs 262144 --steps 6, one --pmc pass"}
-        with open(os.path.join(PROF, "r02_env_sq_262144.json"), "w") as fh:
+        with open(os.path.join(PROF, f"{R}_env_sq_262144.json"), "w") as fh:
             json.dump(res, fh, indent=1)
         print(json.dumps(res))
 
