@@ -261,6 +261,7 @@ class Trainer(CheckpointMixin):
         self.episode = self.env_episode_view()
         self.env.auto_reset(None, out=self.cur)      # all envs: first OD draw + initial obs
         self.env_events = []
+        self.fused_tail = (not self.gru) if FUSED_TAIL is None else FUSED_TAIL
 
     def env_episode_view(self):
         # the env's own per-env episode counter (advanced by each auto-reset; 1 after the first)
@@ -279,6 +280,25 @@ class Trainer(CheckpointMixin):
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
+        if self.fused_tail:
+            # step + replay push + zeroed next hidden rows (GRU) + auto-reset in the step launch
+            # (aac_env_step_tail): the same results as the separate launches below
+            with trace.range("env_step"):
+                if self.gru:
+                    srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, self.h, hn]
+                    self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs, zero_rows=hn)
+                    self.h = hn
+                else:
+                    srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei]
+                    self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs)
+            if time_env:
+                ev1.record()
+                self.env_events.append((ev0, ev1))
+            self.cur, self.nxt = n, c
+            if update and len(self.replay) > self.B:
+                with trace.range("update"):
+                    self.model.update(self.B, use_graph=not NO_GRAPH, want_stats=False)
+            return
         with trace.range("env_step"):
             self.env.step(act, out=n)
         if time_env:
@@ -307,6 +327,12 @@ class Trainer(CheckpointMixin):
 
 NO_GRAPH = False
 OVERLAP_RESET = os.environ.get("AAC_OVERLAP_RESET", "0") == "1"   # measured slower: 1.241 vs 1.164 ms
+# replay push, GRU hidden-row zeroing and auto-reset fused into the env step launch (aac_env_step_tail).
+# Default: on for the ATT env (config 3: env part 0.084 -> 0.070 ms per step, tools/tail_probe.py), off
+# for the WGRU env of config 4, where ~40 % of the envs end every step and the in-step reset lengthens
+# nearly every workgroup of the two-round grid (0.131 -> 0.144 ms).  AAC_FUSED_TAIL=0 / 1 forces it.
+_FT = os.environ.get("AAC_FUSED_TAIL")
+FUSED_TAIL = None if _FT is None else _FT == "1"
 
 
 class side_stream:
@@ -750,6 +776,11 @@ def main():
         bpa = env_bytes_per_agent_step(N, "wgru", float(np.mean(tr.bank.cnt)))
     else:
         bpa = env_bytes_per_agent_step(N)
+    push_bpa = 0.0
+    if not uam and tr.fused_tail:
+        # the fused tail's replay push: each transition row read from its sources and written once
+        push_bpa = 2.0 * 4 * tr.replay.row_width / N
+        bpa += push_bpa
     achieved = bpa * a.envs * N / (env_ms * 1e-3) / 1e9
     traffic = None
     tsrc = None
@@ -762,7 +793,8 @@ def main():
         if t.get("envs") == a.envs and t.get("agents") == N and (
                 bool(t.get("tdcpa")) if uam else (t.get("variant", "att") == ("wgru" if tr.gru else "att") and
                                                   t.get("radar") == ("obstacles" if tr.gru else a.radar) and
-                                                  t.get("maps", 1) == a.maps)):
+                                                  t.get("maps", 1) == a.maps and
+                                                  bool(t.get("tail", False)) == tr.fused_tail)):
             traffic = t.get("hbm_bytes_per_launch")
             tsrc = os.path.relpath(tpath, ROOT)
     if uam:
@@ -794,7 +826,10 @@ def main():
                    "update_graph": (not a.no_graph) and (ws == 1 or uam or tr.gru or tr.model.fused),
                    "graph_segments": "one per update" if ws == 1 else "cut at each gradient all-reduce"},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if (tr.gru or uam) else N),
-        "env_roofline": {"kernel": "uam_step_kernel (fused UAM env step)" if uam else "step_kernel (fused env step)",
+        "env_roofline": {"kernel": "uam_step_kernel (fused UAM env step)" if uam else (
+                             "step_kernel (env step + replay push + auto-reset, aac_env_step_tail)" if tr.fused_tail
+                             else "step_kernel (fused env step)"),
+                         "push_bytes_per_agent_step": push_bpa,
                          "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": tsrc, "bytes_per_agent_step": bpa, "agents_per_launch": a.envs * N,

@@ -87,6 +87,29 @@ int aac_env_reset(aac_env *env, const uint8_t *env_mask_dev, const double *start
  * ATT/main:448-462 for all E envs: actions_dev float[E][N][2] in [-1, 1]. */
 int aac_env_step(aac_env *env, const float *actions_dev, const aac_step_out *out, void *stream);
 
+/* The rest of one ma_main iteration after the env step, fused into the step launch (each step
+ * workgroup does it for its own envs): the replay push of the E transitions (ReplayMemory.push,
+ * ATT/mem:12-15, ATT/main:363-400 -- the rows aac_replay_push_at writes), rows zeroed for the
+ * finished envs (e.g. the GRU actor's next hidden states, WGRU/ma_main:476-478), and the OD-bank
+ * auto-reset of the finished envs (reset_world, ATT/env:199-511).  The results equal aac_env_step,
+ * then aac_replay_push_at(ring, ...), then the zeroing, then aac_env_auto_reset(env_done, out). */
+typedef struct {
+    float *ring;                /* replay ring float[capacity][row_width] (device); NULL = no push     */
+    int32_t row_width;
+    int64_t capacity, pos, size;   /* the host mirror of the ring position / fill before this push  */
+    int64_t *meta;              /* device int64[2] [pos, size], advanced by the launch (for the sampler) */
+    int32_t n_fields;           /* 1..12 sources, in row order                                         */
+    const void *const *srcs;    /* HOST array of device pointers, source f is [E][widths[f]]; a source
+                                   may be one of this step's outputs (``out``), read after the step   */
+    const int32_t *widths;      /* HOST, sum = row_width                                               */
+    const int32_t *dtypes;      /* HOST, 0 float32, 1 uint8 (stored as 0.0 / 1.0); NULL = all float32  */
+    float *zero_rows;           /* device float[E][zero_width], rows of finished envs set to 0; or NULL */
+    int32_t zero_width;
+    int32_t auto_reset;         /* 1: redraw the finished envs from the OD bank (after the push)        */
+} aac_step_tail;
+int aac_env_step_tail(aac_env *env, const float *actions_dev, const aac_step_out *out, const aac_step_tail *tail,
+                      void *stream);
+
 /* Device-resident OD bank for GPU auto-reset.  Host arrays:
  * start [P][2], wps [P][W][2], cnt [P]; one entry = one agent's (start, A* waypoint list). */
 int aac_env_set_od_bank(aac_env *env, const double *start, const double *wps, const int32_t *cnt,

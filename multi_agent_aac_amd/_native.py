@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAC_LIB") or os.path.join(_HERE, "libaac_env.so")
 
 EXPORTS = (
-    "aac_env_create", "aac_env_destroy", "aac_last_error", "aac_env_reset", "aac_env_step",
+    "aac_env_create", "aac_env_destroy", "aac_last_error", "aac_env_reset", "aac_env_step", "aac_env_step_tail",
     "aac_env_set_od_bank", "aac_env_set_od_banks", "aac_env_auto_reset", "aac_env_set_reset_compact", "aac_env_use_episode_buffer", "aac_env_get_state", "aac_env_set_state",
     "aac_astar", "aac_od_bank_build",
 )
@@ -39,6 +39,13 @@ class StepOut(ctypes.Structure):
                                   "tcpa", "dcpa", "conf_cur", "conf_pre")]
 
 
+class StepTail(ctypes.Structure):
+    _fields_ = [("ring", vp), ("row_width", i32), ("capacity", ctypes.c_int64), ("pos", ctypes.c_int64),
+                ("size", ctypes.c_int64), ("meta", vp), ("n_fields", i32), ("srcs", ctypes.POINTER(vp)),
+                ("widths", ctypes.POINTER(i32)), ("dtypes", ctypes.POINTER(i32)), ("zero_rows", vp),
+                ("zero_width", i32), ("auto_reset", i32)]
+
+
 _lib = None
 
 
@@ -56,6 +63,7 @@ def lib():
     L.aac_env_destroy.restype = None
     L.aac_env_reset.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.POINTER(StepOut), vp]
     L.aac_env_step.argtypes = [vp, vp, ctypes.POINTER(StepOut), vp]
+    L.aac_env_step_tail.argtypes = [vp, vp, ctypes.POINTER(StepOut), ctypes.POINTER(StepTail), vp]
     L.aac_env_set_od_bank.argtypes = [vp, vp, vp, vp, i32, ctypes.c_uint64]
     L.aac_env_set_od_banks.argtypes = [vp, i32, vp, vp, vp, vp, ctypes.c_uint64]
     L.aac_env_auto_reset.argtypes = [vp, vp, ctypes.POINTER(StepOut), vp]

@@ -75,6 +75,36 @@ struct ResetArgs {
                               // workgroup b takes envs b*epb ... (mask-filtered)
 };
 
+// The fused step tail (aac_env_step_tail): the replay push of this step's transitions, rows zeroed for
+// the finished envs, and their auto-reset, run by each step workgroup for its own envs.  The push's
+// fields are split by the host: "early" fields (sources written by earlier launches: the current
+// observations, the actions, hidden states) are copied at kernel start; the fields that are this
+// step's outputs (next own / radar / nei rows, reward, done) are written into the ring where the
+// step produces them ("late" columns), so nothing is read back.
+#define TAIL_MAX_FIELDS 12
+enum { LATE_OWN, LATE_RADAR, LATE_NEI, LATE_REW, LATE_DONE, LATE_N };
+struct Tail {
+    float *ring;              // replay ring [cap][rw]; null = no push
+    int rw, nf;               // row width; number of early fields
+    int64_t cap, pos;         // host mirror of the ring position before this push
+    int64_t *meta;            // device [pos, size] for the sampler, stored by workgroup 0
+    int64_t new_pos, new_size;
+    const void *src[TAIL_MAX_FIELDS];          // early fields: [E][width] sources
+    int width[TAIL_MAX_FIELDS], col[TAIL_MAX_FIELDS], dtype[TAIL_MAX_FIELDS];   // col: first ring column
+    int cum[TAIL_MAX_FIELDS + 1];              // early fields' running column counts (cum[nf] = n_early)
+    int late[LATE_N];         // first ring column of each step output, -1 = not pushed
+    float *zero_rows;         // [E][zero_w] rows zeroed for the finished envs (after the push); null = none
+    int zero_w;
+    int reset;                // 1: auto-reset the finished envs from the OD bank (after the push)
+};
+
+// ring row of env e for this push (pos < cap, e < E <= cap)
+__device__ inline float *ring_row(const Tail &T, int e) {
+    int64_t row = T.pos + e;
+    if (row >= T.cap) row -= T.cap;
+    return T.ring + row * T.rw;
+}
+
 // LineString([p0,p1]).buffer(pB) meets one of the 4 infinite bound lines (ATT/env:2507)
 __device__ inline bool bound_crash(const Args &A, double x0, double y0, double x1, double y1) {
     return capsule_crash(A.pb, A.bound, x0, y0, x1, y1);
@@ -345,8 +375,15 @@ __device__ inline void load_maps(const Args &A) {
 
 // all radar rays of the workgroup's (active) agents: one work item per (agent, ray); rmin (variant
 // 1 step): each agent's smallest float64 distance, as an LDS atomic min on the (non-negative) bits
+// the fused step tail's late radar column (RingOut.ring null = none): ring row of env e, column col
+struct RingOut {
+    float *ring;
+    int64_t pos, cap;
+    int rw, col;
+};
+
 __device__ inline void radar_phase(const Args &A, Lds &S, int e0, int nagents, bool check_active,
-                                   const int32_t *emap = nullptr, bool rmin = false) {
+                                   const int32_t *emap = nullptr, bool rmin = false, RingOut ro = RingOut{}) {
     for (int w = threadIdx.x; w < nagents * NRAY; w += BLOCK) {
         const int la = w / NRAY, r = w - la * NRAY;
         const int le = la / A.N, i = la - le * A.N;
@@ -357,6 +394,11 @@ __device__ inline void radar_phase(const Args &A, Lds &S, int e0, int nagents, b
         const uint8_t *occ = s_maps + mi * A.gw * A.gh;
         const double d = radar_ray(A, S, i, r, le * A.N, occ, map_rows(A, mi));
         A.radar[((size_t)e * A.N + i) * NRAY + r] = (float)d;
+        if (ro.ring) {
+            int64_t row = ro.pos + e;
+            if (row >= ro.cap) row -= ro.cap;
+            ro.ring[row * ro.rw + ro.col + i * NRAY + r] = (float)d;
+        }
         if (rmin) atomicMin(&S.rmin[la], (unsigned long long)__double_as_longlong(d));
     }
 }
@@ -523,6 +565,225 @@ __device__ inline void store_rows(float *dst, const float *src, int n) {
     }
 }
 
+// ---------------------------------------------------------------------- reset / auto-reset
+// env slot lq of the workgroup: its entry of the packed list (emap) or the contiguous range
+__device__ inline int env_of(const int32_t *emap, int e0, int lq) { return emap ? emap[lq] : e0 + lq; }
+
+// The reset of the workgroup's envs with S.active[le] set (at least one): OD draw (bank mode) or the
+// given OD, waypoint lists, state, radar and observation rows.  Shared by reset_kernel and the fused
+// step tail (step_kernel<.., true>), which calls it after its replay push with the maps in LDS.
+__device__ __attribute__((always_inline)) void reset_body(const Args &A, const ResetArgs &R, Lds &S, const int32_t *emap,
+                                                          int e0, bool maps_loaded) {
+    const int N = A.N;
+    const int nag = A.epb * N;
+    const int t = threadIdx.x;
+    const int le = t / N, i = t - le * N;
+    const int e = env_of(emap, e0, le < A.epb ? le : 0);
+    const bool active = (t < nag) && (e < A.E) && S.active[le];
+    const int base = le * N;
+    const size_t ai = (size_t)e * N + i;
+    if (!maps_loaded) load_maps(A);
+    if (R.mode == 1) {
+        // draw N OD entries; starts pairwise > 2 pB apart (ATT/env:258-268).  One wave per
+        // resetting env: the 64 lanes test 64 consecutive attempts of agent a at once and the
+        // lowest valid attempt wins, i.e. exactly the sequential rule (first valid attempt, else
+        // the last of 4096).
+        const int lane = t & 63, wv = t >> 6;
+        for (int lq = wv; lq < A.epb; lq += BLOCK / 64) {
+            const int eq = env_of(emap, e0, lq);
+            if (eq >= A.E || !S.active[lq]) continue;
+            const int ep = R.episode[eq] + 1;
+            const int bq = lq * N;
+            // multipleMap variant: random_map_idx = random.randrange(len(world_map_2D_collection)) per
+            // episode (multipleMap/ma_main:464-465), then the OD from that map's bank
+            int mp = 0, boff = 0, bn = R.bank_n;
+            if (R.bank_maps > 1) {
+                mp = (int)(mix64(mix64(mix64(R.seed ^ 0x6d61705f64726177ull ^ (uint64_t)eq) ^ (uint64_t)ep)) %
+                           (uint64_t)R.bank_maps);
+                boff = R.bank_off[mp];
+                bn = R.bank_off[mp + 1] - boff;
+            }
+            for (int a = 0; a < N; ++a) {
+                int chosen = -1, last = 0, pl = 63;
+                double2 sp = make_double2(0.0, 0.0);
+                for (int att0 = 0; att0 < 4096 && chosen < 0; att0 += 64) {
+                    const int att = att0 + lane;
+                    const uint64_t key =
+                        mix64(mix64(mix64(R.seed ^ (uint64_t)eq) ^ (uint64_t)ep) ^ ((uint64_t)a * 65536ull + att));
+                    const int idx = boff + (int)(key % (uint64_t)bn);
+                    sp = R.bank_start[idx];
+                    bool ok = true;
+                    for (int b = 0; b < a; ++b) {
+                        const double2 o = S.ppos[bq + b];
+                        if (!(npnorm(sp.x - o.x, sp.y - o.y) > A.pb * 2)) ok = false;
+                    }
+                    const unsigned long long m = __ballot(ok);
+                    if (m) {
+                        pl = __ffsll((long long)m) - 1;
+                        chosen = __shfl(idx, pl, 64);
+                    }
+                    last = __shfl(idx, 63, 64);
+                }
+                const int pick = chosen >= 0 ? chosen : last;
+                // the chosen start from the lane that loaded it (no second dependent load)
+                const double spx = __shfl(sp.x, pl, 64), spy = __shfl(sp.y, pl, 64);
+                if (lane == 0) {
+                    S.idx[bq + a] = pick;
+                    S.ppos[bq + a] = make_double2(spx, spy);      // the chosen starts
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            }
+            if (lane == 0) {
+                R.episode[eq] = ep;
+                if (A.map_idx) A.map_idx[eq] = mp;
+            }
+        }
+    }
+    __syncthreads();
+    RSTAMP(2, __builtin_amdgcn_s_memtime());
+    // the waypoint lists, copied by all threads over (agent, waypoint) items: a thread copying its
+    // agent's W waypoints in a row waited for every load before the store that might alias it.  Bank
+    // mode: each item also loads its entry's waypoint count (beside the waypoint, no added latency),
+    // and the item holding the last waypoint puts the goal and the count in LDS for the state writes
+    // (they were two more dependent loads on the resetting workgroup's chain).
+    {
+        const int nw = nag * A.W;
+        for (int w0 = 0; w0 < nw; w0 += 4 * BLOCK) {
+            double2 v[4];
+            size_t dst[4];
+            bool ok[4];
+            int cn[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int w = w0 + u * BLOCK + t;
+                const int la = w / A.W, k = w - la * A.W, lq = la / N;
+                ok[u] = w < nw && S.active[lq < A.epb ? lq : 0] && env_of(emap, e0, lq < A.epb ? lq : 0) < A.E;
+                const size_t aq = ok[u] ? (size_t)env_of(emap, e0, lq) * N + (la - lq * N) : 0;
+                dst[u] = aq * A.W + k;
+                const int bi = (R.mode == 1 && ok[u]) ? S.idx[la] : 0;
+                v[u] = !ok[u] ? make_double2(0.0, 0.0)
+                              : (R.mode == 1 ? R.bank_wp[(size_t)bi * A.W + k] : R.wps[aq * A.W + k]);
+                cn[u] = (R.mode == 1 && ok[u]) ? R.bank_cnt[bi] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (ok[u]) A.wp[dst[u]] = v[u];
+                const int w = w0 + u * BLOCK + t;
+                const int la = w / A.W, k = w - la * A.W;
+                if (R.mode == 1 && ok[u] && k == cn[u] - 1) {
+                    S.goal[la] = v[u];
+                    S.rmin[la] = (unsigned long long)cn[u];
+                }
+            }
+        }
+    }
+    if (R.mode == 1) __syncthreads();     // goal / count of each drawn entry in LDS
+    if (active) {
+        double2 st, g;
+        int cnt;
+        if (R.mode == 1) {
+            st = S.ppos[t];        // the chosen start (draw above)
+            cnt = (int)S.rmin[t];
+            g = S.goal[t];
+        } else {
+            st = R.start[ai];
+            cnt = R.cnt[ai];
+            g = R.wps[ai * A.W + cnt - 1];
+            if (i == 0 && A.map_idx) A.map_idx[e] = R.map_idx ? R.map_idx[e] : 0;
+        }
+        A.goal[ai] = g;
+        const double2 z = make_double2(0.0, 0.0);
+        A.pos[ai] = st;
+        A.pre_pos[ai] = st;
+        A.start[ai] = st;
+        A.vel[ai] = z;
+        A.pre_vel[ai] = z;
+        A.wp_cnt[ai] = cnt;
+        A.wp_cur[ai] = 0;
+        A.reach[ai] = 0;
+        A.wall[ai] = 0;
+        if (i == 0) A.step[e] = 0;
+        S.pos[t] = st;
+        S.ppos[t] = st;
+        S.vel[t] = z;
+        S.pvel[t] = z;
+        S.goal[t] = g;
+    }
+    __syncthreads();   // map_idx (explicit or drawn) written above is read by the radar phase below
+    RSTAMP(3, __builtin_amdgcn_s_memtime());
+    radar_phase(A, S, e0, nag, true, emap);
+#ifdef AAC_ENV_STAMPS
+    __syncthreads();
+#endif
+    RSTAMP(4, __builtin_amdgcn_s_memtime());
+    if (active) observe_agent(A, S, e, i, base);
+#ifdef AAC_ENV_STAMPS
+    __syncthreads();
+#endif
+    RSTAMP(5, __builtin_amdgcn_s_memtime());
+    RSTAMP(6, __builtin_amdgcn_s_memrealtime());
+}
+
+// Fused step tail, part 1 (aac_env_step_tail): the early fields of the workgroup's nv transitions,
+// copied at kernel start.  Their descriptors and a compact-column -> field table go to LDS scratch
+// (the observation staging area, free until the observation phase) once per workgroup: looked up per
+// element from the kernel arguments, the descriptors were re-read with scalar loads for every element
+// (0.042 -> 0.075 ms per step at 4096 x 5).  Thread t owns the compact columns t, t + BLOCK, ...;
+// its items are (column, env) pairs with U loads in flight before the stores.
+struct TailDesc {
+    const void *src;
+    int width, shift;      // width | dtype << 30; shift = ring column - compact column
+};
+static_assert(sizeof(TailDesc) == 16, "one ds_read_b128 per descriptor");
+
+__device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, int e0, int nv, float *scratch) {
+    const int t = threadIdx.x;
+    TailDesc *desc = reinterpret_cast<TailDesc *>(scratch);
+    int *cum = reinterpret_cast<int *>(desc + TAIL_MAX_FIELDS);
+    uint8_t *lut = reinterpret_cast<uint8_t *>(cum + TAIL_MAX_FIELDS + 1);
+    const int ne = T.cum[T.nf];
+#pragma unroll
+    for (int q = 0; q < TAIL_MAX_FIELDS; ++q)
+        if (t == q) {
+            desc[q] = TailDesc{T.src[q], T.width[q] | (T.dtype[q] << 30), T.col[q] - T.cum[q]};
+            cum[q] = T.cum[q];
+        }
+    __syncthreads();
+    for (int k = t; k < ne; k += BLOCK) {
+        int f = 0;
+        for (int q = 1; q < T.nf; ++q) f += k >= cum[q];
+        lut[k] = (uint8_t)f;
+    }
+    __syncthreads();
+    const int ncol = t < ne ? (ne - t + BLOCK - 1) / BLOCK : 0;
+    const int items = ncol * nv;
+    constexpr int U = 8;
+    for (int j0 = 0; j0 < items; j0 += U) {
+        float v[U];
+        float *dst[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u;
+            const bool ok = j < items;
+            const int sl = j / nv, r = j - sl * nv;
+            const int k = ok ? t + sl * BLOCK : 0;
+            const int f = lut[k];
+            const TailDesc d = desc[f];
+            const int w = d.width & 0x3fffffff;
+            dst[u] = ok ? ring_row(T, e0 + r) + k + d.shift : nullptr;
+            const size_t si = (size_t)(e0 + r) * w + (k - cum[f]);
+            v[u] = !ok ? 0.f
+                       : ((d.width >> 30) ? (float)reinterpret_cast<const uint8_t *>(d.src)[si]
+                                          : reinterpret_cast<const float *>(d.src)[si]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (dst[u]) *dst[u] = v[u];
+    }
+    __syncthreads();      // the scratch area is the observation staging area of the step
+}
+
 // --------------------------------------------------------------------------------- step
 // Phases: (1) kinematics, one thread per agent; (2) radar, one work item per (agent, ray) over
 // all 256 threads; (3) observation + ss_reward predicates, one thread per agent; (4) team reward
@@ -530,8 +791,9 @@ __device__ inline void store_rows(float *dst, const float *src, int n) {
 // One instantiation per (env variant, radar mode): the other variant's reward code and the unused
 // radar path are compiled out, which keeps the kernel inside its 128-VGPR budget (the run-time
 // branches cost ~66 spilled VGPRs / 240 B of scratch per lane).
-template <int VAR, int RM>
-__global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain, const float2 *__restrict__ act) {
+template <int VAR, int RM, bool TAIL>
+__global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain, const float2 *__restrict__ act,
+                                                                         ResetArgs R, Tail T) {
     Args A = Ain;
     A.variant = VAR;
     A.radar_mode = RM;
@@ -549,6 +811,21 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     const size_t ai = (size_t)e * N + i;
     ESTAMP(0, __builtin_amdgcn_s_memrealtime());
     ESTAMP(1, __builtin_amdgcn_s_memtime());
+    const int nv = e0 + A.epb <= A.E ? A.epb : A.E - e0;     // envs of this workgroup
+    if (TAIL && t < A.epb) S.active[t] = 0;      // env_done of the workgroup's envs (set below)
+    RingOut ro{};
+    if constexpr (TAIL) {
+        if (T.ring) {
+            // replay push, early fields (sources of earlier launches); this step's outputs are written
+            // into the ring where they are produced (radar phase, staged rows, final phase)
+            if (blockIdx.x == 0 && t == 0) {
+                T.meta[0] = T.new_pos;
+                T.meta[1] = T.new_size;
+            }
+            tail_push_early(T, e0, nv, S.obs);
+            if (T.late[LATE_RADAR] >= 0) ro = RingOut{T.ring, T.pos, T.cap, T.rw, T.late[LATE_RADAR]};
+        }
+    }
     load_maps(A);
 
     // ---- a1: kinematics (ATT/env:2639-2713)
@@ -604,7 +881,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     aacw::lds_barrier();
     ESTAMP(2, __builtin_amdgcn_s_memtime());
 #ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
-    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0);
+    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro);
 #endif
     if (A.variant) {
         double2 *wc = wp_cache(A);
@@ -726,13 +1003,34 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     aacw::lds_barrier();
     ESTAMP(4, __builtin_amdgcn_s_memtime());
     if (stage) {      // the workgroup's rows are contiguous in own / nei: whole 16-B stores
-        const int nv = (e0 + A.epb <= A.E ? A.epb : A.E - e0) * N;
-        store_rows(A.own + (size_t)e0 * N * D0, S.obs, nv * D0);
-        store_rows(A.nei + (size_t)e0 * N * K6, S.obs + nag * D0, nv * K6);
+        store_rows(A.own + (size_t)e0 * N * D0, S.obs, nv * N * D0);
+        store_rows(A.nei + (size_t)e0 * N * K6, S.obs + nag * D0, nv * N * K6);
+        if constexpr (TAIL) {     // the same rows into the replay ring (next own / nei fields)
+            if (T.ring) {
+                const int wo = N * D0, wn = N * K6;
+                if (T.late[LATE_OWN] >= 0)
+                    for (int j = t; j < nv * wo; j += BLOCK) {
+                        const int r = j / wo;
+                        ring_row(T, e0 + r)[T.late[LATE_OWN] + (j - r * wo)] = S.obs[j];
+                    }
+                if (T.late[LATE_NEI] >= 0)
+                    for (int j = t; j < nv * wn; j += BLOCK) {
+                        const int r = j / wn;
+                        ring_row(T, e0 + r)[T.late[LATE_NEI] + (j - r * wn)] = S.obs[nag * D0 + j];
+                    }
+            }
+        }
     }
     if (active) {
         double team = A.team_reward ? pairwise_sum(&S.rew[base], N) : S.rew[t];
         A.reward[ai] = (float)team;
+        if constexpr (TAIL) {
+            if (T.ring) {
+                float *rr = ring_row(T, e);
+                if (T.late[LATE_REW] >= 0) rr[T.late[LATE_REW] + i] = (float)team;
+                if (T.late[LATE_DONE] >= 0) rr[T.late[LATE_DONE] + i] = (float)(S.flags[t] & 1);
+            }
+        }
         if (i == 0) {
             int any_done = 0, all_goal = 1, all_reach = 1, b0 = 0, b2 = 0, b3 = 0;
             for (int j = 0; j < N; ++j) {
@@ -752,14 +1050,33 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             A.bbc[4 * e + 3] = (uint8_t)(A.variant ? 0 : b3);
             int st = A.step[e] + 1;
             A.step[e] = st;
-            A.env_done[e] = (uint8_t)((A.episode_length < st) || any_done || all_goal || all_reach);
+            const uint8_t ed = (uint8_t)((A.episode_length < st) || any_done || all_goal || all_reach);
+            A.env_done[e] = ed;
+            if (TAIL) S.active[le] = ed;
+        }
+    }
+    if constexpr (TAIL) {
+        // after the step (whose transitions are in the ring already): zero the given rows of the
+        // finished envs and reset them (aac_env_step_tail = step + replay push + row zeroing +
+        // auto-reset, in that order)
+        __syncthreads();      // env_done flags; the staged rows' ring copies have read S.obs
+        int any = 0;
+        for (int k = 0; k < A.epb; ++k) any |= S.active[k];
+        if (any) {
+            if (T.zero_rows) {
+                const int n = nv * T.zero_w;
+                for (int j = t; j < n; j += BLOCK) {
+                    const int r = j / T.zero_w;
+                    if (S.active[r]) T.zero_rows[(size_t)e0 * T.zero_w + j] = 0.f;
+                }
+            }
+            if (T.reset) reset_body(A, R, S, nullptr, e0, true);
         }
     }
     ESTAMP(5, __builtin_amdgcn_s_memtime());
     ESTAMP(6, __builtin_amdgcn_s_memrealtime());
 }
 
-// ---------------------------------------------------------------------- reset / auto-reset
 __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     __shared__ Lds S;
     const int N = A.N;
@@ -790,133 +1107,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
     }
     RSTAMP(0, __builtin_amdgcn_s_memrealtime());
     RSTAMP(1, __builtin_amdgcn_s_memtime());
-    const int le = t / N, i = t - le * N;
-    const int e = emap[le < A.epb ? le : 0];
-    const bool active = (t < nag) && (e < A.E) && S.active[le];
-    const int base = le * N;
-    const size_t ai = (size_t)e * N + i;
-    load_maps(A);
-    if (R.mode == 1) {
-        // draw N OD entries; starts pairwise > 2 pB apart (ATT/env:258-268).  One wave per
-        // resetting env: the 64 lanes test 64 consecutive attempts of agent a at once and the
-        // lowest valid attempt wins, i.e. exactly the sequential rule (first valid attempt, else
-        // the last of 4096).
-        const int lane = t & 63, wv = t >> 6;
-        for (int lq = wv; lq < A.epb; lq += BLOCK / 64) {
-            const int eq = emap[lq];
-            if (eq >= A.E || !S.active[lq]) continue;
-            const int ep = R.episode[eq] + 1;
-            const int bq = lq * N;
-            // multipleMap variant: random_map_idx = random.randrange(len(world_map_2D_collection)) per
-            // episode (multipleMap/ma_main:464-465), then the OD from that map's bank
-            int mp = 0, boff = 0, bn = R.bank_n;
-            if (R.bank_maps > 1) {
-                mp = (int)(mix64(mix64(mix64(R.seed ^ 0x6d61705f64726177ull ^ (uint64_t)eq) ^ (uint64_t)ep)) %
-                           (uint64_t)R.bank_maps);
-                boff = R.bank_off[mp];
-                bn = R.bank_off[mp + 1] - boff;
-            }
-            for (int a = 0; a < N; ++a) {
-                int chosen = -1, last = 0;
-                for (int att0 = 0; att0 < 4096 && chosen < 0; att0 += 64) {
-                    const int att = att0 + lane;
-                    const uint64_t key =
-                        mix64(mix64(mix64(R.seed ^ (uint64_t)eq) ^ (uint64_t)ep) ^ ((uint64_t)a * 65536ull + att));
-                    const int idx = boff + (int)(key % (uint64_t)bn);
-                    const double2 sp = R.bank_start[idx];
-                    bool ok = true;
-                    for (int b = 0; b < a; ++b) {
-                        const double2 o = S.ppos[bq + b];
-                        if (!(npnorm(sp.x - o.x, sp.y - o.y) > A.pb * 2)) ok = false;
-                    }
-                    const unsigned long long m = __ballot(ok);
-                    if (m) chosen = __shfl(idx, __ffsll((long long)m) - 1, 64);
-                    last = __shfl(idx, 63, 64);
-                }
-                const int pick = chosen >= 0 ? chosen : last;
-                if (lane == 0) {
-                    S.idx[bq + a] = pick;
-                    S.ppos[bq + a] = R.bank_start[pick];      // scratch: chosen starts
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            }
-            if (lane == 0) {
-                R.episode[eq] = ep;
-                if (A.map_idx) A.map_idx[eq] = mp;
-            }
-        }
-    }
-    __syncthreads();
-    RSTAMP(2, __builtin_amdgcn_s_memtime());
-    // the waypoint lists, copied by all threads over (agent, waypoint) items: a thread copying its
-    // agent's W waypoints in a row waited for every load before the store that might alias it
-    {
-        const int nw = nag * A.W;
-        for (int w0 = 0; w0 < nw; w0 += 4 * BLOCK) {
-            double2 v[4];
-            size_t dst[4];
-            bool ok[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int w = w0 + u * BLOCK + t;
-                const int la = w / A.W, k = w - la * A.W, lq = la / N;
-                ok[u] = w < nw && S.active[lq < A.epb ? lq : 0] && emap[lq < A.epb ? lq : 0] < A.E;
-                const size_t aq = ok[u] ? (size_t)emap[lq] * N + (la - lq * N) : 0;
-                dst[u] = aq * A.W + k;
-                v[u] = !ok[u] ? make_double2(0.0, 0.0)
-                              : (R.mode == 1 ? R.bank_wp[(size_t)S.idx[la] * A.W + k] : R.wps[aq * A.W + k]);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (ok[u]) A.wp[dst[u]] = v[u];
-        }
-    }
-    if (active) {
-        double2 st, g;
-        int cnt;
-        if (R.mode == 1) {
-            int idx = S.idx[base + i];
-            st = R.bank_start[idx];
-            cnt = R.bank_cnt[idx];
-            g = R.bank_wp[(size_t)idx * A.W + cnt - 1];
-        } else {
-            st = R.start[ai];
-            cnt = R.cnt[ai];
-            g = R.wps[ai * A.W + cnt - 1];
-            if (i == 0 && A.map_idx) A.map_idx[e] = R.map_idx ? R.map_idx[e] : 0;
-        }
-        A.goal[ai] = g;
-        const double2 z = make_double2(0.0, 0.0);
-        A.pos[ai] = st;
-        A.pre_pos[ai] = st;
-        A.start[ai] = st;
-        A.vel[ai] = z;
-        A.pre_vel[ai] = z;
-        A.wp_cnt[ai] = cnt;
-        A.wp_cur[ai] = 0;
-        A.reach[ai] = 0;
-        A.wall[ai] = 0;
-        if (i == 0) A.step[e] = 0;
-        S.pos[t] = st;
-        S.ppos[t] = st;
-        S.vel[t] = z;
-        S.pvel[t] = z;
-        S.goal[t] = g;
-    }
-    __syncthreads();   // map_idx (explicit or drawn) written above is read by the radar phase below
-    RSTAMP(3, __builtin_amdgcn_s_memtime());
-    radar_phase(A, S, e0, nag, true, emap);
-#ifdef AAC_ENV_STAMPS
-    __syncthreads();
-#endif
-    RSTAMP(4, __builtin_amdgcn_s_memtime());
-    if (active) observe_agent(A, S, e, i, base);
-#ifdef AAC_ENV_STAMPS
-    __syncthreads();
-#endif
-    RSTAMP(5, __builtin_amdgcn_s_memtime());
-    RSTAMP(6, __builtin_amdgcn_s_memrealtime());
+    reset_body(A, R, S, emap, e0, false);
 }
 
 // ordered list of the done envs for the packed auto-reset (aacw::compact_flags)
@@ -1029,6 +1220,20 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
     return A;
 }
 
+static ResetArgs bank_reset_args(const aac_env *h) {
+    ResetArgs R{};
+    R.mode = 1;
+    R.bank_start = h->bank_start;
+    R.bank_wp = h->bank_wp;
+    R.bank_cnt = h->bank_cnt;
+    R.bank_n = h->bank_n;
+    R.bank_off = h->bank_off;
+    R.bank_maps = h->bank_maps;
+    R.seed = h->bank_seed;
+    R.episode = h->episode;
+    return R;
+}
+
 extern "C" {
 
 const char *aac_last_error(void) { return g_err.c_str(); }
@@ -1121,7 +1326,8 @@ static int check_out(const aac_step_out *o) {
     return AAC_OK;
 }
 
-int aac_env_step(aac_env *h, const float *actions, const aac_step_out *o, void *stream) {
+static int launch_step(aac_env *h, const float *actions, const aac_step_out *o, const ResetArgs &R, const Tail &T,
+                       bool tail, void *stream) {
     if (!h || !actions) return fail(AAC_E_INVALID, "null argument");
     int rc = check_out(o);
     if (rc) return rc;
@@ -1132,12 +1338,98 @@ int aac_env_step(aac_env *h, const float *actions, const aac_step_out *o, void *
     if (A.variant) lds = ((lds + 15) & ~(size_t)15) + sizeof(double2) * WPC * (size_t)h->epb * h->cfg.N;
     const hipStream_t st = (hipStream_t)stream;
     const float2 *a2 = reinterpret_cast<const float2 *>(actions);
-    if (A.variant) hipLaunchKernelGGL((step_kernel<1, AAC_RADAR_OBSTACLES>), grid, block, lds, st, A, a2);
-    else if (A.radar_mode == AAC_RADAR_DRONES) hipLaunchKernelGGL((step_kernel<0, AAC_RADAR_DRONES>), grid, block, lds, st, A, a2);
-    else if (A.radar_mode == AAC_RADAR_OBSTACLES) hipLaunchKernelGGL((step_kernel<0, AAC_RADAR_OBSTACLES>), grid, block, lds, st, A, a2);
-    else hipLaunchKernelGGL((step_kernel<0, AAC_RADAR_COMBINED>), grid, block, lds, st, A, a2);
+#define STEP_LAUNCH(V, M)                                                                                        \
+    do {                                                                                                         \
+        if (tail) hipLaunchKernelGGL((step_kernel<V, M, true>), grid, block, lds, st, A, a2, R, T);              \
+        else hipLaunchKernelGGL((step_kernel<V, M, false>), grid, block, lds, st, A, a2, R, T);                  \
+    } while (0)
+    if (A.variant) STEP_LAUNCH(1, AAC_RADAR_OBSTACLES);
+    else if (A.radar_mode == AAC_RADAR_DRONES) STEP_LAUNCH(0, AAC_RADAR_DRONES);
+    else if (A.radar_mode == AAC_RADAR_OBSTACLES) STEP_LAUNCH(0, AAC_RADAR_OBSTACLES);
+    else STEP_LAUNCH(0, AAC_RADAR_COMBINED);
+#undef STEP_LAUNCH
     HIPCHK(hipGetLastError());
     return AAC_OK;
+}
+
+int aac_env_step(aac_env *h, const float *actions, const aac_step_out *o, void *stream) {
+    return launch_step(h, actions, o, ResetArgs{}, Tail{}, false, stream);
+}
+
+int aac_env_step_tail(aac_env *h, const float *actions, const aac_step_out *o, const aac_step_tail *t,
+                      void *stream) {
+    if (!h || !t) return fail(AAC_E_INVALID, "null argument");
+    Tail T{};
+    ResetArgs R{};
+    if (t->ring) {
+        const int n = t->n_fields;
+        if (n < 1 || n > TAIL_MAX_FIELDS || !t->srcs || !t->widths) return fail(AAC_E_INVALID, "step tail: 1..12 push fields");
+        if (t->capacity < h->cfg.E || t->row_width < 1 || !t->meta)
+            return fail(AAC_E_INVALID, "step tail: need E <= capacity, row_width >= 1 and meta");
+        if (t->pos < 0 || t->pos >= t->capacity || t->size < 0 || t->size > t->capacity)
+            return fail(AAC_E_INVALID, "step tail: need 0 <= pos < capacity, size <= capacity");
+        if (!o) return fail(AAC_E_INVALID, "null argument");
+        T.ring = t->ring;
+        T.rw = t->row_width;
+        T.cap = t->capacity;
+        T.pos = t->pos;
+        T.meta = t->meta;
+        T.new_pos = (t->pos + h->cfg.E) % t->capacity;
+        T.new_size = std::min<int64_t>(t->size + h->cfg.E, t->capacity);
+        for (int k = 0; k < LATE_N; ++k) T.late[k] = -1;
+        // a field whose source is one of this step's outputs is written where the step computes it
+        const int N = h->cfg.N, K = h->K;
+        const void *outs[LATE_N] = {o->own, o->radar, o->nei, o->reward, o->done};
+        const int ow[LATE_N] = {N * h->D0, N * NRAY, N * K * 6, N, N};
+        const int odt[LATE_N] = {0, 0, 0, 0, 1};
+        int col = 0, ne = 0;
+        T.cum[0] = 0;
+        for (int f = 0; f < n; ++f) {
+            const int w = t->widths[f], dt = t->dtypes ? t->dtypes[f] : 0;
+            if (!t->srcs[f] || w < 1) return fail(AAC_E_INVALID, "step tail: null source or width < 1");
+            if (dt != 0 && dt != 1) return fail(AAC_E_INVALID, "step tail: dtype 0 (f32) or 1 (u8)");
+            int role = -1;
+            for (int k = 0; k < LATE_N; ++k)
+                if (t->srcs[f] == outs[k]) role = k;
+            if (role >= 0) {
+                if (w != ow[role] || dt != odt[role] || T.late[role] >= 0)
+                    return fail(AAC_E_INVALID, "step tail: a step-output field must have its output's width and dtype");
+                T.late[role] = col;
+            } else {
+                T.src[T.nf] = t->srcs[f];
+                T.width[T.nf] = w;
+                T.dtype[T.nf] = dt;
+                T.col[T.nf] = col;
+                ne += w;
+                T.cum[++T.nf] = ne;
+            }
+            col += w;
+        }
+        if (col != T.rw) return fail(AAC_E_INVALID, "step tail: field widths must sum to row_width");
+        for (int q = T.nf; q < TAIL_MAX_FIELDS; ++q) {     // unused descriptor slots: harmless values
+            T.src[q] = t->srcs[0];
+            T.width[q] = 1;
+            T.dtype[q] = 0;
+            T.col[q] = 0;
+            T.cum[q + 1] = ne;
+        }
+        if (sizeof(TailDesc) * TAIL_MAX_FIELDS + sizeof(int) * (TAIL_MAX_FIELDS + 1) + ne > sizeof(float) * OBS_STAGE_FLOATS)
+            return fail(AAC_E_INVALID, "step tail: too many early columns for the column table");
+        if ((T.late[LATE_OWN] >= 0 || T.late[LATE_NEI] >= 0) &&
+            h->epb * h->cfg.N * (h->D0 + 6 * K) > OBS_STAGE_FLOATS)
+            return fail(AAC_E_INVALID, "step tail: observation rows too wide to push from the staging area");
+    }
+    if (t->zero_rows) {
+        if (t->zero_width < 1) return fail(AAC_E_INVALID, "step tail: zero_width >= 1");
+        T.zero_rows = t->zero_rows;
+        T.zero_w = t->zero_width;
+    }
+    if (t->auto_reset) {
+        if (!h->bank_n) return fail(AAC_E_STATE, "no OD bank installed (aac_env_set_od_bank)");
+        R = bank_reset_args(h);
+        T.reset = 1;
+    }
+    return launch_step(h, actions, o, R, T, true, stream);
 }
 
 int aac_env_reset(aac_env *h, const uint8_t *mask, const double *start, const double *wps, const int32_t *cnt,
@@ -1203,17 +1495,8 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
     int rc = check_out(o);
     if (rc) return rc;
     Args A = make_args(h, o);
-    ResetArgs R{};
-    R.mode = 1;
+    ResetArgs R = bank_reset_args(h);
     R.mask = env_done;
-    R.bank_start = h->bank_start;
-    R.bank_wp = h->bank_wp;
-    R.bank_cnt = h->bank_cnt;
-    R.bank_n = h->bank_n;
-    R.bank_off = h->bank_off;
-    R.bank_maps = h->bank_maps;
-    R.seed = h->bank_seed;
-    R.episode = h->episode;
     const bool packed = g_env_compact < 0 ? h->cfg.variant != 0 : g_env_compact != 0;
     if (env_done && packed) {
         hipLaunchKernelGGL(env_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, env_done, h->cfg.E,

@@ -172,6 +172,32 @@ class BatchedEnv:
         _native.check(_native.lib().aac_env_step(self._h, _ptr(a), ctypes.byref(o), _stream()), "aac_env_step")
         return out
 
+    def step_tail(self, actions, out: Optional[StepBuffers] = None, replay=None, srcs=None, zero_rows=None,
+                  auto_reset=True):
+        """``step`` + ``replay.push_batch(*srcs)`` + zeroing ``zero_rows`` ([E][...] float32) of the
+        finished envs + ``auto_reset(out.env_done, out)``, fused into the one step launch
+        (aac_env_step_tail).  ``srcs`` may name this step's outputs (``out.reward`` ...): the push reads
+        the terminal rows before the reset overwrites them.  Same results as the four calls."""
+        out = out or self.bufs
+        a = actions
+        if a.dtype != torch.float32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        assert a.shape == (self.E, self.N, 2), a.shape
+        t = _native.StepTail()
+        if replay is not None:
+            for k, v in replay.tail_push(srcs, self.E).items():
+                setattr(t, k, v)
+        if zero_rows is not None:
+            assert zero_rows.dtype == torch.float32 and zero_rows.is_contiguous() and zero_rows.shape[0] == self.E
+            assert zero_rows.device == self.device
+            t.zero_rows = zero_rows.data_ptr()
+            t.zero_width = zero_rows.numel() // self.E
+        t.auto_reset = int(bool(auto_reset))
+        o = out.c_struct()
+        _native.check(_native.lib().aac_env_step_tail(self._h, _ptr(a), ctypes.byref(o), ctypes.byref(t), _stream()),
+                      "aac_env_step_tail")
+        return out
+
     def set_od_bank(self, bank, seed=0):
         """Install the device OD bank for auto-reset: a ``world.ODBank`` (one map), or a
         ``world.MapBanks`` for a map stack (each auto-reset draws the env's map, then its OD)."""

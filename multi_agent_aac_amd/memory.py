@@ -13,6 +13,7 @@ position / size and the RNG counter live in device memory).
 ``ReplayMemory`` keeps the reference's ``push(*8 fields)`` / ``sample(B)`` / ``len`` surface for
 an unchanged ``ma_main`` (E = 1); its rows land in the same device ring.
 """
+import ctypes
 from collections import namedtuple
 
 import numpy as np
@@ -66,6 +67,25 @@ class DeviceReplay:
         ops.replay_push_at(self.ring, self.meta, self.pos, self.size, srcs, self.widths, self.dtypes, E)
         self.pos = (self.pos + E) % self.capacity
         self.size = min(self.size + E, self.capacity)
+
+    def tail_push(self, srcs, E):
+        """The push of ``push_batch(*srcs)`` as the replay part of a fused env step tail
+        (``BatchedEnv.step_tail``, aac_env_step_tail): returns the aac_step_tail fields and advances
+        the host mirror of the ring position (the launch advances ``meta``)."""
+        if self.H:
+            assert len(srcs) == 11, "this replay stores hidden states"
+        else:
+            assert len(srcs) == 9
+        for t in srcs:
+            assert t.is_contiguous() and t.device == self.device and t.shape[0] == E
+        n = len(srcs)
+        d = dict(ring=self.ring.data_ptr(), row_width=self.row_width, capacity=self.capacity, pos=self.pos,
+                 size=self.size, meta=self.meta.data_ptr(), n_fields=n,
+                 srcs=(ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs]),
+                 widths=(ctypes.c_int32 * n)(*self.widths[:n]), dtypes=(ctypes.c_int32 * n)(*self.dtypes[:n]))
+        self.pos = (self.pos + E) % self.capacity
+        self.size = min(self.size + E, self.capacity)
+        return d
 
     def check_sample(self, B):
         """random.sample semantics need at least B stored rows (the reference guards with

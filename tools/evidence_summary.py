@@ -99,6 +99,7 @@ def main():
             traffic(fd, wd, "::step_kernel", "median",
                     {"envs": c["envs_per_gpu"] if "envs_per_gpu" in c else c.get("envs"), "agents": c.get("agents"),
                      "radar": radar, "variant": variant, "maps": c.get("maps", 1),
+                     "tail": "aac_env_step_tail" in er["kernel"],
                      "algorithmic_bytes_per_launch": int(er["bytes_per_agent_step"] * er["agents_per_launch"])},
                     names)
         from bench import env_bytes_per_agent_step     # noqa: E402  (ATT env, N = 5)
