@@ -204,10 +204,21 @@ typedef struct {
     const float *cW, *cb;
     float *cf;
     int32_t c_rows, c_n;
+    /* optional (o_h != NULL): the actor's tanh output layer (ATT/nets:213) folded into the riding
+     * job -- the action columns of its input rows are computed first, a_j = tanh(o_h[(b*c_n + n)*256] .
+     * o_w[j*256] + o_b[j]) for j < 2, stored to o_x + b*cx_ld + n*c_din + o_d0 + j (o_x = the
+     * writable view of cx) and used as the encoder's inputs.  The output layer's launch disappears. */
+    const float *o_h, *o_w, *o_b;
+    float *o_x;
+    int32_t o_d0;
 } aac_attn_enc_args;
 /* nset = 1 or 2 independent argument sets in one launch (e.g. the target actor's inference pass
  * beside a training forward; K <= 8 each). */
 int aac_attn_enc_fwd(const aac_attn_enc_args *args, int32_t nset, void *stream);
+/* The same launch with a critic-head job (no chained head) appended as extra workgroups (four rows
+ * each; the arithmetic of aac_critic_head); head may be NULL.  The job must not read what the sets
+ * write, nor the sets what the job writes. */
+int aac_attn_enc_fwd_head(const aac_attn_enc_args *args, int32_t nset, const aac_head_job *head, void *stream);
 
 /* Replay gather with interleaved destinations: element c of field f of sampled row b goes to
  * dsts[f][b*(widths[f]/chunks[f])*dstrides[f] + (c/chunks[f])*dstrides[f] + c%chunks[f]]

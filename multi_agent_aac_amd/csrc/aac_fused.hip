@@ -1858,6 +1858,49 @@ __device__ void critic_enc_rows(const aac_attn_enc_args &A, int job, float *smem
     stage_w_load(gw, A.cW + (size_t)ag * 128 * Din, 128 * Din);
     stage_r_load(gx, A.cx + (size_t)r0 * A.cx_ld + (size_t)ag * Din, A.cx_ld, Din, A.c_rows - r0);
     const float bias = A.cb[ag * 128 + (threadIdx.x & 127)];
+    if (A.o_h) {
+        // the actor's output layer folded in: lanes (row rr, c) take columns 16 c .. 16 c + 15 of the
+        // 256-wide ha row, a 16-lane butterfly sums them (every lane of the row gets the same total),
+        // and the lanes that stage the two action columns put tanh(. + b) in their staged values
+        const int rr = threadIdx.x >> 4, c = threadIdx.x & 15, r = r0 + rr;
+        const bool rok = r < A.c_rows;
+        const f4 *hp = reinterpret_cast<const f4 *>(A.o_h + ((size_t)(rok ? r : 0) * A.c_n + ag) * 256 + 16 * c);
+        const f4 *w0 = reinterpret_cast<const f4 *>(A.o_w + 16 * c), *w1 = reinterpret_cast<const f4 *>(A.o_w + 256 + 16 * c);
+        f4 hv[4], wa[4], wb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            hv[q] = hp[q];
+            wa[q] = w0[q];
+            wb[q] = w1[q];
+        }
+        const float b0 = A.o_b[0], b1 = A.o_b[1];
+        float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                p0 = fmaf(hv[q][t], wa[q][t], p0);
+                p1 = fmaf(hv[q][t], wb[q][t], p1);
+            }
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) {
+            p0 += __shfl_xor(p0, o, 16);
+            p1 += __shfl_xor(p1, o, 16);
+        }
+        const float a0 = tanhf(p0 + b0), a1 = tanhf(p1 + b1);
+        const int d0 = A.o_d0;
+#pragma unroll
+        for (int u = 0; u < (ENC_SMAX + 15) / 16; ++u) {
+            const int k = c + 16 * u;
+            if (rok && k == d0) gx.v[u] = a0;
+            if (rok && k == d0 + 1) gx.v[u] = a1;
+        }
+        if (rok && c == 0) {
+            float *xo = A.o_x + (size_t)r * A.cx_ld + (size_t)ag * Din + d0;
+            xo[0] = a0;
+            xo[1] = a1;
+        }
+    }
     stage_w_store(gw, sW, Din, Dp, 128);
     stage_r_store(gx, sx, Dp);
     if (threadIdx.x < 128) sb[threadIdx.x] = bias;
@@ -1878,6 +1921,8 @@ struct AttnEncBatch {
     aac_attn_enc_args a[2];
     int start[2], nattn[2], nride[2];
     int nset;
+    int hstart;               // workgroups >= hstart run the critic-head job (INT_MAX: none)
+    HeadJob hj;
 };
 
 // LDS (floats): encoder weights | region U (the block's staged input rows, later sQ + sQK) | sE (later
@@ -1898,6 +1943,11 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
     using L = AttnEncLds<KM>;
     __shared__ f4 smem4[L::TOTAL / 4];
     float *smem = reinterpret_cast<float *>(smem4);
+    if ((int)blockIdx.x >= P.hstart) {       // the riding critic-head job (copied by value: static indices)
+        const HeadJob J = P.hj;
+        head_rows<false>(J, blockIdx.x - P.hstart);
+        return;
+    }
     const int s = (P.nset > 1 && (int)blockIdx.x >= P.start[1]) ? 1 : 0;
     const aac_attn_enc_args &A = P.a[s];
     const int nattn = P.nattn[s];
@@ -2624,10 +2674,17 @@ static int attn_enc_check(const aac_attn_enc_args &A) {
     if (A.c_rows > 0 && (!A.cx || !A.cW || !A.cb || !A.cf || A.c_n < 1 || A.c_din < 1 || A.c_din > ENC_DMAX ||
                          !aligned16(A.cf)))
         return ffail("attn_enc_fwd: critic-encoder job operands (c_din <= 40, 16-B aligned cf)");
+    if (A.c_rows > 0 && A.o_h && (!A.o_w || !A.o_b || !A.o_x || A.o_d0 < 0 || A.o_d0 + 2 > A.c_din ||
+                                  !aligned16(A.o_h) || !aligned16(A.o_w)))
+        return ffail("attn_enc_fwd: folded output layer (16-B aligned o_h / o_w, o_d0 + 2 <= c_din)");
     return 0;
 }
 
 int aac_attn_enc_fwd(const aac_attn_enc_args *args, int32_t nset, void *stream) {
+    return aac_attn_enc_fwd_head(args, nset, nullptr, stream);
+}
+
+int aac_attn_enc_fwd_head(const aac_attn_enc_args *args, int32_t nset, const aac_head_job *head, void *stream) {
     if (!args || nset < 1 || nset > 2) return ffail("attn_enc_fwd: 1 or 2 argument sets");
     AttnEncBatch P{};
     P.nset = nset;
@@ -2640,6 +2697,14 @@ int aac_attn_enc_fwd(const aac_attn_enc_args *args, int32_t nset, void *stream) 
         P.nride[s] = args[s].c_rows > 0 ? args[s].c_n * ((args[s].c_rows + 15) / 16) : 0;
         total += P.nattn[s] + P.nride[s];
         if (args[s].R > 0 && args[s].K > kmax) kmax = args[s].K;
+    }
+    P.hstart = INT_MAX;
+    if (head) {
+        if (head_check(*head)) return -1;
+        if (head->M2 > 0) return ffail("attn_enc_fwd_head: a chained head job runs alone (aac_critic_head_job)");
+        P.hj = head_job(*head);
+        P.hstart = total;
+        total += (std::max(head->M, 0) + 3) / 4;
     }
     if (total == 0) return 0;
     const dim3 g(total), b(256);

@@ -58,7 +58,8 @@ class AttnEncArgs(ctypes.Structure):
                 ("Wo", vp), ("bo", vp), ("Wg", vp), ("bg", vp), ("Wn", vp), ("bn", vp), ("Wq", vp), ("Wk", vp),
                 ("Wv", vp), ("cat", vp), ("ld_cat", i32), ("xn", vp), ("q", vp), ("qk", vp), ("alpha", vp),
                 ("xb", vp), ("R", i32), ("K", i32), ("cx", vp), ("cx_ld", i32), ("c_din", i32), ("cW", vp),
-                ("cb", vp), ("cf", vp), ("c_rows", i32), ("c_n", i32)]
+                ("cb", vp), ("cf", vp), ("c_rows", i32), ("c_n", i32), ("o_h", vp), ("o_w", vp), ("o_b", vp),
+                ("o_x", vp), ("o_d0", i32)]
 
 
 GEMM_MAX = 16
@@ -89,6 +90,7 @@ def lib():
         L.aac_attn_train_bwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, i32, i32,
                                          vp]
         L.aac_attn_enc_fwd.argtypes = [ctypes.POINTER(AttnEncArgs), i32, vp]
+        L.aac_attn_enc_fwd_head.argtypes = [ctypes.POINTER(AttnEncArgs), i32, ctypes.POINTER(HeadJob), vp]
         L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         _L = L
     return _L
@@ -172,18 +174,21 @@ class GemmLaunch:
 
 
 class AttnEnc:
-    """One aac_attn_enc_fwd launch over one or two independent argument sets (AttnEncArgs)."""
+    """One aac_attn_enc_fwd launch over one or two independent argument sets (AttnEncArgs), with an
+    optional critic-head job (HeadJob, no chained head) as extra workgroups (aac_attn_enc_fwd_head)."""
 
-    def __init__(self, *sets):
+    def __init__(self, *sets, head=None):
         assert 1 <= len(sets) <= 2
         self.n = len(sets)
         self.arr = (AttnEncArgs * self.n)(*sets)
+        self.head = head
 
     def __call__(self):
-        _chk(lib().aac_attn_enc_fwd(self.arr, self.n, _stream()), "aac_attn_enc_fwd")
+        h = ctypes.byref(self.head) if self.head is not None else None
+        _chk(lib().aac_attn_enc_fwd_head(self.arr, self.n, h, _stream()), "aac_attn_enc_fwd_head")
 
 
-_RIDE = ("cx", "cx_ld", "c_din", "cW", "cb", "cf", "c_rows", "c_n")
+_RIDE = ("cx", "cx_ld", "c_din", "cW", "cb", "cf", "c_rows", "c_n", "o_h", "o_w", "o_b", "o_x", "o_d0")
 
 
 def attn_set(ap, own, ld_own, d_own, radar, nei, R, K, cat, acts=None, ride=None):
@@ -208,11 +213,18 @@ def with_ride(a, ride):
     return b
 
 
-def critic_enc_ride(cp, X, rows, N, Din, f):
+def critic_enc_ride(cp, X, rows, N, Din, f, fold=None):
     """The critic's per-agent encoders f[b][n*128:(n+1)*128] = relu(enc_n X[b][n]) (ATT/nets:697-701,
-    R3) as a riding job of an aac_attn_enc_fwd launch (the per-agent weights are consecutive)."""
-    return {"cx": X, "cx_ld": N * Din, "c_din": Din, "cW": cp.enc_w[0], "cb": cp.enc_b[0], "cf": ptr(f),
-            "c_rows": rows, "c_n": N}
+    R3) as a riding job of an aac_attn_enc_fwd launch (the per-agent weights are consecutive).
+    ``fold`` = (ha, ap, d0): the actor's tanh output layer (ATT/nets:213) over the actor rows
+    ha[b*N + n] is computed inside the job and its actions land in X[b][n][d0:d0+2] (no launch of
+    its own)."""
+    r = {"cx": X, "cx_ld": N * Din, "c_din": Din, "cW": cp.enc_w[0], "cb": cp.enc_b[0], "cf": ptr(f),
+         "c_rows": rows, "c_n": N, "o_h": 0, "o_w": 0, "o_b": 0, "o_x": 0, "o_d0": 0}
+    if fold is not None:
+        ha, ap, d0 = fold
+        r.update(o_h=ha, o_w=ap.Wa, o_b=ap.ba, o_x=X, o_d0=d0)
+    return r
 
 
 def ride_only(ride):
@@ -546,9 +558,12 @@ class FusedUpdate:
         dsts2 = [ptr(self.X2)] + [None] * 8
         self.pre.append(lambda: gather_strided(rep.ring, self.idx, dsts, w, chunks, strides, dsts2=dsts2))
         Bt = nb * B
-        t_attn, t_merge, t_out = actor_infer_stages(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar),
-                                                    ptr(self.nnei), Bt * N, K, D0, ptr(self.Xt, D0), Din)
-        t_cenc, t_comb = critic_forward_stages(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
+        # the target actor's output layer is folded into the target critic's encoder job (its actions
+        # land in Xt's action columns there)
+        t_attn, t_merge, _ = actor_infer_stages(At, self.acts_t, ptr(self.Xt), Din, ptr(self.nradar),
+                                                ptr(self.nnei), Bt * N, K, D0, ptr(self.Xt, D0), Din)
+        _, t_comb = critic_forward_stages(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
+        t_cenc = critic_enc_ride(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, fold=(ptr(self.acts_t.ha), At, D0))
         t_head = lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),  # noqa: E731
                                      done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y))
         self.segs = None
@@ -558,18 +573,18 @@ class FusedUpdate:
             # step 0's forward and the actor forward 0 (current weights, their own buffers) share its
             # launches up to the point where the critic step needs the targets y
             cs0 = self._critic_stages(0, C, self.cbuf[1])
-            a0_attn, a0_merge, a0_out = self._actor_fwd_stages(0, A)
+            a0_attn, a0_merge = self._actor_fwd_stages(0, A)
             self.pre += [AttnEnc(with_ride(t_attn, cs0["enc"]), a0_attn)]
-            self.pre += gemm_launches(t_merge + cs0["comb"] + a0_merge) + gemm_launches(t_out + a0_out)
+            self.pre += gemm_launches(t_merge + cs0["comb"] + a0_merge)
             # the TD target of all batches with critic step 0's mse head chained on batch 0's rows
             f0, h0, dq0, dh0, _ = self.cbuf[1]
             tjob = head_job(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew), done=ptr(self.done), B=B, N=N,
                             gamma=m.GAMMA, yout=ptr(self.y),
                             chain=(ptr(h0), C.Wq, C.bq, ptr(self.q_c), ptr(dq0), ptr(dh0), B))
-            self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [lambda: critic_head_job(tjob)]
+            self.pre += [AttnEnc(ride_only(t_cenc))] + gemm_launches(t_comb) + [lambda: critic_head_job(tjob)]
         else:
-            self.pre += [AttnEnc(t_attn)] + gemm_launches(t_merge) + gemm_launches(t_out)
-            self.pre += gemm_launches(t_cenc) + gemm_launches(t_comb) + [t_head]
+            self.pre += [AttnEnc(t_attn)] + gemm_launches(t_merge)
+            self.pre += [AttnEnc(ride_only(t_cenc))] + gemm_launches(t_comb) + [t_head]
         if m.world > 1:
             self.iters = self._pipelined(A, C)
         elif self.OVERLAP:
@@ -630,13 +645,14 @@ class FusedUpdate:
                 segs.append(L)
                 continue
             if i > 0:
-                a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+                a_attn, a_merge = self._actor_fwd_stages(i, A)
                 if cs is None:
-                    L += [AttnEnc(a_attn)] + gemm_launches(a_merge) + gemm_launches(a_out)
+                    L += [AttnEnc(a_attn)] + gemm_launches(a_merge)
                 else:
                     L += [AttnEnc(with_ride(a_attn, cs["enc"]))] + gemm_launches(a_merge + cs["comb"])
-                    L += gemm_launches(a_out, heads=[cs["head_job"]])
-            L.append(AttnEnc(ride_only(ac["cenc"])))
+            # the actor's output layer runs inside the critic-encoder job on its actions; critic step
+            # i+1's head rides along (it needs only that step's combine, done in the launch before)
+            L.append(AttnEnc(ride_only(ac["cenc"]), head=cs["head_job"] if (cs is not None and i > 0) else None))
             if cs is None:
                 L += gemm_launches(ac["ccomb"]) + gemm_launches(ac["dcomb"])
             else:
@@ -735,13 +751,16 @@ class FusedUpdate:
                 ptr(self.nei, i * B * N * K * 6), ptr(self.y, i * B))
 
     def _actor_fwd_stages(self, i, A):
+        """The actor forward of iteration i up to the merge layer: [attention set, merge products]; its
+        tanh output layer runs inside the actor step's critic-encoder job (``_actor_stages`` cenc)."""
         B, N, D0, K, Din = self.B, self.N, self.D0, self.K, self.Din
         _, X2, radar, nei, _ = self._batch_ptrs(i)
-        return actor_forward_stages(A, self.acts, X2, Din, radar, nei, B * N, K, D0, X2 + 4 * D0, Din)
+        attn, merge, _ = actor_forward_stages(A, self.acts, X2, Din, radar, nei, B * N, K, D0, X2 + 4 * D0, Din)
+        return attn, merge
 
     def _actor_fwd_launches(self, i, A):
-        a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
-        return [AttnEnc(a_attn)] + gemm_launches(a_merge) + gemm_launches(a_out)
+        a_attn, a_merge = self._actor_fwd_stages(i, A)
+        return [AttnEnc(a_attn)] + gemm_launches(a_merge)
 
     def _critic_step(self, i, A, C, cb, fuse_actor_fwd):
         """Critic step of iteration i (ATT/maddpg:375-387) up to its weight-gradient partials.
@@ -750,15 +769,15 @@ class FusedUpdate:
         critic step's launches; the policy actions land in X2 (own columns gathered there too)."""
         cs = self._critic_stages(i, C, cb)
         if fuse_actor_fwd:
-            a_attn, a_merge, a_out = self._actor_fwd_stages(i, A)
+            a_attn, a_merge = self._actor_fwd_stages(i, A)
             L = [AttnEnc(with_ride(a_attn, cs["enc"]))]
         else:
-            a_merge, a_out = [], []
+            a_merge = []
             L = [AttnEnc(ride_only(cs["enc"]))]
         L += gemm_launches(cs["comb"])
         L.append(cs["head"])
         L += gemm_launches(cs["grad"] + a_merge)
-        L += gemm_launches(cs["encw"] + a_out)
+        L += gemm_launches(cs["encw"])
         return L
 
     def _critic_stages(self, i, C, cb):
@@ -811,7 +830,7 @@ class FusedUpdate:
         f, h, dq, dh, df = self.cbuf[0]
         c = self.acts
         st = {}
-        st["cenc"] = critic_enc_ride(C, X, B, N, Din, f)
+        st["cenc"] = critic_enc_ride(C, X, B, N, Din, f, fold=(ptr(c.ha), A, D0))
         # the actor loss -mean Q has the constant gradient dq = -1/B (ATT/maddpg:424), so the head's
         # dh = dq Wo (h > 0) is a second output of the combine layer's epilogue, and Q itself (stats
         # only) is an N = 1 product beside the combine's data gradient: no head launch on this chain

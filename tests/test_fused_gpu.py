@@ -492,6 +492,50 @@ def test_attn_enc_fwd_matches_reference(native_lib, K):
         assert torch.equal(getattr(acts2, n), getattr(acts, n)), n
 
 
+@pytest.mark.parametrize("rows", [1024, 203])
+def test_out_layer_folded_into_critic_encoder_job(native_lib, rows):
+    """The actor's tanh output layer folded into the critic-encoder riding job (o_h: ATT/nets:213 on
+    the actor rows ha[b*N + n]): the actions written into the critic-input rows match fp64 torch,
+    the encoders use them, and a critic-head job riding in the same launch (aac_attn_enc_fwd_head)
+    gives the bits of the standalone aac_critic_head."""
+    from types import SimpleNamespace
+
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(31 + rows)
+    Nc, D0 = 5, 22
+    Din = D0 + 2
+    d = lambda t: t.double().cpu()   # noqa: E731
+    P = fused.ptr
+    X = torch.randn(rows, Nc, Din, device=DEV)
+    X[:, :, D0:] = 99.0                                   # stale actions: must be overwritten
+    ha = torch.relu(torch.randn(rows * Nc, 256, device=DEV))
+    wa, ba = torch.randn(2, 256, device=DEV) * 0.1, torch.randn(2, device=DEV) * 0.1
+    cw, cb = torch.randn(Nc, 128, Din, device=DEV) * 0.2, torch.randn(Nc, 128, device=DEV) * 0.1
+    cp = SimpleNamespace(enc_w=[P(cw, n * 128 * Din) for n in range(Nc)], enc_b=[P(cb, n * 128) for n in range(Nc)])
+    ap = SimpleNamespace(Wa=P(wa), ba=P(ba))
+    f = torch.full((rows, Nc * 128), 7.0, device=DEV)
+    # a head job beside it (mode 0 on unrelated rows)
+    M = 517
+    h = torch.relu(torch.randn(M, 256, device=DEV))
+    w, b, y = torch.randn(256, device=DEV), torch.randn(1, device=DEV), torch.randn(M, device=DEV)
+    outs = [[torch.full((M,), 7.0, device=DEV), torch.full((M,), 7.0, device=DEV),
+             torch.full((M, 256), 7.0, device=DEV)] for _ in range(2)]
+    q, dq, dh = outs[0]
+    fused.critic_head(P(h), M, P(w), P(b), 0, y=P(y), q=P(q), dq=P(dq), dh=P(dh))
+    q, dq, dh = outs[1]
+    job = fused.head_job(P(h), M, P(w), P(b), 0, y=P(y), q=P(q), dq=P(dq), dh=P(dh))
+    ride = fused.critic_enc_ride(cp, P(X), rows, Nc, Din, f, fold=(P(ha), ap, D0))
+    fused.AttnEnc(fused.ride_only(ride), head=job)()
+    torch.cuda.synchronize()
+    a_ref = torch.tanh(d(ha) @ d(wa).t() + d(ba)).reshape(rows, Nc, 2)
+    np.testing.assert_allclose(d(X[:, :, D0:]), a_ref, atol=2e-6, rtol=1e-5)
+    xin = d(X).clone()
+    fw = torch.relu(torch.einsum("bnd,ncd->bnc", xin, d(cw)) + d(cb)).reshape(rows, Nc * 128)
+    np.testing.assert_allclose(d(f), fw, atol=2e-5, rtol=1e-5)
+    for a_, c_ in zip(outs[0], outs[1]):
+        assert torch.equal(a_, c_)
+
+
 @pytest.mark.parametrize("n,ns,pad", [(65536, 32, 0), (180228, 8, 0), (4100, 40, 0), (1001, 8, 0), (1001, 8, 1),
                                       (4098, 16, 1), (4096, 3, 0), (256, 1, 0)])
 def test_adam_sum_matches_torch(native_lib, n, ns, pad):
