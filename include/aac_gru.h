@@ -67,6 +67,32 @@ const char *aac_gru_last_error(void);
 
 int aac_gru_cell(const aac_gru_args *args, void *stream);
 
+/* The whole GRUCELL_actor_TwoPortion forward (WGRU/Nnetworks:181-198: own_fc + own_grid encoders,
+ * GRUCell(128, 64), outlay Linear(64, 2) + Tanh) for E envs x N agents in one launch: rows
+ * r = e*N + i of agent i (own rows ld_own apart, the first d_own <= 8 columns read; radar rows 18
+ * wide; hidden rows 64 wide).  Weights-stationary: a workgroup takes one agent, keeps every weight
+ * fragment of its wave's 16 hidden units in registers and walks 32-row blocks; the input projections
+ * run on the fp32 matrix cores and never reach memory.  Replaces the act path's two grouped-GEMM
+ * launches (encoders, gates) and its aac_gru_cell launch.  Agent i's parameters are at the agent-0
+ * pointers + i*pstride floats.  hout (h', 64 wide, ldho % 4 == 0) and y (tanh actions, 2 wide). */
+typedef struct {
+    const float *own;
+    int32_t ld_own, d_own;
+    const float *radar;
+    int32_t ld_radar;
+    const float *h;
+    int32_t ldh;
+    const float *Wo, *bo, *Wg, *bg, *Wih, *bih, *Whh, *bhh, *Wout, *bout;
+    int32_t pstride;
+    int32_t E, N;
+    float *hout;
+    int32_t ldho;
+    float *y;
+    int32_t ldy;
+} aac_gru_actor_args;
+
+int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream);
+
 /* dst[r][0 .. n0-1] = a[r*lda + ...], dst[r][n0 .. n0+n1-1] = b[r*ldb + ...] for R rows (ldd):
  * the [own, a] critic input rows of critic_single_obs_wGRU_TwoPortion (WGRU/nets:441). */
 int aac_pack_rows(float *dst, int32_t ldd, const float *a, int32_t lda, int32_t n0, const float *b, int32_t ldb,

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <string>
 
 #include "../../include/aac_gru.h"
@@ -105,6 +106,167 @@ __global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
     }
 }
 
+// ------------------------------------------------------------ weights-stationary actor forward
+// The act path of config 4 (E x N rows, every agent its own network): a workgroup takes one agent
+// and walks blocks of 16 NT envs; wave w owns hidden units 16w .. 16w + 15.  The layers run
+// transposed on v_mfma_f32_16x16x4_f32 (y^T = W x^T: A = weight fragments held in registers for the
+// whole launch, B = activations, the block's rows on the n axis), so lane (n, kq) ends with units
+// 16w + 4kq .. + 3 of row n of each gate -- all six gate pre-activations of a unit meet in one lane
+// and the GRU cell runs in registers.  The encoders' outputs pass to the input projection through a
+// [feature][row] LDS image; the output layer's partial dots through LDS in a fixed wave order.
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int GNT = 2;                        // 16-row tiles per block
+constexpr int GROWS = 16 * GNT, GTS = GROWS + 1;
+
+__global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A) {
+    __shared__ float sCat[128 * GTS];         // [e_o | e_g] of the block, [feature][row]
+    __shared__ float sP[4][GROWS][2];         // per-wave partial output dots
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
+    const int G = gridDim.x / A.N;            // workgroups per agent
+    const int ag = blockIdx.x / G, g = blockIdx.x - ag * G;
+    const size_t po = (size_t)ag * A.pstride;
+    const float *Wo = A.Wo + po, *Wg = A.Wg + po, *Wih = A.Wih + po, *Whh = A.Whh + po, *Wout = A.Wout + po;
+    const int d = A.d_own;
+    // A fragments: lane (n, kq) holds W[feature 16t + n][k = 4s + kq]
+    float ao[2], ag5[5], ai[3][32], ah[3][16];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int k = 4 * s + kq;
+        ao[s] = k < d ? Wo[(16 * w + n) * d + k] : 0.0f;
+    }
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int k = 4 * s + kq;
+        ag5[s] = k < 18 ? Wg[(16 * w + n) * 18 + (k < 18 ? k : 0)] : 0.0f;
+    }
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt) {
+#pragma unroll
+        for (int s = 0; s < 32; ++s) ai[gt][s] = Wih[(64 * gt + 16 * w + n) * 128 + 4 * s + kq];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) ah[gt][s] = Whh[(64 * gt + 16 * w + n) * 64 + 4 * s + kq];
+    }
+    // epilogue constants of this lane's features 16w + 4kq + v (f32 C layout)
+    const int u0 = 16 * w + 4 * kq;
+    f4 cbo, cbg, cbi[3], cbh[3], wo0, wo1;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        cbo[v] = A.bo[po + u0 + v];
+        cbg[v] = A.bg[po + u0 + v];
+#pragma unroll
+        for (int gt = 0; gt < 3; ++gt) {
+            cbi[gt][v] = A.bih[po + 64 * gt + u0 + v];
+            cbh[gt][v] = A.bhh[po + 64 * gt + u0 + v];
+        }
+        wo0[v] = Wout[u0 + v];
+        wo1[v] = Wout[64 + u0 + v];
+    }
+    const float bout0 = A.bout[po], bout1 = A.bout[po + 1];
+    const int nblk = (A.E + GROWS - 1) / GROWS;
+    for (int blk = g; blk < nblk; blk += G) {
+        const int e0 = blk * GROWS;
+        float bo_[GNT][2], br[GNT][5], bh[GNT][16];
+        f4 hv[GNT];
+#pragma unroll
+        for (int q = 0; q < GNT; ++q) {
+            const int e = e0 + 16 * q + n;
+            const size_t r = (size_t)(e < A.E ? e : A.E - 1) * A.N + ag;    // rows past E: their own column only
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int k = 4 * s + kq;
+                bo_[q][s] = A.own[r * A.ld_own + (k < d ? k : 0)];
+            }
+#pragma unroll
+            for (int s = 0; s < 5; ++s) {
+                const int k = 4 * s + kq;
+                br[q][s] = A.radar[r * A.ld_radar + (k < 18 ? k : 0)];
+            }
+#pragma unroll
+            for (int s = 0; s < 16; ++s) bh[q][s] = A.h[r * A.ldh + 4 * s + kq];
+            hv[q] = *reinterpret_cast<const f4 *>(A.h + r * A.ldh + u0);
+        }
+        // e_o^T = relu(Wo own^T + bo), e_g^T = relu(Wg radar^T + bg) -> sCat (padded k: zero A)
+#pragma unroll
+        for (int q = 0; q < GNT; ++q) {
+            f4 acc = {0.0f, 0.0f, 0.0f, 0.0f}, acr = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ao[s], bo_[q][s], acc, 0, 0, 0);
+#pragma unroll
+            for (int s = 0; s < 5; ++s) acr = __builtin_amdgcn_mfma_f32_16x16x4f32(ag5[s], br[q][s], acr, 0, 0, 0);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const float x = acc[v] + cbo[v], y = acr[v] + cbg[v];
+                sCat[(u0 + v) * GTS + 16 * q + n] = x > 0.0f ? x : 0.0f;
+                sCat[(64 + u0 + v) * GTS + 16 * q + n] = y > 0.0f ? y : 0.0f;
+            }
+        }
+        __syncthreads();
+        // gi^T = W_ih cat^T, gh^T = W_hh h^T for this wave's units of the three gates
+        f4 gi[3][GNT], gh[3][GNT];
+#pragma unroll
+        for (int gt = 0; gt < 3; ++gt)
+#pragma unroll
+            for (int q = 0; q < GNT; ++q) {
+                gi[gt][q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+                gh[gt][q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+        for (int s = 0; s < 32; ++s)
+#pragma unroll
+            for (int q = 0; q < GNT; ++q) {
+                const float b = sCat[(4 * s + kq) * GTS + 16 * q + n];
+#pragma unroll
+                for (int gt = 0; gt < 3; ++gt)
+                    gi[gt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ai[gt][s], b, gi[gt][q], 0, 0, 0);
+            }
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+            for (int q = 0; q < GNT; ++q)
+#pragma unroll
+                for (int gt = 0; gt < 3; ++gt)
+                    gh[gt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ah[gt][s], bh[q][s], gh[gt][q], 0, 0, 0);
+        // the cell (torch's GRUCell order, as gru_cell_kernel) and this lane's share of the output layer
+#pragma unroll
+        for (int q = 0; q < GNT; ++q) {
+            const int e = e0 + 16 * q + n;
+            f4 hp;
+            float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const float ir = gi[0][q][v] + cbi[0][v], iz = gi[1][q][v] + cbi[1][v], in = gi[2][q][v] + cbi[2][v];
+                const float hr = gh[0][q][v] + cbh[0][v], hz = gh[1][q][v] + cbh[1][v], hn = gh[2][q][v] + cbh[2][v];
+                const float rg = sigm(hr + ir);
+                const float zg = sigm(hz + iz);
+                const float ng = tanhf(in + hn * rg);
+                hp[v] = (hv[q][v] - ng) * zg + ng;
+                p0 = fmaf(wo0[v], hp[v], p0);
+                p1 = fmaf(wo1[v], hp[v], p1);
+            }
+            if (e < A.E) *reinterpret_cast<f4 *>(A.hout + ((size_t)e * A.N + ag) * A.ldho + u0) = hp;
+            p0 += __shfl_xor(p0, 16, 64);
+            p1 += __shfl_xor(p1, 16, 64);
+            p0 += __shfl_xor(p0, 32, 64);
+            p1 += __shfl_xor(p1, 32, 64);
+            if (kq == 0) {
+                sP[w][16 * q + n][0] = p0;
+                sP[w][16 * q + n][1] = p1;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < GROWS) {
+            const int x = threadIdx.x, e = e0 + x;
+            if (e < A.E) {
+                const float s0 = ((sP[0][x][0] + sP[1][x][0]) + sP[2][x][0]) + sP[3][x][0];
+                const float s1 = ((sP[0][x][1] + sP[1][x][1]) + sP[2][x][1]) + sP[3][x][1];
+                float *yo = A.y + ((size_t)e * A.N + ag) * A.ldy;
+                yo[0] = tanhf(s0 + bout0);
+                yo[1] = tanhf(s1 + bout1);
+            }
+        }
+    }
+}
+
 __global__ void pack_rows_kernel(float *dst, int ldd, const float *a, int lda, int n0, const float *b, int ldb, int n1,
                                  int R) {
     const int w = n0 + n1;
@@ -142,6 +304,27 @@ int aac_gru_cell(const aac_gru_args *args, void *stream) {
     hipLaunchKernelGGL(gru_cell_kernel, dim3((a.R + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gfail(std::string("gru_cell: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream) {
+    if (!args) return gfail("gru_actor_fwd: null arguments");
+    const aac_gru_actor_args &a = *args;
+    if (a.E <= 0 || a.N <= 0) return gfail("gru_actor_fwd: E, N > 0");
+    if (a.d_own < 1 || a.d_own > 8 || a.ld_own < a.d_own || a.ld_radar < 18 || a.ldh < H || a.ldy < 2)
+        return gfail("gru_actor_fwd: 1 <= d_own <= 8 and row strides >= the used widths");
+    if (!a.own || !a.radar || !a.h || !a.hout || !a.y || !a.Wo || !a.bo || !a.Wg || !a.bg || !a.Wih || !a.bih ||
+        !a.Whh || !a.bhh || !a.Wout || !a.bout)
+        return gfail("gru_actor_fwd: NULL operand");
+    if (a.ldh % 4 || a.ldho % 4 || a.ldho < H || (reinterpret_cast<uintptr_t>(a.h) & 15) ||
+        (reinterpret_cast<uintptr_t>(a.hout) & 15))
+        return gfail("gru_actor_fwd: h / hout rows must be 16-B aligned");
+    // one workgroup per CU in all (one wave per SIMD: ~250 registers of weights per lane)
+    const int blocks = (a.E + GROWS - 1) / GROWS;
+    const int G = std::max(1, std::min(blocks, 256 / a.N));
+    hipLaunchKernelGGL(gru_actor_fwd_kernel, dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gfail(std::string("gru_actor_fwd: ") + hipGetErrorString(e));
     return 0;
 }
 

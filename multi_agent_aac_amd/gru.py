@@ -56,6 +56,17 @@ class GruArgs(ctypes.Structure):
                 ("dgh", vp), ("ldd", i32)]
 
 
+class GruActorArgs(ctypes.Structure):
+    """aac_gru_actor_args (include/aac_gru.h)."""
+    _fields_ = [("own", vp), ("ld_own", i32), ("d_own", i32), ("radar", vp), ("ld_radar", i32), ("h", vp),
+                ("ldh", i32)] + [(k, vp) for k in ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout", "bout")] + \
+               [("pstride", i32), ("E", i32), ("N", i32), ("hout", vp), ("ldho", i32), ("y", vp), ("ldy", i32)]
+
+
+# the act path as one weights-stationary launch (aac_gru_actor_fwd) instead of the encoder and gate
+# GEMM launches + aac_gru_cell; AAC_GRU_ACT_WS=0 keeps the three launches
+ACT_WS = os.environ.get("AAC_GRU_ACT_WS", "1") == "1"
+
 _GL = None
 
 
@@ -67,6 +78,7 @@ def glib():
         L.aac_gru_cell.argtypes = [ctypes.POINTER(GruArgs), vp]
         L.aac_pack_rows.argtypes = [vp, i32, vp, i32, i32, vp, i32, i32, i32, vp]
         L.aac_gru_reset_hidden.argtypes = [vp, i32, i32, vp, vp]
+        L.aac_gru_actor_fwd.argtypes = [ctypes.POINTER(GruActorArgs), vp]
         _GL = L
     return _GL
 
@@ -381,6 +393,17 @@ class _ActPlan:
         self.hn = h_out if h_out is not None else torch.empty(E, N, H, device=dev)
         assert self.hn.is_contiguous() and self.hn.shape == (E, N, H)
         A = stack_addrs(m.actors, ACTOR_PARAMS, m.fa)
+        if ACT_WS and m.d_own <= 8:
+            sa = m.fa.numel // N
+            for i in range(N):      # agent-major flat buffer: agent i's parameters at agent 0's + i * sa
+                assert all(A[i][k] == A[0][k] + 4 * i * sa for k in ACTOR_PARAMS)
+            self.args = GruActorArgs(ptr(own), D0, m.d_own, ptr(radar), 18, ptr(h), H,
+                                     *[A[0][k] for k in ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout",
+                                                         "bout")],
+                                     sa, E, N, ptr(self.hn), H, ptr(self.a), 2)
+            self.L = [lambda: _chk(glib().aac_gru_actor_fwd(ctypes.byref(self.args), fused._stream()),
+                                   "aac_gru_actor_fwd")]
+            return
         self.L = gemm_launches(enc2_probs(A, "Wo", "bo", "Wg", "bg", ptr(own), D0, m.d_own, ptr(radar), 18, 18,
                                           ptr(self.cat), E, N))
         self.L += gemm_launches(gate_probs(A, ptr(self.cat), ptr(h), ptr(self.gi), ptr(self.gh), E, N))

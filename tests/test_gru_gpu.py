@@ -192,6 +192,32 @@ def test_gru_act_matches_reference(native_lib):
     assert abs(float(z.std()) - 1) < 0.1
 
 
+@pytest.mark.parametrize("E,own_width", [(4096, 6), (301, 34), (17, 6)])
+def test_gru_act_weights_stationary_matches_launch_path(native_lib, monkeypatch, E, own_width):
+    """aac_gru_actor_fwd (the act path in one weights-stationary launch) against the encoder + gate
+    GEMM launches + aac_gru_cell it replaces, and against the fp64 reference actor (config-4 shape
+    E = 4096 x 8; ragged blocks; own rows wider than d_own)."""
+    from multi_agent_aac_amd import gru
+    N = 8
+    m, _ = _model(N, 64, E, seed=5)
+    actors, _, _, _ = _ref_nets(m)
+    tr = gru_ref.random_gru_transitions(E, N, 9)
+    own = torch.zeros(E, N, own_width)
+    own[:, :, :6] = tr["s_own"][:, :, :6]
+    own, radar, h = own.to(DEV), tr["s_radar"].to(DEV), tr["h_cur"].to(DEV)
+    outs = {}
+    for ws in (True, False):
+        monkeypatch.setattr(gru, "ACT_WS", ws)
+        m._acts.clear()
+        a, hn = m.act(own, radar, h, noisy=False)
+        outs[ws] = (a.clone(), hn.clone())
+    torch.testing.assert_close(outs[True][0], outs[False][0], atol=2e-6, rtol=1e-5)
+    torch.testing.assert_close(outs[True][1], outs[False][1], atol=2e-6, rtol=1e-5)
+    ra, rh = gru_ref.ref_gru_act(actors, tr["s_own"], tr["s_radar"], tr["h_cur"], m.d_own)
+    np.testing.assert_allclose(outs[True][0].cpu(), ra, atol=2e-5)
+    np.testing.assert_allclose(outs[True][1].cpu(), rh, atol=2e-5)
+
+
 def test_gru_reset_hidden_and_reference_api(native_lib, tmp_path):
     from multi_agent_aac_amd import gru
     N = 3
