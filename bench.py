@@ -804,7 +804,8 @@ def main():
                     f"1 gradient iteration per update")
     elif tr.gru:      # algorithmic GEMM FLOPs of the plan's launches (2 M N K per product)
         from multi_agent_aac_amd.fused import GemmLaunch
-        upd_fl = sum(op.flops for op in tr.model._plan(a.batch).ops() if isinstance(op, GemmLaunch))
+        from multi_agent_aac_amd.gru import WsProj
+        upd_fl = sum(op.flops for op in tr.model._plan(a.batch).ops() if isinstance(op, (GemmLaunch, WsProj)))
         workload = f"randomOD_gru_radar: {N} agents x {a.envs} envs/GPU, GRU actor, B={a.batch} MADDPG update, " \
                    f"randomOD_Wgru_radar env (obstacle radar, per-agent WGRU ss_reward, max_spd 10)"
     else:

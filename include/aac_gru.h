@@ -89,6 +89,12 @@ typedef struct {
     int32_t ldho;
     float *y;
     int32_t ldy;
+    /* projection mode (gi != NULL; any GRU network of this shape, e.g. update_myown's critics with
+     * d_own = 8 input columns): no cell and no output layer -- cat = [e_o | e_g] (ldc), gi = cat W_ih^T
+     * + b_ih and gh = h W_hh^T + b_hh (ldg) are written for aac_gru_cell and the weight gradients,
+     * in place of the encoder and gate grouped-GEMM launches; hout, y, Wout, bout are not used. */
+    float *cat, *gi, *gh;
+    int32_t ldc, ldg;
 } aac_gru_actor_args;
 
 int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream);

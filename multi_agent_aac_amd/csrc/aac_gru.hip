@@ -115,10 +115,11 @@ __global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
 // and the GRU cell runs in registers.  The encoders' outputs pass to the input projection through a
 // [feature][row] LDS image; the output layer's partial dots through LDS in a fixed wave order.
 typedef float f4 __attribute__((ext_vector_type(4)));
-constexpr int GNT = 2;                        // 16-row tiles per block
-constexpr int GROWS = 16 * GNT, GTS = GROWS + 1;
-
+// GNT 16-row tiles per block (2 for the act path; 1 for the projection mode at B = 512 rows per agent,
+// so that every CU gets a workgroup); PROJ: write cat / gi / gh, no cell.
+template <int GNT, bool PROJ>
 __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A) {
+    constexpr int GROWS = 16 * GNT, GTS = GROWS + 1;
     __shared__ float sCat[128 * GTS];         // [e_o | e_g] of the block, [feature][row]
     __shared__ float sP[4][GROWS][2];         // per-wave partial output dots
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
@@ -127,7 +128,10 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
     const size_t po = (size_t)ag * A.pstride;
     const float *Wo = A.Wo + po, *Wg = A.Wg + po, *Wih = A.Wih + po, *Whh = A.Whh + po, *Wout = A.Wout + po;
     const int d = A.d_own;
-    // A fragments: lane (n, kq) holds W[feature 16t + n][k = 4s + kq]
+    // A fragments: lane (n, kq) holds W[feature 16t + n][k] for its k of step s.  The encoders take
+    // k = 4s + kq; the input projections k = 32 kq + s (W_ih) and 16 kq + s (W_hh), the same k order
+    // on the B side, so that a lane's weights and h values are consecutive floats (16-B loads: the
+    // 4-B form issued ~190 loads per wave against a limit of 63 in flight)
     float ao[2], ag5[5], ai[3][32], ah[3][16];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -141,10 +145,20 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
     }
 #pragma unroll
     for (int gt = 0; gt < 3; ++gt) {
+        const f4 *wi = reinterpret_cast<const f4 *>(Wih + (64 * gt + 16 * w + n) * 128 + 32 * kq);
+        const f4 *wh = reinterpret_cast<const f4 *>(Whh + (64 * gt + 16 * w + n) * 64 + 16 * kq);
 #pragma unroll
-        for (int s = 0; s < 32; ++s) ai[gt][s] = Wih[(64 * gt + 16 * w + n) * 128 + 4 * s + kq];
+        for (int j = 0; j < 8; ++j) {
+            const f4 v = wi[j];
 #pragma unroll
-        for (int s = 0; s < 16; ++s) ah[gt][s] = Whh[(64 * gt + 16 * w + n) * 64 + 4 * s + kq];
+            for (int c = 0; c < 4; ++c) ai[gt][4 * j + c] = v[c];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f4 v = wh[j];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) ah[gt][4 * j + c] = v[c];
+        }
     }
     // epilogue constants of this lane's features 16w + 4kq + v (f32 C layout)
     const int u0 = 16 * w + 4 * kq;
@@ -158,10 +172,10 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
             cbi[gt][v] = A.bih[po + 64 * gt + u0 + v];
             cbh[gt][v] = A.bhh[po + 64 * gt + u0 + v];
         }
-        wo0[v] = Wout[u0 + v];
-        wo1[v] = Wout[64 + u0 + v];
+        wo0[v] = PROJ ? 0.0f : Wout[u0 + v];
+        wo1[v] = PROJ ? 0.0f : Wout[64 + u0 + v];
     }
-    const float bout0 = A.bout[po], bout1 = A.bout[po + 1];
+    const float bout0 = PROJ ? 0.0f : A.bout[po], bout1 = PROJ ? 0.0f : A.bout[po + 1];
     const int nblk = (A.E + GROWS - 1) / GROWS;
     for (int blk = g; blk < nblk; blk += G) {
         const int e0 = blk * GROWS;
@@ -182,7 +196,11 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
                 br[q][s] = A.radar[r * A.ld_radar + (k < 18 ? k : 0)];
             }
 #pragma unroll
-            for (int s = 0; s < 16; ++s) bh[q][s] = A.h[r * A.ldh + 4 * s + kq];
+            for (int j = 0; j < 4; ++j) {
+                const f4 v = *reinterpret_cast<const f4 *>(A.h + r * A.ldh + 16 * kq + 4 * j);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) bh[q][4 * j + c] = v[c];
+            }
             hv[q] = *reinterpret_cast<const f4 *>(A.h + r * A.ldh + u0);
         }
         // e_o^T = relu(Wo own^T + bo), e_g^T = relu(Wg radar^T + bg) -> sCat (padded k: zero A)
@@ -193,11 +211,20 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
             for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ao[s], bo_[q][s], acc, 0, 0, 0);
 #pragma unroll
             for (int s = 0; s < 5; ++s) acr = __builtin_amdgcn_mfma_f32_16x16x4f32(ag5[s], br[q][s], acr, 0, 0, 0);
+            f4 co, cg;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 const float x = acc[v] + cbo[v], y = acr[v] + cbg[v];
-                sCat[(u0 + v) * GTS + 16 * q + n] = x > 0.0f ? x : 0.0f;
-                sCat[(64 + u0 + v) * GTS + 16 * q + n] = y > 0.0f ? y : 0.0f;
+                co[v] = x > 0.0f ? x : 0.0f;
+                cg[v] = y > 0.0f ? y : 0.0f;
+                sCat[(u0 + v) * GTS + 16 * q + n] = co[v];
+                sCat[(64 + u0 + v) * GTS + 16 * q + n] = cg[v];
+            }
+            const int e = e0 + 16 * q + n;
+            if (PROJ && A.cat && e < A.E) {
+                float *c = A.cat + ((size_t)e * A.N + ag) * A.ldc;
+                *reinterpret_cast<f4 *>(c + u0) = co;
+                *reinterpret_cast<f4 *>(c + 64 + u0) = cg;
             }
         }
         __syncthreads();
@@ -214,7 +241,7 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
         for (int s = 0; s < 32; ++s)
 #pragma unroll
             for (int q = 0; q < GNT; ++q) {
-                const float b = sCat[(4 * s + kq) * GTS + 16 * q + n];
+                const float b = sCat[(32 * kq + s) * GTS + 16 * q + n];
 #pragma unroll
                 for (int gt = 0; gt < 3; ++gt)
                     gi[gt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ai[gt][s], b, gi[gt][q], 0, 0, 0);
@@ -226,6 +253,21 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
 #pragma unroll
                 for (int gt = 0; gt < 3; ++gt)
                     gh[gt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ah[gt][s], bh[q][s], gh[gt][q], 0, 0, 0);
+        if (PROJ) {      // gi / gh rows with their biases, for aac_gru_cell and the weight gradients
+#pragma unroll
+            for (int q = 0; q < GNT; ++q) {
+                const int e = e0 + 16 * q + n;
+                if (e >= A.E) continue;
+                const size_t r = (size_t)e * A.N + ag;
+#pragma unroll
+                for (int gt = 0; gt < 3; ++gt) {
+                    *reinterpret_cast<f4 *>(A.gi + r * A.ldg + 64 * gt + u0) = gi[gt][q] + cbi[gt];
+                    *reinterpret_cast<f4 *>(A.gh + r * A.ldg + 64 * gt + u0) = gh[gt][q] + cbh[gt];
+                }
+            }
+            __syncthreads();      // sCat is rewritten by the next block
+            continue;
+        }
         // the cell (torch's GRUCell order, as gru_cell_kernel) and this lane's share of the output layer
 #pragma unroll
         for (int q = 0; q < GNT; ++q) {
@@ -311,18 +353,27 @@ int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream) {
     if (!args) return gfail("gru_actor_fwd: null arguments");
     const aac_gru_actor_args &a = *args;
     if (a.E <= 0 || a.N <= 0) return gfail("gru_actor_fwd: E, N > 0");
-    if (a.d_own < 1 || a.d_own > 8 || a.ld_own < a.d_own || a.ld_radar < 18 || a.ldh < H || a.ldy < 2)
+    const bool proj = a.gi != nullptr;
+    auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (a.d_own < 1 || a.d_own > 8 || a.ld_own < a.d_own || a.ld_radar < 18 || a.ldh < H)
         return gfail("gru_actor_fwd: 1 <= d_own <= 8 and row strides >= the used widths");
-    if (!a.own || !a.radar || !a.h || !a.hout || !a.y || !a.Wo || !a.bo || !a.Wg || !a.bg || !a.Wih || !a.bih ||
-        !a.Whh || !a.bhh || !a.Wout || !a.bout)
+    if (!a.own || !a.radar || !a.h || !a.Wo || !a.bo || !a.Wg || !a.bg || !a.Wih || !a.bih || !a.Whh || !a.bhh)
         return gfail("gru_actor_fwd: NULL operand");
-    if (a.ldh % 4 || a.ldho % 4 || a.ldho < H || (reinterpret_cast<uintptr_t>(a.h) & 15) ||
-        (reinterpret_cast<uintptr_t>(a.hout) & 15))
-        return gfail("gru_actor_fwd: h / hout rows must be 16-B aligned");
+    if (a.ldh % 4 || !al16(a.h)) return gfail("gru_actor_fwd: h rows must be 16-B aligned");
+    if (proj) {
+        if (!a.gh || a.ldg < 3 * H || a.ldg % 4 || !al16(a.gi) || !al16(a.gh) ||
+            (a.cat && (a.ldc < 128 || a.ldc % 4 || !al16(a.cat))))
+            return gfail("gru_actor_fwd: projection outputs gi, gh (and cat) with 16-B aligned rows");
+    } else {
+        if (!a.hout || !a.y || !a.Wout || !a.bout || a.ldy < 2) return gfail("gru_actor_fwd: NULL output operand");
+        if (a.ldho % 4 || a.ldho < H || !al16(a.hout)) return gfail("gru_actor_fwd: hout rows must be 16-B aligned");
+    }
     // one workgroup per CU in all (one wave per SIMD: ~250 registers of weights per lane)
-    const int blocks = (a.E + GROWS - 1) / GROWS;
+    const int rows = proj ? 16 : 32;
+    const int blocks = (a.E + rows - 1) / rows;
     const int G = std::max(1, std::min(blocks, 256 / a.N));
-    hipLaunchKernelGGL(gru_actor_fwd_kernel, dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, a);
+    if (proj) hipLaunchKernelGGL((gru_actor_fwd_kernel<1, true>), dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((gru_actor_fwd_kernel<2, false>), dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gfail(std::string("gru_actor_fwd: ") + hipGetErrorString(e));
     return 0;

@@ -60,12 +60,38 @@ class GruActorArgs(ctypes.Structure):
     """aac_gru_actor_args (include/aac_gru.h)."""
     _fields_ = [("own", vp), ("ld_own", i32), ("d_own", i32), ("radar", vp), ("ld_radar", i32), ("h", vp),
                 ("ldh", i32)] + [(k, vp) for k in ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout", "bout")] + \
-               [("pstride", i32), ("E", i32), ("N", i32), ("hout", vp), ("ldho", i32), ("y", vp), ("ldy", i32)]
+               [("pstride", i32), ("E", i32), ("N", i32), ("hout", vp), ("ldho", i32), ("y", vp), ("ldy", i32),
+                ("cat", vp), ("gi", vp), ("gh", vp), ("ldc", i32), ("ldg", i32)]
 
 
-# the act path as one weights-stationary launch (aac_gru_actor_fwd) instead of the encoder and gate
-# GEMM launches + aac_gru_cell; AAC_GRU_ACT_WS=0 keeps the three launches
-ACT_WS = os.environ.get("AAC_GRU_ACT_WS", "1") == "1"
+# weights-stationary aac_gru_actor_fwd: the act path as one launch instead of the encoder and gate
+# GEMM launches + aac_gru_cell, and in update_myown each network evaluation's encoder + gate GEMM
+# launches as one launch (projection mode); AAC_GRU_WS=0 keeps the grouped-GEMM launches
+ACT_WS = os.environ.get("AAC_GRU_WS", "1") == "1"
+# the projection mode in update_myown (one launch per network evaluation instead of the encoder and
+# gate GEMM launches): config 4 0.463 -> 0.402 ms per step; AAC_GRU_WS_PROJ=0 keeps the GEMM launches
+WS_PROJ = ACT_WS and os.environ.get("AAC_GRU_WS_PROJ", "1") == "1"
+_WS_NAMES = ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout", "bout")
+
+
+def _agent_stride(P, stride):
+    """The agent stacks are agent-major flat buffers: agent i's parameters at agent 0's + i * stride."""
+    for i in range(len(P)):
+        assert all(P[i][k] == P[0][k] + 4 * i * stride for k in _WS_NAMES)
+    return stride
+
+
+class WsProj:
+    """enc2_probs + gate_probs of one network evaluation (cat, gi, gh of M samples x N agents) as one
+    aac_gru_actor_fwd launch in projection mode."""
+
+    def __init__(self, P, stride, X1, w1, k1, radar, h, cat, gi, gh, M, N):
+        self.args = GruActorArgs(X1, w1, k1, radar, 18, h, H, *[P[0][k] for k in _WS_NAMES],
+                                 _agent_stride(P, stride), M, N, None, 0, None, 0, cat, gi, gh, 128, 192)
+        self.flops = 2 * M * N * (64 * k1 + 64 * 18 + 192 * 128 + 192 * H)     # 2 M N K of the four products
+
+    def __call__(self):
+        _chk(glib().aac_gru_actor_fwd(ctypes.byref(self.args), fused._stream()), "aac_gru_actor_fwd")
 
 _GL = None
 
@@ -256,6 +282,15 @@ class GruUpdate:
         self.da, self.dout = z(B, N, 2), z(B, N, 2)
         self._build()
 
+    def _proj(self, P, stride, X1, w1, k1, radar, h, cat, gi, gh):
+        """The encoders + input projections of one network evaluation over the batch: one
+        weights-stationary launch (WsProj) or the two grouped-GEMM launches."""
+        B, N = self.B, self.m.n_agents
+        if WS_PROJ and k1 <= 8:
+            return [WsProj(P, stride, X1, w1, k1, radar, h, cat, gi, gh, B, N)]
+        return (gemm_launches(enc2_probs(P, "Wo", "bo", "Wg", "bg", X1, w1, k1, radar, 18, 18, cat, B, N))
+                + gemm_launches(gate_probs(P, cat, h, gi, gh, B, N)))
+
     def _adam(self, opt, flat):
         m = self.m
         L = []
@@ -280,20 +315,15 @@ class GruUpdate:
         L = [lambda: ops.replay_sample(rep.meta, B, rep.seed, rep.counter, self.bidx),
              lambda: ops.replay_gather(rep.ring, self.bidx, [b[k] for k in rep.fields], rep.widths)]
         # ---------------- TD target (WGRU/maddpg:265, :280-282), target networks
-        L += gemm_launches(enc2_probs(At, "Wo", "bo", "Wg", "bg", nown, D0, d, nradar, 18, 18, P(self.cat_a), B, N))
-        L += gemm_launches(gate_probs(At, P(self.cat_a), hnext, P(self.gi_a), P(self.gh_a), B, N))
+        L += self._proj(At, sa, nown, D0, d, nradar, hnext, P(self.cat_a), P(self.gi_a), P(self.gh_a))
         L.append(gru_cell(At, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hnext, B, N, FWD,
                           pack_src=nown, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa_t), ld_pack_dst=Dsa))
-        L += gemm_launches(enc2_probs(Ct, "Wo", "bo", "Wg", "bg", P(self.Xsa_t), Dsa, Dsa, nradar, 18, 18,
-                                      P(self.cat_c), B, N))
-        L += gemm_launches(gate_probs(Ct, P(self.cat_c), hnext, P(self.gi_c), P(self.gh_c), B, N))
+        L += self._proj(Ct, sc, P(self.Xsa_t), Dsa, Dsa, nradar, hnext, P(self.cat_c), P(self.gi_c), P(self.gh_c))
         L.append(gru_cell(Ct, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hnext, B, N, TD,
                           rew=ptr(b["rew"]), done=ptr(b["done"]), gamma=m.GAMMA, yout=P(self.y)))
         # ---------------- critic step (WGRU/maddpg:272, :284-291)
         L.append(lambda: pack_rows(P(self.Xsa), Dsa, own, D0, d, act, 2, 2, B * N))
-        L += gemm_launches(enc2_probs(C, "Wo", "bo", "Wg", "bg", P(self.Xsa), Dsa, Dsa, radar, 18, 18,
-                                      P(self.cat_c), B, N))
-        L += gemm_launches(gate_probs(C, P(self.cat_c), hcur, P(self.gi_c), P(self.gh_c), B, N))
+        L += self._proj(C, sc, P(self.Xsa), Dsa, Dsa, radar, hcur, P(self.cat_c), P(self.gi_c), P(self.gh_c))
         L.append(gru_cell(C, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hcur, B, N, CRITIC,
                           target=P(self.y), y=P(self.q_c), dq=P(self.dq), hout=P(self.hc), ldho=H, inv_m=1.0 / B,
                           dgi=P(self.dgi_c), dgh=P(self.dgh_c), ldd=192))
@@ -308,14 +338,11 @@ class GruUpdate:
             + wgrad_probs(P(self.dcat_c), 64, 128, radar, 0, 18, 18, gC, "Wg", "bg", 64, B, N))
         L += self._adam(m.critic_optimizer, m.fc)
         # ---------------- actor step (WGRU/maddpg:293-310): 3 - mean Q(s, pi(s, h), h)
-        L += gemm_launches(enc2_probs(A, "Wo", "bo", "Wg", "bg", own, D0, d, radar, 18, 18, P(self.cat_a), B, N))
-        L += gemm_launches(gate_probs(A, P(self.cat_a), hcur, P(self.gi_a), P(self.gh_a), B, N))
+        L += self._proj(A, sa, own, D0, d, radar, hcur, P(self.cat_a), P(self.gi_a), P(self.gh_a))
         L.append(gru_cell(A, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hcur, B, N, FWD,
                           hout=P(self.ha), ldho=H, pack_src=own, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa2),
                           ld_pack_dst=Dsa))
-        L += gemm_launches(enc2_probs(C, "Wo", "bo", "Wg", "bg", P(self.Xsa2), Dsa, Dsa, radar, 18, 18,
-                                      P(self.cat_c), B, N))
-        L += gemm_launches(gate_probs(C, P(self.cat_c), hcur, P(self.gi_c), P(self.gh_c), B, N))
+        L += self._proj(C, sc, P(self.Xsa2), Dsa, Dsa, radar, hcur, P(self.cat_c), P(self.gi_c), P(self.gh_c))
         L.append(gru_cell(C, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hcur, B, N, ACTLOSS,
                           y=P(self.q_a), inv_m=1.0 / B, dgi=P(self.dgi_c), ldd=192))
         # d SA = (dgi W_ih[:, :64]) * (SA > 0); d a = d SA . W_sa[:, d:d+2]
@@ -394,13 +421,8 @@ class _ActPlan:
         assert self.hn.is_contiguous() and self.hn.shape == (E, N, H)
         A = stack_addrs(m.actors, ACTOR_PARAMS, m.fa)
         if ACT_WS and m.d_own <= 8:
-            sa = m.fa.numel // N
-            for i in range(N):      # agent-major flat buffer: agent i's parameters at agent 0's + i * sa
-                assert all(A[i][k] == A[0][k] + 4 * i * sa for k in ACTOR_PARAMS)
-            self.args = GruActorArgs(ptr(own), D0, m.d_own, ptr(radar), 18, ptr(h), H,
-                                     *[A[0][k] for k in ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout",
-                                                         "bout")],
-                                     sa, E, N, ptr(self.hn), H, ptr(self.a), 2)
+            self.args = GruActorArgs(ptr(own), D0, m.d_own, ptr(radar), 18, ptr(h), H, *[A[0][k] for k in _WS_NAMES],
+                                     _agent_stride(A, m.fa.numel // N), E, N, ptr(self.hn), H, ptr(self.a), 2)
             self.L = [lambda: _chk(glib().aac_gru_actor_fwd(ctypes.byref(self.args), fused._stream()),
                                    "aac_gru_actor_fwd")]
             return
