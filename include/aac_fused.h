@@ -175,6 +175,16 @@ int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const flo
                        const float *Wv, float *dxn, float *dqk, float *dq, float *deo, int32_t R, int32_t K,
                        void *stream);
 
+/* The same backward (K <= 8, the MFMA path) that also accumulates the neighbour encoder's weight
+ * gradient: pwn [aac_attn_train_bwd_partials(R)][448] gets one partial row per workgroup, row p =
+ * [sum dx_j^T nei_j (64 x 6, f * 6 + c) | sum dx_j (64)] over the workgroup's rows (nei rows
+ * [(r*K + j)*6]); the rows sum to dWn | dbn (ATT/nets:186-190) in a fixed order.  dxn may be NULL. */
+int aac_attn_train_bwd_wn(const float *dv, int32_t lddv, const float *xn, const float *alpha, const float *qk,
+                          const float *eo, int32_t lde, const float *dcat_o, int32_t ldd, const float *Wq,
+                          const float *Wk, const float *Wv, float *dxn, float *dqk, float *dq, float *deo, int32_t R,
+                          int32_t K, const float *nei, float *pwn, void *stream);
+int32_t aac_attn_train_bwd_partials(int32_t R);
+
 /* Inference form of the actor's neighbour attention (ATT/nets:186-210) for R rows, K <= 32:
  * x_j = relu(Wn nei_j + bn) computed from the 6-wide rows nei[(r*K + j)*6], scores
  * x_j . (Wqk e_o) / 8 with Wqk = Wk^T Wq (64x64, precomputed), masked softmax (mask

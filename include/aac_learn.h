@@ -105,6 +105,16 @@ int aac_actor_out_noise(const float *ha, int64_t R, const float *wa, const float
                         const int32_t *episode, int32_t eps_end, float noise_start, float noise_end, uint64_t seed,
                         uint64_t *counter, int32_t noisy, float *noise_out, void *stream);
 
+/* The actor's merge + output layers with that noise in one weights-stationary launch (ATT/nets:211-213,
+ * ATT/maddpg:476-500): h_a = relu(wm cat[r] + bm) (wm [256][192], cat rows ldc apart = [e_o | e_g |
+ * v_att]), act[r] = tanh(wa h_a + ba), then with noisy != 0 the noise and clamp of aac_noise_clamp (the
+ * same per-row draw; the counter advances by one per call).  Replaces the merge layer's grouped-GEMM
+ * launch and aac_actor_out_noise on the act path; h_a is not stored. */
+int aac_actor_head_ws(const float *cat, int32_t ldc, int64_t R, const float *wm, const float *bm, const float *wa,
+                      const float *ba, float *act, int32_t N, const int32_t *episode, int32_t eps_end,
+                      float noise_start, float noise_end, uint64_t seed, uint64_t *counter, int32_t noisy,
+                      float *noise_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1546,13 +1546,21 @@ __global__ void __launch_bounds__(256) attn_mfma_bwd_kernel(const float *__restr
                                                             const float *__restrict__ Wq, const float *__restrict__ Wk,
                                                             const float *__restrict__ Wv, float *__restrict__ dxn,
                                                             float *__restrict__ dqk_out, float *__restrict__ dq_out,
-                                                            float *__restrict__ deo_out, int R, int K) {
+                                                            float *__restrict__ deo_out, int R, int K,
+                                                            const float *__restrict__ nei, float *__restrict__ pwn) {
     __shared__ float sA[64 * TS], sB[64 * TS];
     __shared__ f4 sD4[16 * QS / 4];
+    __shared__ float sN[16 * KM * 6];         // pwn: the block's neighbour rows
+    __shared__ float sW[4 * 7 * 64];          // pwn: the waves' partial dWn rows
     float *sD = reinterpret_cast<float *>(sD4);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
     const int fo = 16 * w + 4 * h;
     const int nblk = (R + 15) / 16;
+    // pwn != NULL: the neighbour encoder's weight gradient dWn = sum_(r, j) dx_j^T [nei_j | 1] (64 x 7)
+    // accumulated by this workgroup (lane = feature), written as one partial row of pwn
+    // ([gridDim][64 * 6 + 64]: weights f * 6 + c, then the bias); dxn may then be NULL.  It replaces
+    // the 20 480-row GEMM product whose chain was the longest of its launch.
+    float gw[7] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const int r0 = blk * 16, r = r0 + n;
         const bool rin = r < R;
@@ -1582,6 +1590,13 @@ __global__ void __launch_bounds__(256) attn_mfma_bwd_kernel(const float *__restr
         for (int s = 0; s < 16; ++s) aqt[s] = Wq[(16 * h + s) * 64 + 16 * w + n];
         const f4 e = *reinterpret_cast<const f4 *>(eo + (size_t)rc * lde + fo);
         const f4 dc = *reinterpret_cast<const f4 *>(dcat_o + (size_t)rc * ldd + fo);
+        if (pwn) {      // the block's neighbour rows (slots j >= K zero)
+            for (int i = threadIdx.x; i < 16 * KM * 6; i += 256) {
+                const int rl = i / (KM * 6), jc = i - rl * KM * 6, j = jc / 6;
+                const int row = r0 + rl;
+                sN[i] = (row < R && j < K) ? nei[((size_t)row * K + j) * 6 + (jc - j * 6)] : 0.0f;
+            }
+        }
         // dxb^T = Wv^T dv^T
         f4 acc = mfma_k64(avt, b);
         *reinterpret_cast<f4 *>(sD + n * QS + fo) = acc;
@@ -1612,7 +1627,14 @@ __global__ void __launch_bounds__(256) attn_mfma_bwd_kernel(const float *__restr
                 for (int j = 0; j < KM; ++j) {
                     const float ds = al[i][j] * (p[i * KM + j] - S) / 8.0f;
                     const float g = al[i][j] * dxb + ds * qk;
-                    if (j < K && row < R) dxn[((size_t)row * K + j) * 64 + lane] = x[i][j] > 0.0f ? g : 0.0f;
+                    const float gx = x[i][j] > 0.0f ? g : 0.0f;
+                    if (dxn && j < K && row < R) dxn[((size_t)row * K + j) * 64 + lane] = gx;
+                    if (pwn && j < K && row < R) {
+                        const float *nr = sN + (rl * KM + j) * 6;
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) gw[c] = fmaf(gx, nr[c], gw[c]);
+                        gw[6] += gx;
+                    }
                     dqk = fmaf(ds, x[i][j], dqk);
                 }
                 if (row < R) dqk_out[(size_t)row * 64 + lane] = dqk;
@@ -1637,6 +1659,21 @@ __global__ void __launch_bounds__(256) attn_mfma_bwd_kernel(const float *__restr
             o.z = e.z > 0.0f ? dc.z + acc.z : 0.0f;
             o.w = e.w > 0.0f ? dc.w + acc.w : 0.0f;
             *reinterpret_cast<f4 *>(deo_out + (size_t)r * 64 + fo) = o;
+        }
+    }
+    if (pwn) {          // the four waves' partials, summed in wave order
+#pragma unroll
+        for (int c = 0; c < 7; ++c) sW[(w * 7 + c) * 64 + lane] = gw[c];
+        __syncthreads();
+        if (w == 0) {
+            float *o = pwn + (size_t)blockIdx.x * 448;
+#pragma unroll
+            for (int c = 0; c < 7; ++c) {
+                const float v = ((sW[c * 64 + lane] + sW[(7 + c) * 64 + lane]) + sW[(14 + c) * 64 + lane]) +
+                                sW[(21 + c) * 64 + lane];
+                if (c < 6) o[lane * 6 + c] = v;
+                else o[384 + lane] = v;
+            }
         }
     }
 }
@@ -2604,22 +2641,32 @@ int aac_attn_train_fwd(const float *eo, int32_t lde, const float *xn, const floa
     return 0;
 }
 
-int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const float *alpha, const float *qk,
-                       const float *eo, int32_t lde, const float *dcat_o, int32_t ldd, const float *Wq, const float *Wk,
-                       const float *Wv, float *dxn, float *dqk, float *dq, float *deo, int32_t R, int32_t K,
-                       void *stream) {
+static bool attn_bwd_mfma_ok(const float *dv, int32_t lddv, const float *eo, int32_t lde, const float *dcat_o,
+                             int32_t ldd, const float *dq, const float *deo, int32_t K) {
+    return g_attn_mfma && K <= 8 && aligned16(dv) && lddv % 4 == 0 && aligned16(eo) && lde % 4 == 0 &&
+           aligned16(dcat_o) && ldd % 4 == 0 && aligned16(dq) && aligned16(deo);
+}
+
+int32_t aac_attn_train_bwd_partials(int32_t R) { return R > 0 ? mfma_attn_grid(R) : 0; }
+
+int aac_attn_train_bwd_wn(const float *dv, int32_t lddv, const float *xn, const float *alpha, const float *qk,
+                          const float *eo, int32_t lde, const float *dcat_o, int32_t ldd, const float *Wq,
+                          const float *Wk, const float *Wv, float *dxn, float *dqk, float *dq, float *deo, int32_t R,
+                          int32_t K, const float *nei, float *pwn, void *stream) {
     if (R <= 0) return 0;
     if (K < 1 || K > 32) return ffail("attn_train_bwd: 1 <= K <= 32");
     hipStream_t st = (hipStream_t)stream;
-    if (g_attn_mfma && K <= 8 && aligned16(dv) && lddv % 4 == 0 && aligned16(eo) && lde % 4 == 0 && aligned16(dcat_o) &&
-        ldd % 4 == 0 && aligned16(dq) && aligned16(deo)) {
+    const bool mfma = attn_bwd_mfma_ok(dv, lddv, eo, lde, dcat_o, ldd, dq, deo, K);
+    if (pwn && (!nei || !mfma)) return ffail("attn_train_bwd: the dWn partials need nei and the MFMA path (K <= 8)");
+    if (!pwn && !dxn) return ffail("attn_train_bwd: dxn (or the dWn partials) required");
+    if (mfma) {
         const dim3 g(mfma_attn_grid(R)), b(256);
         if (K <= 4)
             hipLaunchKernelGGL(attn_mfma_bwd_kernel<4>, g, b, 0, st, dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq,
-                               Wk, Wv, dxn, dqk, dq, deo, R, K);
+                               Wk, Wv, dxn, dqk, dq, deo, R, K, nei, pwn);
         else
             hipLaunchKernelGGL(attn_mfma_bwd_kernel<8>, g, b, 0, st, dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq,
-                               Wk, Wv, dxn, dqk, dq, deo, R, K);
+                               Wk, Wv, dxn, dqk, dq, deo, R, K, nei, pwn);
         FHIP(hipGetLastError());
         return 0;
     }
@@ -2633,6 +2680,14 @@ int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const flo
 #undef ATB
     FHIP(hipGetLastError());
     return 0;
+}
+
+int aac_attn_train_bwd(const float *dv, int32_t lddv, const float *xn, const float *alpha, const float *qk,
+                       const float *eo, int32_t lde, const float *dcat_o, int32_t ldd, const float *Wq, const float *Wk,
+                       const float *Wv, float *dxn, float *dqk, float *dq, float *deo, int32_t R, int32_t K,
+                       void *stream) {
+    return aac_attn_train_bwd_wn(dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq, Wk, Wv, dxn, dqk, dq, deo, R, K,
+                                 nullptr, nullptr, stream);
 }
 
 int aac_attn_block(const float *eo, int32_t lde, const float *nei, const float *Wn, const float *bn,

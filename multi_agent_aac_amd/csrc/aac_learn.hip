@@ -550,6 +550,133 @@ __global__ void __launch_bounds__(LEARN_BLOCK) actor_out_noise_kernel(const floa
     reinterpret_cast<float2 *>(act)[myrow] = make_float2(a0, a1);
 }
 
+// The actor's merge layer, output layer and exploration noise (ATT/nets:211-213 + choose_action's noise
+// and clamp, ATT/maddpg:476-500) over the E*N act rows in one weights-stationary launch: h_a =
+// relu(Wm cat + bm) (192 -> 256), a = tanh(Wa h_a + ba) (256 -> 2), noise, clamp.  A 512-thread
+// workgroup per CU; wave w owns merge features 32w .. 32w + 31 and keeps their Wm rows in registers
+// (k order 48 kq + s: 16-B loads), the rows of a 16-row block on the MFMA's n axis (h_a^T = Wm cat^T
+// on v_mfma_f32_16x16x4_f32).  The output layer's partial dots meet in LDS in a fixed wave order;
+// h_a never reaches memory.  Replaces the merge layer's grouped-GEMM launch and actor_out_noise.
+constexpr int AH_W = 8;                       // waves per workgroup
+typedef float hf4 __attribute__((ext_vector_type(4)));
+
+constexpr int AH_XS = 193;                   // LDS row stride of the staged input rows (odd: 2-way reads)
+
+__global__ void __launch_bounds__(64 * AH_W) actor_head_ws_kernel(const float *__restrict__ cat, int ldc, int64_t R,
+                                                                 const float *__restrict__ wm,
+                                                                 const float *__restrict__ bm,
+                                                                 const float *__restrict__ wa,
+                                                                 const float *__restrict__ ba, float *act, int N,
+                                                                 const int32_t *episode, int eps_end,
+                                                                 float noise_start, float noise_end, uint64_t seed,
+                                                                 uint64_t *counter, int noisy, float *noise_out) {
+    __shared__ float sX[2][16 * AH_XS];      // the block's input rows, double-buffered
+    __shared__ float2 sP[2][AH_W][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
+    const int t = threadIdx.x;
+    const uint64_t ctr = noisy ? take_epoch(counter) : 0;
+    float a[2][48];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+        const hf4 *src = reinterpret_cast<const hf4 *>(wm + (size_t)(32 * w + 16 * tt + n) * 192 + 48 * kq);
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const hf4 v = src[j];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[tt][4 * j + c] = v[c];
+        }
+    }
+    // this lane's features 32w + 16tt + 4kq + v: bias and output-layer weights
+    hf4 cb[2], u0[2], u1[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+        const int f = 32 * w + 16 * tt + 4 * kq;
+        cb[tt] = *reinterpret_cast<const hf4 *>(bm + f);
+        u0[tt] = *reinterpret_cast<const hf4 *>(wa + f);
+        u1[tt] = *reinterpret_cast<const hf4 *>(wa + 256 + f);
+    }
+    const float ba0 = ba[0], ba1 = ba[1];
+    const int64_t nblk = (R + 15) / 16;
+    // staging of a block's 16 x 192 input floats: 768 16-B items, items t and t + 512 of this thread
+    hf4 pf[2];
+    auto load_rows = [&](int64_t blk) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = t + 512 * u;
+            const int row = i / 48, c4 = i - row * 48;
+            int64_t r = blk * 16 + row;
+            r = r < R ? r : R - 1;
+            pf[u] = (i < 768) ? reinterpret_cast<const hf4 *>(cat + r * ldc)[c4] : hf4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+    auto store_rows = [&](float *dst) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = t + 512 * u;
+            const int row = i / 48, c4 = i - row * 48;
+            if (i < 768)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) dst[row * AH_XS + 4 * c4 + c] = pf[u][c];
+        }
+    };
+    if (blockIdx.x < nblk) {
+        load_rows(blockIdx.x);
+        store_rows(sX[0]);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const bool more = blk + gridDim.x < nblk;
+        if (more) load_rows(blk + gridDim.x);      // in flight across the MFMA chain
+        const float *x = sX[cur] + n * AH_XS + 48 * kq;
+        hf4 acc[2] = {hf4{0.0f, 0.0f, 0.0f, 0.0f}, hf4{0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+        for (int s = 0; s < 48; ++s) {
+            const float bv = x[s];
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[tt][s], bv, acc[tt], 0, 0, 0);
+        }
+        float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                float h = acc[tt][v] + cb[tt][v];
+                h = h > 0.0f ? h : 0.0f;
+                p0 = fmaf(u0[tt][v], h, p0);
+                p1 = fmaf(u1[tt][v], h, p1);
+            }
+        p0 += __shfl_xor(p0, 16, 64);
+        p1 += __shfl_xor(p1, 16, 64);
+        p0 += __shfl_xor(p0, 32, 64);
+        p1 += __shfl_xor(p1, 32, 64);
+        if (kq == 0) sP[cur][w][n] = make_float2(p0, p1);
+        if (more) store_rows(sX[cur ^ 1]);        // read by the next block after the barrier
+        __syncthreads();
+        if (t < 16) {
+            const int64_t row = blk * 16 + t;
+            if (row < R) {
+                float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+                for (int q = 0; q < AH_W; ++q) {
+                    s0 += sP[cur][q][t].x;
+                    s1 += sP[cur][q][t].y;
+                }
+                float a0 = tanhf(s0 + ba0), a1 = tanhf(s1 + ba1);
+                if (noisy) {
+                    float n0, n1;
+                    row_noise(row, N, episode, eps_end, noise_start, noise_end, seed, ctr, n0, n1);
+                    a0 = fminf(fmaxf(a0 + n0, -1.0f), 1.0f);
+                    a1 = fminf(fmaxf(a1 + n1, -1.0f), 1.0f);
+                    if (noise_out) reinterpret_cast<float2 *>(noise_out)[row] = make_float2(n0, n1);
+                }
+                reinterpret_cast<float2 *>(act)[row] = make_float2(a0, a1);
+            }
+        }
+        cur ^= 1;
+    }
+}
+
 #define LHIP(x)                                                                                  \
     do {                                                                                         \
         hipError_t _e = (x);                                                                     \
@@ -753,6 +880,26 @@ int aac_actor_out_noise(const float *ha, int64_t R, const float *wa, const float
     if (noisy && !counter) return lfail("actor_out_noise: noisy needs the counter");
     const int64_t wg = (R + 4 * AON_RW - 1) / (4 * AON_RW);
     hipLaunchKernelGGL(actor_out_noise_kernel, dim3((unsigned)wg), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, ha, R, wa,
+                       ba, act, N, episode, eps_end, noise_start, noise_end, seed, counter, noisy, noise_out);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_actor_head_ws(const float *cat, int32_t ldc, int64_t R, const float *wm, const float *bm, const float *wa,
+                      const float *ba, float *act, int32_t N, const int32_t *episode, int32_t eps_end,
+                      float noise_start, float noise_end, uint64_t seed, uint64_t *counter, int32_t noisy,
+                      float *noise_out, void *stream) {
+    if (R <= 0) return 0;
+    if (N <= 0 || R % N) return lfail("actor_head_ws: R must be a multiple of N > 0");
+    auto al = [](const void *p, int a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+    if (!cat || !wm || !bm || !wa || !ba || !act) return lfail("actor_head_ws: NULL operand");
+    if (ldc < 192 || ldc % 4 || !al(cat, 16) || !al(wm, 16) || !al(bm, 16) || !al(wa, 16) || !al(act, 8) ||
+        !al(noise_out, 8))
+        return lfail("actor_head_ws: cat rows (ldc >= 192, % 4), wm, bm, wa 16-B aligned, act / noise_out 8-B");
+    if (noisy && !counter) return lfail("actor_head_ws: noisy needs the counter");
+    const int64_t nblk = (R + 15) / 16;
+    const int wg = (int)std::min<int64_t>(nblk, 256);      // one workgroup per CU
+    hipLaunchKernelGGL(actor_head_ws_kernel, dim3(wg), dim3(64 * AH_W), 0, (hipStream_t)stream, cat, ldc, R, wm, bm, wa,
                        ba, act, N, episode, eps_end, noise_start, noise_end, seed, counter, noisy, noise_out);
     LHIP(hipGetLastError());
     return 0;

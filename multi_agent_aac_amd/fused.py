@@ -91,6 +91,10 @@ def lib():
                                          vp]
         L.aac_attn_enc_fwd.argtypes = [ctypes.POINTER(AttnEncArgs), i32, vp]
         L.aac_attn_enc_fwd_head.argtypes = [ctypes.POINTER(AttnEncArgs), i32, ctypes.POINTER(HeadJob), vp]
+        L.aac_attn_train_bwd_wn.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, i32,
+                                            i32, vp, vp, vp]
+        L.aac_attn_train_bwd_partials.argtypes = [i32]
+        L.aac_attn_train_bwd_partials.restype = i32
         L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
         _L = L
     return _L
@@ -337,6 +341,18 @@ def attn_train_bwd(dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq, Wk, Wv, dx
          "aac_attn_train_bwd")
 
 
+def attn_train_bwd_wn(dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq, Wk, Wv, dqk, dq, deo, R, K, nei, pwn):
+    """aac_attn_train_bwd_wn: the attention backward with the neighbour encoder's weight-gradient
+    partials (pwn rows) instead of the d x_j rows."""
+    _chk(lib().aac_attn_train_bwd_wn(vp(dv), lddv, vp(xn), vp(alpha), vp(qk), vp(eo), lde, vp(dcat_o), ldd, vp(Wq),
+                                     vp(Wk), vp(Wv), None, vp(dqk), vp(dq), vp(deo), R, K, vp(nei), vp(pwn),
+                                     _stream()), "aac_attn_train_bwd_wn")
+
+
+def attn_bwd_partials(R):
+    return int(lib().aac_attn_train_bwd_partials(R))
+
+
 def attn_block(eo, lde, nei, Wn, bn, Wqk, Wv, out, ldo, R, K):
     _chk(lib().aac_attn_block(vp(eo), lde, vp(nei), vp(Wn), vp(bn), vp(Wqk), vp(Wv), vp(out), ldo, R, K, _stream()),
          "aac_attn_block")
@@ -450,6 +466,12 @@ def critic_forward(cp, X, rows, N, Din, f, h):
     return gemm_launches(enc) + gemm_launches(comb)
 
 
+# the act path's merge + output layer (+ noise) as one weights-stationary launch (aac_actor_head_ws)
+# instead of a grouped-GEMM launch + aac_actor_out_noise: measured slower at config 3 (32.6 us against
+# 17.7 + 10.5 us; the merge product's LDS-tile launch runs at ~110 TF/s), so off by default
+ACT_HEAD_WS = os.environ.get("AAC_ACT_HEAD_WS", "0") == "1"
+
+
 class ActorInfer:
     """Batched choose_action forward (ATT/maddpg:455-550) of one actor over E*N rows, as a cached
     launch list per input buffer set."""
@@ -472,12 +494,21 @@ class ActorInfer:
             out = torch.empty(R, 2, dtype=torch.float32, device=self.dev)
             attn, merge, outp = actor_infer_stages(self.ap, acts, ptr(own), self.D0, ptr(radar), ptr(nei), R,
                                                    self.K, self.D0, ptr(out), 2)
-            L = [AttnEnc(attn)] + gemm_launches(merge)
+            L = [AttnEnc(attn)] + ([] if ACT_HEAD_WS else gemm_launches(merge))
             self.plans[key] = (L, gemm_launches(outp), acts, out, (own, radar, nei))
         L, Lout, acts, out, _ = self.plans[key]
         for op in L:
             op()
-        if noise is None:
+        ap = self.ap
+        if ACT_HEAD_WS:
+            # merge + output layer (+ noise) in one weights-stationary launch (aac_actor_head_ws)
+            if noise is None:
+                ops.actor_head_ws(acts.cat, ap.Wm, ap.bm, ap.Wa, ap.ba, out, self.N, noisy=False)
+            else:
+                episode, eps_end, noise_start, noise_end, seed, counter, noise_out = noise
+                ops.actor_head_ws(acts.cat, ap.Wm, ap.bm, ap.Wa, ap.ba, out, self.N, episode, eps_end, noise_start,
+                                  noise_end, seed, counter, noise_out)
+        elif noise is None:
             for op in Lout:
                 op()
         else:
@@ -537,6 +568,13 @@ class FusedUpdate:
         self.dout, self.dha = z(R, 2), z(R, 256)
         self.dcat_o, self.dcat_g, self.dv = z(R, 64), z(R, 64), z(R, 64)
         self.dqa, self.dqk, self.deo, self.dxn = z(R, 64), z(R, 64), z(R, 64), z(R * K, 64)
+        # K <= 8: the attention backward accumulates dWn | dbn per workgroup (pwn rows, zero rows up to
+        # the split count); a [1 x P] x [P x 448] product sums them into the split copies
+        self.wn_part = K <= 8 and os.environ.get("AAC_ATTN_WN", "1") == "1"
+        if self.wn_part:
+            P = max(attn_bwd_partials(R), self.SPLIT_ACTOR)
+            self.pwn = torch.zeros(P, 448, device=dev)
+            self.ones_p = torch.ones(P, device=dev)
         # weight-gradient partial copies (summed by the Adam kernel)
         self.ga = torch.zeros(self.SPLIT_ACTOR, padded(model.fa.numel), device=dev)
         self.gc = torch.zeros(self.SPLIT_CRITIC, padded(model.fc.numel), device=dev)
@@ -851,16 +889,26 @@ class FusedUpdate:
             prob(ptr(self.dha), A.Wm + 4 * 64, ptr(self.dcat_g), R, 64, 256, 256, 192, 64, mask=ptr(c.cat, 64),
                  ldmask=192, mact=RELU),
             prob(ptr(self.dha), A.Wm + 4 * 128, ptr(self.dv), R, 64, 256, 256, 192, 64)]
-        st["attn_bwd"] = lambda: attn_train_bwd(  # noqa: E731
-            ptr(self.dv), 64, ptr(c.xn), ptr(c.alpha), ptr(c.qk), ptr(c.cat), 192, ptr(self.dcat_o), 64, A.Wq, A.Wkv,
-            A.Wkv + 4 * 64 * 64, ptr(self.dxn), ptr(self.dqk), ptr(self.dqa), ptr(self.deo), R, K)
+        if self.wn_part:
+            st["attn_bwd"] = lambda: attn_train_bwd_wn(  # noqa: E731
+                ptr(self.dv), 64, ptr(c.xn), ptr(c.alpha), ptr(c.qk), ptr(c.cat), 192, ptr(self.dcat_o), 64, A.Wq,
+                A.Wkv, A.Wkv + 4 * 64 * 64, ptr(self.dqk), ptr(self.dqa), ptr(self.deo), R, K, nei, ptr(self.pwn))
+            # dWn | dbn (adjacent in the flat gradient) = the sum of the partial rows
+            assert gA.bn == gA.Wn + 4 * 64 * 6
+            P = self.pwn.shape[0]
+            dwn = prob(ptr(self.ones_p), ptr(self.pwn), gA.Wn, 1, 448, P, P, 448, 448, ksplit=SA, split_stride=nA)
+        else:
+            st["attn_bwd"] = lambda: attn_train_bwd(  # noqa: E731
+                ptr(self.dv), 64, ptr(c.xn), ptr(c.alpha), ptr(c.qk), ptr(c.cat), 192, ptr(self.dcat_o), 64, A.Wq,
+                A.Wkv, A.Wkv + 4 * 64 * 64, ptr(self.dxn), ptr(self.dqk), ptr(self.dqa), ptr(self.deo), R, K)
+            dwn = prob(ptr(self.dxn), nei, gA.Wn, 64, 6, R * K, 64, 6, 6, ta=1, ones=1, cextra=gA.bn, ksplit=SA,
+                       split_stride=nA)
         st["wgrad2"] = [
             prob(ptr(self.dv), ptr(c.xb), gA.Wkv + 4 * 64 * 64, 64, 64, R, 64, 64, 64, ta=1, ksplit=SA,
                  split_stride=nA),                                                         # dWv
             prob(ptr(c.qa), ptr(self.dqk), gA.Wkv, 64, 64, R, 64, 64, 64, ta=1, ksplit=SA, split_stride=nA),  # dWk
             prob(ptr(self.dqa), ptr(c.cat), gA.Wq, 64, 64, R, 64, 192, 64, ta=1, ksplit=SA, split_stride=nA),
-            prob(ptr(self.dxn), nei, gA.Wn, 64, 6, R * K, 64, 6, 6, ta=1, ones=1, cextra=gA.bn, ksplit=SA,
-                 split_stride=nA),
+            dwn,
             prob(ptr(self.deo), X, gA.Wo, 64, D0, R, 64, Din, D0, ta=1, ones=1, cextra=gA.bo, ksplit=SA,
                  split_stride=nA),
             prob(ptr(self.dcat_g), radar, gA.Wg, 64, 18, R, 64, 18, 18, ta=1, ones=1, cextra=gA.bg, ksplit=SA,

@@ -27,6 +27,7 @@ def lib():
         L.aac_attn_bwd.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, i32, i32, vp]
         L.aac_replay_push.argtypes = [vp, i32, i64, vp, i32, vp, vp, vp, i32, vp]
         L.aac_actor_out_noise.argtypes = [vp, i64, vp, vp, vp, i32, vp, i32, f32, f32, u64, vp, i32, vp, vp]
+        L.aac_actor_head_ws.argtypes = [vp, i32, i64, vp, vp, vp, vp, vp, i32, vp, i32, f32, f32, u64, vp, i32, vp, vp]
         L.aac_replay_push_at.argtypes = [vp, i32, i64, vp, i64, i64, i32, vp, vp, vp, i32, vp]
         L.aac_replay_sample.argtypes = [vp, i32, i32, u64, vp, vp, vp]
         L.aac_replay_gather.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp]
@@ -144,6 +145,17 @@ def actor_out_noise(ha, wa, ba, act, N, episode, eps_end, noise_start, noise_end
     R = ha.shape[0]
     _chk(lib().aac_actor_out_noise(_p(ha), R, vp(wa), vp(ba), _p(act), N, _p(episode), eps_end, noise_start, noise_end,
                                    u64(seed), _p(counter), int(noisy), _p(noise_out), _s()), "aac_actor_out_noise")
+
+
+def actor_head_ws(cat, wm, bm, wa, ba, act, N, episode=None, eps_end=1, noise_start=0.0, noise_end=0.0, seed=0,
+                  counter=None, noise_out=None, noisy=True):
+    """act[R][2] = clamp(tanh(wa relu(wm cat + bm) + ba) + noise) over the rows of cat [R][192]
+    (aac_actor_head_ws: merge + output layer + noise in one weights-stationary launch; wm, bm, wa, ba
+    device addresses)."""
+    R = cat.shape[0]
+    _chk(lib().aac_actor_head_ws(_p(cat), cat.stride(0), R, vp(wm), vp(bm), vp(wa), vp(ba), _p(act), N, _p(episode),
+                                 eps_end, noise_start, noise_end, u64(seed), _p(counter), int(noisy), _p(noise_out),
+                                 _s()), "aac_actor_head_ws")
 
 
 def noise_clamp(act, episode, eps_end, noise_start, seed, counter, noise_out=None, noise_end=0.0):

@@ -346,16 +346,21 @@ def test_attn_block_matches_reference_attention(native_lib, K):
     np.testing.assert_allclose(out.cpu().double(), want, atol=2e-5, rtol=1e-5)
 
 
-def test_fused_act_matches_ref_actor(native_lib):
-    """The fused HIP choose_action forward (encoders, aac_attn_block, merge, tanh) at config 2's
-    size (E = 1024 envs x N = 5 agents) against oracle/learner_ref.RefActor, the CPU restatement of
-    ActorNetwork_ATT_TwoPortion (ATT/nets:177-213), loaded with the same reference state_dict."""
+@pytest.mark.parametrize("ws,E", [(True, 1024), (True, 77), (False, 1024)])
+def test_fused_act_matches_ref_actor(native_lib, monkeypatch, ws, E):
+    """The fused HIP choose_action forward (encoders + attention in one launch, then merge + tanh: the
+    weights-stationary aac_actor_head_ws when ``ws``, else a grouped-GEMM launch + aac_actor_out_noise)
+    at config 2's size (E = 1024 envs x N = 5 agents; E = 77: a ragged last row block) against
+    oracle/learner_ref.RefActor, the CPU restatement of ActorNetwork_ATT_TwoPortion (ATT/nets:177-213),
+    loaded with the same reference state_dict."""
+    from multi_agent_aac_amd import fused
     from multi_agent_aac_amd.maddpg import MADDPG
+    monkeypatch.setattr(fused, "ACT_HEAD_WS", ws)
     m = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=5, device=DEV, seed=3)
     ref = learner_ref.RefActor([22, 18, 6], 2)
     ref.load_state_dict({k: v.cpu() for k, v in m.actors.reference_state_dict().items()})
     g = torch.Generator().manual_seed(5)
-    E, N = 1024, 5
+    N = 5
     own, radar = torch.randn(E, N, 22, generator=g), torch.rand(E, N, 18, generator=g) * 15
     nei = torch.randn(E, N, 4, 6, generator=g)
     nei[::7, :, 1] = 0.0                         # masked neighbours
@@ -423,6 +428,21 @@ def test_attn_train_fwd_bwd_matches_autograd(native_lib, K):
     np.testing.assert_allclose(dxn.cpu().double().reshape(R, K, 64), x_r.grad * (d(x) > 0), atol=2e-5, rtol=1e-5)
     np.testing.assert_allclose(dq.cpu().double(), q_r.grad, atol=2e-5, rtol=1e-5)
     np.testing.assert_allclose(deo.cpu().double(), eo_r.grad * (d(eo) > 0), atol=2e-5, rtol=1e-5)
+    if K <= 8:
+        # the same backward with the neighbour encoder's weight-gradient partials instead of the dx_j
+        # rows: the rows sum to dWn | dbn = sum dx_j^T [nei_j | 1]; dqk, dq, deo bit-identical
+        npart = fused.attn_bwd_partials(R)
+        pwn = torch.full((npart, 448), 7.0, device=DEV)
+        dqk2, dq2, deo2 = z(R, 64), z(R, 64), z(R, 64)
+        fused.attn_train_bwd_wn(P(dv), 64, P(x), P(alpha), P(qk), P(cat), 192, P(dcat_o), 64, P(Wq), P(kv),
+                                P(kv, 64 * 64), P(dqk2), P(dq2), P(deo2), R, K, P(nei), P(pwn))
+        torch.cuda.synchronize()
+        assert torch.equal(dqk2, dqk) and torch.equal(dq2, dq) and torch.equal(deo2, deo)
+        g = d(dxn).reshape(R * K, 64)
+        want_w = g.t() @ d(nei).reshape(R * K, 6)
+        tot = d(pwn).sum(0)
+        np.testing.assert_allclose(tot[:384].reshape(64, 6), want_w, atol=2e-4, rtol=1e-5)
+        np.testing.assert_allclose(tot[384:], g.sum(0), atol=2e-4, rtol=1e-5)
 
 
 @pytest.mark.parametrize("K", [1, 4, 7])
