@@ -755,8 +755,10 @@ def main():
     tr.env_events.clear()
     t0 = time.perf_counter()
     with trace.range("timed_steps"):
-        for _ in range(a.steps):
-            tr.step(update=True, time_env=True)
+        for k in range(a.steps):
+            # HIP events around the env launch on every 5th timed step only: an event pair costs ~5 us of
+            # stream time on each side of the launch it brackets
+            tr.step(update=True, time_env=(k % 5 == 0))
     barrier(ws)
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], device="cuda")

@@ -467,9 +467,9 @@ def critic_forward(cp, X, rows, N, Din, f, h):
 
 
 # the act path's merge + output layer (+ noise) as one weights-stationary launch (aac_actor_head_ws)
-# instead of a grouped-GEMM launch + aac_actor_out_noise: measured slower at config 3 (32.6 us against
-# 17.7 + 10.5 us; the merge product's LDS-tile launch runs at ~110 TF/s), so off by default
-ACT_HEAD_WS = os.environ.get("AAC_ACT_HEAD_WS", "0") == "1"
+# instead of a grouped-GEMM launch + aac_actor_out_noise (config 3: 32.6 us against 26.2 + 10.2 us);
+# AAC_ACT_HEAD_WS=0 keeps the two launches
+ACT_HEAD_WS = os.environ.get("AAC_ACT_HEAD_WS", "1") == "1"
 
 
 class ActorInfer:
