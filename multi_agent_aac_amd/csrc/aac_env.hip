@@ -92,7 +92,6 @@ struct Tail {
     const void *src[TAIL_MAX_FIELDS];          // early fields: [E][width] sources
     int width[TAIL_MAX_FIELDS], col[TAIL_MAX_FIELDS], dtype[TAIL_MAX_FIELDS];   // col: first ring column
     int cum[TAIL_MAX_FIELDS + 1];              // early fields' running column counts (cum[nf] = n_early)
-    const uint8_t *lut;       // [n_early] compact column -> early field (device, built by the host)
     int late[LATE_N];         // first ring column of each step output, -1 = not pushed
     float *zero_rows;         // [E][zero_w] rows zeroed for the finished envs (after the push); null = none
     int zero_w;
@@ -727,36 +726,37 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
 }
 
 // Fused step tail, part 1 (aac_env_step_tail): the early fields of the workgroup's nv transitions,
-// copied by the waves that the kinematics phase leaves idle (waves 1..3 when the workgroup's agents
-// fit in wave 0; else every wave, at kernel start).  The compact-column -> field table is built by
-// the host (T.lut, device memory, rebuilt when the layout changes); each copying wave puts its own
-// copy of the field descriptors in LDS scratch (the observation staging area, free until the
-// observation phase), so no workgroup barrier is involved and the copy's load latency hides under
-// the kinematics.  (First form: every thread, at kernel start, with an in-kernel table and two
-// barriers: +8.7 us per step at 4096 x 5; looked up from the kernel arguments per element, the
-// descriptors were re-read with scalar loads for every element: +34 us.)  Items are (column, env)
-// pairs, U loads in flight before the stores.
+// copied at kernel start.  Their descriptors and a compact-column -> field table go to LDS scratch
+// (the observation staging area, free until the observation phase) once per workgroup: looked up per
+// element from the kernel arguments, the descriptors were re-read with scalar loads for every element
+// (0.042 -> 0.075 ms per step at 4096 x 5).  Thread t owns the compact columns t, t + BLOCK, ...;
+// its items are (column, env) pairs with U loads in flight before the stores.
 struct TailDesc {
-    const char *base;      // the field's source, minus its first compact column (bytes)
+    const void *src;
     int width, shift;      // width | dtype << 30; shift = ring column - compact column
 };
 static_assert(sizeof(TailDesc) == 16, "one ds_read_b128 per descriptor");
 
-__device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, int e0, int nv, float *scratch,
-                                                                int t_first, int nthreads) {
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    TailDesc *desc = reinterpret_cast<TailDesc *>(scratch) + w * TAIL_MAX_FIELDS;    // this wave's copy
+__device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, int e0, int nv, float *scratch) {
+    const int t = threadIdx.x;
+    TailDesc *desc = reinterpret_cast<TailDesc *>(scratch);
+    int *cum = reinterpret_cast<int *>(desc + TAIL_MAX_FIELDS);
+    uint8_t *lut = reinterpret_cast<uint8_t *>(cum + TAIL_MAX_FIELDS + 1);
+    const int ne = T.cum[T.nf];
 #pragma unroll
     for (int q = 0; q < TAIL_MAX_FIELDS; ++q)
-        if (lane == q) {
-            const int es = T.dtype[q] ? 1 : 4;
-            desc[q] = TailDesc{reinterpret_cast<const char *>(T.src[q]) - (ptrdiff_t)T.cum[q] * es,
-                               T.width[q] | (T.dtype[q] << 30), T.col[q] - T.cum[q]};
+        if (t == q) {
+            desc[q] = TailDesc{T.src[q], T.width[q] | (T.dtype[q] << 30), T.col[q] - T.cum[q]};
+            cum[q] = T.cum[q];
         }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");      // one wave's LDS operations run in order
-    const int tt = t - t_first, ne = T.cum[T.nf];
-    const int ncol = tt < ne ? (ne - tt + nthreads - 1) / nthreads : 0;
+    __syncthreads();
+    for (int k = t; k < ne; k += BLOCK) {
+        int f = 0;
+        for (int q = 1; q < T.nf; ++q) f += k >= cum[q];
+        lut[k] = (uint8_t)f;
+    }
+    __syncthreads();
+    const int ncol = t < ne ? (ne - t + BLOCK - 1) / BLOCK : 0;
     const int items = ncol * nv;
     constexpr int U = 8;
     for (int j0 = 0; j0 < items; j0 += U) {
@@ -767,19 +767,21 @@ __device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, in
             const int j = j0 + u;
             const bool ok = j < items;
             const int sl = j / nv, r = j - sl * nv;
-            const int k = ok ? tt + sl * nthreads : 0;
-            const TailDesc d = desc[T.lut[k]];
-            const int wd = d.width & 0x3fffffff;
+            const int k = ok ? t + sl * BLOCK : 0;
+            const int f = lut[k];
+            const TailDesc d = desc[f];
+            const int w = d.width & 0x3fffffff;
             dst[u] = ok ? ring_row(T, e0 + r) + k + d.shift : nullptr;
-            const size_t si = (size_t)(e0 + r) * wd + k;
+            const size_t si = (size_t)(e0 + r) * w + (k - cum[f]);
             v[u] = !ok ? 0.f
-                       : ((d.width >> 30) ? (float)reinterpret_cast<const uint8_t *>(d.base)[si]
-                                          : reinterpret_cast<const float *>(d.base)[si]);
+                       : ((d.width >> 30) ? (float)reinterpret_cast<const uint8_t *>(d.src)[si]
+                                          : reinterpret_cast<const float *>(d.src)[si]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (dst[u]) *dst[u] = v[u];
     }
+    __syncthreads();      // the scratch area is the observation staging area of the step
 }
 
 // --------------------------------------------------------------------------------- step
@@ -820,12 +822,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
                 T.meta[0] = T.new_pos;
                 T.meta[1] = T.new_size;
             }
-            // waves 1..3 copy while wave 0 runs the kinematics (agents of the workgroup <= 64), else all
-            if (nag <= 64) {
-                if (t >= 64) tail_push_early(T, e0, nv, S.obs, 64, BLOCK - 64);
-            } else {
-                tail_push_early(T, e0, nv, S.obs, 0, BLOCK);
-            }
+            tail_push_early(T, e0, nv, S.obs);
             if (T.late[LATE_RADAR] >= 0) ro = RingOut{T.ring, T.pos, T.cap, T.rw, T.late[LATE_RADAR]};
         }
     }
@@ -1158,9 +1155,6 @@ struct aac_env {
     int32_t bank_n, bank_maps;
     uint64_t bank_seed;
     int32_t *rlist;           // [1 + E]: packed resetting envs of the last auto-reset
-    uint8_t *tail_lut;        // aac_env_step_tail: compact early column -> field (device)
-    int32_t tail_lut_cap, tail_sig_n;
-    int32_t tail_sig[TAIL_MAX_FIELDS];   // the early field widths the table was built for
 };
 
 // dynamic LDS of the step / reset kernels: the handle's occupancy maps and their row masks
@@ -1319,7 +1313,7 @@ void aac_env_destroy(aac_env *h) {
     if (!h) return;
     void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->start, h->wp, h->wp_cur, h->wp_cnt, h->wall,
                     h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt,
-                    h->bank_off, h->rlist, h->occ_rows, h->tail_lut};
+                    h->bank_off, h->rlist, h->occ_rows};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -1419,26 +1413,8 @@ int aac_env_step_tail(aac_env *h, const float *actions, const aac_step_out *o, c
             T.col[q] = 0;
             T.cum[q + 1] = ne;
         }
-        if (ne > 255 * 256) return fail(AAC_E_INVALID, "step tail: too many early columns");
-        // the compact-column -> field table (device), rebuilt only when the early widths change (the
-        // upload is synchronous: a layout's first call must not be inside a stream capture)
-        bool same = h->tail_lut && h->tail_lut_cap >= ne && h->tail_sig_n == T.nf;
-        for (int q = 0; same && q < T.nf; ++q) same = h->tail_sig[q] == T.width[q];
-        if (!same) {
-            std::vector<uint8_t> lut(std::max(ne, 1), 0);
-            for (int q = 0; q < T.nf; ++q)
-                for (int k = T.cum[q]; k < T.cum[q + 1]; ++k) lut[k] = (uint8_t)q;
-            if (h->tail_lut_cap < ne || !h->tail_lut) {
-                if (h->tail_lut) (void)hipFree(h->tail_lut);
-                h->tail_lut = nullptr;
-                HIPCHK(hipMalloc((void **)&h->tail_lut, lut.size()));
-                h->tail_lut_cap = (int32_t)lut.size();
-            }
-            HIPCHK(hipMemcpy(h->tail_lut, lut.data(), lut.size(), hipMemcpyHostToDevice));
-            h->tail_sig_n = T.nf;
-            for (int q = 0; q < T.nf; ++q) h->tail_sig[q] = T.width[q];
-        }
-        T.lut = h->tail_lut;
+        if (sizeof(TailDesc) * TAIL_MAX_FIELDS + sizeof(int) * (TAIL_MAX_FIELDS + 1) + ne > sizeof(float) * OBS_STAGE_FLOATS)
+            return fail(AAC_E_INVALID, "step tail: too many early columns for the column table");
         if ((T.late[LATE_OWN] >= 0 || T.late[LATE_NEI] >= 0) &&
             h->epb * h->cfg.N * (h->D0 + 6 * K) > OBS_STAGE_FLOATS)
             return fail(AAC_E_INVALID, "step tail: observation rows too wide to push from the staging area");
