@@ -262,6 +262,45 @@ class Trainer(CheckpointMixin):
         self.env.auto_reset(None, out=self.cur)      # all envs: first OD draw + initial obs
         self.env_events = []
         self.fused_tail = (not self.gru) if FUSED_TAIL is None else FUSED_TAIL
+        self.bufs = [self.cur, self.nxt]
+        self._sg = {}                                 # parity -> captured whole-step graph
+        self.pos_dev = torch.zeros(2, dtype=torch.int64, device="cuda")   # ring position ping-pong
+
+    def graph_ok(self):
+        """Whole-step graphs: the ATT env with the fused tail, one rank, the fused learner."""
+        return (STEP_GRAPH and not self.gru and self.fused_tail and self.model.world == 1 and self.model.fused
+                and not NO_GRAPH and len(self.replay) > self.B)
+
+    def _capture_step(self, p):
+        """act + env step tail + update_myown of a step whose current buffers are bufs[p], captured
+        as one HIP graph.  Nothing runs during the capture; the replay's host mirror is restored."""
+        c, n = self.bufs[p], self.bufs[1 - p]
+        fu = self.model._fused_plan(self.B)
+        side = torch.cuda.Stream()
+        saved = (self.replay.pos, self.replay.size)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
+            srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei]
+            self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs, pos_io=(self.pos_dev[p], self.pos_dev[1 - p]))
+            fu.run_streams(side)
+        self.replay.pos, self.replay.size = saved
+        self._sg[p] = (g, side)
+
+    def step_graph(self):
+        """One training step as one graph replay (the same launches as ``step(update=True)``; the
+        ring position lives in device words, the host keeps its mirror)."""
+        p = 0 if self.cur is self.bufs[0] else 1
+        if not self._sg:
+            for q in (0, 1):
+                self._capture_step(q)
+            self.pos_dev[p].fill_(self.replay.pos)
+        with trace.range("step_graph"):
+            self._sg[p][0].replay()
+        rep = self.replay
+        rep.pos = (rep.pos + self.E) % rep.capacity
+        rep.size = min(rep.size + self.E, rep.capacity)
+        self.cur, self.nxt = self.nxt, self.cur
 
     def env_episode_view(self):
         # the env's own per-env episode counter (advanced by each auto-reset; 1 after the first)
@@ -333,6 +372,10 @@ OVERLAP_RESET = os.environ.get("AAC_OVERLAP_RESET", "0") == "1"   # measured slo
 # nearly every workgroup of the two-round grid (0.131 -> 0.144 ms).  AAC_FUSED_TAIL=0 / 1 forces it.
 _FT = os.environ.get("AAC_FUSED_TAIL")
 FUSED_TAIL = None if _FT is None else _FT == "1"
+# config 3: each timed step (act + fused env tail + update) replays one captured HIP graph (one per
+# buffer parity; AAC_STEP_GRAPH=1).  Measured neutral (0.8926 vs 0.8929 ms per step: the host already
+# runs ahead of the device), so the steps are launched from the host by default
+STEP_GRAPH = os.environ.get("AAC_STEP_GRAPH", "0") == "1"
 
 
 class side_stream:
@@ -754,17 +797,32 @@ def main():
     barrier(ws)
     tr.env_events.clear()
     t0 = time.perf_counter()
+    graphed = hasattr(tr, "graph_ok") and tr.graph_ok()
+    if graphed:
+        tr.step_graph()           # capture both parities (untimed) and replay once
+        tr.step_graph()
+        torch.cuda.synchronize()
+        barrier(ws)
+        t0 = time.perf_counter()
     with trace.range("timed_steps"):
         for k in range(a.steps):
-            # HIP events around the env launch on every 5th timed step only: an event pair costs ~5 us of
-            # stream time on each side of the launch it brackets
-            tr.step(update=True, time_env=(k % 5 == 0))
+            if graphed:
+                tr.step_graph()
+            else:
+                # HIP events around the env launch on every 5th timed step only: an event pair costs
+                # ~5 us of stream time on each side of the launch it brackets
+                tr.step(update=True, time_env=(k % 5 == 0))
     barrier(ws)
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], device="cuda")
     if ws > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t)
+    if graphed:
+        # the env launch is inside the step graphs: time it on 10 eager steps after the timed region
+        for k in range(10):
+            tr.step(update=True, time_env=True)
+        torch.cuda.synchronize()
     env_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in tr.env_events]))
     E_total = a.envs * ws
     N = a.agents
@@ -827,6 +885,7 @@ def main():
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
                    "maps": 1 if uam else a.maps, "tdcpa": uam,
                    "update_graph": (not a.no_graph) and (ws == 1 or uam or tr.gru or tr.model.fused),
+                   "step_graph": graphed,
                    "graph_segments": "one per update" if ws == 1 else "cut at each gradient all-reduce"},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if (tr.gru or uam) else N),
         "env_roofline": {"kernel": "uam_step_kernel (fused UAM env step)" if uam else (

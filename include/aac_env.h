@@ -106,6 +106,11 @@ typedef struct {
     float *zero_rows;           /* device float[E][zero_width], rows of finished envs set to 0; or NULL */
     int32_t zero_width;
     int32_t auto_reset;         /* 1: redraw the finished envs from the OD bank (after the push)        */
+    /* graph replays: when pos_in != NULL the ring position is read from that device word (pos and
+     * size above are ignored); the launch stores the advanced position to pos_out (a different word)
+     * and to meta[0], and the advanced size to meta[1].  Alternate the two words between steps. */
+    const int64_t *pos_in;
+    int64_t *pos_out;
 } aac_step_tail;
 int aac_env_step_tail(aac_env *env, const float *actions_dev, const aac_step_out *out, const aac_step_tail *tail,
                       void *stream);

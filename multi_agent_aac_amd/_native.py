@@ -43,7 +43,7 @@ class StepTail(ctypes.Structure):
     _fields_ = [("ring", vp), ("row_width", i32), ("capacity", ctypes.c_int64), ("pos", ctypes.c_int64),
                 ("size", ctypes.c_int64), ("meta", vp), ("n_fields", i32), ("srcs", ctypes.POINTER(vp)),
                 ("widths", ctypes.POINTER(i32)), ("dtypes", ctypes.POINTER(i32)), ("zero_rows", vp),
-                ("zero_width", i32), ("auto_reset", i32)]
+                ("zero_width", i32), ("auto_reset", i32), ("pos_in", vp), ("pos_out", vp)]
 
 
 _lib = None

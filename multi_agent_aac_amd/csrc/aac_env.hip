@@ -89,6 +89,8 @@ struct Tail {
     int64_t cap, pos;         // host mirror of the ring position before this push
     int64_t *meta;            // device [pos, size] for the sampler, stored by workgroup 0
     int64_t new_pos, new_size;
+    const int64_t *pos_in;    // non-null: the position is read here (ignoring pos) and the advanced one is
+    int64_t *pos_out;         // stored to pos_out (another word: every workgroup reads pos_in), size in meta
     const void *src[TAIL_MAX_FIELDS];          // early fields: [E][width] sources
     int width[TAIL_MAX_FIELDS], col[TAIL_MAX_FIELDS], dtype[TAIL_MAX_FIELDS];   // col: first ring column
     int cum[TAIL_MAX_FIELDS + 1];              // early fields' running column counts (cum[nf] = n_early)
@@ -99,8 +101,8 @@ struct Tail {
 };
 
 // ring row of env e for this push (pos < cap, e < E <= cap)
-__device__ inline float *ring_row(const Tail &T, int e) {
-    int64_t row = T.pos + e;
+__device__ inline float *ring_row(const Tail &T, int64_t pos, int e) {
+    int64_t row = pos + e;
     if (row >= T.cap) row -= T.cap;
     return T.ring + row * T.rw;
 }
@@ -737,7 +739,8 @@ struct TailDesc {
 };
 static_assert(sizeof(TailDesc) == 16, "one ds_read_b128 per descriptor");
 
-__device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, int e0, int nv, float *scratch) {
+__device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, int64_t rpos, int e0, int nv,
+                                                                float *scratch) {
     const int t = threadIdx.x;
     TailDesc *desc = reinterpret_cast<TailDesc *>(scratch);
     int *cum = reinterpret_cast<int *>(desc + TAIL_MAX_FIELDS);
@@ -771,7 +774,7 @@ __device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, in
             const int f = lut[k];
             const TailDesc d = desc[f];
             const int w = d.width & 0x3fffffff;
-            dst[u] = ok ? ring_row(T, e0 + r) + k + d.shift : nullptr;
+            dst[u] = ok ? ring_row(T, rpos, e0 + r) + k + d.shift : nullptr;
             const size_t si = (size_t)(e0 + r) * w + (k - cum[f]);
             v[u] = !ok ? 0.f
                        : ((d.width >> 30) ? (float)reinterpret_cast<const uint8_t *>(d.src)[si]
@@ -814,16 +817,26 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     const int nv = e0 + A.epb <= A.E ? A.epb : A.E - e0;     // envs of this workgroup
     if (TAIL && t < A.epb) S.active[t] = 0;      // env_done of the workgroup's envs (set below)
     RingOut ro{};
+    // the ring position of this push: the host's mirror, or (graph replays) a device word
+    const int64_t rpos = TAIL && T.ring ? (T.pos_in ? *T.pos_in : T.pos) : 0;
     if constexpr (TAIL) {
         if (T.ring) {
             // replay push, early fields (sources of earlier launches); this step's outputs are written
             // into the ring where they are produced (radar phase, staged rows, final phase)
             if (blockIdx.x == 0 && t == 0) {
-                T.meta[0] = T.new_pos;
-                T.meta[1] = T.new_size;
+                if (T.pos_in) {      // device-side position (graph replays): advance it here
+                    const int64_t np = rpos + A.E >= T.cap ? rpos + A.E - T.cap : rpos + A.E;
+                    const int64_t ns = T.meta[1] + A.E;
+                    *T.pos_out = np;
+                    T.meta[0] = np;
+                    T.meta[1] = ns < T.cap ? ns : T.cap;
+                } else {
+                    T.meta[0] = T.new_pos;
+                    T.meta[1] = T.new_size;
+                }
             }
-            tail_push_early(T, e0, nv, S.obs);
-            if (T.late[LATE_RADAR] >= 0) ro = RingOut{T.ring, T.pos, T.cap, T.rw, T.late[LATE_RADAR]};
+            tail_push_early(T, rpos, e0, nv, S.obs);
+            if (T.late[LATE_RADAR] >= 0) ro = RingOut{T.ring, rpos, T.cap, T.rw, T.late[LATE_RADAR]};
         }
     }
     load_maps(A);
@@ -1011,12 +1024,12 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
                 if (T.late[LATE_OWN] >= 0)
                     for (int j = t; j < nv * wo; j += BLOCK) {
                         const int r = j / wo;
-                        ring_row(T, e0 + r)[T.late[LATE_OWN] + (j - r * wo)] = S.obs[j];
+                        ring_row(T, rpos, e0 + r)[T.late[LATE_OWN] + (j - r * wo)] = S.obs[j];
                     }
                 if (T.late[LATE_NEI] >= 0)
                     for (int j = t; j < nv * wn; j += BLOCK) {
                         const int r = j / wn;
-                        ring_row(T, e0 + r)[T.late[LATE_NEI] + (j - r * wn)] = S.obs[nag * D0 + j];
+                        ring_row(T, rpos, e0 + r)[T.late[LATE_NEI] + (j - r * wn)] = S.obs[nag * D0 + j];
                     }
             }
         }
@@ -1026,7 +1039,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         A.reward[ai] = (float)team;
         if constexpr (TAIL) {
             if (T.ring) {
-                float *rr = ring_row(T, e);
+                float *rr = ring_row(T, rpos, e);
                 if (T.late[LATE_REW] >= 0) rr[T.late[LATE_REW] + i] = (float)team;
                 if (T.late[LATE_DONE] >= 0) rr[T.late[LATE_DONE] + i] = (float)(S.flags[t] & 1);
             }
@@ -1374,6 +1387,10 @@ int aac_env_step_tail(aac_env *h, const float *actions, const aac_step_out *o, c
         T.cap = t->capacity;
         T.pos = t->pos;
         T.meta = t->meta;
+        if ((t->pos_in == nullptr) != (t->pos_out == nullptr) || (t->pos_in && t->pos_in == t->pos_out))
+            return fail(AAC_E_INVALID, "step tail: pos_in and pos_out both set (two distinct words) or both NULL");
+        T.pos_in = t->pos_in;
+        T.pos_out = t->pos_out;
         T.new_pos = (t->pos + h->cfg.E) % t->capacity;
         T.new_size = std::min<int64_t>(t->size + h->cfg.E, t->capacity);
         for (int k = 0; k < LATE_N; ++k) T.late[k] = -1;

@@ -173,7 +173,7 @@ class BatchedEnv:
         return out
 
     def step_tail(self, actions, out: Optional[StepBuffers] = None, replay=None, srcs=None, zero_rows=None,
-                  auto_reset=True):
+                  auto_reset=True, pos_io=None):
         """``step`` + ``replay.push_batch(*srcs)`` + zeroing ``zero_rows`` ([E][...] float32) of the
         finished envs + ``auto_reset(out.env_done, out)``, fused into the one step launch
         (aac_env_step_tail).  ``srcs`` may name this step's outputs (``out.reward`` ...): the push reads
@@ -187,6 +187,12 @@ class BatchedEnv:
         if replay is not None:
             for k, v in replay.tail_push(srcs, self.E).items():
                 setattr(t, k, v)
+            if pos_io is not None:
+                # graph replays: the ring position is read from / advanced into device int64 words
+                # (alternate the pair between steps); the replay's host mirror advances as usual
+                pin, pout = pos_io
+                assert pin.dtype == torch.int64 and pout.dtype == torch.int64 and pin.data_ptr() != pout.data_ptr()
+                t.pos_in, t.pos_out = pin.data_ptr(), pout.data_ptr()
         if zero_rows is not None:
             assert zero_rows.dtype == torch.float32 and zero_rows.is_contiguous() and zero_rows.shape[0] == self.E
             assert zero_rows.device == self.device

@@ -134,3 +134,33 @@ def test_step_tail_rejects_bad_fields(native_lib, occ):
     rc = _native.lib().aac_env_step_tail(env._h, ctypes.c_void_p(act.data_ptr()), ctypes.byref(o), ctypes.byref(t),
                                          None)
     assert rc != 0 and b"OD bank" in _native.lib().aac_last_error()
+
+
+def test_whole_step_graph_equals_eager(native_lib):
+    """bench.Trainer.step_graph (act + fused env tail + update_myown replayed from one captured HIP graph
+    per buffer parity, the ring position in device words) against the same steps launched eagerly:
+    bit-identical networks, optimiser state, replay ring and env state."""
+    import bench
+    E, N, B = 256, 5, 64
+    tr = [bench.Trainer(E, N, B, 2000, "combined", seed=0) for _ in range(2)]
+    for t in tr:
+        while len(t.replay) <= 3 * B:
+            t.step(update=False)
+        for _ in range(2):
+            t.step(update=True)
+    assert tr[1].graph_ok()
+    for k in range(7):                      # odd: both parities, and the host mirror across the wrap
+        tr[0].step(update=True)
+        tr[1].step_graph()
+    torch.cuda.synchronize()
+    a, b = tr[0], tr[1]
+    for x, y in ((a.model.fa.data, b.model.fa.data), (a.model.fc.data, b.model.fc.data),
+                 (a.model.fa_t.data, b.model.fa_t.data), (a.model.fc_t.data, b.model.fc_t.data),
+                 (a.replay.ring, b.replay.ring), (a.replay.meta, b.replay.meta), (a.replay.counter, b.replay.counter),
+                 (a.model.noise_counter, b.model.noise_counter), (a.episode, b.episode)):
+        assert torch.equal(x, y)
+    assert (a.replay.pos, a.replay.size) == (b.replay.pos, b.replay.size)
+    sa, sb = a.env.get_state(), b.env.get_state()
+    assert all(torch.equal(sa[k], sb[k]) for k in sa)
+    for f in ("own", "radar", "nei", "reward", "env_done"):
+        assert torch.equal(getattr(a.cur, f), getattr(b.cur, f)), f
