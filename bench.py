@@ -261,7 +261,7 @@ class Trainer(CheckpointMixin):
         self.episode = self.env_episode_view()
         self.env.auto_reset(None, out=self.cur)      # all envs: first OD draw + initial obs
         self.env_events = []
-        self.fused_tail = (not self.gru) if FUSED_TAIL is None else FUSED_TAIL
+        self.fused_tail = True if FUSED_TAIL is None else FUSED_TAIL
         self.bufs = [self.cur, self.nxt]
         self._sg = {}                                 # parity -> captured whole-step graph
         self.pos_dev = torch.zeros(2, dtype=torch.int64, device="cuda")   # ring position ping-pong
@@ -366,10 +366,9 @@ class Trainer(CheckpointMixin):
 
 NO_GRAPH = False
 OVERLAP_RESET = os.environ.get("AAC_OVERLAP_RESET", "0") == "1"   # measured slower: 1.241 vs 1.164 ms
-# replay push, GRU hidden-row zeroing and auto-reset fused into the env step launch (aac_env_step_tail).
-# Default: on for the ATT env (config 3: env part 0.084 -> 0.070 ms per step, tools/tail_probe.py), off
-# for the WGRU env of config 4, where ~40 % of the envs end every step and the in-step reset lengthens
-# nearly every workgroup of the two-round grid (0.131 -> 0.144 ms).  AAC_FUSED_TAIL=0 / 1 forces it.
+# replay push, GRU hidden-row zeroing and auto-reset fused into the env step launch (aac_env_step_tail):
+# config 3 env part 0.084 -> 0.070 ms per step (tools/tail_probe.py); config 4 (one round of 1024
+# workgroups since the 4-env workgroups) 0.378 -> 0.371 ms per step.  AAC_FUSED_TAIL=0 / 1 forces it.
 _FT = os.environ.get("AAC_FUSED_TAIL")
 FUSED_TAIL = None if _FT is None else _FT == "1"
 # config 3: each timed step (act + fused env tail + update) replays one captured HIP graph (one per

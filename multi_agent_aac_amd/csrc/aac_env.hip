@@ -1284,8 +1284,17 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
         return k < 0 ? 0 : (k > BLOCK ? BLOCK : k);
     }();
     auto epb_for = [&](int apw) { return c.N > apw ? 1 : apw / c.N; };
-    if (apw_env) h->epb = epb_for(apw_env);
-    else h->epb = (c.E / epb_for(50) >= 1024) ? epb_for(50) : epb_for(24);
+    if (apw_env) {
+        h->epb = epb_for(apw_env);
+    } else if (c.E / epb_for(50) >= 1024) {
+        h->epb = epb_for(50);
+    } else {
+        // ~24 agents per workgroup, raised (up to ~50) until the grid fits one round of 1024
+        // workgroups: at 4096 x 8 (config 4) 3 envs per workgroup made 1366 workgroups, two rounds;
+        // 4 envs: 0.070 -> 0.055 ms per step launch
+        h->epb = epb_for(24);
+        while (h->epb < epb_for(50) && (c.E + h->epb - 1) / h->epb > 1024) ++h->epb;
+    }
     h->blocks = (c.E + h->epb - 1) / h->epb;
     const size_t EN = (size_t)c.E * c.N;
     hipError_t st = hipSuccess;

@@ -136,11 +136,12 @@ def test_step_tail_rejects_bad_fields(native_lib, occ):
     assert rc != 0 and b"OD bank" in _native.lib().aac_last_error()
 
 
-def test_whole_step_graph_equals_eager(native_lib):
+def test_whole_step_graph_equals_eager(native_lib, monkeypatch):
     """bench.Trainer.step_graph (act + fused env tail + update_myown replayed from one captured HIP graph
     per buffer parity, the ring position in device words) against the same steps launched eagerly:
     bit-identical networks, optimiser state, replay ring and env state."""
     import bench
+    monkeypatch.setattr(bench, "STEP_GRAPH", True)        # off by default in the bench (measured neutral)
     E, N, B = 256, 5, 64
     tr = [bench.Trainer(E, N, B, 2000, "combined", seed=0) for _ in range(2)]
     for t in tr:
