@@ -2365,7 +2365,7 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
         waves += (d.wide ? tm * ((tn + 3) / 4) : tm * tn) * ks;
     }
     g.waves = waves;
-    g.xcd_all = g_xcd_all;
+    g.xcd_all = g_xcd_all == 1 || (g_xcd_all == 2 && n >= 12);   // 2: launches of many products only
     g.nh = 0;
     g.hb[0] = g.hb[1] = waves;
     for (int i = n; i < AAC_GEMM_MAX; ++i) g.wb[i] = 0x7fffffff;
