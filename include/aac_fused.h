@@ -89,6 +89,12 @@ int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream);
  * extra workgroups (four rows each; the arithmetic of aac_critic_head).  The jobs must not read what the products write, nor
  * the products what the jobs write: one launch, no ordering between them.  n may be 0. */
 int aac_gemm_batch_heads(const aac_gemm_prob *probs, int32_t n, const aac_head_job *heads, int32_t nh, void *stream);
+/* aac_gemm_batch with an explicit workgroup order: xcd_order != 0 hands each of the 8 XCDs (workgroup
+ * b runs on XCD b % 8) a contiguous range of the launch's workgroups, so the tiles of one product share
+ * one XCD's L2 and read their operands from HBM about once.  Same arithmetic, bit-identical results.
+ * The GRU learner's launches (16 equal per-agent products each) use it: grouped-GEMM HBM traffic
+ * 3.06x -> 1.19x the algorithmic bytes (profiles/r03_gemm_pmc_gru_xcd_*.json). */
+int aac_gemm_batch_ordered(const aac_gemm_prob *probs, int32_t n, int32_t xcd_order, void *stream);
 /* The launch plan of aac_gemm_batch without launching (host only): per product 0 (register
  * fragments, 32x32 wave tiles) or 1 + cfg (LDS-staged workgroup tile: cfg >> 2 = 64x64 / 64x32 /
  * 32x64 / 32x32, cfg & 3 = operand layouts); *workgroups = the grid (may be NULL). */

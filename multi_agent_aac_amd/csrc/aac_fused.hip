@@ -2464,6 +2464,13 @@ int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
     return launch_batch(g, (hipStream_t)stream);
 }
 
+int aac_gemm_batch_ordered(const aac_gemm_prob *probs, int32_t n, int32_t xcd_order, void *stream) {
+    GBatch g{};
+    if (plan(probs, n, g)) return -1;
+    if (xcd_order) g.xcd_all = 1;
+    return launch_batch(g, (hipStream_t)stream);
+}
+
 static int launch_batch(GBatch &g, hipStream_t st) {
     bool deep = false, lds = false;
     for (int i = 0; i < g.n; ++i) {

@@ -73,6 +73,7 @@ def lib():
         L = _native.lib()
         L.aac_fused_last_error.restype = ctypes.c_char_p
         L.aac_gemm_batch.argtypes = [ctypes.POINTER(GemmProb), i32, vp]
+        L.aac_gemm_batch_ordered.argtypes = [ctypes.POINTER(GemmProb), i32, i32, vp]
         L.aac_gemm_batch_heads.argtypes = [ctypes.POINTER(GemmProb), i32, ctypes.POINTER(HeadJob), i32, vp]
         L.aac_critic_head_job.argtypes = [ctypes.POINTER(HeadJob), vp]
         L.aac_gemm_plan.argtypes = [ctypes.POINTER(GemmProb), i32, vp, vp]
@@ -145,9 +146,11 @@ class GemmLaunch:
     """One aac_gemm_batch launch with a fixed problem list (validated when built), plus up to
     HEAD_MAX critic-head jobs that do not depend on the products (aac_gemm_batch_heads)."""
 
-    def __init__(self, probs, heads=()):
+    def __init__(self, probs, heads=(), xcd=False):
         assert 0 <= len(probs) <= GEMM_MAX and len(heads) <= HEAD_MAX and len(probs) + len(heads) >= 1
+        assert not (xcd and heads)
         self.n = len(probs)
+        self.xcd = bool(xcd)        # XCD-aware workgroup order (aac_gemm_batch_ordered)
         self.arr = (GemmProb * max(self.n, 1))(*probs)
         self.nh = len(heads)
         self.heads = (HeadJob * self.nh)(*heads) if heads else None
@@ -164,6 +167,8 @@ class GemmLaunch:
     def __call__(self):
         if self.nh:
             _chk(lib().aac_gemm_batch_heads(self.arr, self.n, self.heads, self.nh, _stream()), "aac_gemm_batch_heads")
+        elif self.xcd:
+            _chk(lib().aac_gemm_batch_ordered(self.arr, self.n, 1, _stream()), "aac_gemm_batch_ordered")
         else:
             _chk(lib().aac_gemm_batch(self.arr, self.n, _stream()), "aac_gemm_batch")
 
@@ -241,11 +246,11 @@ def set_lds_policy(min_workgroups=512, small_tiles=False):
     lib().aac_gemm_set_lds_policy(int(min_workgroups), int(bool(small_tiles)))
 
 
-def gemm_launches(probs, heads=()):
+def gemm_launches(probs, heads=(), xcd=False):
     """Split a product list into launches of at most GEMM_MAX (head jobs ride in the first)."""
     if not probs:
         return [GemmLaunch([], heads)] if heads else []
-    return [GemmLaunch(probs[i:i + GEMM_MAX], heads if i == 0 else ()) for i in range(0, len(probs), GEMM_MAX)]
+    return [GemmLaunch(probs[i:i + GEMM_MAX], heads if i == 0 else (), xcd=xcd) for i in range(0, len(probs), GEMM_MAX)]
 
 
 def critic_head(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0.0, q=None, dq=None, dh=None,

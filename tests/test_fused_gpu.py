@@ -119,6 +119,30 @@ def test_gemm_batch_grouped(native_lib):
                                    rtol=1e-5)
 
 
+def test_gemm_xcd_order_bit_identical(native_lib):
+    """aac_gemm_batch_ordered (XCD-aware workgroup order, the GRU learner's launches) only remaps
+    workgroups to tiles: bit-identical to the round-robin order, on the learner's per-agent weight-
+    gradient shapes (192 x 129 over K = 512 with the ones column) and ragged ones."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(5)
+    shapes = [(192, 128, 512)] * 8 + [(64, 18, 512)] * 5 + [(37, 70, 333)] * 3
+    Gs = [torch.randn(K, M, device=DEV) for M, N, K in shapes]
+    Xs = [torch.randn(K, N, device=DEV) for M, N, K in shapes]
+    out = []
+    for xcd in (False, True):
+        Cs = [torch.full((M * (N + 1),), 7.0, device=DEV) for M, N, K in shapes]
+        probs = [fused.prob(fused.ptr(g), fused.ptr(x), fused.ptr(c), M, N, K, M, N, N, ta=1, ones=1,
+                            cextra=fused.ptr(c, M * N)) for (M, N, K), g, x, c in zip(shapes, Gs, Xs, Cs)]
+        fused.GemmLaunch(probs, xcd=xcd)()
+        out.append(Cs)
+    torch.cuda.synchronize()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+    for (M, N, K), g, x, c in zip(shapes, Gs, Xs, out[1]):
+        np.testing.assert_allclose(c[:M * N].reshape(M, N).cpu().double(), (g.double().t() @ x.double()).cpu(),
+                                   atol=3e-6 * np.sqrt(K) * 3, rtol=1e-5)
+
+
 @pytest.mark.parametrize("N", [23, 64])
 def test_gemm_split_copies(native_lib, lds_everywhere, N):
     """ksplit > 1 writes per-split partial products that sum to the full product (N = 64: the LDS
