@@ -99,7 +99,7 @@ int aac_gemm_batch_ordered(const aac_gemm_prob *probs, int32_t n, int32_t xcd_or
  * fragments, 32x32 wave tiles) or 1 + cfg (LDS-staged workgroup tile: cfg >> 2 = 64x64 / 64x32 /
  * 32x64 / 32x32, cfg & 3 = operand layouts); *workgroups = the grid (may be NULL). */
 int aac_gemm_plan(const aac_gemm_prob *probs, int32_t n, int32_t *lds_cfg, int32_t *workgroups);
-/* Process-wide tile policy (default from AAC_GEMM_LDS_MIN_WG = 512, AAC_GEMM_LDS_SMALL = 0): an
+/* Process-wide tile policy (default from AAC_GEMM_LDS_MIN_WG = 256, AAC_GEMM_LDS_SMALL = 0): an
  * eligible product takes the largest LDS workgroup tile (64x64, then 64x32 / 32x64) that gives at
  * least min_workgroups workgroups, else the register path; small_tiles != 0 falls back to 32x32 LDS
  * tiles instead; min_workgroups = -1 - c forces tile c (0 64x64, 1 64x32, 2 32x64, 3 32x32) on every

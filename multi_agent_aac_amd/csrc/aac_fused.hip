@@ -2245,7 +2245,7 @@ const int g_lw = env_int("AAC_GEMM_LW", 1);                  // row-contiguous o
 const int g_vec = env_int("AAC_GEMM_VEC", 1);                // 16-B epilogue rows
 const int g_lds = env_int("AAC_GEMM_LDS", 1);                // LDS-staged workgroup tiles
 const int g_lds_min_k = env_int("AAC_GEMM_LDS_MIN_K", 64);   // ... for products with K >= this
-int g_lds_min_wg = env_int("AAC_GEMM_LDS_MIN_WG", 512);  // tile choice: largest tile with this many workgroups
+int g_lds_min_wg = env_int("AAC_GEMM_LDS_MIN_WG", 256);  // tile choice: largest tile with this many workgroups
 const int g_lds_min_wg_many = env_int("AAC_GEMM_LDS_MIN_WG_MANY", 48);   // ... in launches of >= 12 products
 const long g_lds_min_mn = env_int("AAC_GEMM_LDS_MIN_MN", 64 * 64);
 int g_lds_small = env_int("AAC_GEMM_LDS_SMALL", 0);         // allow 32x32 LDS workgroup tiles
@@ -2260,7 +2260,7 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
     int waves = 0;
     // launches of many independent products (the GRU learner's per-agent groups: 16 products of
     // 512 x 192) fill the chip together, so each product takes LDS tiles from 48 workgroups on
-    // (config 4: 0.564 -> 0.558 ms per step; config 3's launches of <= 11 products keep 512)
+    // (config 4: 0.564 -> 0.558 ms per step; config 3's launches of <= 11 products keep the default)
     // (only launches without split-K products: the tile choice of a product must not depend on
     // which other products share its launch in the ATT learner, whose merged and serial schedules
     // group them differently and must stay bit-identical)

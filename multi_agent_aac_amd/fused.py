@@ -241,7 +241,7 @@ def ride_only(ride):
     return with_ride(AttnEncArgs(), ride)
 
 
-def set_lds_policy(min_workgroups=512, small_tiles=False):
+def set_lds_policy(min_workgroups=256, small_tiles=False):
     """Tile policy of the plans built from now on (include/aac_fused.h aac_gemm_set_lds_policy)."""
     lib().aac_gemm_set_lds_policy(int(min_workgroups), int(bool(small_tiles)))
 
@@ -528,8 +528,8 @@ class FusedUpdate:
 
     # K splits of the weight gradients (partial copies summed by the Adam kernel); actor K = B*N
     # or B*N*K rows, critic K = B rows.  AAC_SPLIT_ACTOR / AAC_SPLIT_CRITIC override (tuning).
-    SPLIT_ACTOR = int(os.environ.get("AAC_SPLIT_ACTOR", "32"))
-    SPLIT_CRITIC = int(os.environ.get("AAC_SPLIT_CRITIC", "8"))
+    SPLIT_ACTOR = int(os.environ.get("AAC_SPLIT_ACTOR", "20"))
+    SPLIT_CRITIC = int(os.environ.get("AAC_SPLIT_CRITIC", "4"))
     # world == 1: run the critic step of iteration i+1 beside the actor step of iteration i on a
     # second stream of the captured graph (AAC_OVERLAP=1; measured slower, off: DESIGN section 4)
     OVERLAP = os.environ.get("AAC_OVERLAP", "0") == "1"
