@@ -92,8 +92,10 @@ int aac_gemm_batch_heads(const aac_gemm_prob *probs, int32_t n, const aac_head_j
 /* aac_gemm_batch with an explicit workgroup order: xcd_order != 0 hands each of the 8 XCDs (workgroup
  * b runs on XCD b % 8) a contiguous range of the launch's workgroups, so the tiles of one product share
  * one XCD's L2 and read their operands from HBM about once.  Same arithmetic, bit-identical results.
- * The GRU learner's launches (16 equal per-agent products each) use it: grouped-GEMM HBM traffic
- * 3.06x -> 1.19x the algorithmic bytes (profiles/r03_gemm_pmc_gru_xcd_*.json). */
+ * For the GRU learner's launches (16 equal per-agent products each) it cuts grouped-GEMM HBM traffic
+ * 3.06x -> 1.19x the algorithmic bytes (profiles/r03_gemm_pmc_gru_xcd_*.json) but costs ~1 % of the
+ * config-4 step, so the learner uses it only with AAC_GRU_XCD=1.  xcd_order == 0 forces the
+ * round-robin order (also under AAC_GEMM_XCD_ALL). */
 int aac_gemm_batch_ordered(const aac_gemm_prob *probs, int32_t n, int32_t xcd_order, void *stream);
 /* The launch plan of aac_gemm_batch without launching (host only): per product 0 (register
  * fragments, 32x32 wave tiles) or 1 + cfg (LDS-staged workgroup tile: cfg >> 2 = 64x64 / 64x32 /

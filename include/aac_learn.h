@@ -66,6 +66,11 @@ int aac_adam_flat(float *param, const float *grad, float *exp_avg, float *exp_av
  * one device counter that is advanced once afterwards). */
 int aac_adam_flat_at(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr,
                      float beta1, float beta2, float eps, const int32_t *step, int32_t step_add, void *stream);
+/* Same on the gradient grad * gscale: gscale = 1 / world after a SUM all-reduce of the ranks'
+ * gradients (the data-parallel mean of SURVEY.md section 8(e) without a separate division launch). */
+int aac_adam_flat_at_scaled(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr,
+                            float beta1, float beta2, float eps, const int32_t *step, int32_t step_add, float gscale,
+                            void *stream);
 /* tgt = (1 - tau) * tgt + tau * src */
 int aac_polyak_flat(float *tgt, const float *src, int64_t n, float tau, void *stream);
 /* Same, and *step += step_add in the same launch (the optimiser step counter of this network,

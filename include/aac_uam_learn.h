@@ -88,6 +88,10 @@ int aac_uam_td_mse_head(const double *ht, const double *wt, const double *bt, co
 int aac_adam64_sum(double *param, const double *gpart, int32_t nsplit, double *exp_avg, double *exp_avg_sq,
                    int64_t n, double lr, double beta1, double beta2, double eps, const int32_t *step,
                    int32_t step_add, void *stream);
+/* Same on the summed gradient times gscale (1 / world after a SUM all-reduce of the ranks' sums). */
+int aac_adam64_sum_scaled(double *param, const double *gpart, int32_t nsplit, double *exp_avg, double *exp_avg_sq,
+                          int64_t n, double lr, double beta1, double beta2, double eps, const int32_t *step,
+                          int32_t step_add, double gscale, void *stream);
 
 /* out[i] = the sum of the nsplit partial copies gpart[s*n + i] in aac_adam64_sum's order: the
  * gradient a multi-rank update all-reduces before aac_adam64_sum(..., out, nsplit = 1, ...). */

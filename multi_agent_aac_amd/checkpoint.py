@@ -12,10 +12,23 @@ The reference saves the actor ``state_dict`` only (ATT/maddpg:131-139, kept as
   extra     whatever else the loop carries (current observation rows, GRU hidden states)
 
 Every part is a named set of device tensors that ``load`` overwrites IN PLACE (``copy_``), so the
-HIP graphs a running learner already captured stay valid.  The file is a ``torch.save`` of a dict of
-CPU tensors and plain values, read back with ``weights_only=True``.  RNG counters are 32-bit epochs
-(aac_learn.hip ``take_epoch``): values >= 2^32 are rejected on load.
+HIP graphs a running learner already captured keep pointing at the restored storage.  Host scalars
+baked into captured graphs -- the replay sampler's seed and the exploration-noise seed -- are the
+exception: when a load changes either, the learner's captured update graph is dropped (re-captured
+on the next update), and ``trainer.CheckpointMixin`` drops its whole-step graphs.
+
+The env part also records what the auto-reset's future OD draws depend on but ``get_state`` does not
+export: the env configuration (variant, radar mode, episode length, waypoint slots), the OD bank's
+fingerprint and its draw seed.  A bank or configuration mismatch is refused on load; a draw seed that
+differs from the live env's is restored (the bank is re-installed with the saved seed).
+
+The file is a ``torch.save`` of a dict of CPU tensors and plain values, read back with
+``weights_only=True``.  RNG counters are 32-bit epochs (aac_learn.hip ``take_epoch``): values >= 2^32
+are rejected on load.
 """
+import hashlib
+
+import numpy as np
 import torch
 
 FORMAT = "aac-checkpoint-v1"
@@ -52,6 +65,45 @@ def replay_meta(rep):
             "row_width": int(rep.ring.shape[1])}
 
 
+def bank_fingerprint(bank):
+    """sha1 over the bank's arrays (OD starts / waypoints / counts, or UAM starts / goals / clouds),
+    cached on the bank object."""
+    fp = getattr(bank, "_fingerprint", None)
+    if fp is None:
+        h = hashlib.sha1()
+        for name in ("start", "wps", "cnt", "counts", "goal", "clouds"):
+            a = getattr(bank, name, None)
+            if a is not None:
+                h.update(name.encode())
+                h.update(np.ascontiguousarray(a).tobytes())
+        fp = h.hexdigest()
+        try:
+            bank._fingerprint = fp
+        except AttributeError:
+            pass
+    return fp
+
+
+def env_meta(env):
+    """What the env's future steps and auto-reset draws depend on beyond its device state."""
+    m = {"E": int(env.E), "N": int(env.N), "class": type(env).__name__}
+    for k in ("variant", "radar_mode", "W", "D0", "tdcpa", "neighbours", "p3"):
+        if hasattr(env, k):
+            v = getattr(env, k)
+            m[k] = v if isinstance(v, (bool, str)) or v is None else int(v)
+    cfg = getattr(env, "cfg", None)
+    if cfg is not None and hasattr(cfg, "episode_length"):
+        m["episode_length"] = int(cfg.episode_length)
+    occ = getattr(env, "occ", None)
+    if occ is not None:
+        m["maps"] = hashlib.sha1(np.ascontiguousarray(np.asarray(occ, dtype=np.uint8)).tobytes()).hexdigest()
+    bank = getattr(env, "bank", None)
+    if bank is not None:
+        m["bank"] = bank_fingerprint(bank)
+        m["bank_seed"] = int(getattr(env, "bank_seed", 0))
+    return m
+
+
 def env_tensors(env):
     """The env's state as a dict of fresh device tensors (get_state); with its episode buffer."""
     t = dict(env.get_state())
@@ -62,6 +114,12 @@ def env_tensors(env):
 
 
 # --------------------------------------------------------------------------- save / load
+def drop_graphs(learner):
+    """Forget the learner's captured update graph (re-captured by the next ``update``)."""
+    if learner is not None:
+        learner.invalidate_graphs()
+
+
 def _cpu(t):
     return t.detach().to("cpu", copy=True)
 
@@ -80,7 +138,7 @@ def save(path, learner=None, replay=None, env=None, extra=None):
         tens["ring"] = _cpu(ring[:replay.size])
         ck["parts"]["replay"] = {"meta": replay_meta(replay), "tensors": tens}
     if env is not None:
-        ck["parts"]["env"] = {"meta": {"E": int(env.E), "N": int(env.N)},
+        ck["parts"]["env"] = {"meta": env_meta(env),
                               "tensors": {k: _cpu(v) for k, v in env_tensors(env).items()}}
     if extra:
         ck["parts"]["extra"] = {"meta": {}, "tensors": {k: _cpu(v) for k, v in extra.items()}}
@@ -110,6 +168,7 @@ def load(path, learner=None, replay=None, env=None, extra=None):
     for want, obj in (("learner", learner), ("replay", replay), ("env", env), ("extra", extra)):
         if obj is not None and want not in parts:
             raise KeyError(f"{path} holds no {want} state")
+    reseeded = False
     if learner is not None:
         p = parts["learner"]
         meta = learner_meta(learner)
@@ -121,6 +180,7 @@ def load(path, learner=None, replay=None, env=None, extra=None):
             raise ValueError(f"checkpoint learner tensors {sorted(p['tensors'])} != {sorted(live)}")
         for k, v in live.items():
             _copy_into(v, p["tensors"][k], "learner." + k)
+        reseeded |= learner.noise_seed != p["meta"]["noise_seed"]
         learner.noise_seed = p["meta"]["noise_seed"]
     if replay is not None:
         p = parts["replay"]
@@ -132,11 +192,28 @@ def load(path, learner=None, replay=None, env=None, extra=None):
         _copy_into(live["ring"][:m["size"]], p["tensors"]["ring"], "replay.ring")
         _copy_into(live["meta"], p["tensors"]["meta"], "replay.meta")
         _copy_into(live["counter"], p["tensors"]["counter"], "replay.counter")
+        if replay.seed != m["seed"]:
+            if learner is None:
+                raise ValueError("the checkpoint's replay seed differs from the live replay's: load the learner "
+                                 "with it, so that its captured update graph (which bakes the seed) is dropped")
+            reseeded = True
         replay.seed, replay.pos, replay.size = m["seed"], m["pos"], m["size"]
+    if reseeded:
+        drop_graphs(learner)
     if env is not None:
         p = parts["env"]
-        if p["meta"] != {"E": int(env.E), "N": int(env.N)}:
-            raise ValueError(f"checkpoint env {p['meta']} does not match E={env.E} N={env.N}")
+        saved, live = dict(p["meta"]), env_meta(env)
+        seed = saved.pop("bank_seed", None)
+        live_seed = live.pop("bank_seed", None)
+        bad = {k: (saved[k], live.get(k)) for k in saved if saved[k] != live.get(k)}
+        if bad:
+            raise ValueError(f"checkpoint env does not match the live env (saved, live): {bad}")
+        if seed is not None and seed != live_seed:
+            # same bank, other draw seed: restore the saved one (future episodes draw as in the saved run)
+            if hasattr(env, "set_od_bank"):
+                env.set_od_bank(env.bank, seed=seed)
+            else:
+                env.set_bank(env.bank, seed=seed)
         t = dict(p["tensors"])
         ep = t.pop("episode", None)
         env.set_state(**t)

@@ -2467,7 +2467,7 @@ int aac_gemm_batch(const aac_gemm_prob *probs, int32_t n, void *stream) {
 int aac_gemm_batch_ordered(const aac_gemm_prob *probs, int32_t n, int32_t xcd_order, void *stream) {
     GBatch g{};
     if (plan(probs, n, g)) return -1;
-    if (xcd_order) g.xcd_all = 1;
+    g.xcd_all = xcd_order ? 1 : 0;      // explicit: overrides AAC_GEMM_XCD_ALL either way
     return launch_batch(g, (hipStream_t)stream);
 }
 

@@ -319,8 +319,10 @@ __global__ void __launch_bounds__(LEARN_BLOCK) gather_kernel(const float *ring, 
 }
 
 // ------------------------------------------------------------------------------- optimiser
+// gscale multiplies the gradient as it is read: 1 / world after a SUM all-reduce (the mean of the
+// ranks' gradients without a separate division launch; exact for power-of-two worlds)
 __global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2,
-                            float eps, const int32_t *step, int step_add) {
+                            float eps, const int32_t *step, int step_add, float gscale) {
     const int t = *step + step_add;
     const double bc1 = 1.0 - pow((double)b1, (double)t);
     const double bc2 = 1.0 - pow((double)b2, (double)t);
@@ -328,7 +330,7 @@ __global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_
     const float bc2s = (float)sqrt(bc2);
     const float w1 = (float)(1.0 - (double)b1), w2 = (float)(1.0 - (double)b2);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = g[i];
+        const float gi = g[i] * gscale;
         float mi = m[i];
         mi = mi + w1 * (gi - mi);               // exp_avg.lerp_(grad, 1 - beta1)
         float vi = v[i] * b2;                   // exp_avg_sq.mul_(beta2)
@@ -801,8 +803,13 @@ int aac_adam_flat(float *p, const float *g, float *m, float *v, int64_t n, float
 
 int aac_adam_flat_at(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2,
                      float eps, const int32_t *step, int32_t step_add, void *stream) {
+    return aac_adam_flat_at_scaled(p, g, m, v, n, lr, b1, b2, eps, step, step_add, 1.0f, stream);
+}
+
+int aac_adam_flat_at_scaled(float *p, const float *g, float *m, float *v, int64_t n, float lr, float b1, float b2,
+                            float eps, const int32_t *step, int32_t step_add, float gscale, void *stream) {
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(LEARN_BLOCK), 0, (hipStream_t)stream, p, g, m, v, n, lr,
-                       b1, b2, eps, step, step_add);
+                       b1, b2, eps, step, step_add, gscale);
     LHIP(hipGetLastError());
     return 0;
 }

@@ -259,7 +259,8 @@ __global__ void __launch_bounds__(256) uam_td_mse_head_kernel(const double *__re
 }
 
 __global__ void adam64_kernel(double *p, const double *__restrict__ gpart, int ns, double *m, double *v, int64_t n,
-                              double lr, double b1, double b2, double eps, const int32_t *step, int step_add) {
+                              double lr, double b1, double b2, double eps, const int32_t *step, int step_add,
+                              double gscale) {
     const int t = *step + step_add;
     const double bc1 = 1.0 - pow(b1, (double)t), bc2 = 1.0 - pow(b2, (double)t);
     const double step_size = lr / bc1, bc2s = sqrt(bc2);
@@ -274,6 +275,7 @@ __global__ void adam64_kernel(double *p, const double *__restrict__ gpart, int n
             for (int u = 0; u < 8; ++u) gi += x[u];
         }
         for (; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
+        gi *= gscale;           // 1 / world after a SUM all-reduce (1 otherwise: exact)
         const double mi = b1 * m[i] + (1.0 - b1) * gi;
         const double vi = b2 * v[i] + (1.0 - b2) * gi * gi;
         const double den = sqrt(vi) / bc2s + eps;
@@ -494,10 +496,17 @@ int aac_uam_td_mse_head(const double *ht, const double *wt, const double *bt, co
 int aac_adam64_sum(double *param, const double *gpart, int32_t nsplit, double *exp_avg, double *exp_avg_sq, int64_t n,
                    double lr, double beta1, double beta2, double eps, const int32_t *step, int32_t step_add,
                    void *stream) {
+    return aac_adam64_sum_scaled(param, gpart, nsplit, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, step_add,
+                                 1.0, stream);
+}
+
+int aac_adam64_sum_scaled(double *param, const double *gpart, int32_t nsplit, double *exp_avg, double *exp_avg_sq,
+                          int64_t n, double lr, double beta1, double beta2, double eps, const int32_t *step,
+                          int32_t step_add, double gscale, void *stream) {
     if (n <= 0) return 0;
     if (nsplit < 1 || !param || !gpart || !exp_avg || !exp_avg_sq || !step) return lfail("adam64_sum: bad argument");
     hipLaunchKernelGGL(adam64_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, param, gpart, nsplit,
-                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, step_add);
+                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, step_add, gscale);
     LHIP(hipGetLastError());
     return 0;
 }

@@ -219,6 +219,7 @@ class BatchedEnv:
                                                             bank.cnt.ctypes.data, bank.n_pairs,
                                                             ctypes.c_uint64(seed)), "aac_env_set_od_bank")
         self.bank = bank
+        self.bank_seed = int(seed)
 
     def use_episode_buffer(self, episode: torch.Tensor):
         """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E],

@@ -97,6 +97,7 @@ def lib():
         L.aac_attn_train_bwd_partials.argtypes = [i32]
         L.aac_attn_train_bwd_partials.restype = i32
         L.aac_adam_flat_at.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]
+        L.aac_adam_flat_at_scaled.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, f32, vp]
         _L = L
     return _L
 
@@ -323,11 +324,14 @@ def padded(n, q=4):
     return (n + q - 1) // q * q
 
 
-def adam_at(opt, step_add):
-    _chk(lib().aac_adam_flat_at(vp(opt.flat.data.data_ptr()), vp(opt.flat.grad.data_ptr()),
-                                vp(opt.exp_avg.data_ptr()), vp(opt.exp_avg_sq.data_ptr()), opt.flat.data.numel(),
-                                opt.lr, opt.betas[0], opt.betas[1], opt.eps, vp(opt.step_t.data_ptr()), step_add,
-                                _stream()), "aac_adam_flat_at")
+def adam_at(opt, step_add, gscale=1.0):
+    """Adam step ``step_t + step_add`` on ``gscale`` x the flat gradient (1 / world after a SUM
+    all-reduce)."""
+    _chk(lib().aac_adam_flat_at_scaled(vp(opt.flat.data.data_ptr()), vp(opt.flat.grad.data_ptr()),
+                                       vp(opt.exp_avg.data_ptr()), vp(opt.exp_avg_sq.data_ptr()),
+                                       opt.flat.data.numel(), opt.lr, opt.betas[0], opt.betas[1], opt.eps,
+                                       vp(opt.step_t.data_ptr()), step_add, gscale, _stream()),
+         "aac_adam_flat_at_scaled")
 
 
 def actor_out_bwd(df, ldf, wenc, din, d0, X, wa, ha, N, R, dout, dha):
@@ -644,6 +648,10 @@ class FusedUpdate:
         # the Polyak launches also advance the optimisers' step counters (no separate add kernels)
         self.post = [lambda: ops.polyak_flat2(m.fc_t.data, m.fc.data, m.critic_optimizer.step_t, m.fa_t.data,
                                               m.fa.data, m.actor_optimizer.step_t, m.tau, N)]
+        # an update without the soft update (i_episode % UPDATE_EVERY != 0, ATT/maddpg:436-438): the same
+        # launch with tau = 0 (targets kept bit-exactly: 1 * t + 0 * s) still advances the step counters
+        self.post_hold = [lambda: ops.polyak_flat2(m.fc_t.data, m.fc.data, m.critic_optimizer.step_t, m.fa_t.data,
+                                                   m.fa.data, m.actor_optimizer.step_t, 0.0, N)]
         self.n_launches = len(self.pre) + sum(len(it) for it in self.iters) + len(self.post)
 
     def _adam(self, opt, flat, gpart, ns, step_add):
@@ -771,20 +779,21 @@ class FusedUpdate:
         m, N = self.m, self.N
         SA, SC = self.SPLIT_ACTOR, self.SPLIT_CRITIC
         copt, aopt = m.critic_optimizer, m.actor_optimizer
+        gs = 1.0 / m.world          # the collectives SUM; each Adam launch applies the 1 / world
         red_c = lambda: sum_partials(m.fc.grad, self.gc, SC)      # noqa: E731
         red_a = lambda: sum_partials(m.fa.grad, self.ga, SA)      # noqa: E731
         L = self._critic_step(0, A, C, self.cbuf[0], fuse_actor_fwd=False)
-        L += [red_c, Collective(lambda: m._allreduce_grads(critic=True, actor=False)), lambda: adam_at(copt, 1)]
+        L += [red_c, Collective(lambda: m._allreduce_grads(critic=True, actor=False)), lambda: adam_at(copt, 1, gs)]
         segs = [L]
         for i in range(N):
             L = self._actor_fwd_launches(i, A) + self._actor_step(i, A, C)
             if i + 1 < N:
                 L += self._critic_step(i + 1, A, C, self.cbuf[1], fuse_actor_fwd=False)
                 L += [red_a, red_c, Collective(lambda: m._allreduce_grads(critic=True, actor=True)),
-                      lambda i=i: adam_at(copt, i + 2), lambda i=i: adam_at(aopt, i + 1)]
+                      lambda i=i: adam_at(copt, i + 2, gs), lambda i=i: adam_at(aopt, i + 1, gs)]
             else:
                 L += [red_a, Collective(lambda: m._allreduce_grads(critic=False, actor=True)),
-                      lambda i=i: adam_at(aopt, i + 1)]
+                      lambda i=i: adam_at(aopt, i + 1, gs)]
             segs.append(L)
         return segs
 
@@ -924,7 +933,8 @@ class FusedUpdate:
     def ops(self):
         return self.pre + [op for it in self.iters for op in it] + self.post
 
-    def run(self, idx=None):
+    def run(self, idx=None, soft=True):
+        """One eager update; ``soft=False`` skips the Polyak step (the Adam counters still advance)."""
         if idx is None:
             self.pre[0]()
         else:
@@ -934,7 +944,7 @@ class FusedUpdate:
         for it in self.iters:
             for op in it:
                 op()
-        for op in self.post:
+        for op in (self.post if soft else self.post_hold):
             op()
 
     def segments(self):
@@ -965,6 +975,10 @@ class FusedUpdate:
             else:
                 op()
         return rec
+
+    def batch_rewards(self, i):
+        """The reward rows [B][N] of iteration i's sampled batch."""
+        return self.rew[i * self.B:(i + 1) * self.B]
 
     def stats(self):
         """[(loss_q, loss_a, q, target)] per iteration, like MADDPG._iteration."""

@@ -256,12 +256,12 @@ def wgrad_probs(G, g_off, gw, X, x_off, xw, k, Pg, Wn, bn, M, rows, N):
                  ones=1, cextra=Pg[i][bn]) for i in range(N)]
 
 
-# The learner's grouped-GEMM launches hold 8 or 16 equal per-agent products each: with the XCD-aware
-# workgroup order (aac_gemm_batch_ordered) each XCD takes whole products, which read their operands
-# from HBM about once (traffic 3.06x -> 1.19x the algorithmic bytes) at ~1 % of config-4 step time
-# (0.371 -> 0.375 ms: a product's tiles then share one XCD's CUs).  AAC_GRU_XCD=0 restores the
-# round-robin order.
-XCD_ORDER = os.environ.get("AAC_GRU_XCD", "1") == "1"
+# The learner's grouped-GEMM launches hold 8 or 16 equal per-agent products each.  With the XCD-aware
+# workgroup order (aac_gemm_batch_ordered, AAC_GRU_XCD=1) each XCD takes whole products, which read
+# their operands from HBM about once (traffic 3.06x -> 1.19x the algorithmic bytes), but config 4 is
+# ~1 % slower (0.371 -> 0.375 ms per step, profiles/r03_ab_gru_xcd_order.txt: a product's tiles then
+# share one XCD's CUs).  Throughput is the metric, so the round-robin order is the default.
+XCD_ORDER = os.environ.get("AAC_GRU_XCD", "0") == "1"
 
 
 def _glaunch(probs, heads=()):
@@ -306,9 +306,9 @@ class GruUpdate:
     def _adam(self, opt, flat):
         m = self.m
         L = []
-        if m.world > 1:
+        if m.world > 1:     # SUM over the ranks; the Adam launch applies the 1 / world
             L.append(Collective(lambda: m._allreduce(flat)))
-        L.append(lambda: fused.adam_at(opt, 1))
+        L.append(lambda: fused.adam_at(opt, 1, 1.0 / m.world))
         return L
 
     def _build(self):
@@ -380,18 +380,24 @@ class GruUpdate:
         L += [lambda: ops.polyak_flat2(m.fc_t.data, m.fc.data, m.critic_optimizer.step_t, m.fa_t.data, m.fa.data,
                                        m.actor_optimizer.step_t, m.tau, 1)]
         self.L = L
+        # i_episode % UPDATE_EVERY != 0 (WGRU/maddpg:320): the same launch with tau = 0 keeps the targets
+        # bit-exactly (1 * t + 0 * s) and still advances the step counters
+        self.hold = lambda: ops.polyak_flat2(m.fc_t.data, m.fc.data, m.critic_optimizer.step_t, m.fa_t.data,  # noqa
+                                             m.fa.data, m.actor_optimizer.step_t, 0.0, 1)
 
     def ops(self):
         return self.L
 
-    def run(self, idx=None):
+    def run(self, idx=None, soft=True):
+        """One eager update; ``soft=False`` skips the soft update (the step counters still advance)."""
         self.rep.check_sample(self.B)
         if idx is None:
             self.L[0]()
         else:
             self.bidx.copy_(idx.reshape(-1))
-        for op in self.L[1:]:
+        for op in self.L[1:-1]:
             op()
+        (self.L[-1] if soft else self.hold)()
 
     def segments(self):
         segs, colls, cur = [], [], []
@@ -534,8 +540,9 @@ class MADDPG:
         return a, hn
 
     def _allreduce(self, flat):
+        """SUM over the ranks of one flat gradient (the plan's Adam launch applies the 1 / world)."""
         if self.world > 1:
-            parallel.allreduce_mean_(flat.grad, self.pg)
+            parallel.allreduce_sum_(flat.grad, self.pg)
 
     def _plan(self, B, rep=None):
         if rep is None:
@@ -576,6 +583,13 @@ class MADDPG:
         self._graph_B = B
         return self._graph
 
+    def invalidate_graphs(self):
+        """Drop the captured update graph (a checkpoint load changed a seed the graph bakes in)."""
+        self._graph = None
+
+    def has_graph(self):
+        return self._graph is not None
+
     def _replay(self):
         graphs, colls = self._graph
         for k, g in enumerate(graphs):
@@ -585,18 +599,19 @@ class MADDPG:
                 with trace.range("allreduce"):
                     colls[k]()
 
-    def update(self, B=None, use_graph=True, idx=None, want_stats=True, replay=None):
+    def update(self, B=None, use_graph=True, idx=None, want_stats=True, replay=None, soft_update=True):
         """One update_myown on the device replay (no host synchronisation); ``replay`` defaults to
-        the attached batched replay, else the reference-API memory."""
+        the attached batched replay, else the reference-API memory.  ``soft_update=False`` keeps the
+        targets (UPDATE_EVERY > 1, WGRU/maddpg:320) and runs eagerly."""
         B = B or self.batch_size
         plan = self._plan(B, replay)
-        if idx is None and use_graph and replay is None:
+        if idx is None and use_graph and replay is None and soft_update:
             plan.rep.check_sample(B)
             if self._graph is None or self._graph_B != B:
                 self.capture(B)
             self._replay()
         else:
-            plan.run(idx)
+            plan.run(idx, soft=soft_update)
         self._last_src = plan
         return plan.stats() if want_stats else None
 
@@ -627,9 +642,8 @@ class MADDPG:
         """WGRU/maddpg:211 signature and returns (c_loss list, a_loss list)."""
         if len(self.memory) <= self.batch_size:
             return None, None
-        if i_episode % UPDATE_EVERY != 0:
-            raise NotImplementedError("soft update every call (UPDATE_EVERY = 1, WGRU/ma_main:374)")
-        stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev)
+        soft = i_episode % UPDATE_EVERY == 0      # WGRU/maddpg:320
+        stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev, soft_update=soft)
         return [s[0] for s in stats], [s[1] for s in stats]
 
     def save_model(self, episode, file_path):

@@ -144,10 +144,11 @@ class MADDPG:
                 p.grad = g[off:off + k].view_as(p)
 
     def _allreduce_grads(self, critic, actor):
-        """Mean over the ranks of the critic and / or actor gradient (one collective)."""
+        """SUM over the ranks of the critic and / or actor gradient (one collective; the fused plan's
+        Adam launches apply the 1 / world)."""
         nc = self.fc.numel
         t = self.grads if (critic and actor) else (self.grads[:nc] if critic else self.grads[nc:])
-        parallel.allreduce_mean_(t, self.pg)
+        parallel.allreduce_sum_(t, self.pg)
 
     def _targets(self, b, B):
         """y for all N iterations at once.  The target networks only change in the Polyak step
@@ -188,7 +189,7 @@ class MADDPG:
             self._fplans[key] = fused.FusedUpdate(self, rep, B)
         return self._fplans[key]
 
-    def _update_core(self, B, idx_list=None, rep=None):
+    def _update_core(self, B, idx_list=None, rep=None, soft=True):
         if rep is None:
             rep = self.replay if self.replay is not None else self.memory.dev
         N = self.n_agents
@@ -196,7 +197,7 @@ class MADDPG:
         if self.fused:
             rep.check_sample(B)
             fu = self._fused_plan(B, rep)
-            fu.run(idx)
+            fu.run(idx, soft=soft)
             return fu
         ball = rep.sample_batch(B, idx, nb=N)           # N independent batches, one launch each
         target = self._targets(ball, B)
@@ -204,8 +205,10 @@ class MADDPG:
         for agent in range(N):
             b = {k: v[agent * B:(agent + 1) * B] for k, v in ball.items()}
             stats.append(self._iteration(b, target[agent * B:(agent + 1) * B], agent))
-        ops.polyak_flat(self.fc_t.data, self.fc.data, self.tau)
-        ops.polyak_flat(self.fa_t.data, self.fa.data, self.tau)
+        self._last_rew = ball["rew"].reshape(N, B, N)
+        if soft:        # ATT/maddpg:436-438: soft update when i_episode % UPDATE_EVERY == 0
+            ops.polyak_flat(self.fc_t.data, self.fc.data, self.tau)
+            ops.polyak_flat(self.fa_t.data, self.fa.data, self.tau)
         return stats
 
     def _snapshot(self):
@@ -262,6 +265,13 @@ class MADDPG:
         self._graph_B = B
         return self._graph
 
+    def invalidate_graphs(self):
+        """Drop the captured update graph (a checkpoint load changed a seed the graph bakes in)."""
+        self._graph = None
+
+    def has_graph(self):
+        return self._graph is not None
+
     def _replay(self):
         if isinstance(self._graph, tuple):
             graphs, colls = self._graph
@@ -275,14 +285,15 @@ class MADDPG:
             with trace.range("update.graph"):
                 self._graph.replay()
 
-    def update(self, B=None, use_graph=True, idx_list=None, want_stats=True, replay=None):
+    def update(self, B=None, use_graph=True, idx_list=None, want_stats=True, replay=None, soft_update=True):
         """One update_myown-equivalent on the device replay (no host synchronisation).  Returns
         [(loss_q, loss_a, q, target)] per iteration (computed on demand: ``want_stats=False``
         launches nothing beyond the update itself).  ``replay`` defaults to the attached batched
-        replay, else the reference-API memory."""
+        replay, else the reference-API memory.  ``soft_update=False`` (UPDATE_EVERY > 1 between soft
+        updates, ATT/maddpg:436-438) keeps the targets and runs eagerly."""
         B = B or self.batch_size
-        if replay is not None:
-            self._last_src = self._update_core(B, idx_list, replay)
+        if replay is not None or not soft_update:
+            self._last_src = self._update_core(B, idx_list, replay, soft=soft_update)
             return self.last_stats if want_stats else None
         if idx_list is None and use_graph and (self.world == 1 or self.fused):
             (self.replay if self.replay is not None else self.memory.dev).check_sample(B)
@@ -330,21 +341,40 @@ class MADDPG:
 
     def update_myown(self, i_episode, total_step_count, UPDATE_EVERY, single_eps_critic_cal_record,
                      transfer_learning=False, wandb=None, full_observable_critic_flag=True):
-        """ATT/maddpg:219 signature and returns; the work is ``update`` on the device ring."""
+        """ATT/maddpg:219 signature and returns; the work is ``update`` on the device ring.
+
+        The soft update runs when ``i_episode % UPDATE_EVERY == 0`` (ATT/maddpg:436-438).  Each
+        gradient iteration appends the reference's 8-field record (ATT/maddpg:372-379)."""
         if len(self.memory) <= self.batch_size:
             return None, None, single_eps_critic_cal_record
-        if i_episode % UPDATE_EVERY != 0:
-            # The fused plan advances both Adam step counters inside its Polyak launches
-            # (fused.FusedUpdate.post), so an update that skipped the soft update would also skip the
-            # counter increment and mis-bias-correct the next Adam steps.  Supporting UPDATE_EVERY > 1
-            # needs a standalone counter advance (ops.polyak_flat with tau = 0, or an add) there.
-            raise NotImplementedError("soft update every call (UPDATE_EVERY=1) as ATT/params:29")
-        stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev)
+        if transfer_learning and i_episode <= 10000:
+            # ATT/maddpg:411-416 freezes the actor for the first 10000 episodes of a transfer run (its
+            # branch then indexes the single optimiser as a list, so the reference fails there)
+            raise NotImplementedError("transfer_learning: the actor-frozen phase is not part of this path")
+        soft = i_episode % UPDATE_EVERY == 0
+        stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev, soft_update=soft)
         c_loss = [s[0] for s in stats]
         a_loss = [s[1] for s in stats]
-        for s in stats:
-            single_eps_critic_cal_record.append(s)
+        single_eps_critic_cal_record.extend(self.critic_records(stats))
         return c_loss, a_loss, single_eps_critic_cal_record
+
+    def critic_records(self, stats=None):
+        """The 8-field ``single_eps_critic_cal_record`` entry of each gradient iteration of the last
+        update (ATT/maddpg:372-379): [target Q before the reward (B,), the batch rewards (B, N), the
+        target Q (B, 1), the critic loss, and the (min, max) of each].  The target before the reward
+        is gamma Q' (1 - done) = y - r[:, i]."""
+        stats = self.last_stats if stats is None else stats
+        src = self._last_src
+        out = []
+        for i, (loss_q, _, _, y) in enumerate(stats):
+            rew = src.batch_rewards(i) if isinstance(src, fused.FusedUpdate) else self._last_rew[i]
+            r = rew.detach().cpu().numpy()
+            after = y.detach().cpu().numpy().reshape(-1, 1)
+            before = after[:, 0] - r[:, i]
+            loss = loss_q.detach().cpu().numpy()
+            out.append([before, r, after, loss, (before.min(), before.max()), (r.min(), r.max()),
+                        (after.min(), after.max()), (loss.min(), loss.max())])
+        return out
 
     def save_model(self, episode, file_path):
         """ATT/maddpg:131-139: actor state_dict only, reference key names."""

@@ -24,6 +24,15 @@ def allreduce_mean_(t, group=None):
     return t
 
 
+def allreduce_sum_(t, group=None):
+    """In-place sum over the ranks of ``group`` (one collective).  The fused learners divide by the
+    world size inside the Adam launch that consumes the sum (``gscale``), so the mean costs no
+    separate division kernel per collective."""
+    if dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
 def rank_seed(base, rank):
     """Per-rank seed for OD bank / replay sampling / exploration noise (env shards differ)."""
     return int(base) + 1009 * int(rank)

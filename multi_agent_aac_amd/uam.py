@@ -214,6 +214,7 @@ class BatchedUAM:
         _chk(lib().aac_uam_set_bank(self._h, bank.start.ctypes.data, bank.goal.ctypes.data, bank.clouds.ctypes.data,
                                     bank.n, ctypes.c_uint64(seed)), "aac_uam_set_bank")
         self.bank = bank
+        self.bank_seed = int(seed)
 
     def use_episode_buffer(self, episode: torch.Tensor):
         """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E])."""

@@ -194,6 +194,7 @@ def _learn_lib():
         L.aac_uam_head.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, i32, dbl, vp, vp, vp, vp]
         L.aac_uam_td_mse_head.argtypes = [vp, vp, vp, vp, vp, i32, dbl, vp, vp, vp, vp, i32, vp, vp, vp, vp]
         L.aac_adam64_sum.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, vp]
+        L.aac_adam64_sum_scaled.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, dbl, vp]
         L.aac_uam_polyak.argtypes = [vp, vp, i64, dbl, vp, vp, vp, i32, vp, vp]
         L.aac_uam_push.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp, i64, vp]
         L.aac_sum64_partials.argtypes = [vp, vp, i32, i64, vp]
@@ -398,10 +399,12 @@ class FusedUamUpdate:
         from . import fused
         L, st, KS, P = _learn_lib(), self, self.KS, p64
 
+        gs = 1.0 / self.m.world     # world > 1: the collective SUMs, the Adam launch applies 1 / world
+
         def adam(src, ns):
-            return lambda: _ok(L.aac_adam64_sum(P(st.flat, off), src, ns, P(st.m1, off), P(st.m2, off), n, lr,
-                                                st.betas[0], st.betas[1], st.eps, st.step.data_ptr(), 1,
-                                                fused._stream()), "aac_adam64_sum")
+            return lambda: _ok(L.aac_adam64_sum_scaled(P(st.flat, off), src, ns, P(st.m1, off), P(st.m2, off), n, lr,
+                                                       st.betas[0], st.betas[1], st.eps, st.step.data_ptr(), 1, gs,
+                                                       fused._stream()), "aac_adam64_sum")
         if self.m.world == 1:
             return [adam(P(gpart), KS)]
         g = self.gflat[off:off + n]
@@ -548,9 +551,10 @@ class MADDPG:
             torch._foreach_lerp_(list(tgt.parameters()), [p.detach() for p in src.parameters()], self.tau)
 
     def _allreduce_flat(self, t):
-        """Mean over the ranks of one flat float64 gradient (the fused learner's collective)."""
+        """SUM over the ranks of one flat float64 gradient (the fused learner's collective; its Adam
+        launch applies the 1 / world)."""
         from . import parallel
-        parallel.allreduce_mean_(t, self.pg)
+        parallel.allreduce_sum_(t, self.pg)
 
     def _allreduce_grads(self, module):
         if self.world > 1:
@@ -709,6 +713,15 @@ class MADDPG:
         self._opt_steps = [st["step"] for opt in (self.critic_optimizer, self.actor_optimizer)
                            for st in opt.state.values()]
         return self._fstate
+
+    def invalidate_graphs(self):
+        """Drop every captured update graph (a checkpoint load changed a seed the graphs bake in)."""
+        self._graph = None
+        if self._fu is not None:
+            self._fu.graphs = None
+
+    def has_graph(self):
+        return self._graph is not None or getattr(self._fu, "graphs", None) is not None
 
     def fused(self, B, rep):
         """The FusedUamUpdate of (B, replay), built on first use.  Building it moves the parameters

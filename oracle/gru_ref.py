@@ -63,8 +63,10 @@ def soft_update(target, source, t):
         tp.data.copy_((1 - t) * tp.data + t * sp.data)
 
 
-def ref_gru_update(actors, critics, actors_t, critics_t, b, d_own, gamma=0.95, tau=0.01, lr=1e-3, opts=None):
-    """One update_myown on one batch dict of CPU tensors (B, N, .); own rows are cut to d_own."""
+def ref_gru_update(actors, critics, actors_t, critics_t, b, d_own, gamma=0.95, tau=0.01, lr=1e-3, opts=None,
+                   soft=True):
+    """One update_myown on one batch dict of CPU tensors (B, N, .); own rows are cut to d_own.
+    ``soft``: the ``i_episode % UPDATE_EVERY == 0`` soft update of WGRU/maddpg:320-324."""
     N = len(actors)
     if opts is None:
         opts = ([torch.optim.Adam(a.parameters(), lr=lr) for a in actors],
@@ -89,7 +91,7 @@ def ref_gru_update(actors, critics, actors_t, critics_t, b, d_own, gamma=0.95, t
         loss_a.backward()
         a_opts[i].step()
         stats.append((loss_q.item(), loss_a.item(), q.detach().clone(), target.squeeze(1).clone()))
-    for i in range(N):
+    for i in range(N if soft else 0):
         soft_update(critics_t[i], critics[i], tau)
         soft_update(actors_t[i], actors[i], tau)
     return stats, opts

@@ -77,8 +77,11 @@ def soft_update(target, source, t):
         tp.data.copy_((1 - t) * tp.data + t * sp.data)
 
 
-def ref_update(actor, critic, actor_t, critic_t, batches, gamma=0.95, tau=0.01, lr=1e-3, opts=None):
-    """One update_myown on explicit batches (list of N dicts of CPU tensors)."""
+def ref_update(actor, critic, actor_t, critic_t, batches, gamma=0.95, tau=0.01, lr=1e-3, opts=None, soft=True,
+               records=None):
+    """One update_myown on explicit batches (list of N dicts of CPU tensors).  ``soft``: the
+    ``i_episode % UPDATE_EVERY == 0`` soft update (ATT/maddpg:436-438).  ``records`` (a list): the
+    8-field single_eps_critic_cal_record entry of each iteration is appended (ATT/maddpg:372-379)."""
     if opts is None:
         opts = (torch.optim.Adam(actor.parameters(), lr=lr), torch.optim.Adam(critic.parameters(), lr=lr))
     a_opt, c_opt = opts
@@ -89,9 +92,15 @@ def ref_update(actor, critic, actor_t, critic_t, batches, gamma=0.95, tau=0.01, 
         with torch.no_grad():
             qn = critic_t([b["n_own"], b["n_radar"]], na).squeeze()
             done_comb = torch.from_numpy(np.array([1 if any(torch.eq(d, 1)) else 0 for d in b["done"]]))
+            tar_before = gamma * qn * (1 - done_comb)
+            reward_cal = b["rew"].clone()
             target = b["rew"][:, agent] + gamma * qn * (1 - done_comb)
             target = target.unsqueeze(1)
         loss_q = nn.MSELoss()(q, target.detach())
+        if records is not None:
+            tb, rc, ta, lq = (x.detach().cpu().numpy() for x in (tar_before, reward_cal, target, loss_q))
+            records.append([tb, rc, ta, lq, (tb.min(), tb.max()), (rc.min(), rc.max()), (ta.min(), ta.max()),
+                            (lq.min(), lq.max())])
         c_opt.zero_grad()
         loss_q.backward()
         c_opt.step()
@@ -101,8 +110,9 @@ def ref_update(actor, critic, actor_t, critic_t, batches, gamma=0.95, tau=0.01, 
         loss_a.backward()
         a_opt.step()
         stats.append((loss_q.item(), loss_a.item(), q.detach().clone(), target.squeeze(1).clone()))
-    soft_update(critic_t, critic, tau)
-    soft_update(actor_t, actor, tau)
+    if soft:
+        soft_update(critic_t, critic, tau)
+        soft_update(actor_t, actor, tau)
     return stats, opts
 
 
@@ -174,11 +184,14 @@ def random_transitions(E, N, seed, zero_nei_frac=0.1):
 
 
 def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=0, iters=1, eps=1e-8,
-                     param_tol=None):
+                     param_tol=None, update_every=1, check_records=False):
     """Device learner vs this restatement on identical weights and batches; raises on mismatch.
     Q, targets and losses are compared at ``tol``; parameters at ``param_tol`` (default ``tol``).
     ``eps`` is Adam's epsilon on both sides: where a gradient is rounding noise (|g| << eps) Adam's
-    step is ~lr g / eps instead of +-lr, so a larger eps makes the parameters compare the gradients."""
+    step is ~lr g / eps instead of +-lr, so a larger eps makes the parameters compare the gradients.
+    ``update_every``: update ``it`` (i_episode = it + 1) soft-updates the targets only when
+    i_episode % update_every == 0.  ``check_records``: the device's 8-field critic records
+    (``critic_records``) against the restatement's at ``tol``."""
     m = MADDPG_cls([6 + 4 * (N - 1), 18, 6], [6 + 4 * (N - 1), 18, 6], 2, n_agents=N, device=device, seed=seed,
                    memory_length=4 * E, batch_size=B)
     rep = m.attach_replay(4 * E)
@@ -202,7 +215,9 @@ def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=
     opts = None
     for it in range(iters):
         idx = [torch.from_numpy(gen.choice(len(rep), size=B, replace=False).astype(np.int32)) for _ in range(N)]
-        stats = m.update(B, use_graph=False, idx_list=[i.to(device) for i in idx])
+        soft = (it + 1) % update_every == 0
+        stats = m.update(B, use_graph=False, idx_list=[i.to(device) for i in idx], soft_update=soft)
+        recs = m.critic_records(stats) if check_records else None
         batches = []
         for i in idx:
             b = {k: v[i.long()].clone() for k, v in host.items()}
@@ -211,7 +226,19 @@ def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=
         if opts is None:
             opts = (torch.optim.Adam(actor.parameters(), lr=1e-3, eps=eps),
                     torch.optim.Adam(critic.parameters(), lr=1e-3, eps=eps))
-        rstats, opts = ref_update(actor, critic, actor_t, critic_t, batches, opts=opts)
+        rrecs = [] if check_records else None
+        rstats, opts = ref_update(actor, critic, actor_t, critic_t, batches, opts=opts, soft=soft, records=rrecs)
+        if check_records:
+            for mine, ref in zip(recs, rrecs):
+                if len(mine) != 8:
+                    raise AssertionError("critic record: 8 fields")
+                for k in range(4):
+                    a, b = np.asarray(mine[k]), np.asarray(ref[k])
+                    if a.shape != b.shape or not np.allclose(a, b, atol=tol, rtol=tol):
+                        raise AssertionError(f"critic record field {k}: {a.shape} vs {b.shape}")
+                for k in range(4, 8):
+                    if not np.allclose(np.asarray(mine[k]), np.asarray(ref[k]), atol=tol, rtol=tol):
+                        raise AssertionError(f"critic record field {k}: {mine[k]} vs {ref[k]}")
         for (lq, la, q, tg), (rlq, rla, rq, rtg) in zip(stats, rstats):
             if not torch.allclose(q.cpu().squeeze(1), rq.squeeze(1), atol=tol, rtol=tol):
                 raise AssertionError(f"Q mismatch {float((q.cpu().squeeze(1) - rq.squeeze(1)).abs().max())}")
@@ -227,4 +254,7 @@ def check_one_update(MADDPG_cls, device="cuda", N=3, B=64, E=32, tol=1e-5, seed=
             d = float((mine[k] - ref[k]).abs().max())
             if d > (tol if param_tol is None else param_tol):
                 raise AssertionError(f"param {k} differs by {d}")
+    for opt in (m.actor_optimizer, m.critic_optimizer):      # Adam steps: N per update, soft or not
+        if int(opt.step_t) != N * iters:
+            raise AssertionError(f"Adam step counter {int(opt.step_t)} != {N * iters}")
     return True

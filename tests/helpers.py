@@ -85,6 +85,58 @@ def bank_draw(bank_start, n_bank, seed, e, episode, N, pb=2.5, off=0):
     return idx
 
 
+_M64 = np.uint64((1 << 64) - 1)
+
+
+def mix64_np(x):
+    """``mix64`` over a uint64 array (numpy wraps uint64 arithmetic modulo 2^64)."""
+    x = np.asarray(x, dtype=np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def bank_draw_batch(bank_start, n_bank, seed, envs, episodes, N, pb=2.5, off=0):
+    """``bank_draw`` for many envs at once (vectorised over envs): returns the drawn bank indices
+    (len(envs), N).  Separation distances within 1e-9 of the 2 pB threshold are re-decided by the
+    scalar rule (np.linalg.norm of a 2-vector, the kernel's fma form)."""
+    envs = np.asarray(envs, dtype=np.uint64)
+    eps = np.asarray(episodes, dtype=np.uint64)
+    M = len(envs)
+    idx = np.zeros((M, N), dtype=np.int64)
+    if M == 0:
+        return idx
+    h0 = mix64_np(mix64_np(np.uint64(seed) ^ envs) ^ eps)
+    chosen = np.zeros((M, N, 2))
+    for a in range(N):
+        pick = np.full(M, -1, dtype=np.int64)
+        last = np.zeros(M, dtype=np.int64)
+        for att0 in range(0, 4096, 64):
+            todo = np.nonzero(pick < 0)[0]
+            if len(todo) == 0:
+                break
+            att = np.arange(att0, att0 + 64, dtype=np.uint64)
+            key = mix64_np(h0[todo, None] ^ (np.uint64(a * 65536) + att)[None, :])
+            k = off + (key % np.uint64(n_bank)).astype(np.int64)         # (T, 64)
+            s = bank_start[k]                                               # (T, 64, 2)
+            ok = np.ones(k.shape, dtype=bool)
+            for b in range(a):
+                o = chosen[todo, b][:, None, :]
+                d = np.sqrt((s[..., 0] - o[..., 0]) ** 2 + (s[..., 1] - o[..., 1]) ** 2)
+                near = np.abs(d - 2 * pb) < 1e-9
+                ok &= d > 2 * pb
+                for ti, j in zip(*np.nonzero(near)):       # the exact rule at the threshold
+                    ok[ti, j] = all(np.linalg.norm(s[ti, j] - chosen[todo[ti], bb]) > 2 * pb for bb in range(a))
+            first = np.where(ok.any(1), ok.argmax(1), -1)
+            hit = first >= 0
+            pick[todo[hit]] = k[hit, first[hit]]
+            last[todo] = k[:, 63]
+        pick = np.where(pick < 0, last, pick)
+        idx[:, a] = pick
+        chosen[:, a] = bank_start[pick]
+    return idx
+
+
 def uam_oracle_steps(pre, acts, N):
     """Worker for the config-5 parity test (spawned process, numpy only): one oracle/uam_ref.py
     step per env of ``pre`` (a device state dict sliced to the checked envs) from that exact

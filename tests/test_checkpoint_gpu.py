@@ -15,11 +15,11 @@ sys.path.insert(0, ROOT)
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(model):
-    import bench
+def _trainer(model, seed=1):
+    from multi_agent_aac_amd import trainer
     if model == "uam":
-        return bench.UamTrainer(256, 6, 128, 8192, seed=1)
-    return bench.Trainer(256, 5 if model == "att" else 4, 128, 4096, "combined", seed=1, model=model)
+        return trainer.UamTrainer(256, 6, 128, 8192, seed=seed)
+    return trainer.Trainer(256, 5 if model == "att" else 4, 128, 4096, "combined", seed=seed, model=model)
 
 
 def _snapshot(tr):
@@ -70,3 +70,57 @@ def test_checkpoint_refuses_mismatch(native_lib, tmp_path):
     torch.save(ck, path)
     with pytest.raises(ValueError):
         checkpoint.load(path, replay=a.replay)
+
+
+@pytest.mark.parametrize("model", ["att", "uam"])
+def test_resume_into_running_loop_with_other_seeds(native_lib, model, tmp_path, monkeypatch):
+    """a load into a loop that already captured its update graph (and, for ATT, its
+    whole-step graphs) with other replay / noise seeds -- host scalars baked into those graphs --
+    still resumes bit-identically: the load drops the stale graphs and re-seeds the ring word."""
+    from multi_agent_aac_amd import trainer
+    monkeypatch.setattr(trainer, "STEP_GRAPH", True)
+    a = _trainer(model)
+    while len(a.replay) <= a.B:
+        a.step(update=False)
+    for _ in range(2):
+        a.step(update=True)
+    path = str(tmp_path / f"{model}.ckpt")
+    a.save_checkpoint(path)
+    for _ in range(4):
+        a.step(update=True)
+    want = _snapshot(a)
+    b = _trainer(model)
+    b.model.noise_seed += 17                 # other host-side seeds, baked into b's graphs below
+    b.replay.seed += 5
+    while len(b.replay) <= b.B:
+        b.step(update=False)
+    for _ in range(2):
+        b.step(update=True)
+    if model == "att":
+        b.step_graph()
+        assert b._sg
+    assert b.model.has_graph()
+    b.load_checkpoint(path)
+    for k in range(4):
+        if model == "att" and k % 2:
+            b.step_graph()
+        else:
+            b.step(update=True)
+    got = _snapshot(b)
+    bad = [k for k in want if not torch.equal(want[k], got[k])]
+    assert not bad, bad
+
+
+def test_checkpoint_refuses_other_env_bank(native_lib, tmp_path):
+    """the auto-reset's OD bank and draw seed are part of the env's checkpoint: a bank
+    that differs is refused, a draw seed that differs is restored."""
+    a = _trainer("att", seed=1)
+    path = str(tmp_path / "att.ckpt")
+    a.save_checkpoint(path)
+    other = _trainer("att", seed=2)          # other OD bank (seed 2028) and draw seed
+    with pytest.raises(ValueError, match="bank"):
+        other.load_checkpoint(path)
+    same = _trainer("att", seed=1)
+    same.env.set_od_bank(same.bank, seed=999)
+    same.load_checkpoint(path)
+    assert same.env.bank_seed == a.env.bank_seed

@@ -112,9 +112,11 @@ def _ref_nets(m):
 KEYS = ("s_own", "s_radar", "s_nei", "act", "rew", "done", "n_own", "n_radar", "n_nei", "h_cur", "h_next")
 
 
-@pytest.mark.parametrize("N,B,own_width", [(3, 64, None), (8, 256, None), (8, 256, 6)])
-def test_gru_update_matches_cpu_restatement(native_lib, N, B, own_width):
-    """own_width 6: the replay rows of the WGRU env variant (config 4, 6-wide own observation)."""
+@pytest.mark.parametrize("N,B,own_width,every", [(3, 64, None, 1), (8, 256, None, 1), (8, 256, 6, 1),
+                                                  (3, 64, None, 2)])
+def test_gru_update_matches_cpu_restatement(native_lib, N, B, own_width, every):
+    """own_width 6: the replay rows of the WGRU env variant (config 4, 6-wide own observation).
+    every 2: UPDATE_EVERY = 2, the soft update only on even i_episode (WGRU/maddpg:320)."""
     E = 96
     m, rep = _model(N, B, E, seed=N, own_width=own_width)
     assert m.D0 == (own_width or 6 + 4 * (N - 1))
@@ -136,10 +138,11 @@ def test_gru_update_matches_cpu_restatement(native_lib, N, B, own_width):
             [torch.optim.Adam(c.parameters(), lr=1e-3, eps=eps) for c in critics])
     for it in range(3):
         idx = torch.from_numpy(gen.choice(len(rep), size=B, replace=False).astype(np.int32))
-        stats = m.update(B, use_graph=False, idx=idx.to(DEV))
+        soft = (it + 1) % every == 0
+        stats = m.update(B, use_graph=False, idx=idx.to(DEV), soft_update=soft)
         b = {k: v[idx.long()].clone() for k, v in host.items()}
         b["done"] = b["done"].float()
-        rstats, opts = gru_ref.ref_gru_update(actors, critics, actors_t, critics_t, b, m.d_own, opts=opts)
+        rstats, opts = gru_ref.ref_gru_update(actors, critics, actors_t, critics_t, b, m.d_own, opts=opts, soft=soft)
         for ag, ((lq, la, q, tg), (rlq, rla, rq, rtg)) in enumerate(zip(stats, rstats)):
             dt, dqv = float((tg.cpu() - rtg).abs().max()), float((q.cpu() - rq).abs().max())
             assert dt < 2e-5 * max(1.0, float(rtg.abs().max())), ("target", it, ag, dt)
@@ -152,6 +155,7 @@ def test_gru_update_matches_cpu_restatement(native_lib, N, B, own_width):
             for (k, v), (_, rv) in zip(mine.state_dict().items(), ref.state_dict().items()):
                 d = float((v.cpu() - rv).abs().max())
                 assert d < 2e-5, (i, k, d)
+    assert int(m.actor_optimizer.step_t) == int(m.critic_optimizer.step_t) == 3      # one Adam step per update
 
 
 def test_gru_graph_equals_eager(native_lib):

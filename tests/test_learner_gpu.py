@@ -171,6 +171,41 @@ def test_update_matches_cpu_restatement(native_lib, N, B):
     assert learner_ref.check_one_update(MADDPG, device=DEV, N=N, B=B, E=128, tol=1e-5, iters=2)
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_update_every_and_critic_records(native_lib, fused):
+    """UPDATE_EVERY = 2 (ATT/maddpg:436-438: the soft update only when i_episode % 2 == 0; the Adam
+    steps still count) and the 8-field single_eps_critic_cal_record entries (ATT/maddpg:372-379)
+    against the restatement, for the fused and the autograd learner."""
+    from multi_agent_aac_amd.maddpg import MADDPG
+
+    def cls(*a, **k):
+        return MADDPG(*a, fused=fused, **k)
+    assert learner_ref.check_one_update(cls, device=DEV, N=3, B=64, E=128, tol=1e-5, iters=3, update_every=2,
+                                        check_records=True)
+
+
+def test_update_myown_reference_api_update_every(native_lib):
+    """The reference surface: update_myown(i_episode, total, UPDATE_EVERY, record) keeps the targets
+    on odd episodes with UPDATE_EVERY = 2 and appends N 8-field records per call."""
+    from multi_agent_aac_amd.maddpg import MADDPG
+    N, B = 3, 32
+    m = MADDPG([14, 18, 6], [14, 18, 6], 2, n_agents=N, device=DEV, seed=4, batch_size=B, memory_length=256)
+    tr = learner_ref.random_transitions(64, N, 1)
+    for e in range(64):
+        st = [tr["s_own"][e].numpy(), tr["s_radar"][e].numpy(), [list(x.numpy()) for x in tr["s_nei"][e]]]
+        nx = [tr["n_own"][e].numpy(), tr["n_radar"][e].numpy(), [list(x.numpy()) for x in tr["n_nei"][e]]]
+        m.memory.push(st, tr["act"][e].numpy(), nx, tr["rew"][e].numpy(), tr["done"][e].numpy())
+    t0 = (m.fa_t.data.clone(), m.fc_t.data.clone())
+    rec = []
+    c, a, rec = m.update_myown(1, 1, 2, rec)
+    assert len(c) == N and len(rec) == N and all(len(r) == 8 for r in rec)
+    assert rec[0][1].shape == (B, N) and rec[0][2].shape == (B, 1) and rec[0][0].shape == (B,)
+    assert torch.equal(m.fa_t.data, t0[0]) and torch.equal(m.fc_t.data, t0[1])       # odd episode: no soft update
+    c, a, rec = m.update_myown(2, 2, 2, rec)
+    assert len(rec) == 2 * N and not torch.equal(m.fa_t.data, t0[0])
+    assert int(m.actor_optimizer.step_t) == 2 * N
+
+
 def test_graph_replay_equals_eager(native_lib):
     from multi_agent_aac_amd.maddpg import MADDPG
     N, B, E = 5, 128, 256

@@ -1,8 +1,9 @@
 """world_size-2 gloo tests of the data-parallel gradient exchange (CPU, no GPU), on the product's
 own flat-buffer layout: the learners' gradient buffers and the collectives they issue between
 graph segments (maddpg.MADDPG._share_grads / _allreduce_grads, gru.MADDPG._allreduce,
-uam_learner.MADDPG._allreduce_flat over parallel.allreduce_mean_); plus the data-parallel
-restatements of the oracle (``*_dp``) against the update on the union of the shards."""
+uam_learner.MADDPG._allreduce_flat over parallel.allreduce_sum_: the collectives SUM, and the
+Adam launch after each divides by the world size); plus the data-parallel restatements of the
+oracle (``*_dp``) against the update on the union of the shards."""
 import copy
 import os
 import socket
@@ -92,15 +93,15 @@ def test_product_grad_exchange_two_ranks():
             for r in (r0, r1):
                 got = r[f"att_{tag}"][j]
                 if reduced:
-                    torch.testing.assert_close(got, (l0 + l1) / 2, rtol=0, atol=1e-6)
+                    torch.testing.assert_close(got, l0 + l1, rtol=0, atol=1e-6)
                 else:                                      # the other network's half is not touched
                     assert torch.equal(got, r[f"att_{tag}_local"][j])
             if reduced:
                 assert torch.equal(r0[f"att_{tag}"][j], r1[f"att_{tag}"][j])
     for r in (r0, r1):
-        torch.testing.assert_close(r["gru"][0], (r0["gru_local"] + r1["gru_local"]) / 2, rtol=0, atol=1e-6)
-        assert torch.equal(r["gru"][0], r["gru"][1])      # the per-parameter views see the mean
-        torch.testing.assert_close(r["uam"], (r0["uam_local"] + r1["uam_local"]) / 2, rtol=0, atol=1e-15)
+        torch.testing.assert_close(r["gru"][0], r0["gru_local"] + r1["gru_local"], rtol=0, atol=1e-6)
+        assert torch.equal(r["gru"][0], r["gru"][1])      # the per-parameter views see the sum
+        torch.testing.assert_close(r["uam"], r0["uam_local"] + r1["uam_local"], rtol=0, atol=1e-15)
     assert torch.equal(r0["gru"][0], r1["gru"][0]) and torch.equal(r0["uam"], r1["uam"])
 
 

@@ -136,23 +136,28 @@ def test_step_tail_rejects_bad_fields(native_lib, occ):
     assert rc != 0 and b"OD bank" in _native.lib().aac_last_error()
 
 
-def test_whole_step_graph_equals_eager(native_lib, monkeypatch):
-    """bench.Trainer.step_graph (act + fused env tail + update_myown replayed from one captured HIP graph
-    per buffer parity, the ring position in device words) against the same steps launched eagerly:
-    bit-identical networks, optimiser state, replay ring and env state."""
-    import bench
-    monkeypatch.setattr(bench, "STEP_GRAPH", True)        # off by default in the bench (measured neutral)
-    E, N, B = 256, 5, 64
-    tr = [bench.Trainer(E, N, B, 2000, "combined", seed=0) for _ in range(2)]
+@pytest.mark.parametrize("E,N,B,mem,steps", [(256, 5, 64, 2000, 7), (4096, 5, 1024, 20000, 5)])
+def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, steps):
+    """trainer.Trainer.step_graph (act + fused env tail + update_myown replayed from one captured HIP
+    graph per buffer parity, the ring position in device words) against the same steps launched
+    eagerly: bit-identical networks, optimiser state, replay ring and env state.  The second case is
+    config 3 (4096 envs x 5 agents, B = 1024).  An eager step between graph replays re-seeds the
+    device ring-position word."""
+    from multi_agent_aac_amd import trainer
+    monkeypatch.setattr(trainer, "STEP_GRAPH", True)        # off by default in the bench (measured neutral)
+    tr = [trainer.Trainer(E, N, B, mem, "combined", seed=0) for _ in range(2)]
     for t in tr:
         while len(t.replay) <= 3 * B:
             t.step(update=False)
         for _ in range(2):
             t.step(update=True)
     assert tr[1].graph_ok()
-    for k in range(7):                      # odd: both parities, and the host mirror across the wrap
+    for k in range(steps):                  # odd: both parities, and the host mirror across the wrap
         tr[0].step(update=True)
-        tr[1].step_graph()
+        if k == steps // 2:
+            tr[1].step(update=True)         # eager step between replays: pos_dev re-seeded
+        else:
+            tr[1].step_graph()
     torch.cuda.synchronize()
     a, b = tr[0], tr[1]
     for x, y in ((a.model.fa.data, b.model.fa.data), (a.model.fc.data, b.model.fc.data),
