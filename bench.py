@@ -57,6 +57,20 @@ def env_bytes_per_agent_step(N, variant="att", mean_wp=None):
     return 130 + 4 * (24 + 10 * (N - 1))
 
 
+def push_read_floats(replay):
+    """Floats of one transition row the fused tail reads from memory: s_own, s_radar, s_nei, act
+    (fields 0-3) and the hidden states h_cur / h_next (fields 9-10); fields 4-8 are this step's
+    own outputs, written to the ring without a read-back."""
+    w = replay.widths
+    return sum(w[:4]) + sum(w[9:])
+
+
+def env_fp64_flop_per_agent_step(N):
+    """~780 (N - 1) + 300 fp64 FLOP per agent-env-step (18 rays x (N - 1)
+    64-gon clip windows + kinematics, predicates, reward)."""
+    return 780 * (N - 1) + 300
+
+
 def uam_bytes_per_agent_step(N, tdcpa=True):
     """Algorithmic HBM bytes of one UAM agent-env-step (aac_uam.hip): read
     pos, vel, action, goal, start (5 x 16), heading (8), reach (1), top2 (2) = 91; write pos, vel,
@@ -91,15 +105,28 @@ def gemm_roofline(model, B, reps=10):
     rocprof kernel trace reports it (profiles/).  achieved = algorithmic FLOPs of the launches /
     the sum of their durations."""
     from multi_agent_aac_amd.fused import GemmLaunch
+    flops, us, nbytes, n = time_launches(model, B, (GemmLaunch,), reps)
+    achieved = flops / (us * 1e-6) / 1e12
+    return {"kernel": "gemm_kernel (grouped fp32 MFMA GEMM of the fused learner)", "bound": "mfma",
+            "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+            "flop_per_launch": flops / n, "algorithmic_bytes_per_launch": nbytes / n,
+            "avg_launch_ms": us / n / 1e3, "launches_per_update": n,
+            "gemm_ms_per_update": us / 1e3, "timing": f"graph replay x{reps} per launch, HIP events"}
+
+
+def time_launches(model, B, kinds, reps=10):
+    """One eager update_myown-equivalent, then every launch of it whose type is in ``kinds`` replayed
+    ``reps`` times back to back from a captured HIP graph between a HIP event pair on the replay stream
+    (the launch's device duration without host gaps, as in the rocprof kernel trace).  Returns (sum of
+    their algorithmic FLOPs, sum of their durations in us, sum of algorithmic bytes, launch count)."""
     fu = model._fused_plan(B) if hasattr(model, "_fused_plan") else model._plan(B)
     ops = fu.ops()
     for op in ops:
         op()
     torch.cuda.synchronize()
-    flops, us, nbytes = 0.0, 0.0, 0.0
-    n = 0
+    flops, us, nbytes, n = 0.0, 0.0, 0.0, 0
     for op in ops:
-        if not isinstance(op, GemmLaunch):
+        if not isinstance(op, kinds):
             continue
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -116,12 +143,37 @@ def gemm_roofline(model, B, reps=10):
         flops += op.flops
         nbytes += op.bytes
         n += 1
-    achieved = flops / (us * 1e-6) / 1e12
-    return {"kernel": "gemm_kernel (grouped fp32 MFMA GEMM of the fused learner)", "bound": "mfma",
-            "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-            "flop_per_launch": flops / n, "algorithmic_bytes_per_launch": nbytes / n,
-            "avg_launch_ms": us / n / 1e3, "launches_per_update": n,
-            "gemm_ms_per_update": us / 1e3, "timing": f"graph replay x{reps} per launch, HIP events"}
+    return flops, us, nbytes, n
+
+
+def attn_roofline(model, B, reps=10, traffic_file=None):
+    """The actor's attention kernels of the fused learner (ActorNetwork_ATT_TwoPortion, ATT/nets:194-213)
+    against the fp32 MFMA peak: attn_enc_kernel (encoders + attention forward, riding critic encoders
+    and head jobs; fused.attn_enc_cost) and attn_mfma_bwd_kernel (fused.AttnBwd), timed per launch as
+    the GEMM roofline.  With a committed PMC file for this config, the HBM traffic per launch."""
+    from multi_agent_aac_amd.fused import AttnBwd, AttnEnc
+    pm = {}
+    if traffic_file and os.path.exists(traffic_file):
+        with open(traffic_file) as f:
+            pm = json.load(f)
+    out = {}
+    for name, kind in (("attn_enc_kernel", AttnEnc), ("attn_mfma_bwd_kernel", AttnBwd)):
+        flops, us, nbytes, n = time_launches(model, B, (kind,), reps)
+        if not n:
+            continue
+        ach = flops / (us * 1e-6) / 1e12
+        r = {"bound": "mfma", "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": ach / FP32_PEAK_TFLOPS, "flop_per_launch": flops / n, "algorithmic_bytes_per_launch": nbytes / n,
+             "avg_launch_ms": us / n / 1e3, "launches_per_update": n, "ms_per_update": us / 1e3,
+             "hbm_frac_of_algorithmic_bytes": nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS}
+        k = pm.get(name)
+        if k:
+            r["traffic"] = k.get("hbm_bytes_per_launch")
+            r["traffic_over_algorithmic"] = r["traffic"] / r["algorithmic_bytes_per_launch"]
+            r["pmc"] = {x: k[x] for x in k if x.startswith("SQ_")}
+            r["traffic_source"] = os.path.relpath(traffic_file, ROOT)
+        out[name] = r
+    return out
 
 
 def parse():
@@ -359,6 +411,10 @@ def cpu_baseline(E, N, B, radar, seconds, model="att", procs_req=None):
         m2 = pool.starmap(_cpu_numpy_worker, [(min(per, 256), N, radar, slot, w, variant) for w in range(procs)])
         cp = pool.starmap(_cpu_env_worker, [(per, N, radar, slot, w, variant) for w in range(procs)])
     m2_one = _cpu_numpy_worker(min(E, 512), N, radar, slot / 2, 0, variant)
+    # one process alone: with the per-process rate of the pool, shows how the scalar env scales with
+    # processes (the basis of the per-physical-core extrapolation; the box gives each GPU a 16-CPU
+    # share, so no pool of one process per physical core is started there)
+    m1_one = _cpu_scalar_worker(N, radar, slot / 2, 0, variant)
     t_upd, n_upd = _cpu_update_time(N, B, slot, model, procs)
 
     def mode(res, what):
@@ -368,10 +424,12 @@ def cpu_baseline(E, N, B, radar, seconds, model="att", procs_req=None):
 
     sref = "oracle/wgru_env_ref.py" if variant == "wgru" else "oracle/env_ref.py"
     modes = {"scalar_per_core": mode(m1, f"{sref} reference-shaped per-agent Python loop"),
+             "scalar_1proc": mode([m1_one], f"{sref} reference-shaped per-agent Python loop, one process"),
              "numpy_1proc": mode([m2_one], "oracle/env_np.py vectorised over envs, one process"),
              "numpy_per_core": mode(m2, "oracle/env_np.py vectorised over envs, one process per core"),
              "c_port_per_core": mode(cp, "oracle/aac_oracle.c batched C restatement, one process per core")}
     head = modes["scalar_per_core"]
+    per_proc = {"1_process": modes["scalar_1proc"]["env_only"], f"{procs}_processes": head["env_only"] / procs}
     return {"value": head["value"], "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
             "physical_cores": phys, "affinity_cores": cores, "cpu_model": cpu_model(),
             "per_physical_core_extrapolated": _extrapolate(head["env_only"], procs, phys, t_upd, E, N),
@@ -380,7 +438,8 @@ def cpu_baseline(E, N, B, radar, seconds, model="att", procs_req=None):
                        f"({head['env_only']:.3g} agent-env-steps/s env-only) + torch-CPU update_myown restatement "
                        f"B={B} x {n_upd} ({t_upd * 1e3:.1f} ms each, {procs} threads); value = {E}x{N} agent-steps / "
                        f"(env step + update) per iteration; other modes in 'modes'"),
-            "env_only": head["env_only"], "update_ms": t_upd * 1e3, "modes": modes}
+            "env_only": head["env_only"], "update_ms": t_upd * 1e3, "modes": modes,
+            "scalar_env_rate_per_process": per_proc}
 
 
 def _cpu_scalar_worker(N, radar, budget, wid, variant="att"):
@@ -587,8 +646,10 @@ def main():
         bpa = env_bytes_per_agent_step(N)
     push_bpa = 0.0
     if not uam and tr.fused_tail:
-        # the fused tail's replay push: each transition row read from its sources and written once
-        push_bpa = 2.0 * 4 * tr.replay.row_width / N
+        # the fused tail's replay push: every ring row is written once; the fields this step produces
+        # (reward, done, next own / radar / nei) go to the ring from the kernel's registers / LDS, so
+        # only the carried-in fields (current obs rows, actions, hidden states) are read
+        push_bpa = 4.0 * (tr.replay.row_width + push_read_floats(tr.replay)) / N
         bpa += push_bpa
     achieved = bpa * a.envs * N / (env_ms * 1e-3) / 1e9
     traffic = None
@@ -649,6 +710,29 @@ def main():
                             "achieved": upd_fl * upd_per_s / 1e12, "peak": peak,
                             "frac": upd_fl * upd_per_s / 1e12 / peak, "note": "whole-step rate bound"},
     }
+    if not uam and not tr.gru:
+        # the env kernel's second roofline: fp64 arithmetic (SURVEY.md section 8(d) FLOP count), with
+        # the fp64 VALU instruction counts of a PMC pass at this size when one is committed
+        fl = env_fp64_flop_per_agent_step(N)
+        ach = fl * a.envs * N / (env_ms * 1e-3) / 1e12
+        f64 = {"bound": "fp64", "flop_per_agent_step": fl, "achieved": ach, "peak": FP64_PEAK_TFLOPS,
+               "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS}
+        ppath = os.path.join(ROOT, "profiles", "env_fp64_pmc.json")
+        if os.path.exists(ppath):
+            with open(ppath) as f:
+                pm = json.load(f)
+            k = pm.get("step_kernel")
+            if k and pm.get("envs") == a.envs and pm.get("agents") == N and pm.get("radar") == a.radar:
+                # measured fp64 VALU work (every lane counted: an upper bound) at this config
+                fpl = k["fp64_flop_per_launch"]
+                f64["pmc"] = {"fp64_insts_per_launch": k["fp64_insts_per_launch"], "fp64_flop_per_launch": fpl,
+                              "fp64_flop_per_agent_step": fpl / (a.envs * N),
+                              "achieved": fpl / (env_ms * 1e-3) / 1e12,
+                              "frac": fpl / (env_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                              "valu_insts_per_launch": k.get("SQ_INSTS_VALU"),
+                              "int64_insts_per_launch": k.get("SQ_INSTS_VALU_INT64")}
+                f64["pmc_source"] = os.path.relpath(ppath, ROOT)
+        out["env_roofline"]["fp64"] = f64
     if not uam and (tr.gru or tr.model.fused):
         rf = gemm_roofline(tr.model, a.batch)
         rf["traffic"] = None
@@ -661,6 +745,9 @@ def main():
                 rf["traffic_source"] = os.path.relpath(a.gemm_traffic, ROOT)
                 rf["traffic_over_algorithmic"] = rf["traffic"] / rf["algorithmic_bytes_per_launch"]
         out["roofline"] = rf
+        if not tr.gru:
+            out["attn_roofline"] = attn_roofline(tr.model, a.batch,
+                                                 traffic_file=os.path.join(ROOT, "profiles", "r04_attn_pmc.json"))
     else:
         out["roofline"] = out["env_roofline"]
     if rank == 0 and ws == 1 and a.env_micro:

@@ -563,6 +563,7 @@ constexpr int AH_W = 8;                       // waves per workgroup
 typedef float hf4 __attribute__((ext_vector_type(4)));
 
 constexpr int AH_XS = 193;                   // LDS row stride of the staged input rows (odd: 2-way reads)
+constexpr int AH_NB = 8;                     // blocks per workgroup whose noise is drawn up front
 
 __global__ void __launch_bounds__(64 * AH_W) actor_head_ws_kernel(const float *__restrict__ cat, int ldc, int64_t R,
                                                                  const float *__restrict__ wm,
@@ -574,6 +575,7 @@ __global__ void __launch_bounds__(64 * AH_W) actor_head_ws_kernel(const float *_
                                                                  uint64_t *counter, int noisy, float *noise_out) {
     __shared__ float sX[2][16 * AH_XS];      // the block's input rows, double-buffered
     __shared__ float2 sP[2][AH_W][16];
+    __shared__ float2 sN[AH_NB * 16];        // the exploration noise of the workgroup's first AH_NB blocks
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
     const int t = threadIdx.x;
     const uint64_t ctr = noisy ? take_epoch(counter) : 0;
@@ -599,6 +601,15 @@ __global__ void __launch_bounds__(64 * AH_W) actor_head_ws_kernel(const float *_
     }
     const float ba0 = ba[0], ba1 = ba[1];
     const int64_t nblk = (R + 15) / 16;
+    // the noise does not depend on h_a: the rows of the workgroup's first AH_NB blocks get theirs now,
+    // one row per thread while the weight loads fly (in the block tail it was a float64 Box-Muller
+    // chain on 16 lanes after every block's barrier)
+    if (noisy && t < AH_NB * 16) {
+        const int64_t row = (blockIdx.x + (int64_t)(t >> 4) * gridDim.x) * 16 + (t & 15);
+        float n0 = 0.0f, n1 = 0.0f;
+        if (row < R) row_noise(row, N, episode, eps_end, noise_start, noise_end, seed, ctr, n0, n1);
+        sN[t] = make_float2(n0, n1);
+    }
     // staging of a block's 16 x 192 input floats: 768 16-B items, items t and t + 512 of this thread
     hf4 pf[2];
     auto load_rows = [&](int64_t blk) {
@@ -626,8 +637,8 @@ __global__ void __launch_bounds__(64 * AH_W) actor_head_ws_kernel(const float *_
         store_rows(sX[0]);
     }
     __syncthreads();
-    int cur = 0;
-    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    int cur = 0, kb = 0;
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x, ++kb) {
         const bool more = blk + gridDim.x < nblk;
         if (more) load_rows(blk + gridDim.x);      // in flight across the MFMA chain
         const float *x = sX[cur] + n * AH_XS + 48 * kq;
@@ -667,7 +678,13 @@ __global__ void __launch_bounds__(64 * AH_W) actor_head_ws_kernel(const float *_
                 float a0 = tanhf(s0 + ba0), a1 = tanhf(s1 + ba1);
                 if (noisy) {
                     float n0, n1;
-                    row_noise(row, N, episode, eps_end, noise_start, noise_end, seed, ctr, n0, n1);
+                    if (kb < AH_NB) {
+                        const float2 nz = sN[kb * 16 + t];
+                        n0 = nz.x;
+                        n1 = nz.y;
+                    } else {
+                        row_noise(row, N, episode, eps_end, noise_start, noise_end, seed, ctr, n0, n1);
+                    }
                     a0 = fminf(fmaxf(a0 + n0, -1.0f), 1.0f);
                     a1 = fminf(fmaxf(a1 + n1, -1.0f), 1.0f);
                     if (noise_out) reinterpret_cast<float2 *>(noise_out)[row] = make_float2(n0, n1);

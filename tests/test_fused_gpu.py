@@ -653,3 +653,130 @@ def test_merged_schedule_equals_serial(native_lib, monkeypatch):
         assert torch.equal(getattr(ms[0], name).data, getattr(ms[1], name).data), name
     assert torch.equal(ms[0].actor_optimizer.exp_avg_sq, ms[1].actor_optimizer.exp_avg_sq)
     assert nl[0] < nl[1], nl
+
+
+@pytest.mark.parametrize("N,B,with_head", [(5, 1024, False), (3, 200, True), (8, 64, False)])
+def test_dcomb_out_bwd_matches_reference(native_lib, N, B, with_head):
+    """aac_actor_dcomb_out_bwd (the actor step's critic data gradient df = (dh Wc) * (f > 0) reduced
+    straight into the actor output backward, ATT/maddpg:421-425) against fp64 torch, and against the
+    two launches it replaces (grouped-GEMM df + aac_actor_out_bwd) at fp32 rounding; a riding head job
+    equals the standalone aac_critic_head bit for bit.  B = 200: a ragged last sample block."""
+    from multi_agent_aac_amd import fused
+    torch.manual_seed(N * 100 + B)
+    P = fused.ptr
+    D0 = 6 + 4 * (N - 1)
+    Din = D0 + 2
+    R = B * N
+    dh = torch.randn(B, 256, device=DEV) * 0.1
+    Wc = torch.randn(256, 128 * N, device=DEV) * 0.05
+    f = torch.relu(torch.randn(B, 128 * N, device=DEV))
+    wenc = torch.randn(N, 128, Din, device=DEV) * 0.1
+    X = torch.rand(B, N, Din, device=DEV) * 2 - 1
+    wa = torch.randn(2, 256, device=DEV) * 0.1
+    ha = torch.relu(torch.randn(R, 256, device=DEV))
+    dout, dha = torch.full((R, 2), 7.0, device=DEV), torch.full((R, 256), 7.0, device=DEV)
+    head, houts = None, None
+    if with_head:
+        M = 3 * 64 + 5
+        hh = torch.relu(torch.randn(M, 256, device=DEV))
+        hw, hb, hy = torch.randn(256, device=DEV), torch.randn(1, device=DEV), torch.randn(M, device=DEV)
+        houts = [[torch.full((M,), 7.0, device=DEV), torch.full((M,), 7.0, device=DEV),
+                  torch.full((M, 256), 7.0, device=DEV)] for _ in range(2)]
+        q, dq, dhh = houts[0]
+        fused.critic_head(P(hh), M, P(hw), P(hb), 0, y=P(hy), q=P(q), dq=P(dq), dh=P(dhh))
+        q, dq, dhh = houts[1]
+        head = fused.head_job(P(hh), M, P(hw), P(hb), 0, y=P(hy), q=P(q), dq=P(dq), dh=P(dhh))
+    a = fused.DaobArgs(P(dh), P(Wc), P(f), P(wenc), P(X), P(wa), P(ha), P(dout), P(dha), 128 * N, Din, D0, N, B)
+    fused.DcombAob(a, head)()
+    # the two-launch path
+    df = torch.empty(B, 128 * N, device=DEV)
+    fused.GemmLaunch([fused.prob(P(dh), P(Wc), P(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=P(f),
+                                 ldmask=128 * N, mact=fused.RELU)])()
+    dout2, dha2 = torch.empty(R, 2, device=DEV), torch.empty(R, 256, device=DEV)
+    fused.actor_out_bwd(P(df), 128 * N, P(wenc), Din, D0, P(X), P(wa), P(ha), N, R, P(dout2), P(dha2))
+    torch.cuda.synchronize()
+    # fp64 reference
+    d = dh.double() @ Wc.double() * (f > 0)
+    da = torch.einsum("bnc,ncj->bnj", d.view(B, N, 128), wenc.double()[:, :, D0:D0 + 2]).reshape(R, 2)
+    a_ = X.double()[:, :, D0:D0 + 2].reshape(R, 2)
+    o = da * (1 - a_ * a_)
+    dh_ref = (o @ wa.double()) * (ha > 0)
+    np.testing.assert_allclose(dout.cpu().double(), o.cpu(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(dha.cpu().double(), dh_ref.cpu(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(dout.cpu(), dout2.cpu(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(dha.cpu(), dha2.cpu(), rtol=1e-4, atol=1e-6)
+    if with_head:
+        for x, y in zip(*houts):
+            assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("N,Bs,fold,two", [(5, 1024, True, True), (3, 200, False, False), (8, 96, True, False)])
+def test_critic_fwd_matches_reference(native_lib, N, Bs, fold, two):
+    """aac_critic_fwd (CriticCombine.forward, ATT/nets:672-724, R3, in one launch) against fp64 torch:
+    the folded actor output layer (actions into X), the encoders f, the combine h and the actor-loss
+    head's dual output dh; a second independent set and a riding head job in the same launch
+    (the head bit-equal to the standalone aac_critic_head).  Bs = 200 / 96: ragged sample blocks."""
+    from multi_agent_aac_amd import fused
+    from types import SimpleNamespace
+    torch.manual_seed(N * 7 + Bs)
+    P = fused.ptr
+    D0 = 6 + 4 * (N - 1)
+    Din = D0 + 2
+
+    def net():
+        return dict(wenc=torch.randn(N, 128, Din, device=DEV) * 0.2, benc=torch.randn(N, 128, device=DEV) * 0.1,
+                    wc=torch.randn(256, 128 * N, device=DEV) * 0.05, bc=torch.randn(256, device=DEV) * 0.1,
+                    wq=torch.randn(256, device=DEV))
+
+    def cp_of(nt):
+        return SimpleNamespace(enc_w=[P(nt["wenc"], n * 128 * Din) for n in range(N)],
+                               enc_b=[P(nt["benc"], n * 128) for n in range(N)], Wc=P(nt["wc"]), bc=P(nt["bc"]),
+                               Wq=P(nt["wq"]))
+    sets, refs, keep = [], [], []
+    for s in range(2 if two else 1):
+        nt = net()
+        X = torch.rand(Bs, N, Din, device=DEV) * 2 - 1
+        f = torch.full((Bs, 128 * N), 7.0, device=DEV)
+        h = torch.full((Bs, 256), 7.0, device=DEV)
+        dh = torch.full((Bs, 256), 7.0, device=DEV)
+        X0 = X.clone()
+        fo = None
+        if fold and s == 0:
+            ha = torch.relu(torch.randn(Bs * N, 256, device=DEV))
+            wa, ba = torch.randn(2, 256, device=DEV) * 0.1, torch.randn(2, device=DEV) * 0.1
+            ap = SimpleNamespace(Wa=P(wa), ba=P(ba))
+            fo = (P(ha), ap, D0)
+            a = torch.tanh(ha.double() @ wa.double().T + ba.double()).view(Bs, N, 2)
+            X0 = X0.double()
+            X0[:, :, D0:D0 + 2] = a
+            keep += [ha, wa, ba]
+        dscale = -1.0 / Bs
+        sets.append(fused.critic_fwd_set(cp_of(nt), P(X), Bs, N, Din, f, h, fold=fo,
+                                         dual=(P(nt["wq"]), dh, dscale) if s == 0 else None))
+        xe = X0.double()
+        fr = torch.relu(torch.einsum("bnk,nck->bnc", xe, nt["wenc"].double()) + nt["benc"].double()).reshape(Bs, -1)
+        hr = torch.relu(fr @ nt["wc"].double().T + nt["bc"].double())
+        refs.append((X, X0, f, h, dh, fr, hr, nt, s == 0))
+        keep += [X, f, h, dh, nt]
+    head, houts = None, None
+    M = 2 * 64 + 3
+    hh = torch.relu(torch.randn(M, 256, device=DEV))
+    hw, hb, hy = torch.randn(256, device=DEV), torch.randn(1, device=DEV), torch.randn(M, device=DEV)
+    houts = [[torch.full((M,), 7.0, device=DEV), torch.full((M,), 7.0, device=DEV),
+              torch.full((M, 256), 7.0, device=DEV)] for _ in range(2)]
+    q, dq, dhh = houts[0]
+    fused.critic_head(P(hh), M, P(hw), P(hb), 0, y=P(hy), q=P(q), dq=P(dq), dh=P(dhh))
+    q, dq, dhh = houts[1]
+    head = fused.head_job(P(hh), M, P(hw), P(hb), 0, y=P(hy), q=P(q), dq=P(dq), dh=P(dhh))
+    fused.CriticFwd(*sets, head=head)()
+    torch.cuda.synchronize()
+    for X, X0, f, h, dh, fr, hr, nt, first in refs:
+        if fold and first:
+            np.testing.assert_allclose(X[:, :, D0:D0 + 2].cpu().double(), X0[:, :, D0:D0 + 2].cpu(), atol=1e-6)
+        np.testing.assert_allclose(f.cpu().double(), fr.cpu(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(h.cpu().double(), hr.cpu(), rtol=1e-4, atol=1e-5)
+        if first:
+            want = (torch.from_numpy(h.cpu().numpy()) > 0).double() * (-1.0 / Bs) * nt["wq"].double().cpu()
+            np.testing.assert_allclose(dh.cpu().double(), want, rtol=1e-6, atol=1e-9)
+    for x, y in zip(*houts):
+        assert torch.equal(x, y)

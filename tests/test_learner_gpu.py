@@ -171,6 +171,18 @@ def test_update_matches_cpu_restatement(native_lib, N, B):
     assert learner_ref.check_one_update(MADDPG, device=DEV, N=N, B=B, E=128, tol=1e-5, iters=2)
 
 
+@pytest.mark.parametrize("cfwd,daob", [(True, True), (False, False)])
+def test_update_launch_forms_match_cpu_restatement(native_lib, monkeypatch, cfwd, daob):
+    """The non-default launch forms of the fused update (AAC_CFWD=1: CriticCombine.forward as one
+    critic_fwd launch; AAC_DAOB=0: the critic data gradient and actor output backward as two launches)
+    against the same restatement."""
+    from multi_agent_aac_amd import fused
+    from multi_agent_aac_amd.maddpg import MADDPG
+    monkeypatch.setattr(fused.FusedUpdate, "CFWD", cfwd)
+    monkeypatch.setattr(fused.FusedUpdate, "DAOB", daob)
+    assert learner_ref.check_one_update(MADDPG, device=DEV, N=5, B=256, E=128, tol=1e-5, iters=2)
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_update_every_and_critic_records(native_lib, fused):
     """UPDATE_EVERY = 2 (ATT/maddpg:436-438: the soft update only when i_episode % 2 == 0; the Adam
