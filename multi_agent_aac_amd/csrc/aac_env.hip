@@ -47,6 +47,7 @@ struct Args {
     double gx0, gy0, xs, ys;
     double dt, acc_max, vmax, pb, radar_len;
     double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp, *start;
+    double2 *wp0;        // [E][N] = wp[cur] (variant 0): the step reads it coalesced instead of gathering
     int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx;   // variant 1: wp_cur = removed-waypoint bits
     uint8_t *reach;
     const uint8_t *occ;  // n_maps * gw * gh
@@ -98,6 +99,7 @@ struct Tail {
     float *zero_rows;         // [E][zero_w] rows zeroed for the finished envs (after the push); null = none
     int zero_w;
     int reset;                // 1: auto-reset the finished envs from the OD bank (after the push)
+    int spec;                 // 1: their OD draws made during the step by the agent-free waves (spec_draw)
 };
 
 // ring row of env e for this push (pos < cap, e < E <= cap)
@@ -571,11 +573,88 @@ __device__ inline void store_rows(float *dst, const float *src, int n) {
 // env slot lq of the workgroup: its entry of the packed list (emap) or the contiguous range
 __device__ inline int env_of(const int32_t *emap, int e0, int lq) { return emap ? emap[lq] : e0 + lq; }
 
+// The fused tail's OD draws, made speculatively during the step by the waves that hold no agent
+// (they idle through the agent phase): every env of the workgroup draws its next episode's N bank
+// entries as reset_body would (the same keys: episode + 1, the same first-valid-attempt rule), so a
+// finished env's reset starts at its waypoint copy.  Nothing global is written here: bank indices go
+// to S.idx[agent], the starts to spec_starts (the radar-minimum words past the agents; ATT does not
+// use them, WGRU only the first nag), episode and map per env to S.idx[nag + env], S.idx[nag + epb
+// + env].  Needs nag <= SPEC_MAX_AG (spec_ok).
+constexpr int SPEC_MAX_AG = 84;
+__device__ inline double2 *spec_starts(Lds &S, int nag) {
+    return reinterpret_cast<double2 *>(&S.rmin[(nag + 1) & ~1]);
+}
+__device__ inline bool spec_ok(const Args &A, const ResetArgs &R) {
+    return R.mode == 1 && A.epb * A.N <= SPEC_MAX_AG && !R.list;
+}
+__device__ void spec_draw(const Args &A, const ResetArgs &R, Lds &S, int e0, int wv, int nw) {
+    // 16 lanes per env (four envs per wave at once): the draws of different envs are independent,
+    // an env's N draws are a chain of dependent loads; 16 attempts per round (the first attempt
+    // almost always succeeds), the lowest valid one wins as in reset_body
+    const int N = A.N, nag = A.epb * N, lane = threadIdx.x & 63, gq = lane >> 4, gl = lane & 15;
+    double2 *ss = spec_starts(S, nag);
+    for (int l0 = 4 * wv; l0 < A.epb; l0 += 4 * nw) {
+        const int lq = l0 + gq, eq = e0 + lq;
+        const bool live = lq < A.epb && eq < A.E;
+        const int ep = live ? R.episode[eq] + 1 : 0;
+        const int bq = lq * N;
+        int mp = 0, boff = 0, bn = R.bank_n;
+        if (R.bank_maps > 1 && live) {
+            mp = (int)(mix64(mix64(mix64(R.seed ^ 0x6d61705f64726177ull ^ (uint64_t)eq) ^ (uint64_t)ep)) %
+                       (uint64_t)R.bank_maps);
+            boff = R.bank_off[mp];
+            bn = R.bank_off[mp + 1] - boff;
+        }
+        const uint64_t ke = mix64(mix64(R.seed ^ (uint64_t)eq) ^ (uint64_t)ep);
+        for (int a = 0; a < N; ++a) {
+            int chosen = live ? -1 : 0, last = 0, pl = 15;
+            double2 sp = make_double2(0.0, 0.0);
+            for (int att0 = 0; att0 < 4096; att0 += 16) {
+                const bool go = chosen < 0;                  // uniform per 16-lane group
+                if (!__ballot(go)) break;
+                bool ok = false;
+                int idx = 0;
+                if (go) {
+                    const uint64_t key = mix64(ke ^ ((uint64_t)a * 65536ull + (att0 + gl)));
+                    idx = boff + (int)(key % (uint64_t)bn);
+                    sp = R.bank_start[idx];
+                    ok = true;
+                    for (int b = 0; b < a; ++b) {
+                        const double2 o = ss[bq + b];
+                        if (!(npnorm(sp.x - o.x, sp.y - o.y) > A.pb * 2)) ok = false;
+                    }
+                }
+                const unsigned m = (unsigned)(__ballot(ok) >> (16 * gq)) & 0xffffu;
+                const int cidx = __shfl(idx, 16 * gq + (m ? __ffs(m) - 1 : 0), 64);
+                const int lidx = __shfl(idx, 16 * gq + 15, 64);
+                if (go) {
+                    if (m) {
+                        pl = __ffs(m) - 1;
+                        chosen = cidx;
+                    }
+                    last = lidx;
+                }
+            }
+            const double spx = __shfl(sp.x, 16 * gq + pl, 64), spy = __shfl(sp.y, 16 * gq + pl, 64);
+            if (live && gl == 0) {
+                S.idx[bq + a] = chosen >= 0 ? chosen : last;
+                ss[bq + a] = make_double2(spx, spy);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        }
+        if (live && gl == 0) {
+            S.idx[nag + lq] = ep;
+            S.idx[nag + A.epb + lq] = mp;
+        }
+    }
+}
+
 // The reset of the workgroup's envs with S.active[le] set (at least one): OD draw (bank mode) or the
 // given OD, waypoint lists, state, radar and observation rows.  Shared by reset_kernel and the fused
 // step tail (step_kernel<.., true>), which calls it after its replay push with the maps in LDS.
 __device__ __attribute__((always_inline)) void reset_body(const Args &A, const ResetArgs &R, Lds &S, const int32_t *emap,
-                                                          int e0, bool maps_loaded) {
+                                                          int e0, bool maps_loaded, bool predrawn = false) {
     const int N = A.N;
     const int nag = A.epb * N;
     const int t = threadIdx.x;
@@ -585,7 +664,14 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
     if (!maps_loaded) load_maps(A);
-    if (R.mode == 1) {
+    if (predrawn) {
+        // the draws were made during the step (spec_draw): bank indices in S.idx, starts in
+        // spec_starts, episode / map per env after the indices
+        if (t < A.epb && S.active[t] && e0 + t < A.E) {
+            R.episode[e0 + t] = S.idx[nag + t];
+            if (A.map_idx) A.map_idx[e0 + t] = S.idx[nag + A.epb + t];
+        }
+    } else if (R.mode == 1) {
         // draw N OD entries; starts pairwise > 2 pB apart (ATT/env:258-268).  One wave per
         // resetting env: the 64 lanes test 64 consecutive attempts of agent a at once and the
         // lowest valid attempt wins, i.e. exactly the sequential rule (first valid attempt, else
@@ -670,9 +756,12 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                if (ok[u]) A.wp[dst[u]] = v[u];
                 const int w = w0 + u * BLOCK + t;
                 const int la = w / A.W, k = w - la * A.W;
+                if (ok[u]) {
+                    A.wp[dst[u]] = v[u];
+                    if (k == 0) A.wp0[dst[u] / A.W] = v[u];      // the current waypoint (cur = 0)
+                }
                 if (R.mode == 1 && ok[u] && k == cn[u] - 1) {
                     S.goal[la] = v[u];
                     S.rmin[la] = (unsigned long long)cn[u];
@@ -685,7 +774,7 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
         double2 st, g;
         int cnt;
         if (R.mode == 1) {
-            st = S.ppos[t];        // the chosen start (draw above)
+            st = predrawn ? spec_starts(S, nag)[t] : S.ppos[t];        // the chosen start (draw above)
             cnt = (int)S.rmin[t];
             g = S.goal[t];
         } else {
@@ -817,6 +906,21 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     const int nv = e0 + A.epb <= A.E ? A.epb : A.E - e0;     // envs of this workgroup
     if (TAIL && t < A.epb) S.active[t] = 0;      // env_done of the workgroup's envs (set below)
     RingOut ro{};
+    // the kinematics' own state, loaded first: in flight across the push's early copy and the map
+    // load (the agent phase's state stays in flight across the radar)
+    int cur = 0, wcnt = 0;
+    uint8_t reach = 0;
+    double2 pp = make_double2(0.0, 0.0), pv = pp, gl = pp;
+    float2 a = make_float2(0.0f, 0.0f);
+    if (active) {
+        cur = A.wp_cur[ai];
+        wcnt = A.wp_cnt[ai];
+        reach = A.reach[ai];
+        pp = A.pos[ai];
+        pv = A.vel[ai];
+        a = act[ai];
+        gl = A.goal[ai];
+    }
     // the ring position of this push: the host's mirror, or (graph replays) a device word
     const int64_t rpos = TAIL && T.ring ? (T.pos_in ? *T.pos_in : T.pos) : 0;
     if constexpr (TAIL) {
@@ -842,18 +946,8 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     load_maps(A);
 
     // ---- a1: kinematics (ATT/env:2639-2713)
-    double2 np = make_double2(0.0, 0.0), pp = np, w0 = np;
-    int cur = 0, wcnt = 0;
-    uint8_t reach = 0;
+    double2 np = make_double2(0.0, 0.0), w0 = np;
     if (active) {
-        // the agent phase's own state, loaded now: its latency hides under the radar phase
-        // (the barriers below order LDS only, so these loads stay in flight across them)
-        cur = A.wp_cur[ai];
-        wcnt = A.wp_cnt[ai];
-        reach = A.reach[ai];
-        pp = A.pos[ai];
-        const double2 pv = A.vel[ai];
-        const float2 a = act[ai];
         double2 nv;
         double ax = (double)a.x * A.acc_max, ay = (double)a.y * A.acc_max;
         double cvx = pv.x + ax * A.dt, cvy = pv.y + ay * A.dt;
@@ -872,8 +966,8 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         S.vel[t] = nv;
         S.ppos[t] = pp;
         S.pvel[t] = pv;
-        S.goal[t] = A.goal[ai];
-        if (!A.variant) w0 = A.wp[(size_t)ai * A.W + cur];     // variant 1: cur is a bit mask
+        S.goal[t] = gl;
+        if (!A.variant) w0 = A.wp0[ai];     // = wp[cur]; variant 1: cur is a bit mask
     }
     if (A.variant) S.rmin[t] = 0x7ff0000000000000ull;       // +inf
     // variant 1: the first WPC waypoints of every agent of the workgroup, loaded now by all threads
@@ -917,6 +1011,13 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     ESTAMP(3, __builtin_amdgcn_s_memtime());
     const int D0 = A.D0, K6 = A.K * 6;
     const bool stage = nag * (D0 + K6) <= OBS_STAGE_FLOATS;     // uniform
+    bool spec = false;
+    if constexpr (TAIL) {
+        // the next episodes' OD draws on the waves without agents, beside the agent phase
+        const int wfirst = (nag + 63) >> 6;
+        spec = T.reset && spec_ok(A, R) && wfirst < BLOCK / 64 && T.spec;
+        if (spec && (t >> 6) >= wfirst) spec_draw(A, R, S, e0, (t >> 6) - wfirst, BLOCK / 64 - wfirst);
+    }
 #ifdef AAC_DBG_SKIP_AGENT
     if (false) {
 #else
@@ -1001,7 +1102,10 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
                 reach = 1;
                 A.reach[ai] = 1;
             } else {
-                if (wpf && wcnt - cur > 1) A.wp_cur[ai] = cur + 1;
+                if (wpf && wcnt - cur > 1) {
+                    A.wp_cur[ai] = cur + 1;
+                    A.wp0[ai] = A.wp[ai * A.W + cur + 1];
+                }
                 r = dtg - pen;
             }
         }
@@ -1083,11 +1187,21 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
                     if (S.active[r]) T.zero_rows[(size_t)e0 * T.zero_w + j] = 0.f;
                 }
             }
-            if (T.reset) reset_body(A, R, S, nullptr, e0, true);
+            if (T.reset) reset_body(A, R, S, nullptr, e0, true, spec);
         }
     }
     ESTAMP(5, __builtin_amdgcn_s_memtime());
     ESTAMP(6, __builtin_amdgcn_s_memrealtime());
+}
+
+// wp0 = wp[cur] after the host set wp / wp_cur (aac_env_set_state); cur clamped into the list
+__global__ void __launch_bounds__(256) wp0_refresh_kernel(double2 *wp0, const double2 *wp, const int32_t *cur,
+                                                          int64_t EN, int W) {
+    const int64_t ai = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (ai >= EN) return;
+    int c = cur[ai];
+    c = c < 0 ? 0 : (c >= W ? W - 1 : c);
+    wp0[ai] = wp[ai * W + c];
 }
 
 __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
@@ -1158,7 +1272,7 @@ struct aac_env {
     aac_env_cfg cfg;
     int device;
     int K, D0, W, epb, blocks;
-    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp, *start;
+    double2 *pos, *vel, *pre_pos, *pre_vel, *goal, *wp, *start, *wp0;
     int32_t *wp_cur, *wp_cnt, *wall, *step, *map_idx, *episode;
     int32_t *episode_own;     // the handle's own counter buffer (episode may be a caller's buffer)
     uint8_t *reach, *occ;
@@ -1209,6 +1323,7 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
     A.pre_vel = h->pre_vel;
     A.goal = h->goal;
     A.wp = h->wp;
+    A.wp0 = h->wp0;
     A.start = h->start;
     A.wp_cur = h->wp_cur;
     A.wp_cnt = h->wp_cnt;
@@ -1302,7 +1417,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     if (st == hipSuccess) st = hipMalloc((void **)&h->p, (n) * sizeof(*h->p)); \
     if (st == hipSuccess) st = hipMemset(h->p, 0, (n) * sizeof(*h->p));
     ALLOC(pos, EN) ALLOC(vel, EN) ALLOC(pre_pos, EN) ALLOC(pre_vel, EN) ALLOC(goal, EN) ALLOC(start, EN)
-    ALLOC(wp, EN * h->W) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
+    ALLOC(wp, EN * h->W) ALLOC(wp0, EN) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
     ALLOC(rlist, (size_t)c.E + 1)
     h->episode_own = h->episode;
@@ -1333,7 +1448,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
 
 void aac_env_destroy(aac_env *h) {
     if (!h) return;
-    void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->start, h->wp, h->wp_cur, h->wp_cnt, h->wall,
+    void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->start, h->wp, h->wp0, h->wp_cur, h->wp_cnt, h->wall,
                     h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt,
                     h->bank_off, h->rlist, h->occ_rows};
     for (void *p : ptrs)
@@ -1454,6 +1569,12 @@ int aac_env_step_tail(aac_env *h, const float *actions, const aac_step_out *o, c
         if (!h->bank_n) return fail(AAC_E_STATE, "no OD bank installed (aac_env_set_od_bank)");
         R = bank_reset_args(h);
         T.reset = 1;
+        // AAC_ENV_SPEC_DRAW=0: draw after the step, as reset_kernel does (A/B switch; same results)
+        static const int spec = [] {
+            const char *v = getenv("AAC_ENV_SPEC_DRAW");
+            return v ? atoi(v) : 1;
+        }();
+        T.spec = spec;
     }
     return launch_step(h, actions, o, R, T, true, stream);
 }
@@ -1600,6 +1721,11 @@ int aac_env_set_state(aac_env *h, const double *pos, const double *vel, const do
     CPY(h->pre_vel, pre_vel, EN * 16) CPY(h->goal, goal, EN * 16) CPY(h->wp, wp, EN * h->W * 16)
     CPY(h->wp_cur, wp_cur, EN * 4) CPY(h->wp_cnt, wp_cnt, EN * 4) CPY(h->reach, reach, EN)
     CPY(h->wall, wall, EN * 4) CPY(h->step, step, E * 4) CPY(h->map_idx, map_idx, E * 4)
+    if (wp || wp_cur) {      // the compact current-waypoint copy follows wp / wp_cur
+        hipLaunchKernelGGL(wp0_refresh_kernel, dim3((unsigned)((EN + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           h->wp0, h->wp, h->wp_cur, (int64_t)EN, h->W);
+        HIPCHK(hipGetLastError());
+    }
     return AAC_OK;
 }
 #undef CPY
