@@ -100,6 +100,8 @@ struct Tail {
     int zero_w;
     int reset;                // 1: auto-reset the finished envs from the OD bank (after the push)
     int spec;                 // 1: their OD draws made during the step by the agent-free waves (spec_draw)
+    int tab_off;              // float offset of the early fields' column table in the staging area (its end)
+    int late_copy;            // 1: the early fields are copied by the agent-free waves during the agent phase
 };
 
 // ring row of env e for this push (pos < cap, e < E <= cap)
@@ -828,10 +830,11 @@ struct TailDesc {
 };
 static_assert(sizeof(TailDesc) == 16, "one ds_read_b128 per descriptor");
 
-__device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, int64_t rpos, int e0, int nv,
-                                                                float *scratch) {
+// the column table (descriptors, running column counts, compact column -> field), written by all
+// threads at kernel start from the kernel arguments; the caller orders it with a barrier
+__device__ __attribute__((always_inline)) void tail_table(const Tail &T, float *table) {
     const int t = threadIdx.x;
-    TailDesc *desc = reinterpret_cast<TailDesc *>(scratch);
+    TailDesc *desc = reinterpret_cast<TailDesc *>(table);
     int *cum = reinterpret_cast<int *>(desc + TAIL_MAX_FIELDS);
     uint8_t *lut = reinterpret_cast<uint8_t *>(cum + TAIL_MAX_FIELDS + 1);
     const int ne = T.cum[T.nf];
@@ -841,14 +844,23 @@ __device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, in
             desc[q] = TailDesc{T.src[q], T.width[q] | (T.dtype[q] << 30), T.col[q] - T.cum[q]};
             cum[q] = T.cum[q];
         }
-    __syncthreads();
     for (int k = t; k < ne; k += BLOCK) {
         int f = 0;
-        for (int q = 1; q < T.nf; ++q) f += k >= cum[q];
+#pragma unroll
+        for (int q = 1; q < TAIL_MAX_FIELDS; ++q) f += q < T.nf && k >= T.cum[q];
         lut[k] = (uint8_t)f;
     }
-    __syncthreads();
-    const int ncol = t < ne ? (ne - t + BLOCK - 1) / BLOCK : 0;
+}
+
+// the copy of the early fields by threads tid = 0 .. nthr - 1 (all of the workgroup at kernel start,
+// or the waves without agents during the agent phase: T.late_copy)
+__device__ __attribute__((always_inline)) void tail_copy(const Tail &T, int64_t rpos, int e0, int nv,
+                                                          const float *table, int tid, int nthr) {
+    const TailDesc *desc = reinterpret_cast<const TailDesc *>(table);
+    const int *cum = reinterpret_cast<const int *>(desc + TAIL_MAX_FIELDS);
+    const uint8_t *lut = reinterpret_cast<const uint8_t *>(cum + TAIL_MAX_FIELDS + 1);
+    const int ne = T.cum[T.nf];
+    const int ncol = tid < ne ? (ne - tid + nthr - 1) / nthr : 0;
     const int items = ncol * nv;
     constexpr int U = 8;
     for (int j0 = 0; j0 < items; j0 += U) {
@@ -859,7 +871,7 @@ __device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, in
             const int j = j0 + u;
             const bool ok = j < items;
             const int sl = j / nv, r = j - sl * nv;
-            const int k = ok ? t + sl * BLOCK : 0;
+            const int k = ok ? tid + sl * nthr : 0;
             const int f = lut[k];
             const TailDesc d = desc[f];
             const int w = d.width & 0x3fffffff;
@@ -873,7 +885,6 @@ __device__ __attribute__((always_inline)) void tail_push_early(const Tail &T, in
         for (int u = 0; u < U; ++u)
             if (dst[u]) *dst[u] = v[u];
     }
-    __syncthreads();      // the scratch area is the observation staging area of the step
 }
 
 // --------------------------------------------------------------------------------- step
@@ -939,7 +950,9 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
                     T.meta[1] = T.new_size;
                 }
             }
-            tail_push_early(T, rpos, e0, nv, S.obs);
+            tail_table(T, S.obs + T.tab_off);
+            __syncthreads();
+            if (!T.late_copy) tail_copy(T, rpos, e0, nv, S.obs + T.tab_off, t, BLOCK);
             if (T.late[LATE_RADAR] >= 0) ro = RingOut{T.ring, rpos, T.cap, T.rw, T.late[LATE_RADAR]};
         }
     }
@@ -1017,6 +1030,12 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         const int wfirst = (nag + 63) >> 6;
         spec = T.reset && spec_ok(A, R) && wfirst < BLOCK / 64 && T.spec;
         if (spec && (t >> 6) >= wfirst) spec_draw(A, R, S, e0, (t >> 6) - wfirst, BLOCK / 64 - wfirst);
+        // the push's early fields on the waves after those (all agent-free waves when no draw runs; at
+        // kernel start when there are none)
+        if (T.ring && T.late_copy) {
+            const int wc = wfirst + (spec ? 1 : 0) < BLOCK / 64 ? wfirst + (spec ? 1 : 0) : wfirst;
+            if (wc < BLOCK / 64 && (t >> 6) >= wc) tail_copy(T, rpos, e0, nv, S.obs + T.tab_off, t - 64 * wc, BLOCK - 64 * wc);
+        }
     }
 #ifdef AAC_DBG_SKIP_AGENT
     if (false) {
@@ -1554,8 +1573,19 @@ int aac_env_step_tail(aac_env *h, const float *actions, const aac_step_out *o, c
             T.col[q] = 0;
             T.cum[q + 1] = ne;
         }
-        if (sizeof(TailDesc) * TAIL_MAX_FIELDS + sizeof(int) * (TAIL_MAX_FIELDS + 1) + ne > sizeof(float) * OBS_STAGE_FLOATS)
+        const size_t tab = sizeof(TailDesc) * TAIL_MAX_FIELDS + sizeof(int) * (TAIL_MAX_FIELDS + 1) + ne;
+        if (tab > sizeof(float) * OBS_STAGE_FLOATS)
             return fail(AAC_E_INVALID, "step tail: too many early columns for the column table");
+        // the table at the end of the staging area; the early copy moves into the agent phase when the
+        // staged observation rows leave it alone and some wave holds no agent
+        T.tab_off = (int)((sizeof(float) * OBS_STAGE_FLOATS - tab) / sizeof(float)) & ~3;
+        const int nag = h->epb * N, stage = nag * (h->D0 + 6 * K);
+        const int staged = stage <= OBS_STAGE_FLOATS ? stage : 0;
+        static const int late_env = [] {
+            const char *v = getenv("AAC_ENV_LATE_COPY");
+            return v ? atoi(v) : 1;
+        }();
+        T.late_copy = late_env && staged <= T.tab_off && (nag + 63) / 64 < BLOCK / 64;
         if ((T.late[LATE_OWN] >= 0 || T.late[LATE_NEI] >= 0) &&
             h->epb * h->cfg.N * (h->D0 + 6 * K) > OBS_STAGE_FLOATS)
             return fail(AAC_E_INVALID, "step tail: observation rows too wide to push from the staging area");
