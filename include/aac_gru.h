@@ -95,6 +95,16 @@ typedef struct {
      * in place of the encoder and gate grouped-GEMM launches; hout, y, Wout, bout are not used. */
     float *cat, *gi, *gh;
     int32_t ldc, ldg;
+    /* act mode, noisy != 0: the exploration noise and clamp of choose_action (WGRU/maddpg:336-428) on y
+     * in the same launch -- exactly aac_noise_clamp(y, E, N, episode, eps_end, noise_start, noise_end,
+     * seed, counter, noise_out) after it (same per-row noise, the counter's epoch advances once) */
+    int32_t noisy;
+    const int32_t *episode;
+    int32_t eps_end;
+    float noise_start, noise_end;
+    uint64_t seed;
+    uint64_t *counter;
+    float *noise_out;
 } aac_gru_actor_args;
 
 int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream);

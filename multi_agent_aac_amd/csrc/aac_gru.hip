@@ -17,6 +17,7 @@
 
 #include "../../include/aac_gru.h"
 #include "aac_wave.h"
+#include "aac_noise.h"
 
 namespace {
 
@@ -176,8 +177,23 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
         wo1[v] = PROJ ? 0.0f : Wout[64 + u0 + v];
     }
     const float bout0 = PROJ ? 0.0f : A.bout[po], bout1 = PROJ ? 0.0f : A.bout[po + 1];
+    const uint64_t ctr = (!PROJ && A.noisy) ? aacn::take_epoch(A.counter) : 0;     // one epoch per launch
+    // the noise of the workgroup's first GNB blocks, one row per thread up front (its fp64 Box-Muller
+    // beside the weight loads instead of 32 threads per block on the output stage's chain)
+    constexpr int GNB = 256 / GROWS;
+    __shared__ float2 sN[PROJ ? 1 : GNB][PROJ ? 1 : GROWS];
+    if (!PROJ && A.noisy) {
+        const int bi = threadIdx.x / GROWS, x = threadIdx.x - bi * GROWS;
+        const int e = (g + bi * G) * GROWS + x;
+        if (e < A.E) {
+            float n0, n1;
+            aacn::row_noise((int64_t)e * A.N + ag, A.N, A.episode, A.eps_end, A.noise_start, A.noise_end, A.seed,
+                            ctr, n0, n1);
+            sN[bi][x] = make_float2(n0, n1);
+        }
+    }
     const int nblk = (A.E + GROWS - 1) / GROWS;
-    for (int blk = g; blk < nblk; blk += G) {
+    for (int blk = g, bi = 0; blk < nblk; blk += G, ++bi) {
         const int e0 = blk * GROWS;
         float bo_[GNT][2], br[GNT][5], bh[GNT][16];
         f4 hv[GNT];
@@ -301,9 +317,27 @@ __global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A
             if (e < A.E) {
                 const float s0 = ((sP[0][x][0] + sP[1][x][0]) + sP[2][x][0]) + sP[3][x][0];
                 const float s1 = ((sP[0][x][1] + sP[1][x][1]) + sP[2][x][1]) + sP[3][x][1];
-                float *yo = A.y + ((size_t)e * A.N + ag) * A.ldy;
-                yo[0] = tanhf(s0 + bout0);
-                yo[1] = tanhf(s1 + bout1);
+                const size_t row = (size_t)e * A.N + ag;
+                float *yo = A.y + row * A.ldy;
+                float y0 = tanhf(s0 + bout0), y1 = tanhf(s1 + bout1);
+                if (A.noisy) {       // noise_kernel's arithmetic on the stored tanh values
+                    float n0, n1;
+                    if (bi < GNB) {
+                        n0 = sN[bi][x].x;
+                        n1 = sN[bi][x].y;
+                    } else {
+                        aacn::row_noise((int64_t)row, A.N, A.episode, A.eps_end, A.noise_start, A.noise_end, A.seed,
+                                        ctr, n0, n1);
+                    }
+                    y0 = fminf(fmaxf(y0 + n0, -1.0f), 1.0f);
+                    y1 = fminf(fmaxf(y1 + n1, -1.0f), 1.0f);
+                    if (A.noise_out) {
+                        A.noise_out[2 * row] = n0;
+                        A.noise_out[2 * row + 1] = n1;
+                    }
+                }
+                yo[0] = y0;
+                yo[1] = y1;
             }
         }
     }
@@ -367,6 +401,7 @@ int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream) {
     } else {
         if (!a.hout || !a.y || !a.Wout || !a.bout || a.ldy < 2) return gfail("gru_actor_fwd: NULL output operand");
         if (a.ldho % 4 || a.ldho < H || !al16(a.hout)) return gfail("gru_actor_fwd: hout rows must be 16-B aligned");
+        if (a.noisy && (!a.counter || a.ldy != 2)) return gfail("gru_actor_fwd: noisy needs a counter and ldy == 2");
     }
     // one workgroup per CU in all (one wave per SIMD: ~250 registers of weights per lane)
     const int rows = proj ? 16 : 32;

@@ -18,6 +18,10 @@
 
 #include "../../include/aac_learn.h"
 #include "aac_wave.h"
+#include "aac_noise.h"
+
+using aacn::row_noise;
+using aacn::take_epoch;
 
 namespace {
 
@@ -139,22 +143,6 @@ struct Fields {
     int n;
 };
 
-// A launch-wide counter advanced by the launch itself (no one-thread follow-up kernel): word =
-// epoch (low 32 bits) | arrivals (high 32 bits, 0 between launches).  Thread 0 of every workgroup
-// takes the epoch with one atomic add to the arrivals; the last workgroup to arrive has seen every
-// other one take it and stores epoch + 1 with arrivals 0.  Returns the epoch to the whole group.
-__device__ inline uint64_t take_epoch(uint64_t *word) {
-    __shared__ uint64_t ep;
-    if (threadIdx.x == 0) {
-        const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long *>(word), 1ull << 32);
-        ep = old & 0xffffffffull;
-        if ((old >> 32) == (uint64_t)(gridDim.x * gridDim.y * gridDim.z) - 1)
-            // low 32 bits only: the arrival field must restart at 0 even when the epoch wraps
-            atomicExch(reinterpret_cast<unsigned long long *>(word), (unsigned long long)((ep + 1) & 0xffffffffull));
-    }
-    __syncthreads();
-    return ep;
-}
 
 __global__ void __launch_bounds__(LEARN_BLOCK) push_kernel(float *ring, int rw, int64_t cap, const int64_t *meta,
                                                           Fields F) {
@@ -445,28 +433,6 @@ __global__ void bias_act_kernel(float *y, const float *__restrict__ b, int64_t n
 }
 
 // ------------------------------------------------------------------------------ noise
-// the exploration noise of agent row `row` (env row / N): var from the env's episode (linear
-// schedule to eps_end, then noise_end), Box-Muller pair from the hash of (seed, epoch, row)
-__device__ __forceinline__ void row_noise(int64_t row, int N, const int32_t *episode, int eps_end, float noise_start,
-                                          float noise_end, uint64_t seed, uint64_t ctr, float &n0, float &n1) {
-    const int e = (int)(row / N);
-    const int ep = episode ? episode[e] : 1;
-    double var;
-    if (ep <= eps_end) {
-        const double slope = ((double)noise_end - (double)noise_start) / (double)(eps_end - 1);
-        var = (double)noise_start + slope * (double)(ep - 1);
-    } else {
-        var = (double)noise_end;
-    }
-    const uint64_t h1 = mix64(mix64(mix64(seed) ^ ctr) ^ (uint64_t)(2 * row));
-    const uint64_t h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
-    const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
-    const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
-    const double rr = sqrt(-2.0 * log(u1));
-    const double z0 = rr * cos(6.283185307179586 * u2), z1 = rr * sin(6.283185307179586 * u2);
-    n0 = (float)(z0 * var);
-    n1 = (float)(z1 * var);
-}
 
 __global__ void noise_kernel(float *act, int E, int N, const int32_t *episode, int eps_end, float noise_start,
                              float noise_end, uint64_t seed, uint64_t *counter, float *noise_out) {

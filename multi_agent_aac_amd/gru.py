@@ -61,7 +61,9 @@ class GruActorArgs(ctypes.Structure):
     _fields_ = [("own", vp), ("ld_own", i32), ("d_own", i32), ("radar", vp), ("ld_radar", i32), ("h", vp),
                 ("ldh", i32)] + [(k, vp) for k in ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout", "bout")] + \
                [("pstride", i32), ("E", i32), ("N", i32), ("hout", vp), ("ldho", i32), ("y", vp), ("ldy", i32),
-                ("cat", vp), ("gi", vp), ("gh", vp), ("ldc", i32), ("ldg", i32)]
+                ("cat", vp), ("gi", vp), ("gh", vp), ("ldc", i32), ("ldg", i32),
+                ("noisy", i32), ("episode", vp), ("eps_end", i32), ("noise_start", f32), ("noise_end", f32),
+                ("seed", ctypes.c_uint64), ("counter", vp), ("noise_out", vp)]
 
 
 # weights-stationary aac_gru_actor_fwd: the act path as one launch instead of the encoder and gate
@@ -420,6 +422,10 @@ class GruUpdate:
         return out
 
 
+def _p_or_none(t):
+    return None if t is None else ptr(t)
+
+
 class _ActPlan:
     """Batched choose_action for E envs: enc | gates | GRU fwd (actions, next hidden).  Built for
     fixed input / output buffers (no copies): own, radar, h as given, the next hidden into h_out (a
@@ -438,7 +444,8 @@ class _ActPlan:
         self.hn = h_out if h_out is not None else torch.empty(E, N, H, device=dev)
         assert self.hn.is_contiguous() and self.hn.shape == (E, N, H)
         A = stack_addrs(m.actors, ACTOR_PARAMS, m.fa)
-        if ACT_WS and m.d_own <= 8:
+        self.ws = ACT_WS and m.d_own <= 8
+        if self.ws:
             self.args = GruActorArgs(ptr(own), D0, m.d_own, ptr(radar), 18, ptr(h), H, *[A[0][k] for k in _WS_NAMES],
                                      _agent_stride(A, m.fa.numel // N), E, N, ptr(self.hn), H, ptr(self.a), 2)
             self.L = [lambda: _chk(glib().aac_gru_actor_fwd(ctypes.byref(self.args), fused._stream()),
@@ -450,10 +457,19 @@ class _ActPlan:
         self.L.append(gru_cell(A, "Wout", "bout", m.fa.numel // N, 2, TANH, ptr(self.gi), ptr(self.gh), ptr(h),
                                E, N, FWD, hout=ptr(self.hn), ldho=H, y=ptr(self.a), ldy=2))
 
-    def __call__(self):
+    def __call__(self, noise=None):
+        """noise = (episode, eps_end, noise_start, noise_end, seed, counter, noise_out): the weights-
+        stationary launch adds the exploration noise itself; returns whether it did."""
+        if self.ws:
+            a = self.args
+            a.noisy = 0 if noise is None else 1
+            if noise is not None:
+                ep, eps_end, n0, n1, seed, ctr, nout = noise
+                a.episode, a.eps_end, a.noise_start, a.noise_end = _p_or_none(ep), int(eps_end), float(n0), float(n1)
+                a.seed, a.counter, a.noise_out = seed & 0xFFFFFFFFFFFFFFFF, ptr(ctr), _p_or_none(nout)
         for op in self.L:
             op()
-        return self.a, self.hn
+        return self.a, self.hn, self.ws and noise is not None
 
 
 # =============================================================================== MADDPG
@@ -533,8 +549,9 @@ class MADDPG:
             if len(self._acts) > 8:       # callers with fresh tensors every step: do not grow without bound
                 self._acts.clear()
             plan = self._acts[key] = _ActPlan(self, own, radar, h, h_out)
-        a, hn = plan()
-        if noisy:
+        noise = (episode, eps_end, noise_start, noise_end, self.noise_seed, self.noise_counter, noise_out)
+        a, hn, fused_noise = plan(noise if noisy else None)
+        if noisy and not fused_noise:
             ops.noise_clamp(a, episode, eps_end, noise_start, self.noise_seed, self.noise_counter, noise_out,
                             noise_end=noise_end)
         return a, hn

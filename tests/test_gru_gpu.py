@@ -222,6 +222,35 @@ def test_gru_act_weights_stationary_matches_launch_path(native_lib, monkeypatch,
     np.testing.assert_allclose(outs[True][1].cpu(), rh, atol=2e-5)
 
 
+def test_gru_act_fused_noise_matches_noise_launch(native_lib, monkeypatch):
+    """The weights-stationary act launch with the exploration noise inside (noisy=True) against the
+    launch path + aac_noise_clamp: the same noise bit for bit (per-row hash of the same counter epoch),
+    the same clamped actions, and the counter advanced once per call either way."""
+    from multi_agent_aac_amd import gru
+    E, N = 1000, 8
+    m, _ = _model(N, 64, E, seed=6)
+    tr = gru_ref.random_gru_transitions(E, N, 4)
+    own, radar, h = tr["s_own"].to(DEV), tr["s_radar"].to(DEV), tr["h_cur"].to(DEV)
+    episode = torch.randint(1, 9000, (E,), dtype=torch.int32, device=DEV)
+    outs = {}
+    for ws in (True, False):
+        monkeypatch.setattr(gru, "ACT_WS", ws)
+        m._acts.clear()
+        m.noise_counter.zero_()
+        res = []
+        for _ in range(2):
+            nz = torch.empty(E, N, 2, device=DEV)
+            a, _ = m.act(own, radar, h, episode=episode, noisy=True, noise_out=nz)
+            res.append((a.clone(), nz))
+        outs[ws] = (res, int(m.noise_counter.item()))
+    assert outs[True][1] == outs[False][1] == 2
+    for (a1, n1), (a0, n0) in zip(outs[True][0], outs[False][0]):
+        assert torch.equal(n1, n0)
+        torch.testing.assert_close(a1, a0, atol=2e-6, rtol=1e-5)
+        assert float(a1.abs().max()) <= 1.0
+    assert not torch.equal(outs[True][0][0][1], outs[True][0][1][1])      # a new epoch per call
+
+
 def test_gru_reset_hidden_and_reference_api(native_lib, tmp_path):
     from multi_agent_aac_amd import gru
     N = 3
