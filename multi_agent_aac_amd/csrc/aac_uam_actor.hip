@@ -20,6 +20,7 @@
 #include <string>
 
 #include "../../include/aac_uam.h"
+#include "aac_noise.h"
 
 namespace {
 
@@ -50,7 +51,7 @@ struct ActorArgs {
     int eps_end, noisy;
     double noise_start, noise_end;
     uint64_t seed;
-    const uint64_t *counter;
+    uint64_t *counter;          // epoch | arrivals << 32 (aacn::take_epoch): advanced by the launch
 };
 
 // C tile of one 16-wide column block of a layer with K-contiguous weight rows W[o][k]: A
@@ -77,7 +78,7 @@ __global__ void __launch_bounds__(256) uam_actor_kernel(ActorArgs A) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double *H = slab[w];
     const int rl = lane & 15, kl = lane >> 4;
-    const uint64_t ctr = A.noisy ? *A.counter : 0;
+    const uint64_t ctr = A.noisy ? aacn::take_epoch(A.counter) : 0;
     const int nblk = (A.R + 15) / 16;
     for (int blk = blockIdx.x * 4 + w; blk < nblk; blk += gridDim.x * 4) {
         // the slab is rewritten below; this wave's reads of the previous block come first (the
@@ -207,7 +208,6 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
     __shared__ double sH[128 * TS];          // [h_o | h_r] of the block, [feature][row]
     __shared__ double sP[4][ROWS][2];        // per-wave partial output dots
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
-    const uint64_t ctr = A.noisy ? *A.counter : 0;
     // A fragments (lane: output row 16 t + n of the tile, k slot kq of each 4-step)
     double a1[2], a2[5], a3[2][32];
 #pragma unroll
@@ -239,6 +239,8 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
         }
     }
     const double b40 = A.b4[0], b41 = A.b4[1];
+    // the launch's noise epoch (one atomic per workgroup), after the weight loads are in flight
+    const uint64_t ctr = A.noisy ? aacn::take_epoch(A.counter) : 0;
     const int nblk = (A.R + ROWS - 1) / ROWS;
     for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const int r0 = blk * ROWS;
@@ -340,8 +342,6 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
     }
 }
 
-__global__ void actor_counter_kernel(uint64_t *counter) { *counter += 1; }
-
 }  // namespace
 
 extern "C" {
@@ -396,7 +396,6 @@ int aac_uam_actor(const double *own, const double *radar, int32_t R, const doubl
             default: hipLaunchKernelGGL(uam_actor_ws_kernel<4>, dim3(wgs), dim3(256), 0, (hipStream_t)stream, A); break;
         }
     }
-    if (noisy) hipLaunchKernelGGL(actor_counter_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_aerr = std::string("aac_uam_actor: ") + hipGetErrorString(e);

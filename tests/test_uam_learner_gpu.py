@@ -177,6 +177,10 @@ def test_act_and_noise_schedule(native_lib):
     ep[:] = 1
     an = m.act(own, radar, ep, noisy=True)
     assert an.abs().max() <= 1 and not torch.equal(an, a0)
+    # the launch advances the noise epoch itself (one per noisy call, arrivals field back at 0)
+    assert int(m.noise_counter.item()) == 2
+    assert not torch.equal(m.act(own, radar, ep, noisy=True), an)
+    assert int(m.noise_counter.item()) == 3
 
 
 @pytest.mark.parametrize("R", [1, 15, 16, 17, 1000, 131072])
