@@ -534,6 +534,11 @@ __device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, d
     return r;
 }
 
+#ifndef AAC_ENV_AGENT_STAMPS
+#define ASTAMP(k) \
+    do {          \
+    } while (0)
+#endif
 #ifdef AAC_ENV_STAMPS
 // diagnostic build only (tools/env_stamps.py): per-workgroup s_memtime at entry, after kinematics,
 // after the radar, after the agent phase and at exit, plus s_memrealtime at entry / exit
@@ -550,6 +555,12 @@ __device__ unsigned long long g_reset_st[ESTAMP_WG][7];
     do {                                                                                               \
         if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_reset_st[blockIdx.x][k] = (v);              \
     } while (0)
+#ifdef AAC_ENV_AGENT_STAMPS      // agent-phase sub-stamps of thread 0, into the reset stamp array (step only)
+#define ASTAMP(k)                                                                                       \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_reset_st[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#endif
 #else
 #define ESTAMP(k, v) \
     do {             \
@@ -1042,9 +1053,11 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
 #else
     if (active) {
 #endif
+        ASTAMP(0);
         const uint8_t *occ = s_maps + (A.map_idx ? A.map_idx[e] : 0) * A.gw * A.gh;
         if (stage) observe_agent(A, S, e, i, base, S.obs + t * D0, S.obs + nag * D0 + t * K6);
         else observe_agent(A, S, e, i, base);
+        ASTAMP(1);
 
         // ---- ss_reward (ATT/env:2133-2603)
         const double px = np.x, py = np.y, pb = A.pb;
@@ -1072,6 +1085,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             if (d >= 2.5 && d <= 10) pen = pen + (1 * (m_drone * shortest + c_drone));
             else pen = pen + 0;
         }
+        ASTAMP(2);
         int building = 0;
         {
             int ci = (int)floor((px - A.gx0) / 10.0 + 0.5), cj = (int)floor((py - A.gy0) / 10.0 + 0.5);
@@ -1086,9 +1100,11 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
                 }
         }
         if (building) A.wall[ai] += 1;
+        ASTAMP(3);
         const double2 g = S.goal[t];
         const int goal = goal_reached(px, py, g.x, g.y, pb);
         const int bnd = bound_crash(A, pp.x, pp.y, px, py);
+        ASTAMP(4);
         int done = 0, cg = 0, wpf = 0;
         uint8_t fl = 0;
         double r;
@@ -1135,6 +1151,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         S.flags[t] = fl;
         A.done[ai] = (uint8_t)done;
         A.mask[ai] = m;
+        ASTAMP(5);
     }
     aacw::lds_barrier();
     ESTAMP(4, __builtin_amdgcn_s_memtime());
