@@ -439,7 +439,6 @@ class _ActPlan:
             assert t.is_contiguous() and t.device == dev and t.dtype == torch.float32 and t.shape[0] == E
         self.inputs = (own, radar, h)            # kept alive with the plan
         D0 = own.shape[-1]
-        self.cat, self.gi, self.gh = (torch.empty(E, N, w, device=dev) for w in (128, 192, 192))
         self.a = torch.empty(E, N, 2, device=dev)
         self.hn = h_out if h_out is not None else torch.empty(E, N, H, device=dev)
         assert self.hn.is_contiguous() and self.hn.shape == (E, N, H)
@@ -451,6 +450,8 @@ class _ActPlan:
             self.L = [lambda: _chk(glib().aac_gru_actor_fwd(ctypes.byref(self.args), fused._stream()),
                                    "aac_gru_actor_fwd")]
             return
+        # the launch path's intermediate rows (the weights-stationary launch keeps them on chip)
+        self.cat, self.gi, self.gh = (torch.empty(E, N, w, device=dev) for w in (128, 192, 192))
         self.L = gemm_launches(enc2_probs(A, "Wo", "bo", "Wg", "bg", ptr(own), D0, m.d_own, ptr(radar), 18, 18,
                                           ptr(self.cat), E, N))
         self.L += gemm_launches(gate_probs(A, ptr(self.cat), ptr(h), ptr(self.gi), ptr(self.gh), E, N))
@@ -546,9 +547,11 @@ class MADDPG:
                tuple(own.shape))
         plan = self._acts.get(key)
         if plan is None:
-            if len(self._acts) > 8:       # callers with fresh tensors every step: do not grow without bound
-                self._acts.clear()
+            if len(self._acts) >= 8:      # callers with fresh tensors every step: evict the oldest plan only
+                self._acts.pop(next(iter(self._acts)))
             plan = self._acts[key] = _ActPlan(self, own, radar, h, h_out)
+        else:
+            self._acts[key] = self._acts.pop(key)      # most recently used last (dicts keep insertion order)
         noise = (episode, eps_end, noise_start, noise_end, self.noise_seed, self.noise_counter, noise_out)
         a, hn, fused_noise = plan(noise if noisy else None)
         if noisy and not fused_noise:

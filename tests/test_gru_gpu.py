@@ -251,6 +251,21 @@ def test_gru_act_fused_noise_matches_noise_launch(native_lib, monkeypatch):
     assert not torch.equal(outs[True][0][0][1], outs[True][0][1][1])      # a new epoch per call
 
 
+def test_gru_act_plan_cache_is_lru(native_lib):
+    """Act plans are keyed on the caller's buffers: fresh tensors every call evict only the oldest
+    plan (at most 8 kept), and a buffer set in steady use keeps its plan (no rebuild)."""
+    E, N = 64, 3
+    m, _ = _model(N, 4, E, seed=2)
+    own, radar, h = (torch.zeros(E, N, w, device=DEV) for w in (6, 18, H))
+    m.act(own, radar, h, noisy=False)
+    steady = next(iter(m._acts.values()))
+    for _ in range(12):
+        m.act(own.clone(), radar.clone(), h.clone(), noisy=False)
+        m.act(own, radar, h, noisy=False)           # the steady set, used every step
+    assert len(m._acts) <= 8
+    assert any(p is steady for p in m._acts.values())
+
+
 def test_gru_reset_hidden_and_reference_api(native_lib, tmp_path):
     from multi_agent_aac_amd import gru
     N = 3
