@@ -178,6 +178,8 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
 #pragma unroll
         for (int di = 0; di < 8; ++di) rb[di] = rows[i0 + di <= i1 ? i0 + di : 0];
         unsigned long long cand = 0;
+        double almin = INFINITY;
+        int bmin = 0;
 #pragma unroll
         for (int di = 0; di < 8; ++di) {
             unsigned long long row = i0 + di <= i1 ? (rb[di] >> j0) & span : 0ull;
@@ -187,17 +189,34 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
                 row &= row - 1;
                 const double wy = A.gy0 + 10.0 * (j0 + b) - cy;
                 const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
-                if (fabs(cr) <= reach && al >= -reach && al <= L2 + reach) cand |= 1ull << (di * 8 + b);
+                if (fabs(cr) <= reach && al >= -reach && al <= L2 + reach) {
+                    cand |= 1ull << (di * 8 + b);
+                    if (al < almin) {
+                        almin = al;
+                        bmin = di * 8 + b;
+                    }
+                }
             }
         }
 #ifdef AAC_DBG_NO_SQUARE      // timing experiments only
         mind -= (double)__popcll(cand) * 1e-30;
         cand = 0;
 #endif
+        // the candidate nearest along the ray first; then a square whose every point projects past
+        // the current minimum cannot lower it: its hit distance is at least (al - 5(|dx| + |dy|)) / L
+        // (al, reach scaled by L), so it is skipped when (al - reach)^2 > mind^2 L^2 (1 + 1e-8) -- the
+        // relative margin far above the rounding of d, so the minimum is the one the full loop finds
+        if (cand) {
+            const double qx = A.gx0 + 10.0 * (i0 + (bmin >> 3)), qy = A.gy0 + 10.0 * (j0 + (bmin & 7));
+            if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
+            cand &= ~(1ull << bmin);
+        }
         while (cand) {
             const int b = __builtin_ctzll(cand);
             cand &= cand - 1;
             const double qx = A.gx0 + 10.0 * (i0 + (b >> 3)), qy = A.gy0 + 10.0 * (j0 + (b & 7));
+            const double lb = (qx - cx) * ddx + (qy - cy) * ddy - reach;
+            if (lb > 0.0 && lb * lb > mind * mind * L2 * (1.0 + 1e-8)) continue;
             if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
         }
     } else {      // a radar longer than the 8 x 8-cell mask covers, or maps taller than 64 cells
