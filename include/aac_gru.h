@@ -109,6 +109,12 @@ typedef struct {
 
 int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream);
 
+/* n <= 3 projection-mode argument sets (gi != NULL, equal E and N) in one launch: independent
+ * network evaluations of one update_myown (WGRU/maddpg:242-310: the target actor on s', the critic on
+ * (s, a), the actor on s), the CUs shared between them so that each workgroup keeps its weights for
+ * several row blocks.  Same results as n aac_gru_actor_fwd calls. */
+int aac_gru_actor_proj_multi(const aac_gru_actor_args *args, int32_t n, void *stream);
+
 /* dst[r][0 .. n0-1] = a[r*lda + ...], dst[r][n0 .. n0+n1-1] = b[r*ldb + ...] for R rows (ldd):
  * the [own, a] critic input rows of critic_single_obs_wGRU_TwoPortion (WGRU/nets:441). */
 int aac_pack_rows(float *dst, int32_t ldd, const float *a, int32_t lda, int32_t n0, const float *b, int32_t ldb,

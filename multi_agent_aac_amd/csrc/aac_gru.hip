@@ -118,14 +118,27 @@ __global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
 typedef float f4 __attribute__((ext_vector_type(4)));
 // GNT 16-row tiles per block (2 for the act path; 1 for the projection mode at B = 512 rows per agent,
 // so that every CU gets a workgroup); PROJ: write cat / gi / gh, no cell.
+// Up to GMAX argument sets per launch (projection mode: independent network evaluations of one
+// update_myown, e.g. the target actor on s', the critic on (s, a) and the actor on s): blocks of set
+// k are [k G N, (k + 1) G N).
+constexpr int GMAX = 3;
+struct GruActorBatch {
+    aac_gru_actor_args s[GMAX];
+    int n;
+};
 template <int GNT, bool PROJ>
-__global__ void __launch_bounds__(256) gru_actor_fwd_kernel(aac_gru_actor_args A) {
+__global__ void __launch_bounds__(256) gru_actor_fwd_kernel(GruActorBatch Pb) {
+    const int per = gridDim.x / Pb.n;                        // workgroups per set
+    const int set = (int)blockIdx.x / per, bx = (int)blockIdx.x - set * per;
+    // the set's arguments by value, selected with uniform branches (indexing the by-value kernel
+    // argument would move it to scratch)
+    const aac_gru_actor_args A = set == 0 ? Pb.s[0] : (set == 1 ? Pb.s[1] : Pb.s[2]);
     constexpr int GROWS = 16 * GNT, GTS = GROWS + 1;
     __shared__ float sCat[128 * GTS];         // [e_o | e_g] of the block, [feature][row]
     __shared__ float sP[4][GROWS][2];         // per-wave partial output dots
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
-    const int G = gridDim.x / A.N;            // workgroups per agent
-    const int ag = blockIdx.x / G, g = blockIdx.x - ag * G;
+    const int G = per / A.N;                  // workgroups per agent
+    const int ag = bx / G, g = bx - ag * G;
     const size_t po = (size_t)ag * A.pstride;
     const float *Wo = A.Wo + po, *Wg = A.Wg + po, *Wih = A.Wih + po, *Whh = A.Whh + po, *Wout = A.Wout + po;
     const int d = A.d_own;
@@ -383,12 +396,10 @@ int aac_gru_cell(const aac_gru_args *args, void *stream) {
     return 0;
 }
 
-int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream) {
-    if (!args) return gfail("gru_actor_fwd: null arguments");
-    const aac_gru_actor_args &a = *args;
-    if (a.E <= 0 || a.N <= 0) return gfail("gru_actor_fwd: E, N > 0");
+static int actor_fwd_check(const aac_gru_actor_args &a) {
     const bool proj = a.gi != nullptr;
     auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (a.E <= 0 || a.N <= 0) return gfail("gru_actor_fwd: E, N > 0");
     if (a.d_own < 1 || a.d_own > 8 || a.ld_own < a.d_own || a.ld_radar < 18 || a.ldh < H)
         return gfail("gru_actor_fwd: 1 <= d_own <= 8 and row strides >= the used widths");
     if (!a.own || !a.radar || !a.h || !a.Wo || !a.bo || !a.Wg || !a.bg || !a.Wih || !a.bih || !a.Whh || !a.bhh)
@@ -403,14 +414,45 @@ int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream) {
         if (a.ldho % 4 || a.ldho < H || !al16(a.hout)) return gfail("gru_actor_fwd: hout rows must be 16-B aligned");
         if (a.noisy && (!a.counter || a.ldy != 2)) return gfail("gru_actor_fwd: noisy needs a counter and ldy == 2");
     }
+    return 0;
+}
+
+int aac_gru_actor_fwd(const aac_gru_actor_args *args, void *stream) {
+    if (!args) return gfail("gru_actor_fwd: null arguments");
+    const aac_gru_actor_args &a = *args;
+    if (int rc = actor_fwd_check(a)) return rc;
+    const bool proj = a.gi != nullptr;
     // one workgroup per CU in all (one wave per SIMD: ~250 registers of weights per lane)
     const int rows = proj ? 16 : 32;
     const int blocks = (a.E + rows - 1) / rows;
     const int G = std::max(1, std::min(blocks, 256 / a.N));
-    if (proj) hipLaunchKernelGGL((gru_actor_fwd_kernel<1, true>), dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL((gru_actor_fwd_kernel<2, false>), dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, a);
+    GruActorBatch b{};
+    b.s[0] = b.s[1] = b.s[2] = a;
+    b.n = 1;
+    if (proj) hipLaunchKernelGGL((gru_actor_fwd_kernel<1, true>), dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, b);
+    else hipLaunchKernelGGL((gru_actor_fwd_kernel<2, false>), dim3(G * a.N), dim3(256), 0, (hipStream_t)stream, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gfail(std::string("gru_actor_fwd: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int aac_gru_actor_proj_multi(const aac_gru_actor_args *args, int32_t n, void *stream) {
+    if (!args || n < 1 || n > GMAX) return gfail("gru_actor_proj_multi: 1 <= n <= 3 argument sets");
+    GruActorBatch b{};
+    for (int k = 0; k < n; ++k) {
+        if (int rc = actor_fwd_check(args[k])) return rc;
+        if (!args[k].gi) return gfail("gru_actor_proj_multi: projection mode (gi != NULL) only");
+        if (args[k].E != args[0].E || args[k].N != args[0].N) return gfail("gru_actor_proj_multi: equal E and N");
+        b.s[k] = args[k];
+    }
+    for (int k = n; k < GMAX; ++k) b.s[k] = args[0];
+    b.n = n;
+    // the 256 CUs shared by the sets: each workgroup keeps its weights for several 16-row blocks
+    const int blocks = (args[0].E + 15) / 16;
+    const int G = std::max(1, std::min(blocks, 256 / (args[0].N * n)));
+    hipLaunchKernelGGL((gru_actor_fwd_kernel<1, true>), dim3(G * args[0].N * n), dim3(256), 0, (hipStream_t)stream, b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gfail(std::string("gru_actor_proj_multi: ") + hipGetErrorString(e));
     return 0;
 }
 

@@ -73,6 +73,9 @@ ACT_WS = os.environ.get("AAC_GRU_WS", "1") == "1"
 # the projection mode in update_myown (one launch per network evaluation instead of the encoder and
 # gate GEMM launches): config 4 0.463 -> 0.402 ms per step; AAC_GRU_WS_PROJ=0 keeps the GEMM launches
 WS_PROJ = ACT_WS and os.environ.get("AAC_GRU_WS_PROJ", "1") == "1"
+# the three projections that read only the batch (target actor on s', critic on (s, a), actor on s)
+# in one aac_gru_actor_proj_multi launch; AAC_GRU_MULTI_PROJ=0: three launches
+MULTI_PROJ = os.environ.get("AAC_GRU_MULTI_PROJ", "1") == "1"
 _WS_NAMES = ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout", "bout")
 
 
@@ -95,6 +98,18 @@ class WsProj:
     def __call__(self):
         _chk(glib().aac_gru_actor_fwd(ctypes.byref(self.args), fused._stream()), "aac_gru_actor_fwd")
 
+
+class WsProjMulti:
+    """Up to three independent WsProj evaluations in one aac_gru_actor_proj_multi launch."""
+
+    def __init__(self, projs):
+        self.projs = projs
+        self.arr = (GruActorArgs * len(projs))(*[q.args for q in projs])
+        self.flops = sum(q.flops for q in projs)
+
+    def __call__(self):
+        _chk(glib().aac_gru_actor_proj_multi(self.arr, len(self.projs), fused._stream()), "aac_gru_actor_proj_multi")
+
 _GL = None
 
 
@@ -107,6 +122,7 @@ def glib():
         L.aac_pack_rows.argtypes = [vp, i32, vp, i32, i32, vp, i32, i32, i32, vp]
         L.aac_gru_reset_hidden.argtypes = [vp, i32, i32, vp, vp]
         L.aac_gru_actor_fwd.argtypes = [ctypes.POINTER(GruActorArgs), vp]
+        L.aac_gru_actor_proj_multi.argtypes = [ctypes.POINTER(GruActorArgs), i32, vp]
         _GL = L
     return _GL
 
@@ -289,6 +305,10 @@ class GruUpdate:
         self.Xsa, self.Xsa_t, self.Xsa2 = z(B, N, d + 2), z(B, N, d + 2), z(B, N, d + 2)
         self.cat_a, self.cat_c = z(B, N, 128), z(B, N, 128)
         self.gi_a, self.gh_a, self.gi_c, self.gh_c = z(B, N, 192), z(B, N, 192), z(B, N, 192), z(B, N, 192)
+        # the target networks' projections get their own rows (they run beside the critic's and the
+        # actor's in one launch, MULTI_PROJ)
+        self.cat_at, self.cat_ct = z(B, N, 128), z(B, N, 128)
+        self.gi_at, self.gh_at, self.gi_ct, self.gh_ct = z(B, N, 192), z(B, N, 192), z(B, N, 192), z(B, N, 192)
         self.y, self.q_c, self.q_a, self.dq = z(B, N), z(B, N), z(B, N), z(B, N)
         self.hc, self.ha = z(B, N, H), z(B, N, H)
         self.dgi_c, self.dgh_c, self.dgi_a, self.dgh_a = z(B, N, 192), z(B, N, 192), z(B, N, 192), z(B, N, 192)
@@ -328,16 +348,24 @@ class GruUpdate:
         Dsa = d + 2
         L = [lambda: ops.replay_sample(rep.meta, B, rep.seed, rep.counter, self.bidx),
              lambda: ops.replay_gather(rep.ring, self.bidx, [b[k] for k in rep.fields], rep.widths)]
+        # the projections that read only the batch and weights fixed until their step's Adam: the target
+        # actor on s', the critic on (s, a) and the actor on s -- one launch (MULTI_PROJ) or three
+        L.append(lambda: pack_rows(P(self.Xsa), Dsa, own, D0, d, act, 2, 2, B * N))
+        early = [(At, sa, nown, D0, d, nradar, hnext, P(self.cat_at), P(self.gi_at), P(self.gh_at)),
+                 (C, sc, P(self.Xsa), Dsa, Dsa, radar, hcur, P(self.cat_c), P(self.gi_c), P(self.gh_c)),
+                 (A, sa, own, D0, d, radar, hcur, P(self.cat_a), P(self.gi_a), P(self.gh_a))]
+        if MULTI_PROJ and WS_PROJ and max(e[4] for e in early) <= 8:
+            L.append(WsProjMulti([WsProj(*e, B, N) for e in early]))
+        else:
+            for e in early:
+                L += self._proj(*e)
         # ---------------- TD target (WGRU/maddpg:265, :280-282), target networks
-        L += self._proj(At, sa, nown, D0, d, nradar, hnext, P(self.cat_a), P(self.gi_a), P(self.gh_a))
-        L.append(gru_cell(At, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hnext, B, N, FWD,
+        L.append(gru_cell(At, "Wout", "bout", sa, 2, TANH, P(self.gi_at), P(self.gh_at), hnext, B, N, FWD,
                           pack_src=nown, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa_t), ld_pack_dst=Dsa))
-        L += self._proj(Ct, sc, P(self.Xsa_t), Dsa, Dsa, nradar, hnext, P(self.cat_c), P(self.gi_c), P(self.gh_c))
-        L.append(gru_cell(Ct, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hnext, B, N, TD,
+        L += self._proj(Ct, sc, P(self.Xsa_t), Dsa, Dsa, nradar, hnext, P(self.cat_ct), P(self.gi_ct), P(self.gh_ct))
+        L.append(gru_cell(Ct, "Wout", "bout", sc, 1, 0, P(self.gi_ct), P(self.gh_ct), hnext, B, N, TD,
                           rew=ptr(b["rew"]), done=ptr(b["done"]), gamma=m.GAMMA, yout=P(self.y)))
         # ---------------- critic step (WGRU/maddpg:272, :284-291)
-        L.append(lambda: pack_rows(P(self.Xsa), Dsa, own, D0, d, act, 2, 2, B * N))
-        L += self._proj(C, sc, P(self.Xsa), Dsa, Dsa, radar, hcur, P(self.cat_c), P(self.gi_c), P(self.gh_c))
         L.append(gru_cell(C, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hcur, B, N, CRITIC,
                           target=P(self.y), y=P(self.q_c), dq=P(self.dq), hout=P(self.hc), ldho=H, inv_m=1.0 / B,
                           dgi=P(self.dgi_c), dgh=P(self.dgh_c), ldd=192))
@@ -351,8 +379,7 @@ class GruUpdate:
             wgrad_probs(P(self.dcat_c), 0, 128, P(self.Xsa), 0, Dsa, Dsa, gC, "Wo", "bo", 64, B, N)
             + wgrad_probs(P(self.dcat_c), 64, 128, radar, 0, 18, 18, gC, "Wg", "bg", 64, B, N))
         L += self._adam(m.critic_optimizer, m.fc)
-        # ---------------- actor step (WGRU/maddpg:293-310): 3 - mean Q(s, pi(s, h), h)
-        L += self._proj(A, sa, own, D0, d, radar, hcur, P(self.cat_a), P(self.gi_a), P(self.gh_a))
+        # ---------------- actor step (WGRU/maddpg:293-310): 3 - mean Q(s, pi(s, h), h); its projection ran above
         L.append(gru_cell(A, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hcur, B, N, FWD,
                           hout=P(self.ha), ldho=H, pack_src=own, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa2),
                           ld_pack_dst=Dsa))
