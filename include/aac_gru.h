@@ -61,6 +61,13 @@ typedef struct {
     float *dq;                /* CRITIC / ACTLOSS: dq [R]; ACTBWD: dout [R][O] */
     float *dgi, *dgh;         /* gate gradients [R][192] rows ldd apart (dgh may be NULL) */
     int32_t ldd;
+    /* ACTBWD with dsa != NULL (da == NULL): d a computed here as the critic input layer's backward,
+     * da[r][j] = sum_k dsa[r][k] wsa[agent][k][col + j] over k < 64 (dsa rows lddsa apart; agent n's
+     * [64][ldwsa] matrix at wsa + n*wsa_stride) -- in place of a product launch (WGRU/maddpg:302-305) */
+    const float *dsa;
+    int32_t lddsa;
+    const float *wsa;
+    int32_t wsa_stride, ldwsa, wsa_col;
 } aac_gru_args;
 
 const char *aac_gru_last_error(void);

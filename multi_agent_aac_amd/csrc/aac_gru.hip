@@ -80,11 +80,21 @@ __global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
         }
         dh = g * W[u];
     } else {   // AAC_GRU_ACTBWD: tanh output layer backward
-        const float d0 = a.da[(size_t)r * a.ldda] * (1.0f - y0 * y0);
+        float da0, da1 = 0.0f;
+        if (a.dsa) {      // d a = dsa . W_sa[:, col:col+2] of this row's agent (lane u = k)
+            const float s = a.dsa[(size_t)r * a.lddsa + u];
+            const float *ws = a.wsa + (size_t)agent * a.wsa_stride + (size_t)u * a.ldwsa + a.wsa_col;
+            da0 = wsum(s * ws[0]);
+            if (two) da1 = wsum(s * ws[1]);
+        } else {
+            da0 = a.da[(size_t)r * a.ldda];
+            if (two) da1 = a.da[(size_t)r * a.ldda + 1];
+        }
+        const float d0 = da0 * (1.0f - y0 * y0);
         dh = d0 * W[u];
         if (u == 0) a.dq[(size_t)r * a.O] = d0;
         if (two) {
-            const float d1 = a.da[(size_t)r * a.ldda + 1] * (1.0f - y1 * y1);
+            const float d1 = da1 * (1.0f - y1 * y1);
             dh = fmaf(d1, W[H + u], dh);
             if (u == 0) a.dq[(size_t)r * a.O + 1] = d1;
         }
@@ -387,7 +397,8 @@ int aac_gru_cell(const aac_gru_args *args, void *stream) {
     if (a.mode == AAC_GRU_TD && (!a.rew || !a.done || !a.yout || a.O != 1)) return gfail("gru_cell: TD needs rew, done, yout, O = 1");
     if (a.mode == AAC_GRU_CRITIC && (!a.target || a.O != 1)) return gfail("gru_cell: CRITIC needs target, O = 1");
     if (a.mode == AAC_GRU_ACTLOSS && a.O != 1) return gfail("gru_cell: ACTLOSS needs O = 1");
-    if (a.mode == AAC_GRU_ACTBWD && (!a.da || !a.dq)) return gfail("gru_cell: ACTBWD needs da, dq");
+    if (a.mode == AAC_GRU_ACTBWD && ((!a.da && !(a.dsa && a.wsa)) || !a.dq))
+        return gfail("gru_cell: ACTBWD needs da (or dsa and wsa), dq");
     if (a.mode >= AAC_GRU_CRITIC && !a.dgi) return gfail("gru_cell: backward modes need dgi");
     if (a.pack_dst && (!a.pack_src || a.npack < 0 || a.npack + a.O > 64)) return gfail("gru_cell: bad pack");
     hipLaunchKernelGGL(gru_cell_kernel, dim3((a.R + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);

@@ -53,7 +53,8 @@ class GruArgs(ctypes.Structure):
                 ("hout", vp), ("ldho", i32), ("y", vp), ("ldy", i32), ("pack_src", vp), ("ld_pack_src", i32),
                 ("npack", i32), ("pack_dst", vp), ("ld_pack_dst", i32), ("target", vp), ("rew", vp), ("done", vp),
                 ("gamma", f32), ("inv_m", f32), ("yout", vp), ("da", vp), ("ldda", i32), ("dq", vp), ("dgi", vp),
-                ("dgh", vp), ("ldd", i32)]
+                ("dgh", vp), ("ldd", i32), ("dsa", vp), ("lddsa", i32), ("wsa", vp), ("wsa_stride", i32),
+                ("ldwsa", i32), ("wsa_col", i32)]
 
 
 class GruActorArgs(ctypes.Structure):
@@ -76,6 +77,9 @@ WS_PROJ = ACT_WS and os.environ.get("AAC_GRU_WS_PROJ", "1") == "1"
 # the three projections that read only the batch (target actor on s', critic on (s, a), actor on s)
 # in one aac_gru_actor_proj_multi launch; AAC_GRU_MULTI_PROJ=0: three launches
 MULTI_PROJ = os.environ.get("AAC_GRU_MULTI_PROJ", "1") == "1"
+# the actor step's d a (critic input layer backward, 64 -> 2 per row) inside the ACTBWD cell launch;
+# AAC_GRU_CELL_DA=0: a grouped-GEMM launch of N products
+CELL_DA = os.environ.get("AAC_GRU_CELL_DA", "1") == "1"
 _WS_NAMES = ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout", "bout")
 
 
@@ -390,10 +394,15 @@ class GruUpdate:
         L += _glaunch([prob(P(self.dgi_c) + 4 * i * 192, C[i]["Wih"], P(self.dsa) + 4 * i * 64, B, 64, 192,
                                  N * 192, 128, N * 64, mask=P(self.cat_c) + 4 * i * 128, ldmask=N * 128, mact=RELU)
                             for i in range(N)])
-        L += _glaunch([prob(P(self.dsa) + 4 * i * 64, C[i]["Wo"] + 4 * d, P(self.da) + 4 * i * 2, B, 2, 64,
-                                 N * 64, Dsa, N * 2) for i in range(N)])
-        L.append(gru_cell(A, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hcur, B, N, ACTBWD,
-                          da=P(self.da), ldda=2, dq=P(self.dout), dgi=P(self.dgi_a), dgh=P(self.dgh_a), ldd=192))
+        if CELL_DA:      # d a = d SA . W_sa[:, d:d+2] inside the backward cell (no product launch)
+            L.append(gru_cell(A, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hcur, B, N, ACTBWD,
+                              dsa=P(self.dsa), lddsa=64, wsa=C[0]["Wo"], wsa_stride=_agent_stride(C, sc), ldwsa=Dsa, wsa_col=d,
+                              dq=P(self.dout), dgi=P(self.dgi_a), dgh=P(self.dgh_a), ldd=192))
+        else:
+            L += _glaunch([prob(P(self.dsa) + 4 * i * 64, C[i]["Wo"] + 4 * d, P(self.da) + 4 * i * 2, B, 2, 64,
+                                N * 64, Dsa, N * 2) for i in range(N)])
+            L.append(gru_cell(A, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hcur, B, N, ACTBWD,
+                              da=P(self.da), ldda=2, dq=P(self.dout), dgi=P(self.dgi_a), dgh=P(self.dgh_a), ldd=192))
         L += _glaunch(
             wgrad_probs(P(self.dout), 0, 2, P(self.ha), 0, H, H, gA, "Wout", "bout", 2, B, N)
             + wgrad_probs(P(self.dgi_a), 0, 192, P(self.cat_a), 0, 128, 128, gA, "Wih", "bih", 192, B, N)
