@@ -74,6 +74,12 @@ const char *aac_gru_last_error(void);
 
 int aac_gru_cell(const aac_gru_args *args, void *stream);
 
+/* Two aac_gru_cell argument sets in one launch: chain == 0, independent sets (e.g. the target actor's
+ * and the actor's forward cells of one update); chain != 0, per row: set 0 in TD mode, then set 1 in
+ * CRITIC mode with that row's TD target taken from the register (a1->target may be NULL).  Same
+ * results as two aac_gru_cell calls. */
+int aac_gru_cell2(const aac_gru_args *a0, const aac_gru_args *a1, int32_t chain, void *stream);
+
 /* The whole GRUCELL_actor_TwoPortion forward (WGRU/Nnetworks:181-198: own_fc + own_grid encoders,
  * GRUCell(128, 64), outlay Linear(64, 2) + Tanh) for E envs x N agents in one launch: rows
  * r = e*N + i of agent i (own rows ld_own apart, the first d_own <= 8 columns read; radar rows 18

@@ -34,10 +34,11 @@ constexpr int H = AAC_GRU_HIDDEN;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-__global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int u = threadIdx.x & 63;
-    if (r >= a.R) return;
+// one row r of aac_gru_cell (one wave, lane u = hidden unit).  tgt_in: the CRITIC target of this
+// row in a register (a chained launch) instead of a.target[r]; returns the TD value (TD mode) to
+// every lane
+__device__ __forceinline__ float cell_row(const aac_gru_args &a, int r, int u, const float *tgt_in) {
+    float td = 0.0f;
     const float *gi = a.gi + (size_t)r * a.ldg, *gh = a.gh + (size_t)r * a.ldg;
     const float ir = gi[u], iz = gi[H + u], in = gi[2 * H + u];
     const float hr = gh[u], hz = gh[H + u], hn = gh[2 * H + u];
@@ -66,14 +67,16 @@ __global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
             if (u < a.npack) d[u] = a.pack_src[(size_t)r * a.ld_pack_src + u];
             if (u < a.O) d[a.npack + u] = yu;
         }
-        return;
+        return td;
     }
     if (a.mode == AAC_GRU_TD) {
-        if (u == 0) a.yout[r] = a.rew[r] + (a.gamma * y0) * (1.0f - a.done[r]);
-        return;
+        td = a.rew[r] + (a.gamma * y0) * (1.0f - a.done[r]);
+        if (u == 0) a.yout[r] = td;
+        return td;
     }
     if (a.mode == AAC_GRU_CRITIC || a.mode == AAC_GRU_ACTLOSS) {
-        const float g = a.mode == AAC_GRU_CRITIC ? (2.0f * a.inv_m) * (y0 - a.target[r]) : -a.inv_m;
+        const float tg = a.mode == AAC_GRU_CRITIC ? (tgt_in ? *tgt_in : a.target[r]) : 0.0f;
+        const float g = a.mode == AAC_GRU_CRITIC ? (2.0f * a.inv_m) * (y0 - tg) : -a.inv_m;
         if (u == 0) {
             if (a.y) a.y[r] = y0;
             if (a.dq) a.dq[r] = g;
@@ -114,6 +117,39 @@ __global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
         dgh[u] = dar;
         dgh[H + u] = daz;
         dgh[2 * H + u] = dan * rg;
+    }
+    return td;
+}
+
+__global__ void __launch_bounds__(256) gru_cell_kernel(aac_gru_args a) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= a.R) return;
+    cell_row(a, r, threadIdx.x & 63, nullptr);
+}
+
+// two argument sets in one launch: independent (chain 0: set k takes workgroups [k G, (k + 1) G)) or
+// chained per row (chain 1: set 0 in TD mode, then set 1 in CRITIC mode on the same row with the TD
+// value from the register -- the TD target and the critic's mse head of one update, WGRU/maddpg:280-291)
+struct GruCellPair {
+    aac_gru_args s0, s1;
+    int chain;
+};
+__global__ void __launch_bounds__(256) gru_cell2_kernel(GruCellPair P) {
+    const int u = threadIdx.x & 63;
+    if (P.chain) {
+        const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (r >= P.s0.R) return;
+        const float td = cell_row(P.s0, r, u, nullptr);
+        cell_row(P.s1, r, u, &td);
+        return;
+    }
+    const int g0 = (P.s0.R + 3) / 4;
+    if ((int)blockIdx.x < g0) {
+        const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (r < P.s0.R) cell_row(P.s0, r, u, nullptr);
+    } else {
+        const int r = (blockIdx.x - g0) * 4 + (threadIdx.x >> 6);
+        if (r < P.s1.R) cell_row(P.s1, r, u, nullptr);
     }
 }
 
@@ -388,8 +424,7 @@ extern "C" {
 
 const char *aac_gru_last_error(void) { return g_err.c_str(); }
 
-int aac_gru_cell(const aac_gru_args *args, void *stream) {
-    const aac_gru_args &a = *args;
+static int cell_check(const aac_gru_args &a) {
     if (a.R <= 0 || a.N <= 0) return gfail("gru_cell: R, N > 0");
     if (a.O < 1 || a.O > 2) return gfail("gru_cell: 1 <= O <= 2");
     if (!a.gi || !a.gh || !a.h || !a.wout || !a.bout) return gfail("gru_cell: NULL input");
@@ -401,7 +436,33 @@ int aac_gru_cell(const aac_gru_args *args, void *stream) {
         return gfail("gru_cell: ACTBWD needs da (or dsa and wsa), dq");
     if (a.mode >= AAC_GRU_CRITIC && !a.dgi) return gfail("gru_cell: backward modes need dgi");
     if (a.pack_dst && (!a.pack_src || a.npack < 0 || a.npack + a.O > 64)) return gfail("gru_cell: bad pack");
+    return 0;
+}
+
+int aac_gru_cell(const aac_gru_args *args, void *stream) {
+    const aac_gru_args &a = *args;
+    if (int rc = cell_check(a)) return rc;
     hipLaunchKernelGGL(gru_cell_kernel, dim3((a.R + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gfail(std::string("gru_cell: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int aac_gru_cell2(const aac_gru_args *a0, const aac_gru_args *a1, int32_t chain, void *stream) {
+    if (!a0 || !a1) return gfail("gru_cell2: null arguments");
+    if (int rc = cell_check(*a0)) return rc;
+    if (chain) {
+        if (a0->mode != AAC_GRU_TD || a1->mode != AAC_GRU_CRITIC || a0->R != a1->R)
+            return gfail("gru_cell2: chain needs set 0 TD and set 1 CRITIC over the same rows");
+        aac_gru_args b = *a1;
+        if (!b.target) b.target = a0->yout;      // validated below; the chained value is used instead
+        if (int rc = cell_check(b)) return rc;
+    } else if (int rc = cell_check(*a1)) {
+        return rc;
+    }
+    GruCellPair P{*a0, *a1, chain ? 1 : 0};
+    const int grid = chain ? (a0->R + 3) / 4 : (a0->R + 3) / 4 + (a1->R + 3) / 4;
+    hipLaunchKernelGGL(gru_cell2_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gfail(std::string("gru_cell: ") + hipGetErrorString(e));
     return 0;

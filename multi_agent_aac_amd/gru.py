@@ -80,6 +80,9 @@ MULTI_PROJ = os.environ.get("AAC_GRU_MULTI_PROJ", "1") == "1"
 # the actor step's d a (critic input layer backward, 64 -> 2 per row) inside the ACTBWD cell launch;
 # AAC_GRU_CELL_DA=0: a grouped-GEMM launch of N products
 CELL_DA = os.environ.get("AAC_GRU_CELL_DA", "1") == "1"
+# the two forward cells (target actor, actor) in one launch, and the TD cell with the critic's mse cell
+# chained per row (aac_gru_cell2); AAC_GRU_CELL_PAIRS=0: four launches
+CELL_PAIRS = os.environ.get("AAC_GRU_CELL_PAIRS", "1") == "1"
 _WS_NAMES = ("Wo", "bo", "Wg", "bg", "Wih", "bih", "Whh", "bhh", "Wout", "bout")
 
 
@@ -127,6 +130,7 @@ def glib():
         L.aac_gru_reset_hidden.argtypes = [vp, i32, i32, vp, vp]
         L.aac_gru_actor_fwd.argtypes = [ctypes.POINTER(GruActorArgs), vp]
         L.aac_gru_actor_proj_multi.argtypes = [ctypes.POINTER(GruActorArgs), i32, vp]
+        L.aac_gru_cell2.argtypes = [ctypes.POINTER(GruArgs), ctypes.POINTER(GruArgs), i32, vp]
         _GL = L
     return _GL
 
@@ -144,6 +148,18 @@ class GruCell:
 
     def __call__(self):
         _chk(glib().aac_gru_cell(ctypes.byref(self.args), fused._stream()), "aac_gru_cell")
+
+
+class GruCell2:
+    """Two GruCell argument sets in one aac_gru_cell2 launch (independent, or TD -> CRITIC chained)."""
+
+    def __init__(self, c0, c1, chain):
+        self.c = (c0, c1)
+        self.chain = int(chain)
+
+    def __call__(self):
+        _chk(glib().aac_gru_cell2(ctypes.byref(self.c[0].args), ctypes.byref(self.c[1].args), self.chain,
+                                  fused._stream()), "aac_gru_cell2")
 
 
 def pack_rows(dst, ldd, a, lda, n0, b, ldb, n1, R):
@@ -358,21 +374,29 @@ class GruUpdate:
         early = [(At, sa, nown, D0, d, nradar, hnext, P(self.cat_at), P(self.gi_at), P(self.gh_at)),
                  (C, sc, P(self.Xsa), Dsa, Dsa, radar, hcur, P(self.cat_c), P(self.gi_c), P(self.gh_c)),
                  (A, sa, own, D0, d, radar, hcur, P(self.cat_a), P(self.gi_a), P(self.gh_a))]
-        if MULTI_PROJ and WS_PROJ and max(e[4] for e in early) <= 8:
+        multi = MULTI_PROJ and WS_PROJ and max(e[4] for e in early) <= 8
+        if multi:
             L.append(WsProjMulti([WsProj(*e, B, N) for e in early]))
         else:
             for e in early:
                 L += self._proj(*e)
         # ---------------- TD target (WGRU/maddpg:265, :280-282), target networks
-        L.append(gru_cell(At, "Wout", "bout", sa, 2, TANH, P(self.gi_at), P(self.gh_at), hnext, B, N, FWD,
-                          pack_src=nown, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa_t), ld_pack_dst=Dsa))
+        fwd_t = gru_cell(At, "Wout", "bout", sa, 2, TANH, P(self.gi_at), P(self.gh_at), hnext, B, N, FWD,
+                         pack_src=nown, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa_t), ld_pack_dst=Dsa)
+        # the actor step's forward cell (actor weights fixed until its Adam) beside the target actor's
+        fwd_a = gru_cell(A, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hcur, B, N, FWD,
+                         hout=P(self.ha), ldho=H, pack_src=own, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa2),
+                         ld_pack_dst=Dsa)
+        pair = multi and CELL_PAIRS
+        L.append(GruCell2(fwd_t, fwd_a, 0) if pair else fwd_t)
         L += self._proj(Ct, sc, P(self.Xsa_t), Dsa, Dsa, nradar, hnext, P(self.cat_ct), P(self.gi_ct), P(self.gh_ct))
-        L.append(gru_cell(Ct, "Wout", "bout", sc, 1, 0, P(self.gi_ct), P(self.gh_ct), hnext, B, N, TD,
-                          rew=ptr(b["rew"]), done=ptr(b["done"]), gamma=m.GAMMA, yout=P(self.y)))
-        # ---------------- critic step (WGRU/maddpg:272, :284-291)
-        L.append(gru_cell(C, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hcur, B, N, CRITIC,
-                          target=P(self.y), y=P(self.q_c), dq=P(self.dq), hout=P(self.hc), ldho=H, inv_m=1.0 / B,
-                          dgi=P(self.dgi_c), dgh=P(self.dgh_c), ldd=192))
+        td = gru_cell(Ct, "Wout", "bout", sc, 1, 0, P(self.gi_ct), P(self.gh_ct), hnext, B, N, TD,
+                      rew=ptr(b["rew"]), done=ptr(b["done"]), gamma=m.GAMMA, yout=P(self.y))
+        # ---------------- critic step (WGRU/maddpg:272, :284-291); its mse head chained on the TD rows
+        crit = gru_cell(C, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hcur, B, N, CRITIC,
+                        target=P(self.y), y=P(self.q_c), dq=P(self.dq), hout=P(self.hc), ldho=H, inv_m=1.0 / B,
+                        dgi=P(self.dgi_c), dgh=P(self.dgh_c), ldd=192)
+        L += [GruCell2(td, crit, 1)] if pair else [td, crit]
         L += _glaunch(
             wgrad_probs(P(self.dq), 0, 1, P(self.hc), 0, H, H, gC, "Wout", "bout", 1, B, N)
             + wgrad_probs(P(self.dgi_c), 0, 192, P(self.cat_c), 0, 128, 128, gC, "Wih", "bih", 192, B, N)
@@ -383,10 +407,10 @@ class GruUpdate:
             wgrad_probs(P(self.dcat_c), 0, 128, P(self.Xsa), 0, Dsa, Dsa, gC, "Wo", "bo", 64, B, N)
             + wgrad_probs(P(self.dcat_c), 64, 128, radar, 0, 18, 18, gC, "Wg", "bg", 64, B, N))
         L += self._adam(m.critic_optimizer, m.fc)
-        # ---------------- actor step (WGRU/maddpg:293-310): 3 - mean Q(s, pi(s, h), h); its projection ran above
-        L.append(gru_cell(A, "Wout", "bout", sa, 2, TANH, P(self.gi_a), P(self.gh_a), hcur, B, N, FWD,
-                          hout=P(self.ha), ldho=H, pack_src=own, ld_pack_src=D0, npack=d, pack_dst=P(self.Xsa2),
-                          ld_pack_dst=Dsa))
+        # ---------------- actor step (WGRU/maddpg:293-310): 3 - mean Q(s, pi(s, h), h); its projection (and
+        # with CELL_PAIRS its forward cell) ran above
+        if not pair:
+            L.append(fwd_a)
         L += self._proj(C, sc, P(self.Xsa2), Dsa, Dsa, radar, hcur, P(self.cat_c), P(self.gi_c), P(self.gh_c))
         L.append(gru_cell(C, "Wout", "bout", sc, 1, 0, P(self.gi_c), P(self.gh_c), hcur, B, N, ACTLOSS,
                           y=P(self.q_a), inv_m=1.0 / B, dgi=P(self.dgi_c), ldd=192))
