@@ -465,7 +465,7 @@ struct WpView {
 
 __device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, double2 p, double2 v, uint32_t rm,
                               int cnt, double rmin, int goal, int bnd, int building, int &flag, int &done, int &cg,
-                              uint8_t &fl) {
+                              uint8_t &fl, double2 start) {
     const double px = p.x, py = p.y, pb = A.pb;
     int nrem = cnt - __popc(rm & (cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1u)));
     double smallest = INFINITY;
@@ -508,13 +508,23 @@ __device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, d
     }
     const double dtg = 1 * (npnorm(pp.x - nx.x, pp.y - nx.y) - npnorm(px - nx.x, py - nx.y));
     // cross_track_error (WGRU/env:2621-2632): nearest point of the first segment at the smallest
-    // pointToSegment distance, then the point distance to it
+    // pointToSegment distance, then the point distance to it.  A segment whose bounding box lies
+    // farther than the current best (squared, 1e-8 relative margin) cannot be strictly nearer: its
+    // distance is not computed (the loop keeps the first strict minimum either way)
     double cross;
     {
         double best = INFINITY;
-        double2 a = A.start[ai], q = a;
+        double2 a = start, q = a;
         for (int k = 0; k < cnt; ++k) {
             const double2 b = wp[k];
+            {
+                const double ox = fmax(fmax(fmin(a.x, b.x) - px, px - fmax(a.x, b.x)), 0.0);
+                const double oy = fmax(fmax(fmin(a.y, b.y) - py, py - fmax(a.y, b.y)), 0.0);
+                if (ox * ox + oy * oy > best * best * (1.0 + 1e-8)) {
+                    a = b;
+                    continue;
+                }
+            }
             const double d = point_to_segment(px, py, a.x, a.y, b.x, b.y);
             if (d < best) {
                 best = d;
@@ -951,7 +961,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     // load (the agent phase's state stays in flight across the radar)
     int cur = 0, wcnt = 0;
     uint8_t reach = 0;
-    double2 pp = make_double2(0.0, 0.0), pv = pp, gl = pp;
+    double2 pp = make_double2(0.0, 0.0), pv = pp, gl = pp, st0 = pp;
     float2 a = make_float2(0.0f, 0.0f);
     if (active) {
         cur = A.wp_cur[ai];
@@ -961,6 +971,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         pv = A.vel[ai];
         a = act[ai];
         gl = A.goal[ai];
+        if (VAR) st0 = A.start[ai];       // the cross-track reference start (variant 1)
     }
     // the ring position of this push: the host's mirror, or (graph replays) a device word
     const int64_t rpos = TAIL && T.ring ? (T.pos_in ? *T.pos_in : T.pos) : 0;
@@ -1130,7 +1141,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         if (A.variant) {
             const WpView wv{wp_cache(A) + t * WPC, A.wp + ai * A.W};
             r = wgru_reward(A, ai, wv, pp, np, S.vel[t], (uint32_t)cur, wcnt,
-                            __longlong_as_double((long long)S.rmin[t]), goal, bnd, building, wpf, done, cg, fl);
+                            __longlong_as_double((long long)S.rmin[t]), goal, bnd, building, wpf, done, cg, fl, st0);
             if (cg) {
                 reach = 1;
                 A.reach[ai] = 1;

@@ -1,9 +1,9 @@
 """Sub-phase timeline of the env step kernel's agent phase (thread 0 = agent 0 of the workgroup's
 first env) from a stamp build with agent stamps:
   bash tools/variant_lib.sh astamps aac_env.hip -DAAC_ENV_STAMPS -DAAC_ENV_AGENT_STAMPS
-  AAC_LIB=tools/variants/lib_astamps.so python tools/agent_stamps.py [E] [N]
+  AAC_LIB=tools/variants/lib_astamps.so python tools/agent_stamps.py [E] [N] [att|wgru]
 Phases (cycles): observe_agent (obs rows + tdCPA), neighbour loops (collisions, penalty), building
-cells, goal + bound predicates, reward + writes; with the step phases around them."""
+cells, goal + bound predicates, reward + writes (WGRU: wgru_reward); with the step phases around them."""
 import ctypes
 import os
 import sys
@@ -19,8 +19,9 @@ def main():
     from multi_agent_aac_amd.env import BatchedEnv
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    variant = sys.argv[3] if len(sys.argv) > 3 else "att"
     occ = world.synthetic_map(2026)
-    env = BatchedEnv(E, N, occ, radar_mode="combined", max_wp=32)
+    env = BatchedEnv(E, N, occ, radar_mode=None if variant == "wgru" else "combined", max_wp=32, variant=variant)
     env.set_od_bank(world.ODBank(occ, n_pairs=16384, seed=5, max_wp=32), seed=3)
     env.auto_reset(None)
     g = torch.Generator(device="cuda").manual_seed(0)
