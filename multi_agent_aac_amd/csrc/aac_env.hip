@@ -428,6 +428,42 @@ __device__ inline void radar_phase(const Args &A, Lds &S, int e0, int nagents, b
     }
 }
 
+#ifndef AAC_ENV_AGENT_STAMPS
+#define ASTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+#ifdef AAC_ENV_STAMPS
+// diagnostic build only (tools/env_stamps.py): per-workgroup s_memtime at entry, after kinematics,
+// after the radar, after the agent phase and at exit, plus s_memrealtime at entry / exit
+constexpr int ESTAMP_WG = 65536;
+__device__ unsigned long long g_env_st[ESTAMP_WG][7];
+#define ESTAMP(k, v)                                                                                    \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_env_st[blockIdx.x][k] = (v);                \
+    } while (0)
+// reset_kernel: [s_memrealtime at entry, s_memtime at entry / after the OD draw / after the state
+// writes / after the radar / after the observation, s_memrealtime at exit]; zero = workgroup idle
+__device__ unsigned long long g_reset_st[ESTAMP_WG][7];
+#define RSTAMP(k, v)                                                                                    \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_reset_st[blockIdx.x][k] = (v);              \
+    } while (0)
+#ifdef AAC_ENV_AGENT_STAMPS      // agent-phase sub-stamps of thread 0, into the reset stamp array (step only)
+#define ASTAMP(k)                                                                                       \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_reset_st[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#endif
+#else
+#define ESTAMP(k, v) \
+    do {             \
+    } while (0)
+#define RSTAMP(k, v) \
+    do {             \
+    } while (0)
+#endif
+
 // ------------------------------------------------------------- variant 1 (randomOD_Wgru_radar)
 // GEOS algorithm::Distance::pointToSegment and LineSegment::closestPoint (oracle/geos.py)
 __device__ double point_to_segment(double px, double py, double ax, double ay, double bx, double by) {
@@ -507,6 +543,7 @@ __device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, d
             }
     }
     const double dtg = 1 * (npnorm(pp.x - nx.x, pp.y - nx.y) - npnorm(px - nx.x, py - nx.y));
+    ASTAMP(6);
     // cross_track_error (WGRU/env:2621-2632): nearest point of the first segment at the smallest
     // pointToSegment distance, then the point distance to it.  A segment whose bounding box lies
     // farther than the current best (squared, 1e-8 relative margin) cannot be strictly nearer: its
@@ -563,41 +600,6 @@ __device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, d
     return r;
 }
 
-#ifndef AAC_ENV_AGENT_STAMPS
-#define ASTAMP(k) \
-    do {          \
-    } while (0)
-#endif
-#ifdef AAC_ENV_STAMPS
-// diagnostic build only (tools/env_stamps.py): per-workgroup s_memtime at entry, after kinematics,
-// after the radar, after the agent phase and at exit, plus s_memrealtime at entry / exit
-constexpr int ESTAMP_WG = 65536;
-__device__ unsigned long long g_env_st[ESTAMP_WG][7];
-#define ESTAMP(k, v)                                                                                    \
-    do {                                                                                               \
-        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_env_st[blockIdx.x][k] = (v);                \
-    } while (0)
-// reset_kernel: [s_memrealtime at entry, s_memtime at entry / after the OD draw / after the state
-// writes / after the radar / after the observation, s_memrealtime at exit]; zero = workgroup idle
-__device__ unsigned long long g_reset_st[ESTAMP_WG][7];
-#define RSTAMP(k, v)                                                                                    \
-    do {                                                                                               \
-        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_reset_st[blockIdx.x][k] = (v);              \
-    } while (0)
-#ifdef AAC_ENV_AGENT_STAMPS      // agent-phase sub-stamps of thread 0, into the reset stamp array (step only)
-#define ASTAMP(k)                                                                                       \
-    do {                                                                                               \
-        if (threadIdx.x == 0 && blockIdx.x < ESTAMP_WG) g_reset_st[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#endif
-#else
-#define ESTAMP(k, v) \
-    do {             \
-    } while (0)
-#define RSTAMP(k, v) \
-    do {             \
-    } while (0)
-#endif
 
 // copy n floats from LDS to global memory with 16-B stores where the destination allows
 __device__ inline void store_rows(float *dst, const float *src, int n) {

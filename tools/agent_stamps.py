@@ -54,6 +54,9 @@ def main():
         for name, col in zip(("kin", "radar", "agent", "final"), ph.T):
             acc[name] += col.tolist()
         sub = np.diff(a[ok, 0:6], axis=1)
+        if variant == "wgru":      # stamp 6: after the next-waypoint search inside wgru_reward
+            acc.setdefault("r_search", []).extend((a[ok, 6] - a[ok, 4]).tolist())
+            acc.setdefault("r_cross_rest", []).extend((a[ok, 5] - a[ok, 6]).tolist())
         for name, col in zip(("a_obs", "a_nei", "a_bld", "a_goal_bnd", "a_rew"), sub.T):
             acc[name] += col.tolist()
         acc["a_wait"] += (s[ok, 4] - a[ok, 5]).tolist()     # after thread 0's agent to the barrier
