@@ -507,30 +507,43 @@ __device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, d
     double smallest = INFINITY;
     double2 nx = make_double2(0.0, 0.0);
     const uint32_t rm0 = rm;
-    for (int k = 0; k < cnt; ++k) {
-        if ((rm >> k) & 1u) continue;
-        const double2 w = wp[k];
-        const double d = gdist(px, py, w.x, w.y);
-        if (d < smallest) {
-            smallest = d;
-            nx = w;
-            if (smallest < 5) {
-                flag = 1;
-                if (nrem > 1) {
-                    rm |= 1u << k;
-                    --nrem;
-                    double best = INFINITY;
-                    for (int q = 0; q < cnt; ++q) {
-                        if ((rm >> q) & 1u) continue;
-                        const double2 u = wp[q];
-                        const double dd = gdist(u.x, u.y, px, py);
-                        if (dd < best) {
-                            best = dd;
-                            nx = u;
+    // waypoints in groups of WGB loads in flight: past the first WPC (LDS) they come from HBM, and a
+    // wave almost always holds an agent with a longer list
+    constexpr int WGB = 2;
+    bool found = false;
+#pragma unroll 1
+    for (int k0 = 0; k0 < cnt && !found; k0 += WGB) {
+        double2 wg[WGB];
+#pragma unroll
+        for (int u = 0; u < WGB; ++u) wg[u] = k0 + u < cnt ? wp[k0 + u] : make_double2(0.0, 0.0);
+#pragma unroll
+        for (int u = 0; u < WGB; ++u) {
+            const int k = k0 + u;
+            if (k >= cnt || found) break;
+            if ((rm >> k) & 1u) continue;
+            const double2 w = wg[u];
+            const double d = gdist(px, py, w.x, w.y);
+            if (d < smallest) {
+                smallest = d;
+                nx = w;
+                if (smallest < 5) {
+                    flag = 1;
+                    if (nrem > 1) {
+                        rm |= 1u << k;
+                        --nrem;
+                        double best = INFINITY;
+                        for (int q = 0; q < cnt; ++q) {
+                            if ((rm >> q) & 1u) continue;
+                            const double2 uq = wp[q];
+                            const double dd = gdist(uq.x, uq.y, px, py);
+                            if (dd < best) {
+                                best = dd;
+                                nx = uq;
+                            }
                         }
                     }
+                    found = true;
                 }
-                break;
             }
         }
     }
@@ -552,23 +565,35 @@ __device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, d
     {
         double best = INFINITY;
         double2 a = start, q = a;
-        for (int k = 0; k < cnt; ++k) {
-            const double2 b = wp[k];
-            {
-                const double ox = fmax(fmax(fmin(a.x, b.x) - px, px - fmax(a.x, b.x)), 0.0);
-                const double oy = fmax(fmax(fmin(a.y, b.y) - py, py - fmax(a.y, b.y)), 0.0);
-                if (ox * ox + oy * oy > best * best * (1.0 + 1e-8)) {
-                    a = b;
-                    continue;
+        bool stop = false;
+#pragma unroll 1
+        for (int k0 = 0; k0 < cnt && !stop; k0 += WGB) {
+            double2 bg[WGB];
+#pragma unroll
+            for (int u = 0; u < WGB; ++u) bg[u] = k0 + u < cnt ? wp[k0 + u] : make_double2(0.0, 0.0);
+#pragma unroll
+            for (int u = 0; u < WGB; ++u) {
+                if (k0 + u >= cnt || stop) break;
+                const double2 b = bg[u];
+                {
+                    const double ox = fmax(fmax(fmin(a.x, b.x) - px, px - fmax(a.x, b.x)), 0.0);
+                    const double oy = fmax(fmax(fmin(a.y, b.y) - py, py - fmax(a.y, b.y)), 0.0);
+                    if (ox * ox + oy * oy > best * best * (1.0 + 1e-8)) {
+                        a = b;
+                        continue;
+                    }
                 }
+                const double d = point_to_segment(px, py, a.x, a.y, b.x, b.y);
+                if (d < best) {
+                    best = d;
+                    q = segment_closest_point(px, py, a.x, a.y, b.x, b.y);
+                }
+                if (best <= 0.0) {
+                    stop = true;
+                    break;
+                }
+                a = b;
             }
-            const double d = point_to_segment(px, py, a.x, a.y, b.x, b.y);
-            if (d < best) {
-                best = d;
-                q = segment_closest_point(px, py, a.x, a.y, b.x, b.y);
-            }
-            if (best <= 0.0) break;
-            a = b;
         }
         cross = gdist(px, py, q.x, q.y);
     }
