@@ -17,6 +17,8 @@ per agent and zeroed at episode start, ``WGRU/ma_main:476-647``); ``UamTrainer``
 Module flags (environment variables read at import):
   AAC_FUSED_TAIL   0 / 1 forces the separate / fused env tail (default fused)
   AAC_STEP_GRAPH   1: each ATT training step replays one captured graph (measured neutral, off)
+  AAC_STEP_GRAPH_GRU 0: the GRU training step launched from the host (default: one graph replay;
+                   config 4 0.3331 -> 0.3310 ms per step)
   AAC_OVERLAP_RESET 1: separate-launch auto-reset on a side stream (measured slower, off)
 """
 import os
@@ -36,6 +38,9 @@ FUSED_TAIL = None if _FT is None else _FT == "1"
 # buffer parity; AAC_STEP_GRAPH=1).  Measured neutral (0.8926 vs 0.8929 ms per step: the host already
 # runs ahead of the device), so the steps are launched from the host by default
 STEP_GRAPH = os.environ.get("AAC_STEP_GRAPH", "0") == "1"
+# the GRU training step (config 4) as one graph replay: its host-side launch sequence left the GPU idle
+# ~5 % of a step (act, env tail and update launched from Python); AAC_STEP_GRAPH_GRU=0 keeps it eager
+STEP_GRAPH_GRU = os.environ.get("AAC_STEP_GRAPH_GRU", "1") == "1"
 
 
 class CheckpointMixin:
@@ -111,17 +116,35 @@ class Trainer(CheckpointMixin):
         self._pos_dirty = True       # the host mirror moved outside step_graph: re-seed pos_dev
 
     def graph_ok(self):
-        """Whole-step graphs: the ATT env with the fused tail, one rank, the fused learner."""
-        return (STEP_GRAPH and not self.gru and self.fused_tail and self.model.world == 1 and self.model.fused
+        """Whole-step graphs: the fused env tail, one rank, the fused learner (ATT: AAC_STEP_GRAPH; the
+        GRU step: AAC_STEP_GRAPH_GRU)."""
+        if self.gru:
+            return (STEP_GRAPH_GRU and self.fused_tail and self.model.world == 1 and not NO_GRAPH
+                    and len(self.replay) > self.B)
+        return (STEP_GRAPH and self.fused_tail and self.model.world == 1 and self.model.fused
                 and not NO_GRAPH and len(self.replay) > self.B)
 
     def _capture_step(self, p):
         """act + env step tail + update_myown of a step whose current buffers are bufs[p], captured
         as one HIP graph.  Nothing runs during the capture; the replay's host mirror is restored."""
         c, n = self.bufs[p], self.bufs[1 - p]
+        saved = (self.replay.pos, self.replay.size)
+        if self.gru:
+            # the hidden-state pair flips with the buffer pair: parity p reads hp[p ^ hoff]
+            hin, hout = self.hp[p ^ self._hoff], self.hp[1 - (p ^ self._hoff)]
+            plan = self.model._plan(self.B)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                act, hn = self.model.act(c.own, c.radar, hin, self.episode, noisy=True, h_out=hout)
+                srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, hin, hn]
+                self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs, zero_rows=hn,
+                                   pos_io=(self.pos_dev[p], self.pos_dev[1 - p]))
+                plan.run()
+            self.replay.pos, self.replay.size = saved
+            self._sg[p] = (g, None)
+            return
         fu = self.model._fused_plan(self.B)
         side = torch.cuda.Stream()
-        saved = (self.replay.pos, self.replay.size)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
@@ -136,6 +159,8 @@ class Trainer(CheckpointMixin):
         ring position lives in device words, the host keeps its mirror)."""
         p = 0 if self.cur is self.bufs[0] else 1
         if not self._sg:
+            if self.gru:
+                self._hoff = (0 if self.h is self.hp[0] else 1) ^ p
             for q in (0, 1):
                 self._capture_step(q)
         if self._pos_dirty:
@@ -148,6 +173,8 @@ class Trainer(CheckpointMixin):
         rep.pos = (rep.pos + self.E) % rep.capacity
         rep.size = min(rep.size + self.E, rep.capacity)
         self.cur, self.nxt = self.nxt, self.cur
+        if self.gru:
+            self.h = self.hp[1 - (p ^ self._hoff)]
 
     def env_episode_view(self):
         # the env's own per-env episode counter (advanced by each auto-reset; 1 after the first)

@@ -136,16 +136,18 @@ def test_step_tail_rejects_bad_fields(native_lib, occ):
     assert rc != 0 and b"OD bank" in _native.lib().aac_last_error()
 
 
-@pytest.mark.parametrize("E,N,B,mem,steps", [(256, 5, 64, 2000, 7), (4096, 5, 1024, 20000, 5)])
-def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, steps):
+@pytest.mark.parametrize("E,N,B,mem,steps,model", [(256, 5, 64, 2000, 7, "att"), (4096, 5, 1024, 20000, 5, "att"),
+                                                   (512, 8, 128, 3000, 7, "gru"), (4096, 8, 512, 20000, 5, "gru")])
+def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, steps, model):
     """trainer.Trainer.step_graph (act + fused env tail + update_myown replayed from one captured HIP
     graph per buffer parity, the ring position in device words) against the same steps launched
     eagerly: bit-identical networks, optimiser state, replay ring and env state.  The second case is
-    config 3 (4096 envs x 5 agents, B = 1024).  An eager step between graph replays re-seeds the
-    device ring-position word."""
+    config 3 (4096 envs x 5 agents, B = 1024); the GRU step (config 4: 4096 x 8, B = 512) carries the
+    hidden-state pair through the replays.  An eager step between graph replays re-seeds the device
+    ring-position word."""
     from multi_agent_aac_amd import trainer
     monkeypatch.setattr(trainer, "STEP_GRAPH", True)        # off by default in the bench (measured neutral)
-    tr = [trainer.Trainer(E, N, B, mem, "combined", seed=0) for _ in range(2)]
+    tr = [trainer.Trainer(E, N, B, mem, "combined", seed=0, model=model) for _ in range(2)]
     for t in tr:
         while len(t.replay) <= 3 * B:
             t.step(update=False)
@@ -170,3 +172,5 @@ def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, st
     assert all(torch.equal(sa[k], sb[k]) for k in sa)
     for f in ("own", "radar", "nei", "reward", "env_done"):
         assert torch.equal(getattr(a.cur, f), getattr(b.cur, f)), f
+    if model == "gru":
+        assert torch.equal(a.h, b.h)
