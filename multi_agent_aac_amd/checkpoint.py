@@ -146,29 +146,28 @@ def save(path, learner=None, replay=None, env=None, extra=None):
     return path
 
 
-def _copy_into(dst, src, name):
-    if dst.shape != src.shape or dst.dtype != src.dtype:
-        raise ValueError(f"checkpoint tensor {name}: {tuple(src.shape)} {src.dtype} does not fit "
-                         f"{tuple(dst.shape)} {dst.dtype}")
-    dst.copy_(src.to(dst.device))
-
-
 def _check_counter(name, t):
     v = int(t.reshape(-1)[0])
     if v < 0 or v >= _EPOCH_LIMIT:
         raise ValueError(f"{name} = {v}: RNG epochs are 32-bit (0 <= value < 2^32)")
 
 
-def load(path, learner=None, replay=None, env=None, extra=None):
-    """Restore the parts given (each must have been saved) into the live objects, in place."""
-    ck = torch.load(path, map_location="cpu", weights_only=True)
-    if not isinstance(ck, dict) or ck.get("format") != FORMAT:
-        raise ValueError(f"{path}: not an {FORMAT} file")
+def _check_fit(dst, src, name):
+    if tuple(dst.shape) != tuple(src.shape) or dst.dtype != src.dtype:
+        raise ValueError(f"checkpoint tensor {name}: {tuple(src.shape)} {src.dtype} does not fit "
+                         f"{tuple(dst.shape)} {dst.dtype}")
+
+
+def _plan(ck, path, learner, replay, env, extra):
+    """Validate every requested part against the live objects WITHOUT touching them.  Returns the
+    list of (dst, src, name) copies and the scalar updates to apply; raises on any mismatch, so a
+    refused file leaves the running loop exactly as it was (a half-restored loop replayed
+    stale graphs against a moved ring position)."""
     parts = ck["parts"]
     for want, obj in (("learner", learner), ("replay", replay), ("env", env), ("extra", extra)):
         if obj is not None and want not in parts:
             raise KeyError(f"{path} holds no {want} state")
-    reseeded = False
+    copies, todo = [], {}
     if learner is not None:
         p = parts["learner"]
         meta = learner_meta(learner)
@@ -179,27 +178,25 @@ def load(path, learner=None, replay=None, env=None, extra=None):
         if set(live) != set(p["tensors"]):
             raise ValueError(f"checkpoint learner tensors {sorted(p['tensors'])} != {sorted(live)}")
         for k, v in live.items():
-            _copy_into(v, p["tensors"][k], "learner." + k)
-        reseeded |= learner.noise_seed != p["meta"]["noise_seed"]
-        learner.noise_seed = p["meta"]["noise_seed"]
+            _check_fit(v, p["tensors"][k], "learner." + k)
+            copies.append((v, p["tensors"][k], "learner." + k))
+        todo["noise_seed"] = p["meta"]["noise_seed"]
     if replay is not None:
         p = parts["replay"]
         m = p["meta"]
         if m["capacity"] != replay.capacity or m["row_width"] != replay.ring.shape[1]:
             raise ValueError(f"checkpoint replay {m} does not fit capacity {replay.capacity} x {replay.ring.shape[1]}")
+        if not 0 <= m["size"] <= m["capacity"] or not 0 <= m["pos"] < max(1, m["capacity"]):
+            raise ValueError(f"checkpoint replay position {m['pos']} / size {m['size']} out of range")
         _check_counter("replay.counter", p["tensors"]["counter"])
+        if replay.seed != m["seed"] and learner is None:
+            raise ValueError("the checkpoint's replay seed differs from the live replay's: load the learner "
+                             "with it, so that its captured update graph (which bakes the seed) is dropped")
         live = replay_tensors(replay)
-        _copy_into(live["ring"][:m["size"]], p["tensors"]["ring"], "replay.ring")
-        _copy_into(live["meta"], p["tensors"]["meta"], "replay.meta")
-        _copy_into(live["counter"], p["tensors"]["counter"], "replay.counter")
-        if replay.seed != m["seed"]:
-            if learner is None:
-                raise ValueError("the checkpoint's replay seed differs from the live replay's: load the learner "
-                                 "with it, so that its captured update graph (which bakes the seed) is dropped")
-            reseeded = True
-        replay.seed, replay.pos, replay.size = m["seed"], m["pos"], m["size"]
-    if reseeded:
-        drop_graphs(learner)
+        for k, dst in (("ring", live["ring"][:m["size"]]), ("meta", live["meta"]), ("counter", live["counter"])):
+            _check_fit(dst, p["tensors"][k], "replay." + k)
+            copies.append((dst, p["tensors"][k], "replay." + k))
+        todo["replay"] = (m["seed"], m["pos"], m["size"])
     if env is not None:
         p = parts["env"]
         saved, live = dict(p["meta"]), env_meta(env)
@@ -208,24 +205,62 @@ def load(path, learner=None, replay=None, env=None, extra=None):
         bad = {k: (saved[k], live.get(k)) for k in saved if saved[k] != live.get(k)}
         if bad:
             raise ValueError(f"checkpoint env does not match the live env (saved, live): {bad}")
-        if seed is not None and seed != live_seed:
-            # same bank, other draw seed: restore the saved one (future episodes draw as in the saved run)
-            if hasattr(env, "set_od_bank"):
-                env.set_od_bank(env.bank, seed=seed)
-            else:
-                env.set_bank(env.bank, seed=seed)
         t = dict(p["tensors"])
         ep = t.pop("episode", None)
-        env.set_state(**t)
+        cur = env_tensors(env)
+        cur.pop("episode", None)
+        if set(t) != set(cur):
+            raise ValueError(f"checkpoint env tensors {sorted(t)} != {sorted(cur)}")
+        for k, v in cur.items():
+            _check_fit(v, t[k], "env." + k)
         if ep is not None:
             buf = getattr(env, "_episode_buf", None)
             if buf is None:
                 raise ValueError("checkpoint carries episode counters but the env has no episode buffer")
-            _copy_into(buf, ep, "env.episode")
+            _check_fit(buf, ep, "env.episode")
+        todo["env"] = (t, ep, seed if seed is not None and seed != live_seed else None)
     if extra is not None:
         p = parts["extra"]["tensors"]
         for k, v in extra.items():
-            _copy_into(v, p[k], "extra." + k)
+            if k not in p:
+                raise KeyError(f"{path} holds no extra tensor {k}")
+            _check_fit(v, p[k], "extra." + k)
+            copies.append((v, p[k], "extra." + k))
+    return copies, todo
+
+
+def load(path, learner=None, replay=None, env=None, extra=None):
+    """Restore the parts given (each must have been saved) into the live objects, in place.  Every
+    part is checked first; nothing is written unless the whole file fits."""
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    if not isinstance(ck, dict) or ck.get("format") != FORMAT:
+        raise ValueError(f"{path}: not an {FORMAT} file")
+    copies, todo = _plan(ck, path, learner, replay, env, extra)
+    for dst, src, _ in copies:
+        dst.copy_(src.to(dst.device))
+    reseeded = False
+    if "noise_seed" in todo:
+        reseeded |= learner.noise_seed != todo["noise_seed"]
+        learner.noise_seed = todo["noise_seed"]
+    if "replay" in todo:
+        seed, pos, size = todo["replay"]
+        reseeded |= replay.seed != seed
+        replay.seed, replay.pos, replay.size = seed, pos, size
+    if reseeded:
+        drop_graphs(learner)
+    if "env" in todo:
+        t, ep, seed = todo["env"]
+        if seed is not None:
+            # same bank, other draw seed: restore the saved one (future episodes draw as in the saved
+            # run).  The env's bank generation advances, so graphs captured around its step tail or
+            # auto-reset (which bake the bank pointers and seed) are re-captured by their owner.
+            if hasattr(env, "set_od_bank"):
+                env.set_od_bank(env.bank, seed=seed)
+            else:
+                env.set_bank(env.bank, seed=seed)
+        env.set_state(**t)
+        if ep is not None:
+            env._episode_buf.copy_(ep.to(env._episode_buf.device))
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     return ck

@@ -116,15 +116,17 @@ __device__ inline bool bound_crash(const Args &A, double x0, double y0, double x
     return capsule_crash(A.pb, A.bound, x0, y0, x1, y1);
 }
 
-// 64-gon(pos, pB) meets 64-gon(goal, 1) (ATT/env:2266-2269)
+// 64-gon(pos, pB) meets 64-gon(goal, 1) (ATT/env:2266-2269); exact within the threshold band
 __device__ inline bool goal_reached(double px, double py, double gx, double gy, double pb) {
-    return gons_meet(gx - px, gy - py, pb + 1.0, false);
+    return goal_meet_exact(px, py, gx, gy, pb);
 }
 
-// 64-gon(pos, pB) meets the closed square cell (ATT/env:2243-2250): separating axes
-__device__ bool building_hit(double px, double py, double cx, double cy, double pb) {
+// 64-gon(pos, pB) meets the closed square cell (ATT/env:2243-2250): separating axes; an axis within
+// EXACT_BAND of separating hands the decision to the exact test on the GEOS float vertices
+__device__ __attribute__((always_inline)) bool building_hit(double px, double py, double cx, double cy, double pb) {
     double dx = cx - px, dy = cy - py;
-    if (fabs(dx) > 5.0 + pb || fabs(dy) > 5.0 + pb) return false;
+    if (fabs(dx) > 5.0 + pb + EXACT_BAND || fabs(dy) > 5.0 + pb + EXACT_BAND) return false;
+    bool unsure = fabs(dx) > 5.0 + pb - EXACT_BAND || fabs(dy) > 5.0 + pb - EXACT_BAND;
     // the 64-gon lies between its inscribed (pb cos(pi/64)) and circumscribed (pb) circles:
     // away from that band the distance to the square decides
     {
@@ -139,6 +141,18 @@ __device__ bool building_hit(double px, double py, double cx, double cy, double 
     for (int k = 0; k < 32; ++k) {
         double proj = fabs(dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k]);
         double lim = 5.0 * (fabs(c_tab.nrm_c[k]) + fabs(c_tab.nrm_s[k])) + pb * c_tab.apothem;
+        if (proj > lim + EXACT_BAND) return false;
+        unsure |= proj > lim - EXACT_BAND;
+    }
+    if (!unsure) return true;
+    const int m = gon_square_meet(px, py, pb, cx - 5.0, cx + 5.0, cy - 5.0, cy + 5.0);
+    if (m >= 0) return m == 1;
+    // undecidable: the closed form
+    if (fabs(dx) > 5.0 + pb || fabs(dy) > 5.0 + pb) return false;
+#pragma unroll 1
+    for (int k = 0; k < 32; ++k) {
+        double proj = fabs(dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k]);
+        double lim = 5.0 * (fabs(c_tab.nrm_c[k]) + fabs(c_tab.nrm_s[k])) + pb * c_tab.apothem;
         if (proj > lim) return false;
     }
     return true;
@@ -149,8 +163,9 @@ __device__ bool building_hit(double px, double py, double cx, double cy, double 
 // lanes together: the per-cell loop ran the slab test whenever any lane of the wave had a
 // candidate in that cell slot, the candidate loop runs it max-popcount times.  The minimum does
 // not depend on the order (OM/env:1089-1141 takes the nearest intersection).
-__device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsigned long long *rows, double cx,
-                                  double cy, double ex, double ey, double len) {
+template <int EX>
+__device__ __attribute__((always_inline)) double radar_obstacles(const Args &A, const uint8_t *occ, const unsigned long long *rows, double cx,
+                                  double cy, double ex, double ey, double len, bool &band) {
     double mind = len, d;
     // only cells whose square meets the segment's bounding box can meet the segment (index range
     // by a product with 0.1: it rounds within an ulp of the quotient, and floor / ceil of it still
@@ -170,7 +185,7 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
     const double reach = 5.0 * (fabs(ddx) + fabs(ddy)) * (1.0 + 1e-9) + 1e-12;
     if (i1 < i0 || j1 < j0) {
         // the box lies off the grid: no cell
-    } else if (rows && i1 - i0 < 8 && j1 - j0 < 8) {
+    } else if (EX != 2 && rows && i1 - i0 < 8 && j1 - j0 < 8) {   // (the exact re-run: the lean loop below)
         // the box's occupied cells from the row masks (one 8-B LDS read per row, all issued
         // up front), the line filter on those only
         const unsigned long long span = (2ull << (j1 - j0)) - 1;
@@ -208,7 +223,7 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
         // relative margin far above the rounding of d, so the minimum is the one the full loop finds
         if (cand) {
             const double qx = A.gx0 + 10.0 * (i0 + (bmin >> 3)), qy = A.gy0 + 10.0 * (j0 + (bmin & 7));
-            if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
+            if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band) && d <= mind) mind = d;
             cand &= ~(1ull << bmin);
         }
         while (cand) {
@@ -217,7 +232,7 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
             const double qx = A.gx0 + 10.0 * (i0 + (b >> 3)), qy = A.gy0 + 10.0 * (j0 + (b & 7));
             const double lb = (qx - cx) * ddx + (qy - cy) * ddy - reach;
             if (lb > 0.0 && lb * lb > mind * mind * L2 * (1.0 + 1e-8)) continue;
-            if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
+            if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band) && d <= mind) mind = d;
         }
     } else {      // a radar longer than the 8 x 8-cell mask covers, or maps taller than 64 cells
         for (int i = i0; i <= i1; ++i)
@@ -227,7 +242,7 @@ __device__ double radar_obstacles(const Args &A, const uint8_t *occ, const unsig
                 const double wx = qx - cx, wy = qy - cy;
                 const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
                 if (fabs(cr) > reach || al < -reach || al > L2 + reach) continue;
-                if (ray_square(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d) && d <= mind) mind = d;
+                if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band) && d <= mind) mind = d;
             }
     }
 #ifdef AAC_DBG_NO_LINES
@@ -268,7 +283,7 @@ __device__ inline const unsigned long long *map_rows(const Args &A, int m) {
 }
 
 // own + neighbour observation and tdCPA of agent i of env e (ATT/env:1285-1469)
-__device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int base, float *own = nullptr,
+__device__ __attribute__((always_inline)) void observe_agent(const Args &A, const Lds &S, int e, int i, int base, float *own = nullptr,
                               float *nei = nullptr) {
     const int N = A.N, K = A.K;
     const size_t ai = (size_t)e * N + i;
@@ -344,8 +359,11 @@ __device__ void observe_agent(const Args &A, const Lds &S, int e, int i, int bas
 }
 
 // one radar ray r of agent i (ATT/env:1089-1164 drones, OM/env:1089-1141 obstacles)
-__device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ,
-                            const unsigned long long *rows) {
+// EX: 1 flags a ray with a band case (exact threshold, see ray_poly_entry_full) in band and returns the
+// float answer, 2 decides the band cases exactly
+template <int EX>
+__device__ __attribute__((always_inline)) double radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ,
+                            const unsigned long long *rows, bool &band) {
     const int N = A.N;
     const double pb = A.pb;
     const double2 p = S.pos[base + i];
@@ -353,7 +371,20 @@ __device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base,
     const double ex = px + A.radar_len * c_tab.ray_c[r], ey = py + A.radar_len * c_tab.ray_s[r];
     const double len = gdist(ex, ey, px, py);
     double dd = len, dob = len;
-    if (A.radar_mode != AAC_RADAR_OBSTACLES) {
+    if (EX == 2 && A.radar_mode != AAC_RADAR_OBSTACLES) {
+        // the exact re-run of a flagged ray (cold, lean on registers): the full clip for every neighbour
+        double shortest = INFINITY;
+#pragma unroll 1
+        for (int j = 0; j < N; ++j) {
+            if (j == i) continue;
+            const double2 q = S.pos[base + j];
+            double t;
+            if (!ray_poly_entry_full<2>(px, py, ex, ey, q.x, q.y, pb, t, band)) continue;
+            const double d = gdist(px + t * (ex - px), py + t * (ey - py), px, py);
+            shortest = d < shortest ? d : shortest;
+        }
+        if (shortest < INFINITY) dd = shortest;
+    } else if (A.radar_mode != AAC_RADAR_OBSTACLES) {
         // neighbours whose 64-gon can meet the segment (closest point within pb: the GEOS 64-gon
         // lies inside the circle of radius pb (+1e-15)), collected per 64 as a mask, then the
         // exact entry for each candidate (same lane-compaction argument as radar_obstacles)
@@ -377,7 +408,7 @@ __device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base,
                 cand &= cand - 1;
                 const double2 q = S.pos[base + j];
                 double t;
-                if (!ray_poly_entry(px, py, ex, ey, q.x, q.y, pb, t)) continue;
+                if (!ray_poly_entry<EX>(px, py, ex, ey, q.x, q.y, pb, t, band)) continue;
                 const double ix = px + t * (ex - px), iy = py + t * (ey - py);
                 const double d = gdist(ix, iy, px, py);
                 shortest = d < shortest ? d : shortest;
@@ -385,7 +416,7 @@ __device__ double radar_ray(const Args &A, const Lds &S, int i, int r, int base,
         }
         if (shortest < INFINITY) dd = shortest;
     }
-    if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles(A, occ, rows, px, py, ex, ey, len);
+    if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles<EX>(A, occ, rows, px, py, ex, ey, len, band);
     return A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
 }
 
@@ -407,24 +438,49 @@ struct RingOut {
     int rw, col;
 };
 
-__device__ inline void radar_phase(const Args &A, Lds &S, int e0, int nagents, bool check_active,
-                                   const int32_t *emap = nullptr, bool rmin = false, RingOut ro = RingOut{}) {
+__device__ inline void radar_out(const Args &A, Lds &S, int e, int i, int r, int la, bool rmin, const RingOut &ro,
+                                 double d) {
+    A.radar[((size_t)e * A.N + i) * NRAY + r] = (float)d;
+    if (ro.ring) {
+        int64_t row = ro.pos + e;
+        if (row >= ro.cap) row -= ro.cap;
+        ro.ring[row * ro.rw + ro.col + i * NRAY + r] = (float)d;
+    }
+    if (rmin) atomicMin(&S.rmin[la], (unsigned long long)__double_as_longlong(d));
+}
+
+// radar ray w of the phase's enumeration (agent la = w / NRAY of the workgroup's list, ray w % NRAY);
+// returns whether (EX = 1) the ray had a threshold-band case -- its float value is written all the same
+template <int EX>
+__device__ __attribute__((always_inline)) bool radar_item(const Args &A, Lds &S, int e0, int w, const int32_t *emap,
+                                                          bool rmin, const RingOut &ro) {
+    const int la = w / NRAY, r = w - la * NRAY;
+    const int le = la / A.N, i = la - le * A.N;
+    const int e = emap ? emap[le] : e0 + le;
+    const int mi = A.map_idx ? A.map_idx[e] : 0;
+    bool band = false;
+    const double d = radar_ray<EX>(A, S, i, r, le * A.N, s_maps + mi * A.gw * A.gh, map_rows(A, mi), band);
+    radar_out(A, S, e, i, r, la, rmin, ro, d);
+    return EX == 1 && band;
+}
+
+// Exact radar (ray_poly_entry_full): the phase computes every ray with its threshold-band cases -- a ray
+// within ~1e-9 of touching a 64-gon or a cell corner, rare -- only flagged: the env's bit band_bit of
+// S.active (1 is the reset / env_done flag), set by every flagging thread.  The caller runs the flagged
+// envs' rays again with the exact tests (radar_item<2>) later, where few registers are live: inlined into
+// this loop the exact tests spilled the step-tail kernels' registers to scratch.
+__device__ __attribute__((always_inline)) void radar_phase(const Args &A, Lds &S, int e0, int nagents,
+                                                               bool check_active, const int32_t *emap = nullptr,
+                                                               bool rmin = false, RingOut ro = RingOut{},
+                                                               uint8_t band_bit = 0) {
     for (int w = threadIdx.x; w < nagents * NRAY; w += BLOCK) {
-        const int la = w / NRAY, r = w - la * NRAY;
-        const int le = la / A.N, i = la - le * A.N;
+        const int la = w / NRAY;
+        const int le = la / A.N;
         const int e = emap ? emap[le] : e0 + le;
         if (e >= A.E) continue;
-        if (check_active && !S.active[le]) continue;
-        const int mi = A.map_idx ? A.map_idx[e] : 0;
-        const uint8_t *occ = s_maps + mi * A.gw * A.gh;
-        const double d = radar_ray(A, S, i, r, le * A.N, occ, map_rows(A, mi));
-        A.radar[((size_t)e * A.N + i) * NRAY + r] = (float)d;
-        if (ro.ring) {
-            int64_t row = ro.pos + e;
-            if (row >= ro.cap) row -= ro.cap;
-            ro.ring[row * ro.rw + ro.col + i * NRAY + r] = (float)d;
-        }
-        if (rmin) atomicMin(&S.rmin[la], (unsigned long long)__double_as_longlong(d));
+        if (check_active && !(S.active[le] & 1)) continue;
+        if (radar_item<1>(A, S, e0, w, emap, rmin, ro) && band_bit)
+            S.active[le] |= band_bit;       // the same value from every flagging thread
     }
 }
 
@@ -466,7 +522,7 @@ __device__ unsigned long long g_reset_st[ESTAMP_WG][7];
 
 // ------------------------------------------------------------- variant 1 (randomOD_Wgru_radar)
 // GEOS algorithm::Distance::pointToSegment and LineSegment::closestPoint (oracle/geos.py)
-__device__ double point_to_segment(double px, double py, double ax, double ay, double bx, double by) {
+__device__ __attribute__((always_inline)) double point_to_segment(double px, double py, double ax, double ay, double bx, double by) {
     if (ax == bx && ay == by) return gdist(px, py, ax, ay);
     const double len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay);
     const double r = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2;
@@ -476,7 +532,7 @@ __device__ double point_to_segment(double px, double py, double ax, double ay, d
     return fabs(sv) * sqrt(len2);
 }
 
-__device__ double2 segment_closest_point(double px, double py, double ax, double ay, double bx, double by) {
+__device__ __attribute__((always_inline)) double2 segment_closest_point(double px, double py, double ax, double ay, double bx, double by) {
     double f;
     if (px == ax && py == ay) f = 0.0;
     else if (px == bx && py == by) f = 1.0;
@@ -499,7 +555,7 @@ struct WpView {
     __device__ double2 operator[](int k) const { return k < WPC ? lds[k] : hbm[k]; }
 };
 
-__device__ double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, double2 p, double2 v, uint32_t rm,
+__device__ __attribute__((always_inline)) double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, double2 p, double2 v, uint32_t rm,
                               int cnt, double rmin, int goal, int bnd, int building, int &flag, int &done, int &cg,
                               uint8_t &fl, double2 start) {
     const double px = p.x, py = p.y, pb = A.pb;
@@ -656,7 +712,7 @@ __device__ inline double2 *spec_starts(Lds &S, int nag) {
 __device__ inline bool spec_ok(const Args &A, const ResetArgs &R) {
     return R.mode == 1 && A.epb * A.N <= SPEC_MAX_AG && !R.list;
 }
-__device__ void spec_draw(const Args &A, const ResetArgs &R, Lds &S, int e0, int wv, int nw) {
+__device__ __attribute__((always_inline)) void spec_draw(const Args &A, const ResetArgs &R, Lds &S, int e0, int wv, int nw) {
     // 16 lanes per env (four envs per wave at once): the draws of different envs are independent,
     // an env's N draws are a chain of dependent loads; 16 attempts per round (the first attempt
     // almost always succeeds), the lowest valid one wins as in reset_body
@@ -729,14 +785,14 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
     const int t = threadIdx.x;
     const int le = t / N, i = t - le * N;
     const int e = env_of(emap, e0, le < A.epb ? le : 0);
-    const bool active = (t < nag) && (e < A.E) && S.active[le];
+    const bool active = (t < nag) && (e < A.E) && (S.active[le] & 1);
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
     if (!maps_loaded) load_maps(A);
     if (predrawn) {
         // the draws were made during the step (spec_draw): bank indices in S.idx, starts in
         // spec_starts, episode / map per env after the indices
-        if (t < A.epb && S.active[t] && e0 + t < A.E) {
+        if (t < A.epb && (S.active[t] & 1) && e0 + t < A.E) {
             R.episode[e0 + t] = S.idx[nag + t];
             if (A.map_idx) A.map_idx[e0 + t] = S.idx[nag + A.epb + t];
         }
@@ -748,7 +804,7 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
         const int lane = t & 63, wv = t >> 6;
         for (int lq = wv; lq < A.epb; lq += BLOCK / 64) {
             const int eq = env_of(emap, e0, lq);
-            if (eq >= A.E || !S.active[lq]) continue;
+            if (eq >= A.E || !(S.active[lq] & 1)) continue;
             const int ep = R.episode[eq] + 1;
             const int bq = lq * N;
             // multipleMap variant: random_map_idx = random.randrange(len(world_map_2D_collection)) per
@@ -815,7 +871,7 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
             for (int u = 0; u < 4; ++u) {
                 const int w = w0 + u * BLOCK + t;
                 const int la = w / A.W, k = w - la * A.W, lq = la / N;
-                ok[u] = w < nw && S.active[lq < A.epb ? lq : 0] && env_of(emap, e0, lq < A.epb ? lq : 0) < A.E;
+                ok[u] = w < nw && (S.active[lq < A.epb ? lq : 0] & 1) && env_of(emap, e0, lq < A.epb ? lq : 0) < A.E;
                 const size_t aq = ok[u] ? (size_t)env_of(emap, e0, lq) * N + (la - lq * N) : 0;
                 dst[u] = aq * A.W + k;
                 const int bi = (R.mode == 1 && ok[u]) ? S.idx[la] : 0;
@@ -872,7 +928,17 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
     }
     __syncthreads();   // map_idx (explicit or drawn) written above is read by the radar phase below
     RSTAMP(3, __builtin_amdgcn_s_memtime());
-    radar_phase(A, S, e0, nag, true, emap);
+    radar_phase(A, S, e0, nag, true, emap, false, RingOut{}, 4);
+    __syncthreads();   // the band flags (S.active bit 2) of every thread
+    {
+        int band = 0;
+        for (int k = 0; k < A.epb; ++k) band |= S.active[k] & 4;
+        if (band)           // uniform: the flagged envs' rays again, exactly
+            for (int w = t; w < nag * NRAY; w += BLOCK) {
+                const int le = w / NRAY / A.N;
+                if ((S.active[le] & 4) && env_of(emap, e0, le) < A.E) radar_item<2>(A, S, e0, w, emap, false, RingOut{});
+            }
+    }
 #ifdef AAC_ENV_STAMPS
     __syncthreads();
 #endif
@@ -982,7 +1048,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     ESTAMP(0, __builtin_amdgcn_s_memrealtime());
     ESTAMP(1, __builtin_amdgcn_s_memtime());
     const int nv = e0 + A.epb <= A.E ? A.epb : A.E - e0;     // envs of this workgroup
-    if (TAIL && t < A.epb) S.active[t] = 0;      // env_done of the workgroup's envs (set below)
+    if (t < A.epb) S.active[t] = 0;      // radar band flags (bit 1); TAIL: env_done of the workgroup's envs (set below)
     RingOut ro{};
     // the kinematics' own state, loaded first: in flight across the push's early copy and the map
     // load (the agent phase's state stays in flight across the radar)
@@ -1069,7 +1135,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     aacw::lds_barrier();
     ESTAMP(2, __builtin_amdgcn_s_memtime());
 #ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
-    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro);
+    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro, 2);
 #endif
     if (A.variant) {
         double2 *wc = wp_cache(A);
@@ -1262,7 +1328,22 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             A.step[e] = st;
             const uint8_t ed = (uint8_t)((A.episode_length < st) || any_done || all_goal || all_reach);
             A.env_done[e] = ed;
-            if (TAIL) S.active[le] = ed;
+            if (TAIL) S.active[le] = ed | (S.active[le] & 2);    // keeps the radar band flag
+        }
+    }
+    {   // the radar rays of envs with a threshold-band case (S.active bit 1, set in the radar phase before
+        // the barrier after the agent phase, kept by the env_done write), again with the exact tests
+        int band = 0;
+        for (int k = 0; k < A.epb; ++k) band |= S.active[k] & 2;
+        if (band) {         // uniform
+            for (int w = t; w < nag * NRAY; w += BLOCK) {
+                const int le = w / NRAY / N;
+                if (!(S.active[le] & 2) || e0 + le >= A.E) continue;
+                RingOut rf{};
+                if constexpr (TAIL)
+                    if (T.ring && T.late[LATE_RADAR] >= 0) rf = RingOut{T.ring, rpos, T.cap, T.rw, T.late[LATE_RADAR]};
+                radar_item<2>(A, S, e0, w, nullptr, false, rf);
+            }
         }
     }
     if constexpr (TAIL) {
@@ -1271,13 +1352,13 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         // auto-reset, in that order)
         __syncthreads();      // env_done flags; the staged rows' ring copies have read S.obs
         int any = 0;
-        for (int k = 0; k < A.epb; ++k) any |= S.active[k];
+        for (int k = 0; k < A.epb; ++k) any |= S.active[k] & 1;
         if (any) {
             if (T.zero_rows) {
                 const int n = nv * T.zero_w;
                 for (int j = t; j < n; j += BLOCK) {
                     const int r = j / T.zero_w;
-                    if (S.active[r]) T.zero_rows[(size_t)e0 * T.zero_w + j] = 0.f;
+                    if (S.active[r] & 1) T.zero_rows[(size_t)e0 * T.zero_w + j] = 0.f;
                 }
             }
             if (T.reset) reset_body(A, R, S, nullptr, e0, true, spec);

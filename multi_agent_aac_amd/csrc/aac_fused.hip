@@ -842,7 +842,8 @@ __global__ void adam_sum_kernel(float *p, const float *__restrict__ gpart, int n
 // kernel is bound by how many of their loads are in flight (2048 x 256 threads vs one element per
 // thread and a dependent batch chain in adam_sum_kernel)
 // the four-group copy sum of adam_sum4_kernel / sum_partials4_kernel (one order for both, so a
-// world > 1 update -- sum, all-reduce, Adam on the sum -- is bit-equal to one rank's fused step)
+// world > 1 update -- sum, all-reduce, Adam on the sum x 1 / world -- is bit-equal to one rank's fused
+// step on identical data when world is a power of two)
 __device__ __forceinline__ f4 copy_sum4(const float *__restrict__ gpart, int ns, int64_t gs, int64_t ii, int g) {
     f4 acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
     for (int s0 = g; s0 < ns; s0 += 32) {

@@ -61,7 +61,7 @@ __device__ inline void upd(double x, double y, double &mnx, double &mxx, double 
 // r = 2.5), far above rounding.  So the three vertices around theta plus the two arc ends hold
 // the extreme of the computed values: the same number as the full loop with 5 instead of 31
 // fp64 cos/sin pairs per fillet.
-__device__ double fillet_extreme(double px, double py, double start, double end, double r, int ax, bool mx) {
+__device__ __attribute__((always_inline)) double fillet_extreme(double px, double py, double start, double end, double r, int ax, bool mx) {
     const double total = fabs(start - end);
     const int nseg = (int)(total / c_tab.quantum + 0.5);
     double best = mx ? -INFINITY : INFINITY;
@@ -87,7 +87,7 @@ __device__ double fillet_extreme(double px, double py, double start, double end,
 
 // LineString([p0,p1]).buffer(r, round caps) meets one of the 4 infinite lines x = b[0], x = b[1],
 // y = b[2], y = b[3] (ATT/env:2507, UAM/env:4488-4491)
-__device__ bool capsule_crash(double r, const double *b, double x0, double y0, double x1, double y1) {
+__device__ __attribute__((always_inline)) bool capsule_crash(double r, const double *b, double x0, double y0, double x1, double y1) {
     // every capsule vertex lies within r (1 + 1e-15) of p0 or p1: cheap exact pre-filter
     const double m = r + 1e-6;
     double lx = fmin(x0, x1), hx = fmax(x0, x1), ly = fmin(y0, y1), hy = fmax(y0, y1);
@@ -150,7 +150,7 @@ __device__ bool capsule_crash(double r, const double *b, double x0, double y0, d
 // max_k d.n_k <= R cos(pi/64) (touching counts); ``strict``: interiors overlap, i.e. GEOS
 // ``intersects and not touches`` (max_k d.n_k < R cos(pi/64)).  ATT/env:2266-2269 (goal),
 // UAM/env:3933-3936, UAM/util:41-51, :291-297.
-__device__ bool gons_meet(double dx, double dy, double R, bool strict) {
+__device__ __attribute__((always_inline)) bool gons_meet(double dx, double dy, double R, bool strict) {
     const double thr = R * c_tab.apothem;
     // max_k d.n_k lies in [|d| cos(pi/64), |d|]: outside the band the answer is certain
     const double dist = sqrt(dx * dx + dy * dy);
@@ -165,9 +165,190 @@ __device__ bool gons_meet(double dx, double dy, double R, bool strict) {
     return strict ? m < thr : m <= thr;
 }
 
-// Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p
-__device__ bool ray_poly_entry_full(double cx, double cy, double ex, double ey, double px, double py, double r,
-                                    double &tout) {
+
+// ------------------------------------------------------------------ exact threshold predicates
+// The closed forms in this file use the ideal polygons (exact edge normals / apothem); GEOS decides
+// its predicates exactly (DD orientation) on the ROUNDED float vertices, ~1e-13 m away from the ideal
+// ones.  Within EXACT_BAND of a threshold the ATT / OM predicates hand the decision to the exact
+// separating-axis test below on those vertices (oracle/geos.py BAND: the C oracle restates it with
+// 128-bit integers, the tests with rationals).  Orientation signs are exact: the coordinate
+// differences are exact (Sterbenz) when the coordinates of an axis lie within a factor of 2 of each
+// other -- every coordinate of the ATT / OM world ([455, 680] x [255, 385], the 15-m radar and the
+// step around it) -- so orient = A B - C D with exact A, B, C, D, and its sign is that of the 4-term
+// nonoverlapping expansion fl(AB) + err(AB) - fl(CD) - err(CD) (Shewchuk's Two_Two_Diff).  A
+// difference that is not exact makes the test report "undecidable" and the float closed form stands.
+constexpr double EXACT_BAND = 1e-9;     // metres: projections, orientations
+constexpr double EXACT_BAND_T = 1e-9;   // the ray parameter t
+
+__device__ inline void two_sum(double a, double b, double &x, double &y) {
+    x = a + b;
+    const double bv = x - a, av = x - bv;
+    y = (a - av) + (b - bv);
+}
+__device__ inline void two_diff(double a, double b, double &x, double &y) {
+    x = a - b;
+    const double bv = a - x, av = x + bv;
+    y = (a - av) + (bv - b);
+}
+
+// sign of (bx - ax)(qy - ay) - (by - ay)(qx - ax), exactly; ok = false when a difference rounds
+__device__ __attribute__((always_inline)) int orient_sign(double ax, double ay, double bx, double by, double qx, double qy, bool &ok) {
+    double A, B, C, D, ta, tb, tc, td;
+    two_diff(bx, ax, A, ta);
+    two_diff(qy, ay, B, tb);
+    two_diff(by, ay, C, tc);
+    two_diff(qx, ax, D, td);
+    ok = ta == 0.0 && tb == 0.0 && tc == 0.0 && td == 0.0;
+    const double p1 = A * B, e1 = __builtin_fma(A, B, -p1);
+    const double p2 = C * D, e2 = __builtin_fma(C, D, -p2);
+    // Two_Two_Diff(p1, e1, p2, e2) -> x3 x2 x1 x0 (x3 the most significant)
+    double i0, x0, j, k0, x3, x2, x1, m0;
+    two_diff(e1, e2, i0, x0);       // Two_One_Diff(p1, e1, e2 -> j, k0, x0)
+    two_sum(p1, i0, j, k0);
+    two_diff(k0, p2, m0, x1);       // Two_One_Diff(j, k0, p2 -> x3, x2, x1)
+    two_sum(j, m0, x3, x2);
+    const double top = x3 != 0.0 ? x3 : (x2 != 0.0 ? x2 : (x1 != 0.0 ? x1 : x0));
+    return (top > 0.0) - (top < 0.0);
+}
+
+// orientation sign of q against v -> w: the float value when it is clearly away from 0, else exact
+// (0 when undecidable: ok = false)
+__device__ inline int orient_banded(double vx, double vy, double wx, double wy, double qx, double qy, bool &ok) {
+    const double o = (wx - vx) * (qy - vy) - (wy - vy) * (qx - vx);
+    ok = true;
+    if (o > EXACT_BAND) return 1;
+    if (o < -EXACT_BAND) return -1;
+    return orient_sign(vx, vy, wx, wy, qx, qy, ok);
+}
+
+// GEOS 64-gon(p, r) meets the closed square [x0, x1] x [y0, y1], exactly on the float vertices: the
+// square's axes against the 64-gon's extreme vertices (0: max x, 16: min y, 32: min x, 48: max y;
+// their neighbours are r (1 - cos(pi/32)) = 0.012 m inside), then each 64-gon edge against the
+// square corner nearest to it (the other corners lie >= 10 sin(pi/64) = 0.49 m further out).  Lean on
+// registers: it runs inside the step kernel's agent phase.  1 / 0, -1 undecidable.
+__device__ __attribute__((always_inline)) int gon_square_meet(double px, double py, double r, double x0, double x1, double y0, double y1) {
+    if (px + r * c_tab.circ_c[32] > x1 || px + r * c_tab.circ_c[0] < x0 || py + r * c_tab.circ_s[16] > y1 ||
+        py + r * c_tab.circ_s[48] < y0)
+        return 0;
+    int und = 0;
+#pragma unroll 1
+    for (int i = 0; i < 64; ++i) {
+        const int k = 63 - i;            // edge i -> i + 1 has the outward normal of index 63 - i
+        const double qx = c_tab.nrm_c[k] > 0.0 ? x0 : x1, qy = c_tab.nrm_s[k] > 0.0 ? y0 : y1;
+        const int i1 = (i + 1) & 63;
+        bool ok;
+        const int sg = orient_banded(px + r * c_tab.circ_c[i], py + r * c_tab.circ_s[i], px + r * c_tab.circ_c[i1],
+                                     py + r * c_tab.circ_s[i1], qx, qy, ok);
+        if (!ok) und = 1;
+        else if (sg > 0) return 0;       // the corner, hence the square, strictly outside this edge
+    }
+    return und ? -1 : 1;
+}
+
+// segment c -> e meets the GEOS 64-gon (p, r), exactly on the float vertices: no 64-gon edge has both
+// endpoints strictly outside, and the vertices are not all strictly on one side of the segment's line.
+// 1 / 0, -1 undecidable.
+__device__ __attribute__((always_inline)) int seg_gon_meet(double cx, double cy, double ex, double ey, double px, double py, double r) {
+    int und = 0;
+#pragma unroll 1
+    for (int i = 0; i < 64; ++i) {
+        const int i1 = (i + 1) & 63;
+        const double vx = px + r * c_tab.circ_c[i], vy = py + r * c_tab.circ_s[i];
+        const double wx = px + r * c_tab.circ_c[i1], wy = py + r * c_tab.circ_s[i1];
+        bool ok;
+        int sg = orient_banded(vx, vy, wx, wy, cx, cy, ok);
+        if (!ok) { und = 1; continue; }
+        if (sg <= 0) continue;
+        sg = orient_banded(vx, vy, wx, wy, ex, ey, ok);
+        if (!ok) und = 1;
+        else if (sg > 0) return 0;
+    }
+    int pos = 0, neg = 0;
+#pragma unroll 1
+    for (int i = 0; i < 64; ++i) {
+        bool ok;
+        const int sg = orient_banded(cx, cy, ex, ey, px + r * c_tab.circ_c[i], py + r * c_tab.circ_s[i], ok);
+        if (!ok) und = 1;
+        pos |= sg > 0 ? 1 : 2;           // bit 1: a vertex not strictly on the left
+        neg |= sg < 0 ? 1 : 2;
+    }
+    if (!und && (pos == 1 || neg == 1)) return 0;     // every vertex strictly on one side
+    return und ? -1 : 1;
+}
+
+// segment c -> e meets the closed square, exactly: bounding boxes overlap, and the corners are not all
+// strictly on one side of the segment's line.  1 / 0, -1 undecidable.
+__device__ __attribute__((always_inline)) int seg_square_meet(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1) {
+    if (fmax(cx, ex) < x0 || fmin(cx, ex) > x1 || fmax(cy, ey) < y0 || fmin(cy, ey) > y1) return 0;
+    int pos = 0, neg = 0, und = 0;
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        bool ok;
+        const int sg = orient_banded(cx, cy, ex, ey, i < 2 ? x0 : x1, (i == 1 || i == 2) ? y1 : y0, ok);
+        if (!ok) und = 1;
+        pos |= sg > 0 ? 1 : 2;
+        neg |= sg < 0 ? 1 : 2;
+    }
+    if (!und && (pos == 1 || neg == 1)) return 0;
+    return und ? -1 : 1;
+}
+
+// 64-gon(p, pb) meets 64-gon(g, 1) (ATT/env:2266-2269): gons_meet's closed form, and within EXACT_BAND
+// of the threshold the exact test on the float vertices.  Both rings have their edge normals at the
+// angles (k + 1/2) pi/32, so the axis n_k separates them (ideally) iff d.n_k > (pb + 1) cos(pi/64): only
+// the normals within 1e-6 of the maximum projection m (at most two adjacent ones) can separate the
+// float polygons, by the A edge with outward normal n_k (vertices 63 - k, 64 - k) or the B edge facing
+// it; the exact test checks each against the two vertices of the other's facing edge (the other
+// vertices lie >= 1 (cos(pi/64) - cos(3 pi/64)) = 0.0096 m further out)
+__device__ __attribute__((always_inline)) bool goal_meet_exact(double px, double py, double gx, double gy, double pb) {
+    const double dx = gx - px, dy = gy - py, R = pb + 1.0;
+    const double thr = R * c_tab.apothem;
+    const double dist = sqrt(dx * dx + dy * dy);
+    if (dist > R * (1.0 + 1e-12) + 1e-12) return false;
+    if (dist < thr * (1.0 - 1e-12) - 1e-12) return true;
+    double m = -INFINITY;
+    int km = 0;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) {
+        double v = dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k];
+        km = v > m ? k : km;
+        m = v > m ? v : m;
+    }
+    if (m > thr + EXACT_BAND) return false;
+    if (m < thr - EXACT_BAND) return true;
+#pragma unroll 1
+    for (int c = -1; c <= 1; ++c) {
+        const int k = (km + c) & 63;
+        if (c != 0 && dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k] < m - 1e-6) continue;
+        const int ia = 63 - k, ib = 63 - ((k + 32) & 63);
+        int sep = 3;                          // bit 0: A's edge separates, bit 1: B's facing edge
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {         // one orientation at a time (registers: agent phase)
+            const bool ea = j < 2;            // j 0, 1: A's edge vs B's vertices; 2, 3: B's edge vs A's
+            const double ox = ea ? px : gx, oy = ea ? py : gy, orr = ea ? pb : 1.0;
+            const double qx0 = ea ? gx : px, qy0 = ea ? gy : py, qr = ea ? 1.0 : pb;
+            const int ie = ea ? ia : ib, iq = ((ea ? ib : ia) + (j & 1)) & 63;
+            bool ok;
+            const int sg = orient_banded(ox + orr * c_tab.circ_c[ie], oy + orr * c_tab.circ_s[ie],
+                                         ox + orr * c_tab.circ_c[(ie + 1) & 63], oy + orr * c_tab.circ_s[(ie + 1) & 63],
+                                         qx0 + qr * c_tab.circ_c[iq], qy0 + qr * c_tab.circ_s[iq], ok);
+            if (!ok) return m <= thr;         // undecidable: the closed form
+            if (sg <= 0) sep &= ea ? ~1 : ~2;
+        }
+        if (sep) return false;
+    }
+    return true;
+}
+
+// Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p.  EX (the ATT / OM
+// radar's threshold band; 0: the float clip as it stands): an interval [tlo, thi] within EXACT_BAND_T
+// of empty -- a ray touching the polygon, or ending or starting on its boundary -- is a band case.
+// EX = 1 flags it (band = true) and returns the float clip's answer; EX = 2 decides it by the exact
+// segment / polygon test, a touching ray entering at clamp(tlo, 0, 1).  The radar phase runs the
+// flagged rays again with EX = 2 after its main loop, where few registers are live.
+template <int EX = 0>
+__device__ __attribute__((always_inline)) bool ray_poly_entry_full(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                    double &tout, bool &band) {
     double ddx = ex - cx, ddy = ey - cy;
     double tlo = 0.0, thi = 1.0;
     double vx = px + r * c_tab.circ_c[0], vy = py + r * c_tab.circ_s[0];
@@ -186,9 +367,22 @@ __device__ bool ray_poly_entry_full(double cx, double cy, double ex, double ey, 
             double t = -a / b;
             thi = t < thi ? t : thi;
         }
-        if (tlo > thi) return false;
+        if (EX == 0 ? tlo > thi : tlo - thi > EXACT_BAND_T) return false;   // (empty beyond the band: certain)
         vx = wx;
         vy = wy;
+    }
+    if (EX != 0) {
+        if (tlo - thi > EXACT_BAND_T) return false;
+        if (tlo - thi >= -EXACT_BAND_T) {
+            if (EX == 1) {
+                band = true;
+                if (tlo > thi) return false;
+            } else {
+                const int m = seg_gon_meet(cx, cy, ex, ey, px, py, r);
+                if (m == 0 || (m < 0 && tlo > thi)) return false;
+                tlo = tlo < 0.0 ? 0.0 : (tlo > 1.0 ? 1.0 : tlo);
+            }
+        }
     }
     tout = tlo;
     return true;
@@ -201,8 +395,9 @@ __device__ bool ray_poly_entry_full(double cx, double cy, double ex, double ey, 
 // circumscribed circle, so the maximum over the six edges around it is the same number (same
 // vertices, same arithmetic) as over all 64.  The exit lies beyond the entry, so the segment
 // meets the polygon iff that maximum is <= 1.  Anything else takes the full clip.
-__device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
-                               double &tout) {
+template <int EX = 0>
+__device__ __attribute__((always_inline)) bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
+                               double &tout, bool &band) {
     const double ddx = ex - cx, ddy = ey - cy;
     const double L2 = ddx * ddx + ddy * ddy;
     const double wx = px - cx, wy = py - cy;
@@ -218,7 +413,7 @@ __device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, doubl
         return true;
     }
     if (!(h < ap * (1.0 - 1e-9)) || !(w2 > r * r * (1.0 + 1e-9)) || !(s0 > 0.0))
-        return ray_poly_entry_full(cx, cy, ex, ey, px, py, r, tout);
+        return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band);
     const double tc = (s0 - sqrt(r * r - h * h)) / L;              // circumscribed-circle entry
     const float phi = atan2f((float)(cy + tc * ddy - py), (float)(cx + tc * ddx - px));
     // vertex angles are -i 2pi/64: nearest vertex index
@@ -239,14 +434,21 @@ __device__ bool ray_poly_entry(double cx, double cy, double ex, double ey, doubl
             any = true;
         }
     }
-    if (!any) return ray_poly_entry_full(cx, cy, ex, ey, px, py, r, tout);
+    if (!any) return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band);
+    // the segment ends on the boundary (within the band): the full clip and its band test decide
+    if (EX != 0 && fabs(tlo - 1.0) <= EXACT_BAND_T) return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band);
     if (tlo > 1.0) return false;
     tout = tlo;
     return true;
 }
 
-__device__ bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1,
-                           double &dout) {
+// EX (ATT / OM; see ray_poly_entry_full): where the rounded slab quotients tie (a ray through a corner)
+// or meet t = 1 (a ray ending on an edge) within EXACT_BAND_T, EX = 1 flags a band case, EX = 2
+// decides: the segment meets the square's boundary iff it meets the closed square and does not lie
+// inside the open one (exact test)
+template <int EX = 0>
+__device__ __attribute__((always_inline)) bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1,
+                           double &dout, bool &band) {
     double ddx = ex - cx, ddy = ey - cy;
     double tx0, tx1, ty0, ty1;
     // a ray running along an edge from a start point on that edge: the intersection with the
@@ -274,6 +476,20 @@ __device__ bool ray_square(double cx, double cy, double ex, double ey, double x0
     }
     double tin = tx0 > ty0 ? tx0 : ty0;
     double tout = tx1 < ty1 ? tx1 : ty1;
+    if (EX == 1 && (fabs(tin - tout) <= EXACT_BAND_T || fabs(tin - 1.0) <= EXACT_BAND_T ||
+                    fabs(tout - 1.0) <= EXACT_BAND_T))
+        band = true;
+    if (EX == 2 && (fabs(tin - tout) <= EXACT_BAND_T || fabs(tin - 1.0) <= EXACT_BAND_T ||
+                    fabs(tout - 1.0) <= EXACT_BAND_T)) {
+        const bool inside = x0 < cx && cx < x1 && y0 < cy && cy < y1 && x0 < ex && ex < x1 && y0 < ey && ey < y1;
+        int m = inside ? 0 : seg_square_meet(cx, cy, ex, ey, x0, x1, y0, y1);
+        if (m < 0) m = !(tin > tout || tout < 0.0 || tin > 1.0 || (tin < 0.0 && tout > 1.0));
+        if (!m) return false;
+        double t = tin >= 0.0 ? tin : tout;
+        t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+        dout = gdist(cx + t * ddx, cy + t * ddy, cx, cy);
+        return true;
+    }
     if (tin > tout || tout < 0.0 || tin > 1.0) return false;
     double t = tin >= 0.0 ? tin : tout;
     if (t > 1.0) return false;
@@ -281,7 +497,19 @@ __device__ bool ray_square(double cx, double cy, double ex, double ey, double x0
     return true;
 }
 
-__device__ bool ray_vline(double cx, double cy, double ex, double ey, double lx, double &dout) {
+// the float-only forms (UAM radar)
+__device__ inline bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
+                                      double &tout) {
+    bool band = false;
+    return ray_poly_entry<0>(cx, cy, ex, ey, px, py, r, tout, band);
+}
+__device__ inline bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0,
+                                  double y1, double &dout) {
+    bool band = false;
+    return ray_square<0>(cx, cy, ex, ey, x0, x1, y0, y1, dout, band);
+}
+
+__device__ __attribute__((always_inline)) bool ray_vline(double cx, double cy, double ex, double ey, double lx, double &dout) {
     if (cx == lx && ex == lx) { dout = 0.0; return true; }
     if ((cx - lx) * (ex - lx) > 0.0) return false;
     double t = (lx - cx) / (ex - cx);
@@ -289,7 +517,7 @@ __device__ bool ray_vline(double cx, double cy, double ex, double ey, double lx,
     return true;
 }
 
-__device__ bool ray_hline(double cx, double cy, double ex, double ey, double ly, double &dout) {
+__device__ __attribute__((always_inline)) bool ray_hline(double cx, double cy, double ex, double ey, double ly, double &dout) {
     if (cy == ly && ey == ly) { dout = 0.0; return true; }
     if ((cy - ly) * (ey - ly) > 0.0) return false;
     double t = (ly - cy) / (ey - cy);
@@ -297,7 +525,7 @@ __device__ bool ray_hline(double cx, double cy, double ex, double ey, double ly,
     return true;
 }
 
-__device__ void tdcpa(double ox, double oy, double hx, double hy, double ovx, double ovy, double hvx, double hvy,
+__device__ __attribute__((always_inline)) void tdcpa(double ox, double oy, double hx, double hy, double ovx, double ovy, double hvx, double hvy,
                       double pb, double &tcpa, double &dcpa, int &total) {
     double rx = -1 * (ox - hx), ry = -1 * (oy - hy);
     double wx = ovx - hvx, wy = ovy - hvy;
@@ -319,7 +547,7 @@ __device__ void tdcpa(double ox, double oy, double hx, double hy, double ovx, do
     dcpa = d;
 }
 
-__device__ double pairwise_sum(const double *a, int n) {
+__device__ __attribute__((always_inline)) double pairwise_sum(const double *a, int n) {
     if (n < 8) {
         double s = a[0];
         for (int i = 1; i < n; ++i) s += a[i];

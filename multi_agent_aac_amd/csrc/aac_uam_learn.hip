@@ -275,7 +275,7 @@ __global__ void adam64_kernel(double *p, const double *__restrict__ gpart, int n
             for (int u = 0; u < 8; ++u) gi += x[u];
         }
         for (; s < ns; ++s) gi += gpart[(int64_t)s * n + i];
-        gi *= gscale;           // 1 / world after a SUM all-reduce (1 otherwise: exact)
+        gi *= gscale;           // 1 / world after a SUM all-reduce (1 otherwise); the mean exactly for power-of-two worlds
         const double mi = b1 * m[i] + (1.0 - b1) * gi;
         const double vi = b2 * v[i] + (1.0 - b2) * gi * gi;
         const double den = sqrt(vi) / bc2s + eps;

@@ -206,7 +206,11 @@ class BatchedEnv:
 
     def set_od_bank(self, bank, seed=0):
         """Install the device OD bank for auto-reset: a ``world.ODBank`` (one map), or a
-        ``world.MapBanks`` for a map stack (each auto-reset draws the env's map, then its OD)."""
+        ``world.MapBanks`` for a map stack (each auto-reset draws the env's map, then its OD).
+
+        The device bank is re-allocated and the draw seed changes: a graph captured around
+        ``step_tail`` / ``auto_reset`` bakes both, so ``bank_generation`` advances and the graph's
+        owner must re-capture (``trainer.Trainer`` checks it before every whole-step replay)."""
         if isinstance(bank, _world.MapBanks):
             if bank.n_maps != self.occ.shape[0]:
                 raise ValueError(f"{bank.n_maps} banks for {self.occ.shape[0]} maps")
@@ -220,6 +224,7 @@ class BatchedEnv:
                                                             ctypes.c_uint64(seed)), "aac_env_set_od_bank")
         self.bank = bank
         self.bank_seed = int(seed)
+        self.bank_generation = getattr(self, "bank_generation", 0) + 1
 
     def use_episode_buffer(self, episode: torch.Tensor):
         """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E],

@@ -696,6 +696,7 @@ class FusedUpdate:
         self.nradar, self.nnei = z(Bt, N, 18), z(Bt, N, K, 6)
         self.rew, self.done = z(Bt, N), z(Bt, N)
         self.y = z(Bt)
+        self.qn = z(Bt)                              # target critic Q' of every TD row (records)
         self.q_c, self.q_a = z(Bt), z(Bt)            # per-iteration Q (stats)
         # activations / gradients
         self.acts_t = ActorInferActs(Bt * N, dev)    # target actor over all batches
@@ -747,7 +748,7 @@ class FusedUpdate:
         _, t_comb = critic_forward_stages(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, self.h_t)
         t_cenc = critic_enc_ride(Ct, ptr(self.Xt), Bt, N, Din, self.f_t, fold=(ptr(self.acts_t.ha), At, D0))
         t_head = lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),  # noqa: E731
-                                     done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, yout=ptr(self.y))
+                                     done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, q=ptr(self.qn), yout=ptr(self.y))
         self.segs = None
         self.cfwd = self.CFWD and self.DAOB
         zip0 = m.world == 1 and not self.OVERLAP and self.MERGED
@@ -760,7 +761,7 @@ class FusedUpdate:
             self.pre += [AttnEnc(t_attn, a0_attn)] + gemm_launches(t_merge + a0_merge)
             f0, h0, dq0, dh0, _ = self.cbuf[1]
             tjob = head_job(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew), done=ptr(self.done), B=B, N=N,
-                            gamma=m.GAMMA, yout=ptr(self.y),
+                            gamma=m.GAMMA, q=ptr(self.qn), yout=ptr(self.y),
                             chain=(ptr(h0), C.Wq, C.bq, ptr(self.q_c), ptr(dq0), ptr(dh0), B))
             self.pre += [CriticFwd(t_cf, cs0["cfwd"]), lambda: critic_head_job(tjob)]
         elif zip0:
@@ -774,7 +775,7 @@ class FusedUpdate:
             # the TD target of all batches with critic step 0's mse head chained on batch 0's rows
             f0, h0, dq0, dh0, _ = self.cbuf[1]
             tjob = head_job(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew), done=ptr(self.done), B=B, N=N,
-                            gamma=m.GAMMA, yout=ptr(self.y),
+                            gamma=m.GAMMA, q=ptr(self.qn), yout=ptr(self.y),
                             chain=(ptr(h0), C.Wq, C.bq, ptr(self.q_c), ptr(dq0), ptr(dh0), B))
             self.pre += [AttnEnc(ride_only(t_cenc))] + gemm_launches(t_comb) + [lambda: critic_head_job(tjob)]
         elif self.cfwd:
@@ -1203,6 +1204,15 @@ class FusedUpdate:
     def batch_rewards(self, i):
         """The reward rows [B][N] of iteration i's sampled batch."""
         return self.rew[i * self.B:(i + 1) * self.B]
+
+    def pre_reward_target(self, i):
+        """gamma Q' (1 - any done) of iteration i's batch -- the reference's ``tar_Q_before_rew``
+        (ATT/maddpg:357) -- in the TD head's own fp32 operation order, from the Q' it stored."""
+        B = self.B
+        qn = self.qn[i * B:(i + 1) * B]
+        done_any = (self.done[i * B:(i + 1) * B] == 1.0).any(dim=1).to(torch.float32)
+        g = torch.tensor(self.m.GAMMA, dtype=torch.float32, device=qn.device)
+        return (g * qn) * (1.0 - done_any)
 
     def stats(self):
         """[(loss_q, loss_a, q, target)] per iteration, like MADDPG._iteration."""

@@ -160,15 +160,24 @@ class MADDPG:
             q_next = self.critics_target([b["n_own"], b["n_radar"]], na).squeeze(-1)      # (N*B,)
             done_any = (b["done"] == 1).any(dim=1).to(torch.float32)
             rew = b["rew"].reshape(N, B, N).diagonal(dim1=0, dim2=2).transpose(0, 1)      # r[:, i] of batch i
-            return rew.reshape(-1) + self.GAMMA * q_next * (1 - done_any)
+            # ATT/maddpg:357: tar_Q_before_rew = GAMMA * Q' * (1 - done), kept for the records
+            self._last_pre = self.GAMMA * q_next * (1 - done_any)
+            return rew.reshape(-1) + self._last_pre
 
-    def _iteration(self, b, target, agent):
+    def _iteration(self, b, target, agent, freeze_actor=False):
         q = self.critics([b["s_own"], b["s_radar"]], b["act"])
         loss_q = F.mse_loss(q, target.unsqueeze(1))
         self.critic_optimizer.zero_grad()
         loss_q.backward()            # fused layers write the critic's grads into its flat buffer
         self._allreduce(self.fc)
         self.critic_optimizer.step()
+        if freeze_actor:
+            # transfer learning, i_episode <= 10000 (ATT/maddpg:411-416): the actor loss is computed
+            # and returned, but no actor backward and no actor Adam step (moments and count untouched)
+            with torch.no_grad():
+                a_pi = self.actors([b["s_own"], b["s_radar"], b["s_nei"]])
+                loss_a = -self.critics([b["s_own"], b["s_radar"]], a_pi).mean()
+            return loss_q.detach(), loss_a.detach(), q.detach(), target
         a_pi = self.actors([b["s_own"], b["s_radar"], b["s_nei"]])
         loss_a = -self.critics([b["s_own"], b["s_radar"]], a_pi).mean()
         self.actor_optimizer.zero_grad()
@@ -189,12 +198,12 @@ class MADDPG:
             self._fplans[key] = fused.FusedUpdate(self, rep, B)
         return self._fplans[key]
 
-    def _update_core(self, B, idx_list=None, rep=None, soft=True):
+    def _update_core(self, B, idx_list=None, rep=None, soft=True, freeze_actor=False):
         if rep is None:
             rep = self.replay if self.replay is not None else self.memory.dev
         N = self.n_agents
         idx = None if idx_list is None else torch.cat([i.reshape(-1) for i in idx_list])
-        if self.fused:
+        if self.fused and not freeze_actor:     # the frozen-actor phase runs on the autograd path
             rep.check_sample(B)
             fu = self._fused_plan(B, rep)
             fu.run(idx, soft=soft)
@@ -204,7 +213,7 @@ class MADDPG:
         stats = []
         for agent in range(N):
             b = {k: v[agent * B:(agent + 1) * B] for k, v in ball.items()}
-            stats.append(self._iteration(b, target[agent * B:(agent + 1) * B], agent))
+            stats.append(self._iteration(b, target[agent * B:(agent + 1) * B], agent, freeze_actor))
         self._last_rew = ball["rew"].reshape(N, B, N)
         if soft:        # ATT/maddpg:436-438: soft update when i_episode % UPDATE_EVERY == 0
             ops.polyak_flat(self.fc_t.data, self.fc.data, self.tau)
@@ -285,15 +294,17 @@ class MADDPG:
             with trace.range("update.graph"):
                 self._graph.replay()
 
-    def update(self, B=None, use_graph=True, idx_list=None, want_stats=True, replay=None, soft_update=True):
+    def update(self, B=None, use_graph=True, idx_list=None, want_stats=True, replay=None, soft_update=True,
+               freeze_actor=False):
         """One update_myown-equivalent on the device replay (no host synchronisation).  Returns
         [(loss_q, loss_a, q, target)] per iteration (computed on demand: ``want_stats=False``
         launches nothing beyond the update itself).  ``replay`` defaults to the attached batched
         replay, else the reference-API memory.  ``soft_update=False`` (UPDATE_EVERY > 1 between soft
-        updates, ATT/maddpg:436-438) keeps the targets and runs eagerly."""
+        updates, ATT/maddpg:436-438) keeps the targets and runs eagerly.  ``freeze_actor`` (the
+        transfer-learning phase of ATT/maddpg:411-416) runs the critic steps only, eagerly."""
         B = B or self.batch_size
-        if replay is not None or not soft_update:
-            self._last_src = self._update_core(B, idx_list, replay, soft=soft_update)
+        if replay is not None or not soft_update or freeze_actor:
+            self._last_src = self._update_core(B, idx_list, replay, soft=soft_update, freeze_actor=freeze_actor)
             return self.last_stats if want_stats else None
         if idx_list is None and use_graph and (self.world == 1 or self.fused):
             (self.replay if self.replay is not None else self.memory.dev).check_sample(B)
@@ -347,12 +358,15 @@ class MADDPG:
         gradient iteration appends the reference's 8-field record (ATT/maddpg:372-379)."""
         if len(self.memory) <= self.batch_size:
             return None, None, single_eps_critic_cal_record
-        if transfer_learning and i_episode <= 10000:
-            # ATT/maddpg:411-416 freezes the actor for the first 10000 episodes of a transfer run (its
-            # branch then indexes the single optimiser as a list, so the reference fails there)
-            raise NotImplementedError("transfer_learning: the actor-frozen phase is not part of this path")
+        if transfer_learning and i_episode > 10000:
+            # ATT/maddpg:411-416: after episode 10000 a transfer run indexes the one-model actor
+            # optimiser as a list (self.actor_optimizer[agent]), which raises in the reference
+            raise NotImplementedError("transfer_learning past episode 10000: the reference's branch indexes its "
+                                      "single actor optimiser as a list (ATT/maddpg:413-416) and fails")
         soft = i_episode % UPDATE_EVERY == 0
-        stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev, soft_update=soft)
+        # transfer learning up to episode 10000: the actor is frozen (critic steps only)
+        stats = self.update(self.batch_size, use_graph=False, replay=self.memory.dev, soft_update=soft,
+                            freeze_actor=bool(transfer_learning))
         c_loss = [s[0] for s in stats]
         a_loss = [s[1] for s in stats]
         single_eps_critic_cal_record.extend(self.critic_records(stats))
@@ -362,15 +376,19 @@ class MADDPG:
         """The 8-field ``single_eps_critic_cal_record`` entry of each gradient iteration of the last
         update (ATT/maddpg:372-379): [target Q before the reward (B,), the batch rewards (B, N), the
         target Q (B, 1), the critic loss, and the (min, max) of each].  The target before the reward
-        is gamma Q' (1 - done) = y - r[:, i]."""
+        is gamma Q' (1 - done) as the TD head computed it (not re-derived as y - r, which rounds)."""
         stats = self.last_stats if stats is None else stats
         src = self._last_src
         out = []
         for i, (loss_q, _, _, y) in enumerate(stats):
-            rew = src.batch_rewards(i) if isinstance(src, fused.FusedUpdate) else self._last_rew[i]
+            if isinstance(src, fused.FusedUpdate):
+                rew, pre = src.batch_rewards(i), src.pre_reward_target(i)
+            else:
+                B = y.numel()
+                rew, pre = self._last_rew[i], self._last_pre[i * B:(i + 1) * B]
             r = rew.detach().cpu().numpy()
             after = y.detach().cpu().numpy().reshape(-1, 1)
-            before = after[:, 0] - r[:, i]
+            before = pre.detach().cpu().numpy().reshape(-1)
             loss = loss_q.detach().cpu().numpy()
             out.append([before, r, after, loss, (before.min(), before.max()), (r.min(), r.max()),
                         (after.min(), after.max()), (loss.min(), loss.max())])

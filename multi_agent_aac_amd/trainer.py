@@ -60,12 +60,14 @@ class CheckpointMixin:
 
     def load_checkpoint(self, path):
         from . import checkpoint
-        ck = checkpoint.load(path, **self.checkpoint_parts())
-        # whole-step graphs bake the noise seed and the ring position word: re-capture / re-seed them
-        if hasattr(self, "_sg"):
-            self._sg = {}
-        self._pos_dirty = True
-        return ck
+        try:
+            return checkpoint.load(path, **self.checkpoint_parts())
+        finally:
+            # whole-step graphs bake the noise seed and the ring position word: re-capture / re-seed
+            # them whatever the load did (a refused file changes nothing, but re-capturing is cheap)
+            if hasattr(self, "_sg"):
+                self._sg = {}
+            self._pos_dirty = True
 
 
 class Trainer(CheckpointMixin):
@@ -158,7 +160,11 @@ class Trainer(CheckpointMixin):
         """One training step as one graph replay (the same launches as ``step(update=True)``; the
         ring position lives in device words, the host keeps its mirror)."""
         p = 0 if self.cur is self.bufs[0] else 1
+        gen = getattr(self.env, "bank_generation", 0)
+        if self._sg and getattr(self, "_sg_bank_gen", gen) != gen:
+            self._sg = {}             # the env's OD bank / seed changed under the captured graphs
         if not self._sg:
+            self._sg_bank_gen = gen
             if self.gru:
                 self._hoff = (0 if self.h is self.hp[0] else 1) ^ p
             for q in (0, 1):

@@ -215,6 +215,9 @@ class BatchedUAM:
                                     bank.n, ctypes.c_uint64(seed)), "aac_uam_set_bank")
         self.bank = bank
         self.bank_seed = int(seed)
+        # graphs captured around step_tail / auto_reset bake the bank pointers and seed: owners
+        # re-capture when this advances (see env.BatchedEnv.set_od_bank)
+        self.bank_generation = getattr(self, "bank_generation", 0) + 1
 
     def use_episode_buffer(self, episode: torch.Tensor):
         """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E])."""

@@ -394,8 +394,10 @@ class FusedUamUpdate:
     def _adam_launches(self, off, n, gpart, lr):
         """The Adam step of the network at [off, off + n) of the flat buffers.  world == 1: Adam sums
         the KS partial copies itself.  world > 1: sum them, average over the ranks (one collective,
-        between graph segments), Adam on the average -- bit-identical to one rank when every rank
-        holds the same data."""
+        between graph segments), Adam on the average.  The collective SUMs and Adam multiplies by
+        1 / world, which equals the mean exactly only for power-of-two worlds: there the update is
+        bit-identical to one rank when every rank holds the same data; for other world sizes it is
+        within one rounding of the mean per gradient element."""
         from . import fused
         L, st, KS, P = _learn_lib(), self, self.KS, p64
 

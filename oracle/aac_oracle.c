@@ -146,6 +146,59 @@ static int bound_crash(double x0, double y0, double x1, double y1, double r, con
            (mny <= b[2] && b[2] <= mxy) || (mny <= b[3] && b[3] <= mxy);
 }
 
+
+/* ------------------------------------------------ exact predicates (threshold bands)
+ * The closed forms above use the ideal polygons (exact edge normals, apothem); GEOS decides
+ * intersects / intersection exactly (DD orientation) on the ROUNDED float vertices.  Within BAND of
+ * a threshold the exact formulation on those vertices decides (oracle/geos.py BAND, BAND_T; the
+ * kernel does the same with floating-point expansions, csrc/aac_geom.h).  This restatement is
+ * independent of the kernel's: every coordinate is scaled to an integer (x * 2^52 is one for
+ * 1 <= |x| < 1024, which holds for every coordinate of the ATT / OM world) and the separating-axis
+ * projections are evaluated in 128-bit integers. */
+#define BAND 1e-9
+#define BAND_T 1e-9
+
+typedef __int128 i128;
+
+static i128 iscale(double x) {
+    const double a = fabs(x);
+    if (!(x == 0.0 || (a >= 1.0 && a < 1024.0))) abort();      /* outside the exact domain */
+    return (i128)(int64_t)ldexp(x, 52);
+}
+
+/* closed convex polygons P (np points) and Q (nq points) meet (touching counts): no edge of either
+ * (nq == 2: a segment, its one axis) separates them; projections onto the edge normal in i128 */
+static int convex_meet_exact(const double *px, const double *py, int np, const double *qx, const double *qy, int nq) {
+    i128 PX[64], PY[64], QX[64], QY[64];
+    for (int i = 0; i < np; ++i) { PX[i] = iscale(px[i]); PY[i] = iscale(py[i]); }
+    for (int i = 0; i < nq; ++i) { QX[i] = iscale(qx[i]); QY[i] = iscale(qy[i]); }
+    for (int side = 0; side < 2; ++side) {
+        const i128 *EX = side ? QX : PX, *EY = side ? QY : PY;
+        const int ne = side ? nq : np;
+        for (int k = 0; k < ne; ++k) {
+            const i128 vx = EX[k], vy = EY[k], wx = EX[(k + 1) % ne], wy = EY[(k + 1) % ne];
+            const i128 nx = wy - vy, ny = -(wx - vx);
+            i128 amin = 0, amax = 0, bmin = 0, bmax = 0;
+            for (int i = 0; i < np; ++i) {
+                const i128 v = nx * (PX[i] - vx) + ny * (PY[i] - vy);
+                if (i == 0 || v < amin) amin = v;
+                if (i == 0 || v > amax) amax = v;
+            }
+            for (int i = 0; i < nq; ++i) {
+                const i128 v = nx * (QX[i] - vx) + ny * (QY[i] - vy);
+                if (i == 0 || v < bmin) bmin = v;
+                if (i == 0 || v > bmax) bmax = v;
+            }
+            if (amax < bmin || bmax < amin) return 0;
+        }
+    }
+    return 1;
+}
+
+static void gon(double px, double py, double r, double *x, double *y) {
+    for (int i = 0; i < 64; ++i) { x[i] = px + r * circ_c[i]; y[i] = py + r * circ_s[i]; }
+}
+
 static int goal_reached(double px, double py, double gx, double gy, double pb) {
     double dx = gx - px, dy = gy - py;
     double thr = (pb + 1.0) * apothem;
@@ -154,21 +207,37 @@ static int goal_reached(double px, double py, double gx, double gy, double pb) {
         double v = dx * nrm_c[k] + dy * nrm_s[k];
         if (v > m) m = v;
     }
-    return m <= thr;
+    if (m > thr + BAND) return 0;
+    if (m < thr - BAND) return 1;
+    double ax[64], ay[64], bx[64], by[64];
+    gon(px, py, pb, ax, ay);
+    gon(gx, gy, 1.0, bx, by);
+    return convex_meet_exact(ax, ay, 64, bx, by, 64);
 }
 
 static int building_hit(double px, double py, double cx, double cy, double pb) {
     double dx = cx - px, dy = cy - py;
-    if (fabs(dx) > 5.0 + pb || fabs(dy) > 5.0 + pb) return 0;
+    int unsure = 0;
+    const double v2[2] = {fabs(dx), fabs(dy)};
+    for (int q = 0; q < 2; ++q) {
+        if (v2[q] > 5.0 + pb + BAND) return 0;
+        if (v2[q] > 5.0 + pb - BAND) unsure = 1;
+    }
     for (int k = 0; k < 32; ++k) {
         double proj = fabs(dx * nrm_c[k] + dy * nrm_s[k]);
         double lim = 5.0 * (fabs(nrm_c[k]) + fabs(nrm_s[k])) + pb * apothem;
-        if (proj > lim) return 0;
+        if (proj > lim + BAND) return 0;
+        if (proj > lim - BAND) unsure = 1;
     }
-    return 1;
+    if (!unsure) return 1;
+    double ax[64], ay[64];
+    gon(px, py, pb, ax, ay);
+    const double sx[4] = {cx - 5.0, cx - 5.0, cx + 5.0, cx + 5.0}, sy[4] = {cy - 5.0, cy + 5.0, cy + 5.0, cy - 5.0};
+    return convex_meet_exact(ax, ay, 64, sx, sy, 4);
 }
 
-/* Cyrus-Beck entry of segment c->e into the clockwise 64-gon of circumradius r at (px,py) */
+/* Cyrus-Beck entry of segment c->e into the clockwise 64-gon of circumradius r at (px,py); an
+ * interval [tlo, thi] within BAND_T of empty (touching) is decided by the exact test */
 static int ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r, double *tout) {
     double ddx = ex - cx, ddy = ey - cy;
     double tlo = 0.0, thi = 1.0;
@@ -188,7 +257,14 @@ static int ray_poly_entry(double cx, double cy, double ex, double ey, double px,
             double t = -a / b;
             if (t < thi) thi = t;
         }
-        if (tlo > thi) return 0;
+    }
+    if (tlo - thi > BAND_T) return 0;
+    if (tlo - thi >= -BAND_T) {
+        double gx[64], gy[64];
+        const double sx[2] = {cx, ex}, sy[2] = {cy, ey};
+        gon(px, py, r, gx, gy);
+        if (!convex_meet_exact(gx, gy, 64, sx, sy, 2)) return 0;
+        tlo = tlo < 0.0 ? 0.0 : (tlo > 1.0 ? 1.0 : tlo);
     }
     *tout = tlo;
     return 1;
@@ -219,6 +295,17 @@ static int ray_square(double cx, double cy, double ex, double ey, double x0, dou
     }
     double tin = tx0 > ty0 ? tx0 : ty0;
     double tout = tx1 < ty1 ? tx1 : ty1;
+    if (fabs(tin - tout) <= BAND_T || fabs(tin - 1.0) <= BAND_T || fabs(tout - 1.0) <= BAND_T) {
+        /* the rounded slab quotients tie (a ray through a corner) or meet t = 1: the segment meets
+         * the boundary iff it meets the closed square and does not lie inside the open one */
+        const double qx[4] = {x0, x0, x1, x1}, qy[4] = {y0, y1, y1, y0}, sx[2] = {cx, ex}, sy[2] = {cy, ey};
+        const int inside = x0 < cx && cx < x1 && y0 < cy && cy < y1 && x0 < ex && ex < x1 && y0 < ey && ey < y1;
+        if (inside || !convex_meet_exact(qx, qy, 4, sx, sy, 2)) return 0;
+        double t = tin >= 0.0 ? tin : tout;
+        t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+        *dout = gdist(cx + t * ddx, cy + t * ddy, cx, cy);
+        return 1;
+    }
     if (tin > tout || tout < 0.0 || tin > 1.0) return 0;
     double t = tin >= 0.0 ? tin : tout;
     if (t > 1.0) return 0;

@@ -130,11 +130,21 @@ def edge_normal_table():
 APOTHEM_UNIT = math.cos(MATH_PI / 64.0)
 
 
+# Threshold bands.  The closed forms use the ideal polygon (exact edge normals / apothem); GEOS
+# evaluates its predicates exactly (DD orientation) on the rounded float vertices, ~1e-13 away from
+# the ideal ones.  Inside these bands around a threshold the exact formulation on the float
+# vertices decides (exact-threshold states); outside them the closed form cannot
+# differ from it.  BAND is in metres (projections), BAND_T in units of the ray parameter t.
+BAND = 1e-9
+BAND_T = 1e-9
+
+
 def goal_reached(px, py, gx, gy):
     """64-gon(pos, 2.5) intersects 64-gon(goal, 1)   (ATT/env:2266-2269, :2546).
 
     Both shapes share the vertex angles k*pi/32, so their Minkowski difference is the
-    regular 64-gon of circumradius 3.5 and the test is ``max_k d.n_k <= 3.5 cos(pi/64)``.
+    regular 64-gon of circumradius 3.5 and the test is ``max_k d.n_k <= 3.5 cos(pi/64)``;
+    within BAND of the threshold the exact test on the GEOS float vertices decides.
     """
     dx = gx - px
     dy = gy - py
@@ -144,23 +154,37 @@ def goal_reached(px, py, gx, gy):
         v = dx * nx + dy * ny
         if v > m:
             m = v
-    return m <= thr
+    if m > thr + BAND:
+        return False
+    if m < thr - BAND:
+        return True
+    return convex_polys_intersect_exact(circle_vertices(px, py, PB), circle_vertices(gx, gy, 1.0))
 
 
 def building_hit_cell(px, py, cx, cy, half=5.0):
     """64-gon(pos, 2.5) intersects the closed square cell centred (cx, cy)  (ATT/env:2243-2250).
 
-    Separating-axis test on the square axes and the 32 distinct 64-gon edge normals.
+    Separating-axis test on the square axes and the 32 distinct 64-gon edge normals; an axis
+    within BAND of separating hands the decision to the exact test on the float vertices.
     """
     dx = cx - px
     dy = cy - py
-    if abs(dx) > half + PB or abs(dy) > half + PB:
-        return False
+    unsure = False
+    for v in (abs(dx), abs(dy)):
+        if v > half + PB + BAND:
+            return False
+        if v > half + PB - BAND:
+            unsure = True
     for nx, ny in edge_normal_table()[:32]:
         proj = abs(dx * nx + dy * ny)
         lim = half * (abs(nx) + abs(ny)) + PB * APOTHEM_UNIT
-        if proj > lim:
+        if proj > lim + BAND:
             return False
+        if proj > lim - BAND:
+            unsure = True
+    if unsure:
+        sq = [(cx - half, cy - half), (cx + half, cy - half), (cx + half, cy + half), (cx - half, cy + half)]
+        return convex_polys_intersect_exact(circle_vertices(px, py, PB), sq)
     return True
 
 
@@ -184,7 +208,11 @@ def bound_crash(p0, p1, bound, r=PB):
 
 def ray_polygon_entry(cx, cy, ex, ey, poly):
     """Parameter t in [0,1] of the first point of segment c->e inside the convex
-    clockwise polygon ``poly`` (Cyrus-Beck), or None.  Same operation order as the kernel."""
+    clockwise polygon ``poly`` (Cyrus-Beck), or None.  Same operation order as the kernel.
+
+    When the clip's interval [t_lo, t_hi] is within BAND_T of empty (a ray touching the polygon
+    at a vertex, or ending on / starting on its boundary) the exact segment-polygon test on the
+    float vertices decides; a touching ray then enters at clamp(t_lo, 0, 1)."""
     ddx = ex - cx
     ddy = ey - cy
     t_lo, t_hi = 0.0, 1.0
@@ -207,9 +235,13 @@ def ray_polygon_entry(cx, cy, ex, ey, poly):
             t = -a / b
             if t < t_hi:
                 t_hi = t
-        if t_lo > t_hi:
-            return None
-    return t_lo
+    if t_lo - t_hi > BAND_T:
+        return None
+    if t_lo - t_hi < -BAND_T:
+        return t_lo
+    if segment_convex_entry_exact((cx, cy), (ex, ey), poly) is None:
+        return None
+    return min(max(t_lo, 0.0), 1.0)
 
 
 def point_dist(ax, ay, bx, by):
@@ -221,7 +253,10 @@ def point_dist(ax, ay, bx, by):
 
 def ray_square_crossing(cx, cy, ex, ey, x0, x1, y0, y1):
     """Distance from c to the nearest point of segment(c,e) ∩ boundary(square), or None
-    (OM/env:1117-1126: ``line.intersection(polygon.boundary)`` then ``distance``)."""
+    (OM/env:1117-1126: ``line.intersection(polygon.boundary)`` then ``distance``).
+
+    The slab parameters are rounded quotients: where they tie (a ray through a corner) or meet
+    t = 1 (a ray ending on an edge) within BAND_T, the exact segment / boundary test decides."""
     ddx = ex - cx
     ddy = ey - cy
     # a ray running along an edge from a start point on that edge: line.intersection(boundary) is
@@ -246,6 +281,12 @@ def ray_square_crossing(cx, cy, ex, ey, x0, x1, y0, y1):
         ty0, ty1 = (ta, tb) if ta < tb else (tb, ta)
     t_in = tx0 if tx0 > ty0 else ty0
     t_out = tx1 if tx1 < ty1 else ty1
+    if abs(t_in - t_out) <= BAND_T or abs(t_in - 1.0) <= BAND_T or abs(t_out - 1.0) <= BAND_T:
+        if ray_square_boundary_t_exact((cx, cy), (ex, ey), x0, x1, y0, y1) is None:
+            return None
+        t = t_in if t_in >= 0.0 else t_out
+        t = min(max(t, 0.0), 1.0)
+        return point_dist(cx + t * ddx, cy + t * ddy, cx, cy)
     if t_in > t_out or t_out < 0.0 or t_in > 1.0:
         return None
     t = t_in if t_in >= 0.0 else t_out

@@ -115,12 +115,41 @@ def test_checkpoint_refuses_other_env_bank(native_lib, tmp_path):
     """the auto-reset's OD bank and draw seed are part of the env's checkpoint: a bank
     that differs is refused, a draw seed that differs is restored."""
     a = _trainer("att", seed=1)
+    while len(a.replay) <= a.B:
+        a.step(update=False)
+    a.step(update=True)
     path = str(tmp_path / "att.ckpt")
     a.save_checkpoint(path)
     other = _trainer("att", seed=2)          # other OD bank (seed 2028) and draw seed
+    for _ in range(3):
+        other.step(update=False)
+    before = _snapshot(other)
+    pos, size, seed = other.replay.pos, other.replay.size, other.replay.seed
     with pytest.raises(ValueError, match="bank"):
         other.load_checkpoint(path)
+    # ADVICE r4: a refused file changes nothing -- learner, replay rows / position, env, extra
+    after = _snapshot(other)
+    bad = [k for k in before if not torch.equal(before[k], after[k])]
+    assert not bad, bad
+    assert (other.replay.pos, other.replay.size, other.replay.seed) == (pos, size, seed)
     same = _trainer("att", seed=1)
     same.env.set_od_bank(same.bank, seed=999)
+    gen = same.env.bank_generation
     same.load_checkpoint(path)
     assert same.env.bank_seed == a.env.bank_seed
+    assert same.env.bank_generation == gen + 1      # captured step graphs are re-captured
+
+
+def test_step_graph_recaptures_after_bank_change(native_lib, monkeypatch):
+    """a whole-step graph bakes the OD bank's device pointers and draw seed; re-installing
+    the bank (set_od_bank re-allocates it) must not leave the trainer replaying the old graph."""
+    from multi_agent_aac_amd import trainer
+    monkeypatch.setattr(trainer, "STEP_GRAPH", True)
+    a = _trainer("att", seed=1)
+    while len(a.replay) <= a.B:
+        a.step(update=False)
+    a.step_graph()
+    g0 = a._sg[0][0]
+    a.env.set_od_bank(a.bank, seed=4321)
+    a.step_graph()
+    assert a._sg and a._sg[0][0] is not g0

@@ -253,3 +253,36 @@ def test_actor_pth_roundtrip(native_lib, tmp_path):
     m2 = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=5, device=DEV, seed=3)
     m2.load_model([str(tmp_path / "episode_7_actor_net.pth")])
     assert torch.equal(m2.fa.data, m.fa.data)
+
+
+def test_transfer_learning_freezes_actor(native_lib):
+    """ATT/maddpg:411-416: with transfer_learning the actor is frozen up to episode 10000 (critic
+    steps only: the actor's parameters, Adam moments and step count stay; its target still moves
+    by the soft update), and the reference's branch fails past it (NotImplementedError here).  The
+    critic trajectory is the normal update's (the critic steps never read the online actor)."""
+    from multi_agent_aac_amd.maddpg import MADDPG
+    N, B = 3, 32
+    ms = []
+    for _ in range(2):
+        m = MADDPG([14, 18, 6], [14, 18, 6], 2, n_agents=N, device=DEV, seed=4, batch_size=B, memory_length=256)
+        tr = learner_ref.random_transitions(64, N, 1)
+        for e in range(64):
+            st = [tr["s_own"][e].numpy(), tr["s_radar"][e].numpy(), [list(x.numpy()) for x in tr["s_nei"][e]]]
+            nx = [tr["n_own"][e].numpy(), tr["n_radar"][e].numpy(), [list(x.numpy()) for x in tr["n_nei"][e]]]
+            m.memory.push(st, tr["act"][e].numpy(), nx, tr["rew"][e].numpy(), tr["done"][e].numpy())
+        ms.append(m)
+    frozen, normal = ms
+    fa0 = frozen.fa.data.clone()
+    mom0 = [t.clone() for t in frozen.actor_optimizer.state()]
+    fat0 = frozen.fa_t.data.clone()
+    c, a, rec = frozen.update_myown(5, 5, 1, [], transfer_learning=True)
+    normal.update_myown(5, 5, 1, [], transfer_learning=False)
+    torch.cuda.synchronize()
+    assert len(c) == N and len(a) == N and len(rec) == N and all(torch.isfinite(x) for x in a)
+    assert torch.equal(frozen.fa.data, fa0)
+    assert all(torch.equal(x, y) for x, y in zip(frozen.actor_optimizer.state(), mom0))
+    assert not torch.equal(frozen.fa_t.data, fat0)                  # the soft update still runs
+    np.testing.assert_allclose(frozen.fc.data.cpu(), normal.fc.data.cpu(), atol=1e-4, rtol=1e-5)
+    assert not torch.equal(normal.fa.data, fa0)
+    with pytest.raises(NotImplementedError):
+        frozen.update_myown(10001, 10001, 1, [], transfer_learning=True)

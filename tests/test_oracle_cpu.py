@@ -463,3 +463,50 @@ def test_numpy_env_matches_c_oracle(occ, mode):
             co.reset(s2, w2, c2, env_mask=d.astype(np.uint8))
             ne.reset(s2, w2, c2, env_mask=d)
     assert seen & 0b11 == 0b11
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_threshold_states_oracles(mode):
+    """SURVEY 8(c) exact-threshold states (tests/thresholds.py): the C oracle's integer outputs and
+    radar against the reference's semantics at each threshold (float norms where the reference compares
+    float distances, exact rationals on the GEOS float vertices where it asks GEOS), and the scalar
+    restatement (oracle/env_ref.py) against the C oracle bit for bit.  Both outcomes of every boolean
+    threshold occur (the 1-ulp neighbours)."""
+    from oracle import env_ref
+    from tests import thresholds as T
+    N = 3
+    fam, var, st, occ = T.build(N)
+    E = len(fam)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode)
+    T.oracle_state(co, st)
+    act = np.zeros((E, N, 2), np.float32)
+    co.step(act)
+    post = {"pos": co.pos.copy(), "pre_pos": co.pre_pos.copy(), "goal": co.goal.copy(), "wp": co.wp.copy()}
+    assert np.array_equal(post["pos"][:, 0], st["pos"][:, 0] + st["vel"][:, 0] * 0.5)
+    seen = T.check(fam, var, post, occ, mode, co.mask, co.radar, where=f"c-oracle mode{mode}")
+    for f, outs in seen.items():
+        if f not in ("kat", "start_on", "edge_run") and f not in T.RADAR_FAMILIES:
+            assert outs == {True, False}, (f, outs)
+    kat = [e for e, f in enumerate(fam) if f == "kat"]        # ATT/geometry_test.py:13-15: cur_pos reaches,
+    assert [bool(co.mask[e, 0] & 4) for e in kat] == [True, False]   # pre_pos (1.885 vs 5.9 m) does not
+    # the states are discriminating: the ideal-polygon closed forms alone (no threshold band) would get
+    # some of them wrong -- the goal 64-gons, the building squares and the tangent radar rays
+    thr = 3.5 * geos.APOTHEM_UNIT
+    wrong = 0
+    for e, f in enumerate(fam):
+        if f in ("goal_apo", "goal_vtx"):
+            d = post["goal"][e, 0] - post["pos"][e, 0]
+            closed = max(d[0] * nx + d[1] * ny for nx, ny in geos.edge_normal_table()) <= thr
+            wrong += closed != bool(co.mask[e, 0] & 4)
+    assert wrong > 0
+    # the scalar restatement, env by env (the families exercising every predicate)
+    for e in range(0, E, 3 if mode else 1):
+        se = env_ref.ScalarEnv(N, occ, radar_mode=mode)
+        se.reset([tuple(x) for x in st["pos"][e]], [[tuple(st["wp"][e, i, k]) for k in range(st["cnt"][e, i])]
+                                                   for i in range(N)])
+        for i, ag in se.all_agents.items():
+            ag.vel = st["vel"][e, i].copy()
+        (o, radar, n), rew, d, cg, bbc, masks, over = se.full_step(act[e])
+        assert np.array_equal(np.asarray(masks, np.uint8), co.mask[e]), (fam[e], e)
+        assert np.array_equal(radar.astype(np.float32), co.radar[e]), (fam[e], e)
+        assert np.array_equal(co.reward[e], np.array([float(x) for x in rew], np.float32)), (fam[e], e)
