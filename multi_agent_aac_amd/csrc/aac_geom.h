@@ -342,7 +342,8 @@ __device__ __attribute__((always_inline)) bool goal_meet_exact(double px, double
 
 // Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p.  EX (the ATT / OM
 // radar's threshold band; 0: the float clip as it stands): an interval [tlo, thi] within EXACT_BAND_T
-// of empty -- a ray touching the polygon, or ending or starting on its boundary -- is a band case.
+// of empty -- a ray touching the polygon, or starting on its boundary -- is a band case (a touch at the
+// segment's end, tlo ~ 1, gives the distance L either way: the float decision stands).
 // EX = 1 flags it (band = true) and returns the float clip's answer; EX = 2 decides it by the exact
 // segment / polygon test, a touching ray entering at clamp(tlo, 0, 1).  The radar phase runs the
 // flagged rays again with EX = 2 after its main loop, where few registers are live.
@@ -373,7 +374,8 @@ __device__ __attribute__((always_inline)) bool ray_poly_entry_full(double cx, do
     }
     if (EX != 0) {
         if (tlo - thi > EXACT_BAND_T) return false;
-        if (tlo - thi >= -EXACT_BAND_T) {
+        // a touch at the segment's end (tlo ~ 1) gives the distance L either way: the float decision
+        if (tlo - thi >= -EXACT_BAND_T && tlo < 1.0 - EXACT_BAND_T) {
             if (EX == 1) {
                 band = true;
                 if (tlo > thi) return false;
@@ -382,6 +384,8 @@ __device__ __attribute__((always_inline)) bool ray_poly_entry_full(double cx, do
                 if (m == 0 || (m < 0 && tlo > thi)) return false;
                 tlo = tlo < 0.0 ? 0.0 : (tlo > 1.0 ? 1.0 : tlo);
             }
+        } else if (tlo > thi) {
+            return false;
         }
     }
     tout = tlo;
@@ -435,17 +439,15 @@ __device__ __attribute__((always_inline)) bool ray_poly_entry(double cx, double 
         }
     }
     if (!any) return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band);
-    // the segment ends on the boundary (within the band): the full clip and its band test decide
-    if (EX != 0 && fabs(tlo - 1.0) <= EXACT_BAND_T) return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band);
     if (tlo > 1.0) return false;
     tout = tlo;
     return true;
 }
 
-// EX (ATT / OM; see ray_poly_entry_full): where the rounded slab quotients tie (a ray through a corner)
-// or meet t = 1 (a ray ending on an edge) within EXACT_BAND_T, EX = 1 flags a band case, EX = 2
-// decides: the segment meets the square's boundary iff it meets the closed square and does not lie
-// inside the open one (exact test)
+// EX (ATT / OM; see ray_poly_entry_full): where the rounded slab quotients tie within EXACT_BAND_T (a ray
+// through a corner) away from the segment's end, EX = 1 flags a band case, EX = 2 decides: the segment
+// meets the square's boundary iff it meets the closed square and does not lie inside the open one
+// (exact test).  Ties and exits at t ~ 1 give the distance L either way (the float decision stands).
 template <int EX = 0>
 __device__ __attribute__((always_inline)) bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1,
                            double &dout, bool &band) {
@@ -476,11 +478,10 @@ __device__ __attribute__((always_inline)) bool ray_square(double cx, double cy, 
     }
     double tin = tx0 > ty0 ? tx0 : ty0;
     double tout = tx1 < ty1 ? tx1 : ty1;
-    if (EX == 1 && (fabs(tin - tout) <= EXACT_BAND_T || fabs(tin - 1.0) <= EXACT_BAND_T ||
-                    fabs(tout - 1.0) <= EXACT_BAND_T))
-        band = true;
-    if (EX == 2 && (fabs(tin - tout) <= EXACT_BAND_T || fabs(tin - 1.0) <= EXACT_BAND_T ||
-                    fabs(tout - 1.0) <= EXACT_BAND_T)) {
+    // a corner tie away from the segment's end (near t = 1 the distance is L either way)
+    const bool tie = fabs(tin - tout) <= EXACT_BAND_T && tin < 1.0 - EXACT_BAND_T;
+    if (EX == 1 && tie) band = true;
+    if (EX == 2 && tie) {
         const bool inside = x0 < cx && cx < x1 && y0 < cy && cy < y1 && x0 < ex && ex < x1 && y0 < ey && ey < y1;
         int m = inside ? 0 : seg_square_meet(cx, cy, ex, ey, x0, x1, y0, y1);
         if (m < 0) m = !(tin > tout || tout < 0.0 || tin > 1.0 || (tin < 0.0 && tout > 1.0));

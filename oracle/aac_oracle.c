@@ -259,12 +259,14 @@ static int ray_poly_entry(double cx, double cy, double ex, double ey, double px,
         }
     }
     if (tlo - thi > BAND_T) return 0;
-    if (tlo - thi >= -BAND_T) {
+    if (tlo - thi >= -BAND_T && tlo < 1.0 - BAND_T) {      /* (a touch at t ~ 1: distance L either way) */
         double gx[64], gy[64];
         const double sx[2] = {cx, ex}, sy[2] = {cy, ey};
         gon(px, py, r, gx, gy);
         if (!convex_meet_exact(gx, gy, 64, sx, sy, 2)) return 0;
         tlo = tlo < 0.0 ? 0.0 : (tlo > 1.0 ? 1.0 : tlo);
+    } else if (tlo > thi) {
+        return 0;
     }
     *tout = tlo;
     return 1;
@@ -295,9 +297,9 @@ static int ray_square(double cx, double cy, double ex, double ey, double x0, dou
     }
     double tin = tx0 > ty0 ? tx0 : ty0;
     double tout = tx1 < ty1 ? tx1 : ty1;
-    if (fabs(tin - tout) <= BAND_T || fabs(tin - 1.0) <= BAND_T || fabs(tout - 1.0) <= BAND_T) {
-        /* the rounded slab quotients tie (a ray through a corner) or meet t = 1: the segment meets
-         * the boundary iff it meets the closed square and does not lie inside the open one */
+    if (fabs(tin - tout) <= BAND_T && tin < 1.0 - BAND_T) {
+        /* the rounded slab quotients tie (a ray through a corner; near t = 1 the distance is L either
+         * way): the segment meets the boundary iff it meets the closed square and not only the open one */
         const double qx[4] = {x0, x0, x1, x1}, qy[4] = {y0, y1, y1, y0}, sx[2] = {cx, ex}, sy[2] = {cy, ey};
         const int inside = x0 < cx && cx < x1 && y0 < cy && cy < y1 && x0 < ex && ex < x1 && y0 < ey && ey < y1;
         if (inside || !convex_meet_exact(qx, qy, 4, sx, sy, 2)) return 0;

@@ -12,11 +12,16 @@ decision away from a tie (tests/test_oracle_cpu.py::test_numpy_env_matches_c_ora
 ``variant="wgru"``: the randomOD_Wgru_radar env of config 4 (oracle/wgru_env_ref.py, WGRU/env:824-2131,
 WGRU/ma_main:653-661) -- obstacle radar, 6-wide own rows, per-agent reward against the next waypoint and
 the reference path, the goal list as removed-waypoint bits in ``wp_cur``.
+
+Threshold bands (oracle/geos.py BAND, BAND_T): the elements whose closed form lies within the band of
+its threshold -- a goal or building separating-axis margin, a radar clip interval, a slab tie -- are
+decided again by the scalar geos functions (their exact fallbacks), as in the C oracle and the kernel.
 """
 import math
 
 import numpy as np
 
+from . import geos
 from .consts import ACC_MAX, BOUND, DT, GRID_LEN, EPISODE_LENGTH, MATH_PI, PB, RADAR_DIST, VMAX
 
 N_RAYS = 18
@@ -107,6 +112,15 @@ class NumpyEnv:
             tlo = np.maximum(np.where(bb < 0, t, 0.0).max(-1), 0.0)
             thi = np.minimum(np.where(bb > 0, t, 1.0).min(-1), 1.0)
             hit = ~((bb == 0) & (a > 0)).any(-1) & (tlo <= thi)
+            for idx in zip(*np.nonzero(~((bb == 0) & (a > 0)).any(-1) & (np.abs(tlo - thi) <= geos.BAND_T)
+                                       & (tlo < 1.0 - geos.BAND_T))):
+                e, i, r, k = idx                           # threshold band: the scalar clip + exact test
+                c = (float(px[e, i, 0]), float(py[e, i, 0]))
+                qq = q[e, i, k]
+                t = geos.ray_polygon_entry(c[0], c[1], float(ex[e, i, r]), float(ey[e, i, r]),
+                                           geos.circle_vertices(float(qq[0]), float(qq[1]), PB))
+                hit[idx] = t is not None
+                tlo[idx] = t if t is not None else tlo[idx]
             ix, iy = px[..., None] + tlo * ddx[..., None], py[..., None] + tlo * ddy[..., None]
             d = np.where(hit, _norm(ix - px[..., None], iy - py[..., None]), np.inf)
             dmin = d.min(-1)
@@ -132,6 +146,12 @@ class NumpyEnv:
             on_edge = ((dx_ == 0) & ((cx == x0) | (cx == x1)) & (cy >= y0) & (cy <= y1)) | \
                       ((dy_ == 0) & ((cy == y0) | (cy == y1)) & (cx >= x0) & (cx <= x1))
             d = np.where(on_edge, 0.0, np.where(ok, _norm((cx + t * dx_) - cx, (cy + t * dy_) - cy), np.inf))
+            band = ~on_edge & (np.abs(tin - tout) <= geos.BAND_T) & (tin < 1.0 - geos.BAND_T)
+            for idx in zip(*np.nonzero(band)):          # threshold band: the scalar slab + exact test
+                e, i, r, k = idx
+                v = geos.ray_square_crossing(float(px[e, i, 0]), float(py[e, i, 0]), float(ex[e, i, r]),
+                                             float(ey[e, i, r]), float(x0[k]), float(x1[k]), float(y0[k]), float(y1[k]))
+                d[idx] = np.inf if v is None else v
             dob = np.minimum(dob, d.min(-1)) if len(C) else dob
             b = self.b
             for lx in (b[0], b[1]):
@@ -219,6 +239,16 @@ class NumpyEnv:
         return ((mnx <= b[0]) & (b[0] <= mxx)) | ((mnx <= b[1]) & (b[1] <= mxx)) | \
                ((mny <= b[2]) & (b[2] <= mxy)) | ((mny <= b[3]) & (b[3] <= mxy))
 
+    def _goal(self, g, dxg, dyg):
+        """goal 64-gon predicate (ATT/env:2266-2269); the threshold band by the scalar exact fallback."""
+        m = (dxg[..., None] * NRM_C + dyg[..., None] * NRM_S).max(-1)
+        thr = (PB + 1.0) * APOTHEM
+        goal = m <= thr
+        for e, a in zip(*np.nonzero(np.abs(m - thr) <= geos.BAND)):
+            goal[e, a] = geos.goal_reached(float(self.pos[e, a, 0]), float(self.pos[e, a, 1]),
+                                           float(g[e, a, 0]), float(g[e, a, 1]))
+        return goal
+
     def _building(self):
         p = self.pos
         ci = np.floor((p[..., 0] - self.gx0) / 10.0 + 0.5).astype(np.int64)
@@ -235,7 +265,14 @@ class NumpyEnv:
                 dx, dy = (self.gx0 + 10.0 * ii) - p[..., 0], (self.gy0 + 10.0 * jj) - p[..., 1]
                 near = (np.abs(dx) <= 5.0 + PB) & (np.abs(dy) <= 5.0 + PB)
                 proj = np.abs(dx[..., None] * NRM_C[:32] + dy[..., None] * NRM_S[:32])
-                hit |= inb & occ & near & (proj <= lim).all(-1)
+                h = inb & occ & near & (proj <= lim).all(-1)
+                lim0 = 5.0 + PB
+                band = inb & occ & ((np.abs(np.abs(dx) - lim0) <= geos.BAND) | (np.abs(np.abs(dy) - lim0) <= geos.BAND)
+                                    | (np.abs(proj - lim) <= geos.BAND).any(-1))
+                for e, a in zip(*np.nonzero(band)):     # threshold band: the scalar test + exact fallback
+                    h[e, a] = geos.building_hit_cell(float(p[e, a, 0]), float(p[e, a, 1]),
+                                                     float(self.gx0 + 10.0 * ii[e, a]), float(self.gy0 + 10.0 * jj[e, a]))
+                hit |= h
         return hit
 
     def step(self, act):
@@ -271,7 +308,7 @@ class NumpyEnv:
         self.wall += building
         g = self.goal
         dxg, dyg = g[..., 0] - p[..., 0], g[..., 1] - p[..., 1]
-        goal = (dxg[..., None] * NRM_C + dyg[..., None] * NRM_S).max(-1) <= (PB + 1.0) * APOTHEM
+        goal = self._goal(g, dxg, dyg)
         w0 = np.take_along_axis(self.wp, self.wp_cur[..., None, None].repeat(2, -1), 2)[:, :, 0]
         wpf = _norm(p[..., 0] - w0[..., 0], p[..., 1] - w0[..., 1]) < 5
         before = _norm(self.pre_pos[..., 0] - g[..., 0], self.pre_pos[..., 1] - g[..., 1])
@@ -314,7 +351,7 @@ class NumpyEnv:
         building = self._building()
         self.wall += building
         g = self.goal
-        goal = ((g[..., 0] - px)[..., None] * NRM_C + (g[..., 1] - py)[..., None] * NRM_S).max(-1) <= (PB + 1.0) * APOTHEM
+        goal = self._goal(g, g[..., 0] - px, g[..., 1] - py)
         # next waypoint (:1815-1832): the first strict running minimum below 5 stops the scan
         k = np.arange(W)
         rm = self.wp_cur

@@ -239,6 +239,8 @@ def ray_polygon_entry(cx, cy, ex, ey, poly):
         return None
     if t_lo - t_hi < -BAND_T:
         return t_lo
+    if t_lo >= 1.0 - BAND_T:          # a touch at the segment's end: the distance is L either way
+        return None if t_lo > t_hi else t_lo
     if segment_convex_entry_exact((cx, cy), (ex, ey), poly) is None:
         return None
     return min(max(t_lo, 0.0), 1.0)
@@ -255,8 +257,9 @@ def ray_square_crossing(cx, cy, ex, ey, x0, x1, y0, y1):
     """Distance from c to the nearest point of segment(c,e) ∩ boundary(square), or None
     (OM/env:1117-1126: ``line.intersection(polygon.boundary)`` then ``distance``).
 
-    The slab parameters are rounded quotients: where they tie (a ray through a corner) or meet
-    t = 1 (a ray ending on an edge) within BAND_T, the exact segment / boundary test decides."""
+    The slab parameters are rounded quotients: where they tie within BAND_T (a ray through a corner)
+    away from the segment's end, the exact segment / boundary test decides (near t = 1 the distance is
+    L hit or not)."""
     ddx = ex - cx
     ddy = ey - cy
     # a ray running along an edge from a start point on that edge: line.intersection(boundary) is
@@ -281,7 +284,7 @@ def ray_square_crossing(cx, cy, ex, ey, x0, x1, y0, y1):
         ty0, ty1 = (ta, tb) if ta < tb else (tb, ta)
     t_in = tx0 if tx0 > ty0 else ty0
     t_out = tx1 if tx1 < ty1 else ty1
-    if abs(t_in - t_out) <= BAND_T or abs(t_in - 1.0) <= BAND_T or abs(t_out - 1.0) <= BAND_T:
+    if abs(t_in - t_out) <= BAND_T and t_in < 1.0 - BAND_T:
         if ray_square_boundary_t_exact((cx, cy), (ex, ey), x0, x1, y0, y1) is None:
             return None
         t = t_in if t_in >= 0.0 else t_out

@@ -510,3 +510,25 @@ def test_threshold_states_oracles(mode):
         assert np.array_equal(np.asarray(masks, np.uint8), co.mask[e]), (fam[e], e)
         assert np.array_equal(radar.astype(np.float32), co.radar[e]), (fam[e], e)
         assert np.array_equal(co.reward[e], np.array([float(x) for x in rew], np.float32)), (fam[e], e)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_threshold_states_numpy_env(mode):
+    """The vectorised NumPy env (oracle/env_np.py, the CPU baseline's mode 2) on the exact-threshold
+    states: its band re-decisions give the C oracle's masks, and radar within 1e-9."""
+    from oracle.env_np import NumpyEnv
+    from tests import thresholds as T
+    N = 3
+    fam, var, st, occ = T.build(N, seed=7)
+    E = len(fam)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode)
+    T.oracle_state(co, st)
+    ne = NumpyEnv(E, N, occ, W=32, radar_mode=mode)
+    ne.pos[:], ne.pre_pos[:], ne.vel[:], ne.pre_vel[:] = st["pos"], st["pre_pos"], st["vel"], st["vel"]
+    ne.goal[:], ne.wp[:], ne.wp_cnt[:], ne.start[:] = st["goal"], st["wp"], st["cnt"], st["pos"]
+    ne.wp_cur[:] = 0
+    act = np.zeros((E, N, 2), np.float32)
+    co.step(act)
+    own, radar, nei, reward, done, mask, env_done, bbc = ne.step(act)
+    assert np.array_equal(np.asarray(mask, np.uint8), co.mask)
+    np.testing.assert_allclose(ne.radar64, co.radar.astype(np.float64), rtol=0, atol=1e-5)
