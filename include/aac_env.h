@@ -159,6 +159,11 @@ int aac_env_set_state(aac_env *env, const double *pos, const double *vel, const 
                       const int32_t *wp_cnt, const uint8_t *reach, const int32_t *wall, const int32_t *step,
                       const int32_t *map_idx, const double *start, void *stream);
 
+/* Exact radar threshold bands: the most radar rays one launch flagged for the exact fix-up (a ray within
+ * ~1e-9 of touching another agent's 64-gon or a cell corner, ATT/env:1089-1164, OM/env:1100-1141) and the
+ * list's capacity (more would keep their float values).  Synchronises the stream. */
+int aac_env_band_max(aac_env *env, int32_t *out, int32_t *cap, void *stream);
+
 /* Host utilities (no GPU). A* restates ATT/jps_straight.py:17-72 on a grid_w x grid_h x-major
  * grid (0 = free); writes up to max_len (x, y) cells, returns the path length or 0 if none. */
 int aac_astar(const uint8_t *grid, int32_t w, int32_t h, int32_t sx, int32_t sy, int32_t ex, int32_t ey,

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("AAC_LIB") or os.path.join(_HERE, "libaac_env.so")
 EXPORTS = (
     "aac_env_create", "aac_env_destroy", "aac_last_error", "aac_env_reset", "aac_env_step", "aac_env_step_tail",
     "aac_env_set_od_bank", "aac_env_set_od_banks", "aac_env_auto_reset", "aac_env_set_reset_compact", "aac_env_use_episode_buffer", "aac_env_get_state", "aac_env_set_state",
-    "aac_astar", "aac_od_bank_build",
+    "aac_env_band_max", "aac_astar", "aac_od_bank_build",
 )
 
 vp = ctypes.c_void_p
@@ -70,11 +70,15 @@ def lib():
     L.aac_env_set_reset_compact.argtypes = [ctypes.c_int32]
     L.aac_env_set_reset_compact.restype = None
     L.aac_env_use_episode_buffer.argtypes = [vp, vp, vp]
+    if hasattr(L, "aac_env_band_max") or not os.environ.get("AAC_LIB"):   # (older A/B builds lack it)
+        L.aac_env_band_max.argtypes = [vp, vp, vp, vp]
     L.aac_env_get_state.argtypes = [vp] + [vp] * 13 + [vp]
     L.aac_env_set_state.argtypes = [vp] + [vp] * 13 + [vp]
     L.aac_astar.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32]
     L.aac_od_bank_build.argtypes = [vp, i32, i32, vp, ctypes.c_double, i32, ctypes.c_uint64, i32, vp, vp, vp]
     for name in EXPORTS:
+        if os.environ.get("AAC_LIB") and not hasattr(L, name):
+            continue          # an A/B experiment build of an earlier revision
         getattr(L, name)
     _lib = L
     return L

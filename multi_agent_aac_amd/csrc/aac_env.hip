@@ -31,6 +31,15 @@
 #include "aac_wave.h"
 
 #define BLOCK 256
+// the exact goal / building threshold tests as real calls (1) or inline (0), per env variant: whichever
+// the variant's step kernel runs faster with (they only execute within 1e-9 of a threshold)
+#ifndef AAC_EXACT_COLD_ATT
+#define AAC_EXACT_COLD_ATT 0
+#endif
+#ifndef AAC_EXACT_COLD_WGRU
+#define AAC_EXACT_COLD_WGRU 1
+#endif
+#define EXACT_COLD(V) ((V) == 0 ? AAC_EXACT_COLD_ATT != 0 : AAC_EXACT_COLD_WGRU != 0)
 #define MAX_MAP_BYTES 8192
 #ifndef AAC_ENV_MIN_WAVES         // minimum waves per SIMD the step kernel is compiled for: 4 keeps
 #define AAC_ENV_MIN_WAVES 4       // 4 workgroups per CU resident (179 -> 128 VGPRs, a few spilled to
@@ -56,6 +65,19 @@ struct Args {
     uint8_t *done, *mask, *env_done, *bbc;
     double *tcpa, *dcpa;
     int32_t *conf_cur, *conf_pre;
+    // radar rays with a threshold-band case (radar_phase): header + the env's N positions per entry,
+    // resolved exactly by band_fix_kernel after the launch
+    struct BandHdr *band_hdr;
+    double2 *band_pos;
+    int32_t *band_cnt;   // [0] entries this launch (zeroed by band_fix_kernel), [1] most ever (overflow check)
+    int band_cap;
+};
+
+// one flagged radar ray: env, agent, ray, kind (0 step: radar output + ring column, 1 reset: radar
+// output), the env's map, the ring row of its transition (-1: none)
+struct BandHdr {
+    int32_t e, i, r, kind, map, pad;
+    int64_t row;
 };
 
 struct ResetArgs {
@@ -117,12 +139,14 @@ __device__ inline bool bound_crash(const Args &A, double x0, double y0, double x
 }
 
 // 64-gon(pos, pB) meets 64-gon(goal, 1) (ATT/env:2266-2269); exact within the threshold band
+template <bool COLD>
 __device__ inline bool goal_reached(double px, double py, double gx, double gy, double pb) {
-    return goal_meet_exact(px, py, gx, gy, pb);
+    return goal_meet_exact<COLD>(px, py, gx, gy, pb);
 }
 
 // 64-gon(pos, pB) meets the closed square cell (ATT/env:2243-2250): separating axes; an axis within
 // EXACT_BAND of separating hands the decision to the exact test on the GEOS float vertices
+template <bool COLD>
 __device__ __attribute__((always_inline)) bool building_hit(double px, double py, double cx, double cy, double pb) {
     double dx = cx - px, dy = cy - py;
     if (fabs(dx) > 5.0 + pb + EXACT_BAND || fabs(dy) > 5.0 + pb + EXACT_BAND) return false;
@@ -145,7 +169,8 @@ __device__ __attribute__((always_inline)) bool building_hit(double px, double py
         unsure |= proj > lim - EXACT_BAND;
     }
     if (!unsure) return true;
-    const int m = gon_square_meet(px, py, pb, cx - 5.0, cx + 5.0, cy - 5.0, cy + 5.0);
+    const int m = COLD ? gon_square_meet_call(px, py, pb, cx - 5.0, cx + 5.0, cy - 5.0, cy + 5.0)
+                       : gon_square_meet(px, py, pb, cx - 5.0, cx + 5.0, cy - 5.0, cy + 5.0);
     if (m >= 0) return m == 1;
     // undecidable: the closed form
     if (fabs(dx) > 5.0 + pb || fabs(dy) > 5.0 + pb) return false;
@@ -165,7 +190,7 @@ __device__ __attribute__((always_inline)) bool building_hit(double px, double py
 // not depend on the order (OM/env:1089-1141 takes the nearest intersection).
 template <int EX>
 __device__ __attribute__((always_inline)) double radar_obstacles(const Args &A, const uint8_t *occ, const unsigned long long *rows, double cx,
-                                  double cy, double ex, double ey, double len, bool &band) {
+                                  double cy, double ex, double ey, double len, bool &band, int mode) {
     double mind = len, d;
     // only cells whose square meets the segment's bounding box can meet the segment (index range
     // by a product with 0.1: it rounds within an ulp of the quotient, and floor / ceil of it still
@@ -185,7 +210,7 @@ __device__ __attribute__((always_inline)) double radar_obstacles(const Args &A, 
     const double reach = 5.0 * (fabs(ddx) + fabs(ddy)) * (1.0 + 1e-9) + 1e-12;
     if (i1 < i0 || j1 < j0) {
         // the box lies off the grid: no cell
-    } else if (EX != 2 && rows && i1 - i0 < 8 && j1 - j0 < 8) {   // (the exact re-run: the lean loop below)
+    } else if (rows && i1 - i0 < 8 && j1 - j0 < 8) {
         // the box's occupied cells from the row masks (one 8-B LDS read per row, all issued
         // up front), the line filter on those only
         const unsigned long long span = (2ull << (j1 - j0)) - 1;
@@ -223,7 +248,7 @@ __device__ __attribute__((always_inline)) double radar_obstacles(const Args &A, 
         // relative margin far above the rounding of d, so the minimum is the one the full loop finds
         if (cand) {
             const double qx = A.gx0 + 10.0 * (i0 + (bmin >> 3)), qy = A.gy0 + 10.0 * (j0 + (bmin & 7));
-            if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band) && d <= mind) mind = d;
+            if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band, mode) && d <= mind) mind = d;
             cand &= ~(1ull << bmin);
         }
         while (cand) {
@@ -232,7 +257,7 @@ __device__ __attribute__((always_inline)) double radar_obstacles(const Args &A, 
             const double qx = A.gx0 + 10.0 * (i0 + (b >> 3)), qy = A.gy0 + 10.0 * (j0 + (b & 7));
             const double lb = (qx - cx) * ddx + (qy - cy) * ddy - reach;
             if (lb > 0.0 && lb * lb > mind * mind * L2 * (1.0 + 1e-8)) continue;
-            if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band) && d <= mind) mind = d;
+            if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band, mode) && d <= mind) mind = d;
         }
     } else {      // a radar longer than the 8 x 8-cell mask covers, or maps taller than 64 cells
         for (int i = i0; i <= i1; ++i)
@@ -242,7 +267,7 @@ __device__ __attribute__((always_inline)) double radar_obstacles(const Args &A, 
                 const double wx = qx - cx, wy = qy - cy;
                 const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
                 if (fabs(cr) > reach || al < -reach || al > L2 + reach) continue;
-                if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band) && d <= mind) mind = d;
+                if (ray_square<EX>(cx, cy, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band, mode) && d <= mind) mind = d;
             }
     }
 #ifdef AAC_DBG_NO_LINES
@@ -359,11 +384,11 @@ __device__ __attribute__((always_inline)) void observe_agent(const Args &A, cons
 }
 
 // one radar ray r of agent i (ATT/env:1089-1164 drones, OM/env:1089-1141 obstacles)
-// EX: 1 flags a ray with a band case (exact threshold, see ray_poly_entry_full) in band and returns the
-// float answer, 2 decides the band cases exactly
+// EX = 1: the threshold bands (ray_poly_entry_full): mode 1 flags a ray with a band case in band and
+// returns the float answer, mode 2 decides its band cases exactly
 template <int EX>
 __device__ __attribute__((always_inline)) double radar_ray(const Args &A, const Lds &S, int i, int r, int base, const uint8_t *occ,
-                            const unsigned long long *rows, bool &band) {
+                            const unsigned long long *rows, bool &band, int mode) {
     const int N = A.N;
     const double pb = A.pb;
     const double2 p = S.pos[base + i];
@@ -371,20 +396,7 @@ __device__ __attribute__((always_inline)) double radar_ray(const Args &A, const 
     const double ex = px + A.radar_len * c_tab.ray_c[r], ey = py + A.radar_len * c_tab.ray_s[r];
     const double len = gdist(ex, ey, px, py);
     double dd = len, dob = len;
-    if (EX == 2 && A.radar_mode != AAC_RADAR_OBSTACLES) {
-        // the exact re-run of a flagged ray (cold, lean on registers): the full clip for every neighbour
-        double shortest = INFINITY;
-#pragma unroll 1
-        for (int j = 0; j < N; ++j) {
-            if (j == i) continue;
-            const double2 q = S.pos[base + j];
-            double t;
-            if (!ray_poly_entry_full<2>(px, py, ex, ey, q.x, q.y, pb, t, band)) continue;
-            const double d = gdist(px + t * (ex - px), py + t * (ey - py), px, py);
-            shortest = d < shortest ? d : shortest;
-        }
-        if (shortest < INFINITY) dd = shortest;
-    } else if (A.radar_mode != AAC_RADAR_OBSTACLES) {
+    if (A.radar_mode != AAC_RADAR_OBSTACLES) {
         // neighbours whose 64-gon can meet the segment (closest point within pb: the GEOS 64-gon
         // lies inside the circle of radius pb (+1e-15)), collected per 64 as a mask, then the
         // exact entry for each candidate (same lane-compaction argument as radar_obstacles)
@@ -408,7 +420,7 @@ __device__ __attribute__((always_inline)) double radar_ray(const Args &A, const 
                 cand &= cand - 1;
                 const double2 q = S.pos[base + j];
                 double t;
-                if (!ray_poly_entry<EX>(px, py, ex, ey, q.x, q.y, pb, t, band)) continue;
+                if (!ray_poly_entry<EX>(px, py, ex, ey, q.x, q.y, pb, t, band, mode)) continue;
                 const double ix = px + t * (ex - px), iy = py + t * (ey - py);
                 const double d = gdist(ix, iy, px, py);
                 shortest = d < shortest ? d : shortest;
@@ -416,7 +428,7 @@ __device__ __attribute__((always_inline)) double radar_ray(const Args &A, const 
         }
         if (shortest < INFINITY) dd = shortest;
     }
-    if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles<EX>(A, occ, rows, px, py, ex, ey, len, band);
+    if (A.radar_mode != AAC_RADAR_DRONES) dob = radar_obstacles<EX>(A, occ, rows, px, py, ex, ey, len, band, mode);
     return A.radar_mode == AAC_RADAR_DRONES ? dd : (A.radar_mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
 }
 
@@ -449,38 +461,46 @@ __device__ inline void radar_out(const Args &A, Lds &S, int e, int i, int r, int
     if (rmin) atomicMin(&S.rmin[la], (unsigned long long)__double_as_longlong(d));
 }
 
-// radar ray w of the phase's enumeration (agent la = w / NRAY of the workgroup's list, ray w % NRAY);
-// returns whether (EX = 1) the ray had a threshold-band case -- its float value is written all the same
-template <int EX>
-__device__ __attribute__((always_inline)) bool radar_item(const Args &A, Lds &S, int e0, int w, const int32_t *emap,
-                                                          bool rmin, const RingOut &ro) {
-    const int la = w / NRAY, r = w - la * NRAY;
-    const int le = la / A.N, i = la - le * A.N;
-    const int e = emap ? emap[le] : e0 + le;
-    const int mi = A.map_idx ? A.map_idx[e] : 0;
-    bool band = false;
-    const double d = radar_ray<EX>(A, S, i, r, le * A.N, s_maps + mi * A.gw * A.gh, map_rows(A, mi), band);
-    radar_out(A, S, e, i, r, la, rmin, ro, d);
-    return EX == 1 && band;
-}
-
-// Exact radar (ray_poly_entry_full): the phase computes every ray with its threshold-band cases -- a ray
-// within ~1e-9 of touching a 64-gon or a cell corner, rare -- only flagged: the env's bit band_bit of
-// S.active (1 is the reset / env_done flag), set by every flagging thread.  The caller runs the flagged
-// envs' rays again with the exact tests (radar_item<2>) later, where few registers are live: inlined into
-// this loop the exact tests spilled the step-tail kernels' registers to scratch.
+// Exact radar (threshold bands, ray_poly_entry_full): the radar code here only flags a ray with a band
+// case -- within ~1e-9 of touching a 64-gon or a cell corner away from the segment's end, rare -- and
+// writes its float value; the ray (with its env's positions) goes to the band list, and
+// band_fix_kernel, launched right after this kernel, re-runs it exactly and rewrites the outputs.
+// Resolved in this kernel, the exact code slowed the step kernels' hot phases by ~10 us (inlined:
+// register allocation and scheduling; as calls from the radar loop: scratch spills).  kind: 0 step
+// (row: the ring row of the env's transition, or -1), 1 reset.
 __device__ __attribute__((always_inline)) void radar_phase(const Args &A, Lds &S, int e0, int nagents,
-                                                               bool check_active, const int32_t *emap = nullptr,
-                                                               bool rmin = false, RingOut ro = RingOut{},
-                                                               uint8_t band_bit = 0) {
+                                                           bool check_active, const int32_t *emap = nullptr,
+                                                           bool rmin = false, RingOut ro = RingOut{}, int kind = 0) {
+    static_assert(NRAY <= 32 && BLOCK == 256, "a thread's work items (nagents <= BLOCK: k < NRAY) index a 32-bit mask");
+    uint32_t flagged = 0;     // this thread's work items w = threadIdx.x + k BLOCK with a band case
     for (int w = threadIdx.x; w < nagents * NRAY; w += BLOCK) {
-        const int la = w / NRAY;
-        const int le = la / A.N;
+        const int la = w / NRAY, r = w - la * NRAY;
+        const int le = la / A.N, i = la - le * A.N;
         const int e = emap ? emap[le] : e0 + le;
         if (e >= A.E) continue;
-        if (check_active && !(S.active[le] & 1)) continue;
-        if (radar_item<1>(A, S, e0, w, emap, rmin, ro) && band_bit)
-            S.active[le] |= band_bit;       // the same value from every flagging thread
+        if (check_active && !S.active[le]) continue;
+        const int mi = A.map_idx ? A.map_idx[e] : 0;
+        bool band = false;
+        const double d = radar_ray<1>(A, S, i, r, le * A.N, s_maps + mi * A.gw * A.gh, map_rows(A, mi), band, 1);
+        radar_out(A, S, e, i, r, la, rmin, ro, d);
+        if (band) flagged |= 1u << (w >> 8);
+    }
+    // the flagged rays (with their env's positions) into the band list, outside the loop's registers
+    while (flagged && A.band_cnt) {
+        const int w = threadIdx.x + __builtin_ctz(flagged) * BLOCK;
+        flagged &= flagged - 1;
+        const int la = w / NRAY, r = w - la * NRAY;
+        const int le = la / A.N, i = la - le * A.N;
+        const int e = emap ? emap[le] : e0 + le;
+        const int slot = atomicAdd(A.band_cnt, 1);
+        if (slot >= A.band_cap) continue;
+        int64_t row = -1;
+        if (ro.ring) {
+            row = ro.pos + e;
+            if (row >= ro.cap) row -= ro.cap;
+        }
+        A.band_hdr[slot] = BandHdr{e, i, r, kind, A.map_idx ? A.map_idx[e] : 0, 0, row};
+        for (int j = 0; j < A.N; ++j) A.band_pos[(size_t)slot * A.N + j] = S.pos[le * A.N + j];
     }
 }
 
@@ -785,14 +805,14 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
     const int t = threadIdx.x;
     const int le = t / N, i = t - le * N;
     const int e = env_of(emap, e0, le < A.epb ? le : 0);
-    const bool active = (t < nag) && (e < A.E) && (S.active[le] & 1);
+    const bool active = (t < nag) && (e < A.E) && S.active[le];
     const int base = le * N;
     const size_t ai = (size_t)e * N + i;
     if (!maps_loaded) load_maps(A);
     if (predrawn) {
         // the draws were made during the step (spec_draw): bank indices in S.idx, starts in
         // spec_starts, episode / map per env after the indices
-        if (t < A.epb && (S.active[t] & 1) && e0 + t < A.E) {
+        if (t < A.epb && S.active[t] && e0 + t < A.E) {
             R.episode[e0 + t] = S.idx[nag + t];
             if (A.map_idx) A.map_idx[e0 + t] = S.idx[nag + A.epb + t];
         }
@@ -804,7 +824,7 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
         const int lane = t & 63, wv = t >> 6;
         for (int lq = wv; lq < A.epb; lq += BLOCK / 64) {
             const int eq = env_of(emap, e0, lq);
-            if (eq >= A.E || !(S.active[lq] & 1)) continue;
+            if (eq >= A.E || !S.active[lq]) continue;
             const int ep = R.episode[eq] + 1;
             const int bq = lq * N;
             // multipleMap variant: random_map_idx = random.randrange(len(world_map_2D_collection)) per
@@ -871,7 +891,7 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
             for (int u = 0; u < 4; ++u) {
                 const int w = w0 + u * BLOCK + t;
                 const int la = w / A.W, k = w - la * A.W, lq = la / N;
-                ok[u] = w < nw && (S.active[lq < A.epb ? lq : 0] & 1) && env_of(emap, e0, lq < A.epb ? lq : 0) < A.E;
+                ok[u] = w < nw && S.active[lq < A.epb ? lq : 0] && env_of(emap, e0, lq < A.epb ? lq : 0) < A.E;
                 const size_t aq = ok[u] ? (size_t)env_of(emap, e0, lq) * N + (la - lq * N) : 0;
                 dst[u] = aq * A.W + k;
                 const int bi = (R.mode == 1 && ok[u]) ? S.idx[la] : 0;
@@ -928,17 +948,7 @@ __device__ __attribute__((always_inline)) void reset_body(const Args &A, const R
     }
     __syncthreads();   // map_idx (explicit or drawn) written above is read by the radar phase below
     RSTAMP(3, __builtin_amdgcn_s_memtime());
-    radar_phase(A, S, e0, nag, true, emap, false, RingOut{}, 4);
-    __syncthreads();   // the band flags (S.active bit 2) of every thread
-    {
-        int band = 0;
-        for (int k = 0; k < A.epb; ++k) band |= S.active[k] & 4;
-        if (band)           // uniform: the flagged envs' rays again, exactly
-            for (int w = t; w < nag * NRAY; w += BLOCK) {
-                const int le = w / NRAY / A.N;
-                if ((S.active[le] & 4) && env_of(emap, e0, le) < A.E) radar_item<2>(A, S, e0, w, emap, false, RingOut{});
-            }
-    }
+    radar_phase(A, S, e0, nag, true, emap, false, RingOut{}, 1);
 #ifdef AAC_ENV_STAMPS
     __syncthreads();
 #endif
@@ -1048,7 +1058,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     ESTAMP(0, __builtin_amdgcn_s_memrealtime());
     ESTAMP(1, __builtin_amdgcn_s_memtime());
     const int nv = e0 + A.epb <= A.E ? A.epb : A.E - e0;     // envs of this workgroup
-    if (t < A.epb) S.active[t] = 0;      // radar band flags (bit 1); TAIL: env_done of the workgroup's envs (set below)
+    if (TAIL && t < A.epb) S.active[t] = 0;      // env_done of the workgroup's envs (set below)
     RingOut ro{};
     // the kinematics' own state, loaded first: in flight across the push's early copy and the map
     // load (the agent phase's state stays in flight across the radar)
@@ -1135,7 +1145,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     aacw::lds_barrier();
     ESTAMP(2, __builtin_amdgcn_s_memtime());
 #ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
-    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro, 2);
+    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro);
 #endif
     if (A.variant) {
         double2 *wc = wp_cache(A);
@@ -1216,7 +1226,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
                 for (int jj = cj - 1; jj <= cj + 1; ++jj) {
                     if (ii < 0 || jj < 0 || ii >= A.gw || jj >= A.gh) continue;
                     if (!occ[ii * A.gh + jj]) continue;
-                    if (building_hit(px, py, A.gx0 + 10.0 * ii, A.gy0 + 10.0 * jj, pb)) {
+                    if (building_hit<EXACT_COLD(VAR)>(px, py, A.gx0 + 10.0 * ii, A.gy0 + 10.0 * jj, pb)) {
                         building = 1;
                         break;
                     }
@@ -1225,7 +1235,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         if (building) A.wall[ai] += 1;
         ASTAMP(3);
         const double2 g = S.goal[t];
-        const int goal = goal_reached(px, py, g.x, g.y, pb);
+        const int goal = goal_reached<EXACT_COLD(VAR)>(px, py, g.x, g.y, pb);
         const int bnd = bound_crash(A, pp.x, pp.y, px, py);
         ASTAMP(4);
         int done = 0, cg = 0, wpf = 0;
@@ -1328,22 +1338,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             A.step[e] = st;
             const uint8_t ed = (uint8_t)((A.episode_length < st) || any_done || all_goal || all_reach);
             A.env_done[e] = ed;
-            if (TAIL) S.active[le] = ed | (S.active[le] & 2);    // keeps the radar band flag
-        }
-    }
-    {   // the radar rays of envs with a threshold-band case (S.active bit 1, set in the radar phase before
-        // the barrier after the agent phase, kept by the env_done write), again with the exact tests
-        int band = 0;
-        for (int k = 0; k < A.epb; ++k) band |= S.active[k] & 2;
-        if (band) {         // uniform
-            for (int w = t; w < nag * NRAY; w += BLOCK) {
-                const int le = w / NRAY / N;
-                if (!(S.active[le] & 2) || e0 + le >= A.E) continue;
-                RingOut rf{};
-                if constexpr (TAIL)
-                    if (T.ring && T.late[LATE_RADAR] >= 0) rf = RingOut{T.ring, rpos, T.cap, T.rw, T.late[LATE_RADAR]};
-                radar_item<2>(A, S, e0, w, nullptr, false, rf);
-            }
+            if (TAIL) S.active[le] = ed;
         }
     }
     if constexpr (TAIL) {
@@ -1352,13 +1347,13 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         // auto-reset, in that order)
         __syncthreads();      // env_done flags; the staged rows' ring copies have read S.obs
         int any = 0;
-        for (int k = 0; k < A.epb; ++k) any |= S.active[k] & 1;
+        for (int k = 0; k < A.epb; ++k) any |= S.active[k];
         if (any) {
             if (T.zero_rows) {
                 const int n = nv * T.zero_w;
                 for (int j = t; j < n; j += BLOCK) {
                     const int r = j / T.zero_w;
-                    if (S.active[r] & 1) T.zero_rows[(size_t)e0 * T.zero_w + j] = 0.f;
+                    if (S.active[r]) T.zero_rows[(size_t)e0 * T.zero_w + j] = 0.f;
                 }
             }
             if (T.reset) reset_body(A, R, S, nullptr, e0, true, spec);
@@ -1416,6 +1411,87 @@ __global__ void __launch_bounds__(1024) env_compact_kernel(const uint8_t *__rest
     aacw::compact_flags(mask, E, rlist);
 }
 
+// ------------------------------------------------------------------------- exact radar fix-up
+// One radar ray decided exactly (the threshold bands resolved: ray_poly_entry_full / ray_square in mode
+// 2, whose exact tests are the calls seg_gon_meet / seg_square_meet) from an env's positions and map
+// in global memory.  No candidate pre-filter: every other agent's 64-gon gets the full clip, every
+// occupied cell of the segment's box the slab test (the same decisions as the filtered radar loop
+// outside the bands).
+__device__ double radar_ray_exact(const double2 *pos, int N, int i, int r, double pb, double rlen, int mode,
+                                  const uint8_t *occ, int gw, int gh, double gx0, double gy0, const double *b) {
+    const double2 p = pos[i];
+    const double px = p.x, py = p.y;
+    const double ex = px + rlen * c_tab.ray_c[r], ey = py + rlen * c_tab.ray_s[r];
+    const double len = gdist(ex, ey, px, py);
+    bool band = false;
+    double dd = len, dob = len;
+    if (mode != AAC_RADAR_OBSTACLES) {
+        double shortest = INFINITY;
+        for (int j = 0; j < N; ++j) {
+            if (j == i) continue;
+            double t;
+            if (!ray_poly_entry_full<1>(px, py, ex, ey, pos[j].x, pos[j].y, pb, t, band, 2)) continue;
+            const double d = gdist(px + t * (ex - px), py + t * (ey - py), px, py);
+            shortest = d < shortest ? d : shortest;
+        }
+        if (shortest < INFINITY) dd = shortest;
+    }
+    if (mode != AAC_RADAR_DRONES) {
+        double d;
+        int i0 = (int)floor((fmin(px, ex) - 5.0 - gx0) * 0.1), i1 = (int)ceil((fmax(px, ex) + 5.0 - gx0) * 0.1);
+        int j0 = (int)floor((fmin(py, ey) - 5.0 - gy0) * 0.1), j1 = (int)ceil((fmax(py, ey) + 5.0 - gy0) * 0.1);
+        i0 = i0 < 0 ? 0 : i0;
+        j0 = j0 < 0 ? 0 : j0;
+        i1 = i1 > gw - 1 ? gw - 1 : i1;
+        j1 = j1 > gh - 1 ? gh - 1 : j1;
+        for (int ii = i0; ii <= i1; ++ii)
+            for (int jj = j0; jj <= j1; ++jj) {
+                if (!occ[ii * gh + jj]) continue;
+                const double qx = gx0 + 10.0 * ii, qy = gy0 + 10.0 * jj;
+                if (ray_square<1>(px, py, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band, 2) && d <= dob) dob = d;
+            }
+        if (ray_vline(px, py, ex, ey, b[0], d) && d < dob) dob = d;
+        if (ray_vline(px, py, ex, ey, b[1], d) && d < dob) dob = d;
+        if (ray_hline(px, py, ex, ey, b[2], d) && d < dob) dob = d;
+        if (ray_hline(px, py, ex, ey, b[3], d) && d < dob) dob = d;
+    }
+    return mode == AAC_RADAR_DRONES ? dd : (mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
+}
+
+struct FixArgs {
+    const BandHdr *hdr;
+    const double2 *pos;
+    int32_t *cnt;
+    int cap, N, mode, gw, gh;
+    double pb, rlen, gx0, gy0, bound[4];
+    const uint8_t *occ;
+    float *radar;
+    const uint8_t *env_done;   // non-null: a step entry of an env that was auto-reset in the launch keeps
+                               // the reset observation's radar (its ring row is still fixed)
+    float *ring;
+    int rw, col;
+};
+
+// The flagged rays of the launch before it (one workgroup; nothing to do in the common case), then the
+// list is emptied for the next launch.
+__global__ void __launch_bounds__(256) band_fix_kernel(FixArgs F) {
+    const int n = *F.cnt;
+    const int m = n < F.cap ? n : F.cap;
+    for (int k = threadIdx.x; k < m; k += 256) {
+        const BandHdr h = F.hdr[k];
+        const double d = radar_ray_exact(F.pos + (size_t)k * F.N, F.N, h.i, h.r, F.pb, F.rlen, F.mode,
+                                         F.occ + (size_t)h.map * F.gw * F.gh, F.gw, F.gh, F.gx0, F.gy0, F.bound);
+        const size_t oi = ((size_t)h.e * F.N + h.i) * NRAY + h.r;
+        if (h.kind == 1 || !(F.env_done && F.env_done[h.e])) F.radar[oi] = (float)d;
+        if (h.kind == 0 && F.ring && h.row >= 0) F.ring[h.row * F.rw + F.col + h.i * NRAY + h.r] = (float)d;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && n) {
+        if (n > F.cnt[1]) F.cnt[1] = n;
+        F.cnt[0] = 0;
+    }
+}
+
 // ------------------------------------------------------------------------------ host side
 thread_local std::string g_err;
 // Auto-reset over the packed list of done envs: -1 (default) per variant -- off for the ATT env, where
@@ -1456,7 +1532,13 @@ struct aac_env {
     int32_t bank_n, bank_maps;
     uint64_t bank_seed;
     int32_t *rlist;           // [1 + E]: packed resetting envs of the last auto-reset
+    BandHdr *band_hdr;        // radar threshold-band list (radar_phase, band_fix_kernel)
+    double2 *band_pos;
+    int32_t *band_cnt;
 };
+
+constexpr int BAND_CAP = 16384;   // flagged rays per launch: never more than a few in practice; the
+                                  // threshold tests flag hundreds.  More are counted (aac_env_band_max)
 
 // dynamic LDS of the step / reset kernels: the handle's occupancy maps and their row masks
 static size_t map_bytes(const aac_env *h) {
@@ -1519,7 +1601,38 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
     A.dcpa = o->dcpa;
     A.conf_cur = o->conf_cur;
     A.conf_pre = o->conf_pre;
+    A.band_hdr = h->band_hdr;
+    A.band_pos = h->band_pos;
+    A.band_cnt = h->band_cnt;
+    A.band_cap = BAND_CAP;
     return A;
+}
+
+// band_fix_kernel after a step / reset launch on the same stream (ring: the step tail's ring and its
+// late radar column, env_done: skip the radar output of envs the launch reset)
+static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, const uint8_t *env_done = nullptr,
+                            float *ring = nullptr, int rw = 0, int col = -1) {
+    FixArgs F;
+    F.hdr = h->band_hdr;
+    F.pos = h->band_pos;
+    F.cnt = h->band_cnt;
+    F.cap = BAND_CAP;
+    F.N = A.N;
+    F.mode = A.radar_mode;
+    F.gw = A.gw;
+    F.gh = A.gh;
+    F.pb = A.pb;
+    F.rlen = A.radar_len;
+    F.gx0 = A.gx0;
+    F.gy0 = A.gy0;
+    for (int k = 0; k < 4; ++k) F.bound[k] = A.bound[k];
+    F.occ = A.occ;
+    F.radar = A.radar;
+    F.env_done = env_done;
+    F.ring = col >= 0 ? ring : nullptr;
+    F.rw = rw;
+    F.col = col;
+    hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, F);
 }
 
 static ResetArgs bank_reset_args(const aac_env *h) {
@@ -1594,6 +1707,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     ALLOC(wp, EN * h->W) ALLOC(wp0, EN) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
     ALLOC(rlist, (size_t)c.E + 1)
+    ALLOC(band_hdr, (size_t)BAND_CAP) ALLOC(band_pos, (size_t)BAND_CAP * c.N) ALLOC(band_cnt, 2)
     h->episode_own = h->episode;
     ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
 #undef ALLOC
@@ -1624,7 +1738,7 @@ void aac_env_destroy(aac_env *h) {
     if (!h) return;
     void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->start, h->wp, h->wp0, h->wp_cur, h->wp_cnt, h->wall,
                     h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt,
-                    h->bank_off, h->rlist, h->occ_rows};
+                    h->bank_off, h->rlist, h->occ_rows, h->band_hdr, h->band_pos, h->band_cnt};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -1659,6 +1773,8 @@ static int launch_step(aac_env *h, const float *actions, const aac_step_out *o, 
     else if (A.radar_mode == AAC_RADAR_OBSTACLES) STEP_LAUNCH(0, AAC_RADAR_OBSTACLES);
     else STEP_LAUNCH(0, AAC_RADAR_COMBINED);
 #undef STEP_LAUNCH
+    if (tail) launch_band_fix(h, A, st, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR]);
+    else launch_band_fix(h, A, st);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
@@ -1779,6 +1895,7 @@ int aac_env_reset(aac_env *h, const uint8_t *mask, const double *start, const do
     R.map_idx = map_idx;
     R.episode = h->episode;
     hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), map_bytes(h), (hipStream_t)stream, A, R);
+    launch_band_fix(h, A, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
@@ -1837,6 +1954,7 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
         R.list = h->rlist;
     }
     hipLaunchKernelGGL(reset_kernel, dim3(h->blocks), dim3(BLOCK), map_bytes(h), (hipStream_t)stream, A, R);
+    launch_band_fix(h, A, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
@@ -1865,6 +1983,14 @@ int aac_env_reset_stamps(unsigned long long *out, int32_t n_wg) {
     (void)n_wg;
     return fail(AAC_E_STATE, "built without AAC_ENV_STAMPS");
 #endif
+}
+
+int aac_env_band_max(aac_env *h, int32_t *out, int32_t *cap, void *stream) {
+    if (!h || !out) return fail(AAC_E_INVALID, "null argument");
+    HIPCHK(hipMemcpyAsync(out, h->band_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    if (cap) *cap = BAND_CAP;
+    return AAC_OK;
 }
 
 int aac_env_use_episode_buffer(aac_env *h, int32_t *episode_dev, void *stream) {

@@ -61,7 +61,8 @@ __device__ inline void upd(double x, double y, double &mnx, double &mxx, double 
 // r = 2.5), far above rounding.  So the three vertices around theta plus the two arc ends hold
 // the extreme of the computed values: the same number as the full loop with 5 instead of 31
 // fp64 cos/sin pairs per fillet.
-__device__ __attribute__((always_inline)) double fillet_extreme(double px, double py, double start, double end, double r, int ax, bool mx) {
+// (out of line: only the capsule's uncertain band reaches it)
+__device__ __attribute__((noinline)) double fillet_extreme(double px, double py, double start, double end, double r, int ax, bool mx) {
     const double total = fabs(start - end);
     const int nseg = (int)(total / c_tab.quantum + 0.5);
     double best = mx ? -INFINITY : INFINITY;
@@ -224,8 +225,8 @@ __device__ inline int orient_banded(double vx, double vy, double wx, double wy, 
 // GEOS 64-gon(p, r) meets the closed square [x0, x1] x [y0, y1], exactly on the float vertices: the
 // square's axes against the 64-gon's extreme vertices (0: max x, 16: min y, 32: min x, 48: max y;
 // their neighbours are r (1 - cos(pi/32)) = 0.012 m inside), then each 64-gon edge against the
-// square corner nearest to it (the other corners lie >= 10 sin(pi/64) = 0.49 m further out).  Lean on
-// registers: it runs inside the step kernel's agent phase.  1 / 0, -1 undecidable.
+// square corner nearest to it (the other corners lie >= 10 sin(pi/64) = 0.49 m further out).  A real call
+// (rare; inlined into the agent phase it slowed the WGRU step by ~12 us).  1 / 0, -1 undecidable.
 __device__ __attribute__((always_inline)) int gon_square_meet(double px, double py, double r, double x0, double x1, double y0, double y1) {
     if (px + r * c_tab.circ_c[32] > x1 || px + r * c_tab.circ_c[0] < x0 || py + r * c_tab.circ_s[16] > y1 ||
         py + r * c_tab.circ_s[48] < y0)
@@ -245,10 +246,16 @@ __device__ __attribute__((always_inline)) int gon_square_meet(double px, double 
     return und ? -1 : 1;
 }
 
+// the same as a real call: rare, and the WGRU step kernel runs faster with it out of line
+__device__ __attribute__((noinline)) int gon_square_meet_call(double px, double py, double r, double x0, double x1,
+                                                             double y0, double y1) {
+    return gon_square_meet(px, py, r, x0, x1, y0, y1);
+}
+
 // segment c -> e meets the GEOS 64-gon (p, r), exactly on the float vertices: no 64-gon edge has both
 // endpoints strictly outside, and the vertices are not all strictly on one side of the segment's line.
 // 1 / 0, -1 undecidable.
-__device__ __attribute__((always_inline)) int seg_gon_meet(double cx, double cy, double ex, double ey, double px, double py, double r) {
+__device__ __attribute__((noinline)) int seg_gon_meet(double cx, double cy, double ex, double ey, double px, double py, double r) {
     int und = 0;
 #pragma unroll 1
     for (int i = 0; i < 64; ++i) {
@@ -278,7 +285,7 @@ __device__ __attribute__((always_inline)) int seg_gon_meet(double cx, double cy,
 
 // segment c -> e meets the closed square, exactly: bounding boxes overlap, and the corners are not all
 // strictly on one side of the segment's line.  1 / 0, -1 undecidable.
-__device__ __attribute__((always_inline)) int seg_square_meet(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1) {
+__device__ __attribute__((noinline)) int seg_square_meet(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1) {
     if (fmax(cx, ex) < x0 || fmin(cx, ex) > x1 || fmax(cy, ey) < y0 || fmin(cy, ey) > y1) return 0;
     int pos = 0, neg = 0, und = 0;
 #pragma unroll 1
@@ -293,29 +300,9 @@ __device__ __attribute__((always_inline)) int seg_square_meet(double cx, double 
     return und ? -1 : 1;
 }
 
-// 64-gon(p, pb) meets 64-gon(g, 1) (ATT/env:2266-2269): gons_meet's closed form, and within EXACT_BAND
-// of the threshold the exact test on the float vertices.  Both rings have their edge normals at the
-// angles (k + 1/2) pi/32, so the axis n_k separates them (ideally) iff d.n_k > (pb + 1) cos(pi/64): only
-// the normals within 1e-6 of the maximum projection m (at most two adjacent ones) can separate the
-// float polygons, by the A edge with outward normal n_k (vertices 63 - k, 64 - k) or the B edge facing
-// it; the exact test checks each against the two vertices of the other's facing edge (the other
-// vertices lie >= 1 (cos(pi/64) - cos(3 pi/64)) = 0.0096 m further out)
-__device__ __attribute__((always_inline)) bool goal_meet_exact(double px, double py, double gx, double gy, double pb) {
-    const double dx = gx - px, dy = gy - py, R = pb + 1.0;
-    const double thr = R * c_tab.apothem;
-    const double dist = sqrt(dx * dx + dy * dy);
-    if (dist > R * (1.0 + 1e-12) + 1e-12) return false;
-    if (dist < thr * (1.0 - 1e-12) - 1e-12) return true;
-    double m = -INFINITY;
-    int km = 0;
-#pragma unroll 8
-    for (int k = 0; k < 64; ++k) {
-        double v = dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k];
-        km = v > m ? k : km;
-        m = v > m ? v : m;
-    }
-    if (m > thr + EXACT_BAND) return false;
-    if (m < thr - EXACT_BAND) return true;
+// the band part of goal_meet_exact (inline, or as the real call goal_band_exact_call)
+__device__ __attribute__((always_inline)) bool goal_band_exact(double px, double py, double gx, double gy, double pb,
+                                                          double dx, double dy, double m, double thr, int km) {
 #pragma unroll 1
     for (int c = -1; c <= 1; ++c) {
         const int k = (km + c) & 63;
@@ -340,16 +327,49 @@ __device__ __attribute__((always_inline)) bool goal_meet_exact(double px, double
     return true;
 }
 
-// Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p.  EX (the ATT / OM
-// radar's threshold band; 0: the float clip as it stands): an interval [tlo, thi] within EXACT_BAND_T
-// of empty -- a ray touching the polygon, or starting on its boundary -- is a band case (a touch at the
-// segment's end, tlo ~ 1, gives the distance L either way: the float decision stands).
-// EX = 1 flags it (band = true) and returns the float clip's answer; EX = 2 decides it by the exact
-// segment / polygon test, a touching ray entering at clamp(tlo, 0, 1).  The radar phase runs the
-// flagged rays again with EX = 2 after its main loop, where few registers are live.
+__device__ __attribute__((noinline)) bool goal_band_exact_call(double px, double py, double gx, double gy, double pb,
+                                                                double dx, double dy, double m, double thr, int km) {
+    return goal_band_exact(px, py, gx, gy, pb, dx, dy, m, thr, km);
+}
+
+// 64-gon(p, pb) meets 64-gon(g, 1) (ATT/env:2266-2269): gons_meet's closed form, and within EXACT_BAND
+// of the threshold the exact test on the float vertices.  Both rings have their edge normals at the
+// angles (k + 1/2) pi/32, so the axis n_k separates them (ideally) iff d.n_k > (pb + 1) cos(pi/64): only
+// the normals within 1e-6 of the maximum projection m (at most two adjacent ones) can separate the
+// float polygons, by the A edge with outward normal n_k (vertices 63 - k, 64 - k) or the B edge facing
+// it; the exact test checks each against the two vertices of the other's facing edge (the other
+// vertices lie >= 1 (cos(pi/64) - cos(3 pi/64)) = 0.0096 m further out)
+template <bool COLD>
+__device__ __attribute__((always_inline)) bool goal_meet_exact(double px, double py, double gx, double gy, double pb) {
+    const double dx = gx - px, dy = gy - py, R = pb + 1.0;
+    const double thr = R * c_tab.apothem;
+    const double dist = sqrt(dx * dx + dy * dy);
+    if (dist > R * (1.0 + 1e-12) + 1e-12) return false;
+    if (dist < thr * (1.0 - 1e-12) - 1e-12) return true;
+    double m = -INFINITY;
+    int km = 0;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) {
+        double v = dx * c_tab.nrm_c[k] + dy * c_tab.nrm_s[k];
+        km = v > m ? k : km;
+        m = v > m ? v : m;
+    }
+    if (m > thr + EXACT_BAND) return false;
+    if (m < thr - EXACT_BAND) return true;
+    return COLD ? goal_band_exact_call(px, py, gx, gy, pb, dx, dy, m, thr, km)
+                : goal_band_exact(px, py, gx, gy, pb, dx, dy, m, thr, km);
+}
+
+// Cyrus-Beck entry of segment c->e into the clockwise GEOS 64-gon of radius r at p.  EX = 1 (the ATT / OM
+// radar's threshold band; EX = 0: the float clip as it stands): an interval [tlo, thi] within
+// EXACT_BAND_T of empty -- a ray touching the polygon, or starting on its boundary -- is a band case (a
+// touch at the segment's end, tlo ~ 1, gives the distance L either way: the float decision stands).
+// mode 1 flags it (band = true) and returns the float clip's answer; mode 2 decides it by the exact
+// segment / polygon test (a real call), a touching ray entering at clamp(tlo, 0, 1).
 template <int EX = 0>
-__device__ __attribute__((always_inline)) bool ray_poly_entry_full(double cx, double cy, double ex, double ey, double px, double py, double r,
-                                    double &tout, bool &band) {
+__device__ __attribute__((always_inline)) bool ray_poly_entry_full(double cx, double cy, double ex, double ey,
+                                                                   double px, double py, double r, double &tout,
+                                                                   bool &band, int mode = 1) {
     double ddx = ex - cx, ddy = ey - cy;
     double tlo = 0.0, thi = 1.0;
     double vx = px + r * c_tab.circ_c[0], vy = py + r * c_tab.circ_s[0];
@@ -372,22 +392,17 @@ __device__ __attribute__((always_inline)) bool ray_poly_entry_full(double cx, do
         vx = wx;
         vy = wy;
     }
-    if (EX != 0) {
-        if (tlo - thi > EXACT_BAND_T) return false;
-        // a touch at the segment's end (tlo ~ 1) gives the distance L either way: the float decision
-        if (tlo - thi >= -EXACT_BAND_T && tlo < 1.0 - EXACT_BAND_T) {
-            if (EX == 1) {
-                band = true;
-                if (tlo > thi) return false;
-            } else {
-                const int m = seg_gon_meet(cx, cy, ex, ey, px, py, r);
-                if (m == 0 || (m < 0 && tlo > thi)) return false;
-                tlo = tlo < 0.0 ? 0.0 : (tlo > 1.0 ? 1.0 : tlo);
-            }
-        } else if (tlo > thi) {
-            return false;
+    if (EX != 0 && tlo - thi >= -EXACT_BAND_T && tlo < 1.0 - EXACT_BAND_T) {
+        if (mode == 1) {
+            band = true;
+        } else {
+            const int m = seg_gon_meet(cx, cy, ex, ey, px, py, r);
+            if (m == 0 || (m < 0 && tlo > thi)) return false;
+            tout = tlo < 0.0 ? 0.0 : (tlo > 1.0 ? 1.0 : tlo);
+            return true;
         }
     }
+    if (tlo > thi) return false;
     tout = tlo;
     return true;
 }
@@ -401,7 +416,7 @@ __device__ __attribute__((always_inline)) bool ray_poly_entry_full(double cx, do
 // meets the polygon iff that maximum is <= 1.  Anything else takes the full clip.
 template <int EX = 0>
 __device__ __attribute__((always_inline)) bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
-                               double &tout, bool &band) {
+                               double &tout, bool &band, int mode = 1) {
     const double ddx = ex - cx, ddy = ey - cy;
     const double L2 = ddx * ddx + ddy * ddy;
     const double wx = px - cx, wy = py - cy;
@@ -417,7 +432,7 @@ __device__ __attribute__((always_inline)) bool ray_poly_entry(double cx, double 
         return true;
     }
     if (!(h < ap * (1.0 - 1e-9)) || !(w2 > r * r * (1.0 + 1e-9)) || !(s0 > 0.0))
-        return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band);
+        return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band, mode);
     const double tc = (s0 - sqrt(r * r - h * h)) / L;              // circumscribed-circle entry
     const float phi = atan2f((float)(cy + tc * ddy - py), (float)(cx + tc * ddx - px));
     // vertex angles are -i 2pi/64: nearest vertex index
@@ -438,19 +453,20 @@ __device__ __attribute__((always_inline)) bool ray_poly_entry(double cx, double 
             any = true;
         }
     }
-    if (!any) return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band);
+    if (!any) return ray_poly_entry_full<EX>(cx, cy, ex, ey, px, py, r, tout, band, mode);
     if (tlo > 1.0) return false;
     tout = tlo;
     return true;
 }
 
-// EX (ATT / OM; see ray_poly_entry_full): where the rounded slab quotients tie within EXACT_BAND_T (a ray
-// through a corner) away from the segment's end, EX = 1 flags a band case, EX = 2 decides: the segment
-// meets the square's boundary iff it meets the closed square and does not lie inside the open one
-// (exact test).  Ties and exits at t ~ 1 give the distance L either way (the float decision stands).
+// EX = 1 (ATT / OM; see ray_poly_entry_full): where the rounded slab quotients tie within EXACT_BAND_T (a
+// ray through a corner) away from the segment's end, mode 1 flags a band case and mode 2 decides: the
+// segment meets the square's boundary iff it meets the closed square and does not lie inside the open
+// one (exact test, a real call).  Ties and exits at t ~ 1 give the distance L either way.
 template <int EX = 0>
-__device__ __attribute__((always_inline)) bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0, double y1,
-                           double &dout, bool &band) {
+__device__ __attribute__((always_inline)) bool ray_square(double cx, double cy, double ex, double ey, double x0,
+                                                          double x1, double y0, double y1, double &dout, bool &band,
+                                                          int mode = 1) {
     double ddx = ex - cx, ddy = ey - cy;
     double tx0, tx1, ty0, ty1;
     // a ray running along an edge from a start point on that edge: the intersection with the
@@ -478,18 +494,19 @@ __device__ __attribute__((always_inline)) bool ray_square(double cx, double cy, 
     }
     double tin = tx0 > ty0 ? tx0 : ty0;
     double tout = tx1 < ty1 ? tx1 : ty1;
-    // a corner tie away from the segment's end (near t = 1 the distance is L either way)
-    const bool tie = fabs(tin - tout) <= EXACT_BAND_T && tin < 1.0 - EXACT_BAND_T;
-    if (EX == 1 && tie) band = true;
-    if (EX == 2 && tie) {
-        const bool inside = x0 < cx && cx < x1 && y0 < cy && cy < y1 && x0 < ex && ex < x1 && y0 < ey && ey < y1;
-        int m = inside ? 0 : seg_square_meet(cx, cy, ex, ey, x0, x1, y0, y1);
-        if (m < 0) m = !(tin > tout || tout < 0.0 || tin > 1.0 || (tin < 0.0 && tout > 1.0));
-        if (!m) return false;
-        double t = tin >= 0.0 ? tin : tout;
-        t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-        dout = gdist(cx + t * ddx, cy + t * ddy, cx, cy);
-        return true;
+    if (EX != 0 && fabs(tin - tout) <= EXACT_BAND_T && tin < 1.0 - EXACT_BAND_T) {
+        if (mode == 1) {
+            band = true;
+        } else {
+            const bool inside = x0 < cx && cx < x1 && y0 < cy && cy < y1 && x0 < ex && ex < x1 && y0 < ey && ey < y1;
+            int m = inside ? 0 : seg_square_meet(cx, cy, ex, ey, x0, x1, y0, y1);
+            if (m < 0) m = !(tin > tout || tout < 0.0 || tin > 1.0 || (tin < 0.0 && tout > 1.0));
+            if (!m) return false;
+            double t = tin >= 0.0 ? tin : tout;
+            t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+            dout = gdist(cx + t * ddx, cy + t * ddy, cx, cy);
+            return true;
+        }
     }
     if (tin > tout || tout < 0.0 || tin > 1.0) return false;
     double t = tin >= 0.0 ? tin : tout;
@@ -502,7 +519,7 @@ __device__ __attribute__((always_inline)) bool ray_square(double cx, double cy, 
 __device__ inline bool ray_poly_entry(double cx, double cy, double ex, double ey, double px, double py, double r,
                                       double &tout) {
     bool band = false;
-    return ray_poly_entry<0>(cx, cy, ex, ey, px, py, r, tout, band);
+    return ray_poly_entry<0>(cx, cy, ex, ey, px, py, r, tout, band, 1);
 }
 __device__ inline bool ray_square(double cx, double cy, double ex, double ey, double x0, double x1, double y0,
                                   double y1, double &dout) {

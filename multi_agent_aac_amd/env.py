@@ -226,6 +226,14 @@ class BatchedEnv:
         self.bank_seed = int(seed)
         self.bank_generation = getattr(self, "bank_generation", 0) + 1
 
+    def band_max(self):
+        """(most radar rays one launch flagged for the exact threshold fix-up, the list's capacity):
+        aac_env_band_max (synchronises)."""
+        n, cap = ctypes.c_int32(0), ctypes.c_int32(0)
+        _native.check(_native.lib().aac_env_band_max(self._h, ctypes.byref(n), ctypes.byref(cap), _stream()),
+                      "aac_env_band_max")
+        return n.value, cap.value
+
     def use_episode_buffer(self, episode: torch.Tensor):
         """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E],
         on this device): a trainer's noise schedule then reads it with no per-step update."""

@@ -77,6 +77,8 @@ def test_step_kernel_on_thresholds(native_lib, N, mode):
     _both_ways(seen)
     kat = [e for e, f in enumerate(fam) if f == "kat"]            # ATT/geometry_test.py:13-15
     assert [bool(_np(env.bufs.mask)[e, 0] & 4) for e in kat] == [True, False]
+    most, cap = env.band_max()          # the radar rays flagged for the exact fix-up all fit its list
+    assert (mode == 1 or most > 0) and most <= cap, (most, cap)
 
 
 @pytest.mark.parametrize("mode", [0, 2])
