@@ -202,6 +202,8 @@ def parse():
                    help="N > 1 plumbing check: every rank joins the process group (gloo), prints its rank and "
                         "exits without touching the GPU")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--no-seg-overhead", dest="seg_overhead", action="store_false",
+                   help="skip the one-GPU timing of the world > 1 update schedule (tools/seg_overhead.py)")
     p.add_argument("--env-micro", type=int, default=1 << 18, help="envs for the env-only HBM microbench (0 = skip)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "env_step_pmc.json"))
     p.add_argument("--gemm-traffic", default=None,
@@ -250,6 +252,7 @@ def barrier(ws):
     torch.cuda.synchronize()
 
 
+from multi_agent_aac_amd import parallel  # noqa: E402
 from multi_agent_aac_amd import trainer as _trainer  # noqa: E402
 from multi_agent_aac_amd.trainer import Trainer, UamTrainer  # noqa: E402,F401  (the vectorised ma_main loops)
 
@@ -517,6 +520,32 @@ def _cpu_env_worker(E, N, radar, budget, wid, variant="att"):
     return steps, time.perf_counter() - t0, E
 
 
+def world_schedule_overhead(N, B, updates=20):
+    """The world > 1 update schedule's cost per update on this one GPU: the
+    N + 1 gradient all-reduces captured in the update graph over a one-rank RCCL group, against the
+    world = 1 graph, and the eager segmented alternative (tools/seg_overhead.py, a child process: it
+    initialises its own process group).  The 1 -> 8 GPU curve itself is the driver's run."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "seg_overhead.py"), "--updates", str(updates),
+                            "--agents", str(N), "--batch", str(B)], capture_output=True, text=True, timeout=240,
+                           env=env)
+        if r.returncode != 0:
+            return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:       # reported, never fatal to the bench line
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    res["note"] = ("one GPU, one-rank RCCL group, world = 2 schedule: per-update overhead vs the world = 1 "
+                   "graph; segmented_overhead_us is the default (collectives captured in the graph)")
+    return res
+
+
 def env_microbench(E, N, radar, iters=20, variant="att"):
     """Env-only kernel throughput at large E (the HBM-roofline regime of SURVEY 8(d))."""
     from multi_agent_aac_amd import world
@@ -696,7 +725,8 @@ def main():
                    "maps": 1 if uam else a.maps, "tdcpa": uam,
                    "update_graph": (not a.no_graph) and (ws == 1 or uam or tr.gru or tr.model.fused),
                    "step_graph": graphed,
-                   "graph_segments": "one per update" if ws == 1 else "cut at each gradient all-reduce"},
+                   "graph_segments": "one per update" if (ws == 1 or parallel.capturable(pg)) else
+                   "cut at each gradient all-reduce"},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if (tr.gru or uam) else N),
         "env_roofline": {"kernel": "uam_step_kernel (fused UAM env step)" if uam else (
                              "step_kernel (env step + replay push + auto-reset, aac_env_step_tail)" if tr.fused_tail
@@ -753,6 +783,9 @@ def main():
     if rank == 0 and ws == 1 and a.env_micro:
         out["env_microbench"] = uam_env_microbench(1 << 16, N) if uam else env_microbench(
             a.env_micro, N, a.radar, variant="wgru" if a.model == "gru" else "att")
+    if rank == 0 and ws == 1 and not uam and not tr.gru and a.seg_overhead:
+        out["world_schedule"] = world_schedule_overhead(a.agents, a.batch)
+        out["segmented_overhead_us"] = out["world_schedule"].get("segmented_overhead_us")
     if rank == 0 and cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

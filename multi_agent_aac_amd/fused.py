@@ -27,7 +27,7 @@ import os
 import numpy as np
 import torch
 
-from . import _native, ops
+from . import _native, ops, parallel
 
 vp = ctypes.c_void_p
 i32 = ctypes.c_int32
@@ -751,7 +751,7 @@ class FusedUpdate:
                                      done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, q=ptr(self.qn), yout=ptr(self.y))
         self.segs = None
         self.cfwd = self.CFWD and self.DAOB
-        zip0 = m.world == 1 and not self.OVERLAP and self.MERGED
+        zip0 = not self.OVERLAP and self.MERGED
         t_cf = critic_fwd_set(Ct, ptr(self.Xt), Bt, N, Din, None, self.h_t, fold=(ptr(self.acts_t.ha), At, D0))
         if zip0 and self.cfwd:
             # as below, with the target critic forward (its actor output layer folded in) and critic step
@@ -783,7 +783,7 @@ class FusedUpdate:
         else:
             self.pre += [AttnEnc(t_attn)] + gemm_launches(t_merge)
             self.pre += [AttnEnc(ride_only(t_cenc))] + gemm_launches(t_comb) + [t_head]
-        if m.world > 1:
+        if m.world > 1 and not zip0:
             self.iters = self._pipelined(A, C)
         elif self.OVERLAP:
             self.segs = self._overlapped(A, C)
@@ -808,14 +808,29 @@ class FusedUpdate:
         self.n_launches = len(self.pre) + sum(len(it) for it in self.iters) + len(self.post)
 
     def _adam(self, opt, flat, gpart, ns, step_add):
-        """world == 1: the Adam step sums the split-K partial copies itself."""
-        return [lambda: adam_sum(opt, gpart, ns, step_add, grad_out=flat.grad)]
+        """world == 1: the Adam step sums the split-K partial copies itself.  world > 1: the partial
+        copies are summed into the shared gradient buffer, all-reduced (SUM) and the Adam launch
+        applies the 1 / world."""
+        m = self.m
+        if m.world == 1:
+            return [lambda: adam_sum(opt, gpart, ns, step_add, grad_out=flat.grad)]
+        critic = opt is m.critic_optimizer
+        return [lambda: sum_partials(flat.grad, gpart, ns),
+                Collective(lambda: m._allreduce_grads(critic=critic, actor=not critic)),
+                lambda: adam_at(opt, step_add, 1.0 / m.world)]
 
     def _adam_pair(self, i_critic, i_actor):
-        """Critic Adam step i_critic + 1 and actor Adam step i_actor + 1 as one launch (or two)."""
+        """Critic Adam step i_critic + 1 and actor Adam step i_actor + 1 as one launch (or two); at
+        world > 1 behind ONE all-reduce of both gradients (contiguous in MADDPG._share_grads)."""
         m = self.m
         ca = (m.critic_optimizer, self.gc, self.SPLIT_CRITIC, i_critic + 1, m.fc.grad)
         aa = (m.actor_optimizer, self.ga, self.SPLIT_ACTOR, i_actor + 1, m.fa.grad)
+        if m.world > 1:
+            gs = 1.0 / m.world
+            return [lambda: sum_partials(m.fa.grad, self.ga, self.SPLIT_ACTOR),
+                    lambda: sum_partials(m.fc.grad, self.gc, self.SPLIT_CRITIC),
+                    Collective(lambda: m._allreduce_grads(critic=True, actor=True)),
+                    lambda: adam_at(ca[0], ca[3], gs), lambda: adam_at(aa[0], aa[3], gs)]
         if adam_pair_ok(self.gc, self.ga):
             return [lambda: adam_sum_pair(ca, aa)]
         return [lambda: adam_sum(*ca[:4], grad_out=ca[4]), lambda: adam_sum(*aa[:4], grad_out=aa[4])]
@@ -851,7 +866,7 @@ class FusedUpdate:
         return segs
 
     def _merged(self, A, C, cs0):
-        """world == 1: fewer, fuller launches.  The critic step of iteration i+1 reads the critic
+        """Fewer, fuller launches.  The critic step of iteration i+1 reads the critic
         weights after critic Adam step i (and the fixed targets) -- exactly what the actor step of
         iteration i reads -- and neither reads the other's result (as in ``_pipelined``).  So
         segment i+1 zips the actor forward + actor step of iteration i with the critic step of
@@ -859,7 +874,9 @@ class FusedUpdate:
         critic head riding along as a head job) and ends with both Adam steps in one launch.  The
         forward half of critic step 0 and the actor forward 0 ran inside the TD-target launches
         (``pre``).  Every product's arithmetic is unchanged, so the update is bit-identical to the
-        serial order (tests/test_fused_gpu.py)."""
+        serial order (tests/test_fused_gpu.py).  At world > 1 each Adam boundary becomes partial sums +
+        ONE all-reduce + the Adam launches (``_adam`` / ``_adam_pair``): the same N + 1 collectives as
+        ``_pipelined`` with the merged launches between them (tests/test_parallel_gpu.py)."""
         m, N = self.m, self.N
         segs = [gemm_launches(cs0["grad"]) + gemm_launches(cs0["encw"])      # its head ran chained in pre
                 + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, 1)]
@@ -961,7 +978,8 @@ class FusedUpdate:
             op()
 
     def _pipelined(self, A, C):
-        """world > 1: one gradient all-reduce per ``update_myown`` iteration boundary instead of two.
+        """world > 1 with AAC_MERGED=0 (the merged schedules are the default at every world size):
+        one gradient all-reduce per ``update_myown`` iteration boundary instead of two.
 
         The critic step of iteration i+1 reads the critic weights after critic Adam step i (and
         the fixed targets), exactly what the actor step of iteration i reads, and neither reads
@@ -1174,7 +1192,10 @@ class FusedUpdate:
 
     def segments(self):
         """The launch list cut at the collectives: ([segment ops], [collective]) with
-        len(segments) == len(collectives) + 1."""
+        len(segments) == len(collectives) + 1.  Collectives a HIP graph can hold (RCCL,
+        parallel.capturable) stay inline: one segment, no cut."""
+        if parallel.capturable(self.m.pg):
+            return [self.ops()], []
         segs, colls, cur = [], [], []
         for op in self.ops():
             if isinstance(op, Collective):

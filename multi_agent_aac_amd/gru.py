@@ -462,6 +462,9 @@ class GruUpdate:
         (self.L[-1] if soft else self.hold)()
 
     def segments(self):
+        """The launch list cut at the collectives (kept inline when RCCL can be captured)."""
+        if parallel.capturable(self.m.pg):
+            return [list(self.L)], []
         segs, colls, cur = [], [], []
         for op in self.L:
             if isinstance(op, Collective):

@@ -229,9 +229,10 @@ class MADDPG:
     def capture(self, B, warmup=2):
         """Capture one update_myown-equivalent into HIP graphs (state restored afterwards).
 
-        world == 1: one graph.  world > 1 (fused learner): one graph per segment between the
-        gradient all-reduces; the collectives are issued between the replays (RCCL enqueues them
-        on its own stream, ordered against the current stream), so no collective is captured."""
+        world == 1: one graph.  world > 1 (fused learner) over RCCL: one graph with the gradient
+        all-reduces captured in it (parallel.capturable).  Otherwise (gloo, AAC_GRAPH_COLL=0): one
+        graph per segment between the all-reduces, the collectives issued between the replays (RCCL
+        enqueues them on its own stream, ordered against the current stream)."""
         if self.world > 1 and not self.fused:
             self._graph = None
             return None

@@ -14,6 +14,19 @@ import os
 import torch
 import torch.distributed as dist
 
+# the gradient all-reduces of a world > 1 update captured INSIDE the update's HIP graph (RCCL kernels
+# are graph nodes, ordered by the graph's edges) instead of issued eagerly between graph segments:
+# 6 eager collectives + 7 segment replays cost ~117 us per update on one GPU, one graph with them
+# captured ~27 us (tools/seg_overhead.py, profiles/r05_seg_overhead.json).  AAC_GRAPH_COLL=0 keeps
+# the segmented replay
+GRAPH_COLL = os.environ.get("AAC_GRAPH_COLL", "1") == "1"
+
+
+def capturable(group=None):
+    """Whether the collectives of ``group`` can be captured into a HIP graph: RCCL (backend "nccl")
+    enqueues device work; gloo runs on the host and cannot be."""
+    return GRAPH_COLL and dist.is_initialized() and dist.get_backend(group) == "nccl"
+
 
 def allreduce_mean_(t, group=None):
     """In-place mean over the ranks of ``group`` (one collective)."""

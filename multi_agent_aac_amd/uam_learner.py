@@ -32,7 +32,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import ops, trace, uam
+from . import ops, parallel, trace, uam
 
 F64 = torch.float64
 ROW = 7 + 18 + 2 + 1 + 1 + 7 + 18           # [own | radar | a | r | done | own' | radar']
@@ -416,8 +416,11 @@ class FusedUamUpdate:
                 adam(P(g), 1)]
 
     def segments(self):
-        """The launch list cut at the collectives: ([segment launches], [collective])."""
+        """The launch list cut at the collectives: ([segment launches], [collective]); kept inline
+        (one segment) when RCCL can capture them (parallel.capturable)."""
         from . import fused
+        if parallel.capturable(self.m.pg):
+            return [list(self._launches)], []
         segs, colls, cur = [], [], []
         for f in self._launches:
             if isinstance(f, fused.Collective):

@@ -1,6 +1,6 @@
 """Two ranks on the one GPU of the test box (gloo backend, world_size 2), each holding a DIFFERENT
 replay shard (env shards per rank, the gradient mean before every Adam
-step).  For the three learners (ATT ``fused.FusedUpdate._pipelined``, GRU, UAM):
+step).  For the three learners (ATT ``fused.FusedUpdate._merged`` with its N + 1 collectives, GRU, UAM):
 
 * two update_myown calls on explicitly sampled rows are checked against the CPU restatement that
   applies the MEAN of the two ranks' gradients (``learner_ref.ref_update_dp``,
@@ -339,3 +339,22 @@ def test_two_rank_shards_match_mean_gradient_oracle(native_lib, kind):
         assert out[r]["n_segments"] > 1 and (SEGMENTS[kind] is None or out[r]["n_segments"] == SEGMENTS[kind]), out[r][
             "n_segments"]
         assert out[r]["graph_equal"], r
+
+
+def test_rccl_collectives_captured_in_graph(native_lib):
+    """The default world > 1 path over RCCL (parallel.capturable): the update's all-reduces captured
+    inside ONE graph end bit-identical to the 7 segments with eager RCCL all-reduces between them
+    (a one-rank "nccl" group, world = 2 schedule; tools/seg_overhead.py), and the schedule's cost is
+    reported."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "seg_overhead.py"), "--updates", "5"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["graph_rccl_graphs"] == 1 and out["graph_rccl_eager_collectives"] == 0, out
+    assert out["seg_rccl_graphs"] == 7 and out["seg_rccl_eager_collectives"] == 6, out
+    assert out["graph_equals_segmented"], out

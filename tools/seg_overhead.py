@@ -1,18 +1,19 @@
 """Cost of the world > 1 update schedule, measured on one GPU.
 
-At world > 1 the fused ATT update_myown runs as N + 2 = 7 captured graph segments with N + 1 = 6
-gradient all-reduces between them (fused.FusedUpdate._pipelined).  One process, one GPU, three forms
-of the same update (N = 5, B = 1024, replay of synthetic transitions), each timed over K updates with
-HIP events on the launching stream:
-  one      world = 1: the merged schedule, one graph (what bench.py runs at N = 1)
-  seg_noop the pipelined schedule's 7 graph segments, the collectives replaced by no-ops
-  seg_rccl the same with a real RCCL all-reduce per boundary on a one-rank "nccl" process group (the
-           collective's launch and its kernel; no xGMI traffic on one rank)
-  pipe_one the pipelined schedule's launches (no-op collectives) as ONE graph: separates the cost of the
-           schedule itself from the cost of cutting it into segments
-  pipe_rccl_one  the same with the RCCL all-reduces captured inside the one graph
-The difference seg_* - one is the schedule's overhead per update (the 1 -> 8 GPU curve itself is the
-driver's round-end run); /6 is the per-boundary cost c_seg of DESIGN.md section 6's model.
+At world > 1 the fused ATT update_myown has N + 1 = 6 gradient all-reduces (one per Adam boundary of
+fused.FusedUpdate._merged).  One process, one GPU, the same update (N = 5, B = 1024, replay of
+synthetic transitions) in five forms, each timed over K updates with HIP events on the launching
+stream, every form through the product's own capture (MADDPG.update -> capture):
+  one         world = 1: one graph (what bench.py runs at N = 1)
+  graph_noop  world = 2 schedule, collectives no-ops, one graph (the schedule's own cost)
+  graph_rccl  the same with a real RCCL all-reduce per boundary CAPTURED in the graph, on a one-rank
+              "nccl" group (the collective's kernels; no xGMI traffic on one rank) -- the default
+              world > 1 path (parallel.capturable)
+  seg_noop    AAC_GRAPH_COLL=0: 7 graph segments, the collectives (no-ops) issued between replays
+  seg_rccl    the same with real eager RCCL all-reduces
+and check: graph_rccl and seg_rccl end bit-identical (parameters + optimiser state).
+The differences x - one are per-update overheads; /6 is the per-boundary cost c_seg of DESIGN.md
+section 6's model.  The 1 -> 8 GPU curve itself is the driver's round-end run.
 
 python tools/seg_overhead.py [--updates 50]   (prints one JSON line)
 """
@@ -67,6 +68,11 @@ def time_updates(m, B, K):
     return e0.elapsed_time(e1) / K
 
 
+def state(m):
+    return [t.clone() for t in [m.fa.data, m.fc.data, m.fa_t.data, m.fc_t.data]
+            + m.actor_optimizer.state() + m.critic_optimizer.state()]
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--updates", type=int, default=50)
@@ -81,44 +87,29 @@ def main():
     pg = dist.new_group([0])
     out = {"agents": N, "batch": B, "updates": K}
     out["one_ms"] = time_updates(model(N, B, 1, None), B, K)
-    real = parallel.allreduce_sum_
-    parallel.allreduce_sum_ = lambda t, group=None: t                              # no-op collectives
-    m = model(N, B, 2, pg)
-    out["seg_noop_ms"] = time_updates(m, B, K)
-    segs, colls = m._graph if isinstance(m._graph, tuple) else ([], [])
-    out["segments"], out["collectives"] = len(segs), len(colls)
-    parallel.allreduce_sum_ = lambda t, group=None: (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg), t)[1]
-    out["seg_rccl_ms"] = time_updates(model(N, B, 2, pg), B, K)
-    for tag, fn in (("pipe_one_ms", lambda t, group=None: t),
-                    ("pipe_rccl_one_ms", lambda t, group=None: (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg), t)[1])):
-        parallel.allreduce_sum_ = fn
+    noop = lambda t, group=None: t                                                          # noqa: E731
+    rccl = lambda t, group=None: (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg), t)[1]  # noqa: E731
+    # (parallel.allreduce_sum_ skips a one-rank group: the forms below call RCCL themselves)
+    real, graph_coll = parallel.allreduce_sum_, parallel.GRAPH_COLL
+    final = {}
+    for tag, cap, fn in (("graph_noop", True, noop), ("graph_rccl", True, rccl),
+                         ("seg_noop", False, noop), ("seg_rccl", False, rccl)):
+        parallel.allreduce_sum_, parallel.GRAPH_COLL = fn, cap
         m = model(N, B, 2, pg)
-        m.update(B, want_stats=False)        # builds the plan (eager warm-up of every launch)
-        fu = m._fused_plan(B)
-        try:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for op in fu.ops():
-                    op()
+        out[tag + "_ms"] = time_updates(m, B, K)
+        segs, colls = m._graph
+        out[tag + "_graphs"], out[tag + "_eager_collectives"] = len(segs), len(colls)
+        if tag.endswith("rccl"):
             torch.cuda.synchronize()
-            for _ in range(3):
-                g.replay()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(K):
-                g.replay()
-            e1.record()
-            torch.cuda.synchronize()
-            out[tag] = e0.elapsed_time(e1) / K
-        except Exception as ex:       # capture of the collective not supported
-            out[tag] = f"failed: {type(ex).__name__}: {ex}"[:200]
-    parallel.allreduce_sum_ = real
-    nb = max(out["collectives"], 1)
-    out["segmented_overhead_us"] = round(1e3 * (out["seg_noop_ms"] - out["one_ms"]), 2)
-    out["segmented_rccl_overhead_us"] = round(1e3 * (out["seg_rccl_ms"] - out["one_ms"]), 2)
-    out["c_seg_us"] = round(1e3 * (out["seg_noop_ms"] - out["one_ms"]) / nb, 2)
-    out["c_seg_rccl_us"] = round(1e3 * (out["seg_rccl_ms"] - out["one_ms"]) / nb, 2)
+            final[tag] = state(m)
+    parallel.allreduce_sum_, parallel.GRAPH_COLL = real, graph_coll
+    out["graph_equals_segmented"] = all(torch.equal(x, y) for x, y in zip(final["graph_rccl"], final["seg_rccl"]))
+    nb = N + 1
+    for tag in ("graph_noop", "graph_rccl", "seg_noop", "seg_rccl"):
+        out[tag + "_overhead_us"] = round(1e3 * (out[tag + "_ms"] - out["one_ms"]), 2)
+    out["segmented_overhead_us"] = out["graph_rccl_overhead_us"]      # the default world > 1 path
+    out["c_seg_us"] = round(out["graph_rccl_overhead_us"] / nb, 2)
+    out["c_seg_eager_us"] = round(out["seg_rccl_overhead_us"] / nb, 2)
     print(json.dumps(out))
     dist.destroy_process_group()
 
