@@ -2304,19 +2304,23 @@ __device__ __forceinline__ void stage_r_store(const Stage<MAXI> &st, float *dst,
 
 // 16 x 16 tile of e^T = W x^T over K inputs from LDS (k = 4 s + h; A = W[f0 + n][k], B = x[row n][k],
 // W rows of stride Kw, x rows of stride Kx, both zero-padded past K); lane (n, h) gets the
-// pre-activations of features f0 + 4 h .. + 3 of row n.  Steps past ceil(K / 4) are skipped (uniform).
+// pre-activations of features f0 + 4 h .. + 3 of row n.  All KS steps run: the steps past ceil(K / 4)
+// read zeros for both operands (a select, not a branch: branches around every LDS read serialised
+// their latencies) and add exact zeros, so the result is that of the ceil(K / 4)-step chain.
 template <int KS>
 __device__ __forceinline__ f4 enc_lds(const float *sW, int Kw, const float *sx, int Kx, int K, int f0, int n, int h) {
     float a[KS], b[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-        a[s] = 4 * s < K ? sW[(f0 + n) * Kw + 4 * s + h] : 0.0f;
-        b[s] = 4 * s < K ? sx[n * Kx + 4 * s + h] : 0.0f;
+        const bool on = 4 * s < K;
+        const int k = on ? 4 * s + h : h;
+        const float wa = sW[(f0 + n) * Kw + k], xb = sx[n * Kx + k];
+        a[s] = on ? wa : 0.0f;
+        b[s] = on ? xb : 0.0f;
     }
     f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-        if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
     return acc;
 }
 
@@ -2333,72 +2337,84 @@ __device__ __forceinline__ f4 relu_bias4(f4 v, const float *b) {
     return r;
 }
 
-// the riding job: the critic encoders of 16 rows of one agent (eight 16-feature tiles, two per wave),
-// W_n, b_n and the 16 input rows staged in LDS
-__device__ void critic_enc_rows(const aac_attn_enc_args &A, int job, float *smem) {
+// the riding job: the critic encoders of row blocks jb, jb + rjobs, ... of one agent (16 rows each:
+// eight 16-feature tiles, two per wave), W_n and b_n staged in LDS once per job, the next block's
+// input rows (and its folded actor outputs) loaded while the current block is multiplied.
+// KSO = the encoder's k steps (ceil(Din / 4) <= KSO)
+template <int KSO>
+__device__ void critic_enc_rows(const aac_attn_enc_args &A, int job, int rjobs, float *smem) {
     const int nrb = (A.c_rows + 15) / 16;
-    const int ag = job / nrb, rb = job - ag * nrb;
+    const int ag = job / rjobs, jb = job - ag * rjobs;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
-    const int Din = A.c_din, Dp = enc_stride(Din), r0 = rb * 16;
+    const int Din = A.c_din, Dp = enc_stride(Din);
     float *sW = smem, *sx = smem + 128 * ENC_SMAX, *sb = sx + 16 * ENC_SMAX;
-    Stage<128 * ENC_DMAX / 256> gw;
+    Stage<128 * 4 * KSO / 256> gw;
     Stage<(ENC_SMAX + 15) / 16> gx;
     stage_w_load(gw, A.cW + (size_t)ag * 128 * Din, 128 * Din);
-    stage_r_load(gx, A.cx + (size_t)r0 * A.cx_ld + (size_t)ag * Din, A.cx_ld, Din, A.c_rows - r0);
-    const float bias = A.cb[ag * 128 + (threadIdx.x & 127)];
-    if (A.o_h) {
-        // the actor's output layer folded in: lanes (row rr, c) take columns 16 c .. 16 c + 15 of the
-        // 256-wide ha row, a 16-lane butterfly sums them (every lane of the row gets the same total),
-        // and the lanes that stage the two action columns put tanh(. + b) in their staged values
-        const int rr = threadIdx.x >> 4, c = threadIdx.x & 15, r = r0 + rr;
-        const bool rok = r < A.c_rows;
-        const f4 *hp = reinterpret_cast<const f4 *>(A.o_h + ((size_t)(rok ? r : 0) * A.c_n + ag) * 256 + 16 * c);
-        const f4 *w0 = reinterpret_cast<const f4 *>(A.o_w + 16 * c), *w1 = reinterpret_cast<const f4 *>(A.o_w + 256 + 16 * c);
-        f4 hv[4], wa[4], wb[4];
+    // the 16 input rows of block rb into gx; with the actor's output layer folded in, lanes (row rr,
+    // c) take columns 16 c .. 16 c + 15 of the 256-wide ha row, a 16-lane butterfly sums them (every
+    // lane of the row gets the same total), and the lanes that stage the two action columns put
+    // tanh(. + b) in their staged values
+    auto load_x = [&](int rb) {
+        const int r0 = rb * 16;
+        stage_r_load(gx, A.cx + (size_t)r0 * A.cx_ld + (size_t)ag * Din, A.cx_ld, Din, A.c_rows - r0);
+        if (A.o_h) {
+            const int rr = threadIdx.x >> 4, c = threadIdx.x & 15, r = r0 + rr;
+            const bool rok = r < A.c_rows;
+            const f4 *hp = reinterpret_cast<const f4 *>(A.o_h + ((size_t)(rok ? r : 0) * A.c_n + ag) * 256 + 16 * c);
+            const f4 *w0 = reinterpret_cast<const f4 *>(A.o_w + 16 * c), *w1 = reinterpret_cast<const f4 *>(A.o_w + 256 + 16 * c);
+            f4 hv[4], wa[4], wb[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            hv[q] = hp[q];
-            wa[q] = w0[q];
-            wb[q] = w1[q];
-        }
-        const float b0 = A.o_b[0], b1 = A.o_b[1];
-        float p0 = 0.0f, p1 = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                p0 = fmaf(hv[q][t], wa[q][t], p0);
-                p1 = fmaf(hv[q][t], wb[q][t], p1);
+            for (int q = 0; q < 4; ++q) {
+                hv[q] = hp[q];
+                wa[q] = w0[q];
+                wb[q] = w1[q];
             }
+            const float b0 = A.o_b[0], b1 = A.o_b[1];
+            float p0 = 0.0f, p1 = 0.0f;
 #pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) {
-            p0 += __shfl_xor(p0, o, 16);
-            p1 += __shfl_xor(p1, o, 16);
-        }
-        const float a0 = tanhf(p0 + b0), a1 = tanhf(p1 + b1);
-        const int d0 = A.o_d0;
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int u = 0; u < (ENC_SMAX + 15) / 16; ++u) {
-            const int k = c + 16 * u;
-            if (rok && k == d0) gx.v[u] = a0;
-            if (rok && k == d0 + 1) gx.v[u] = a1;
+                for (int t = 0; t < 4; ++t) {
+                    p0 = fmaf(hv[q][t], wa[q][t], p0);
+                    p1 = fmaf(hv[q][t], wb[q][t], p1);
+                }
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) {
+                p0 += __shfl_xor(p0, o, 16);
+                p1 += __shfl_xor(p1, o, 16);
+            }
+            const float a0 = tanhf(p0 + b0), a1 = tanhf(p1 + b1);
+            const int d0 = A.o_d0;
+#pragma unroll
+            for (int u = 0; u < (ENC_SMAX + 15) / 16; ++u) {
+                const int k = c + 16 * u;
+                if (rok && k == d0) gx.v[u] = a0;
+                if (rok && k == d0 + 1) gx.v[u] = a1;
+            }
+            if (rok && c == 0) {
+                float *xo = A.o_x + (size_t)r * A.cx_ld + (size_t)ag * Din + d0;
+                xo[0] = a0;
+                xo[1] = a1;
+            }
         }
-        if (rok && c == 0) {
-            float *xo = A.o_x + (size_t)r * A.cx_ld + (size_t)ag * Din + d0;
-            xo[0] = a0;
-            xo[1] = a1;
-        }
-    }
+    };
+    const float bias = A.cb[ag * 128 + (threadIdx.x & 127)];
+    load_x(jb);
     stage_w_store(gw, sW, Din, Dp, 128);
-    stage_r_store(gx, sx, Dp);
     if (threadIdx.x < 128) sb[threadIdx.x] = bias;
-    __syncthreads();
-    const int r = r0 + n;
+    for (int rb = jb; rb < nrb; rb += rjobs) {
+        stage_r_store(gx, sx, Dp);
+        __syncthreads();
+        if (rb + rjobs < nrb) load_x(rb + rjobs);        // in flight under this block's products
+        const int r = rb * 16 + n;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int f0 = 32 * w + 16 * t;
-        const f4 v = relu_bias4(enc_lds<ENC_DMAX / 4>(sW, Dp, sx, Dp, Din, f0, n, h), sb + f0 + 4 * h);
-        if (r < A.c_rows) *reinterpret_cast<f4 *>(A.cf + (size_t)r * A.c_n * 128 + ag * 128 + f0 + 4 * h) = v;
+        for (int t = 0; t < 2; ++t) {
+            const int f0 = 32 * w + 16 * t;
+            const f4 v = relu_bias4(enc_lds<KSO>(sW, Dp, sx, Dp, Din, f0, n, h), sb + f0 + 4 * h);
+            if (r < A.c_rows) *reinterpret_cast<f4 *>(A.cf + (size_t)r * A.c_n * 128 + ag * 128 + f0 + 4 * h) = v;
+        }
+        __syncthreads();       // every wave is done with sx before the next block's rows land there
     }
 }
 
@@ -2407,27 +2423,28 @@ __device__ void critic_enc_rows(const aac_attn_enc_args &A, int job, float *smem
 // nride[s] for its riding critic-encoder jobs
 struct AttnEncBatch {
     aac_attn_enc_args a[2];
-    int start[2], nattn[2], nride[2];
+    int start[2], nattn[2], nride[2], rjobs[2];     // rjobs: riding jobs per agent
     int nset;
     int hstart;               // workgroups >= hstart run the critic-head job (INT_MAX: none)
     HeadJob hj;
 };
 
-// LDS (floats): encoder weights | region U (the block's staged input rows, later sQ + sQK) | sE (later
-// sX) | sXn
+// LDS (floats): encoder weights | region U (the block's staged input rows, later sQ) | sE (later sX) |
+// sP (the four waves' partial scores [wave][row][slot])
 template <int KM>
 struct AttnEncLds {
     static constexpr int NS = 8 * KM + 1;        // staged neighbour rows: slot j at j * 8, odd row stride
     static constexpr int IN = 16 * ENC_SMAX + 16 * ENC_SG + 16 * NS;
-    static constexpr int U = IN > 2 * 64 * TS ? IN : 2 * 64 * TS;
-    static constexpr int OFF_U = ENC_W_FLOATS, OFF_E = OFF_U + ((U + 3) & ~3), OFF_XN = OFF_E + ((64 * TS + 3) & ~3);
-    static constexpr int OFF_S = OFF_XN + 16 * KM * QS;       // scores, then alpha: [16][KM] each
-    static constexpr int TOTAL = OFF_S + 2 * 16 * KM;
+    static constexpr int U = IN > 64 * TS ? IN : 64 * TS;
+    static constexpr int OFF_U = ENC_W_FLOATS, OFF_E = OFF_U + ((U + 3) & ~3), OFF_P = OFF_E + ((64 * TS + 3) & ~3);
+    static constexpr int TOTAL = OFF_P + 4 * 16 * KM;
 };
 static_assert(AttnEncLds<4>::TOTAL >= 128 * ENC_SMAX + 16 * ENC_SMAX + 128, "ride job fits in the attention's LDS");
 
-template <int KM>
-__global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
+// KM: neighbour slots (>= K); KSO: k steps of the own-row and critic-row encoders (6: <= 24 inputs, 10:
+// <= 40).  3 waves per SIMD at the config-3 shapes (the LDS allows 5; 4 spilled and measured slower)
+template <int KM, int KSO>
+__global__ void __launch_bounds__(256, (KM > 4 || KSO > 6) ? 2 : 3) attn_enc_kernel(AttnEncBatch P) {
     using L = AttnEncLds<KM>;
     __shared__ f4 smem4[L::TOTAL / 4];
     float *smem = reinterpret_cast<float *>(smem4);
@@ -2441,17 +2458,16 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
     const int nattn = P.nattn[s];
     const int lb = blockIdx.x - P.start[s];
     if (lb >= nattn) {
-        critic_enc_rows(A, lb - nattn, smem);
+        critic_enc_rows<KSO>(A, lb - nattn, P.rjobs[s], smem);
         return;
     }
     ASTAMP(0);
     const bool train = A.xn != nullptr;       // uniform: inference leaves the backward's operands NULL
     float *sWo = smem, *sWg = smem + ENC_OFF_WG, *sWn = smem + ENC_OFF_WN, *sB = smem + ENC_OFF_B;
     float *sOwn = smem + L::OFF_U, *sRad = sOwn + 16 * ENC_SMAX, *sNei = sRad + 16 * ENC_SG;
-    float *sQ = smem + L::OFF_U, *sQK = sQ + 64 * TS;          // alias the staged rows (dead by then)
+    float *sQ = smem + L::OFF_U;                                // aliases the staged rows (dead by then)
     float *sE = smem + L::OFF_E, *sX = sE;                      // sE dead after the q stage
-    float *sXn = smem + L::OFF_XN;                              // x_j of the block: [(row * KM + j)][feature]
-    float *sS = smem + L::OFF_S, *sA = sS + 16 * KM;
+    float *sP = smem + L::OFF_P;                                // partial scores [wave][row][slot]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, h = lane >> 4;
     const int fo = 16 * w + 4 * h;
     const int R = A.R, K = A.K, Do = A.d_own, Dop = enc_stride(Do);
@@ -2503,35 +2519,33 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
     for (int blk = lb; blk < nblk; blk += nattn) {
         const int r0 = blk * 16, r = r0 + n;
         const bool rin = r < R;
-        // (region U was last read before the previous block's final barrier)
+        // (region U was last read in the previous block's qk stage, before its score barrier)
         if (blk != lb) load_in(r0);
         store_in();
-        // the projections' weight fragments (in flight across the staging barrier)
+        // the q projection's weight fragments (in flight across the staging barrier); those of qk and v
+        // are issued one stage ahead of their use (registers: 4 waves per SIMD)
         float b[16], aq[16], ak[16], av[16];
         ld16w(A.Wq + (16 * w + n) * 64 + 16 * h, aq);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) ak[t] = A.Wk[(16 * h + t) * 64 + 16 * w + n];
-        ld16w(A.Wv + (16 * w + n) * 64 + 16 * h, av);
         ASTAMP(1);
         __syncthreads();
         ASTAMP(2);
-        // encoders: this wave's 16 features of e_o, e_g and of every x_j (transposed, rows on n)
-        const f4 eo = relu_bias4(enc_lds<ENC_DMAX / 4>(sWo, Dop, sOwn, Dop, Do, 16 * w, n, h), sB + fo);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ak[t] = A.Wk[(16 * h + t) * 64 + 16 * w + n];
+        // encoders: this wave's 16 features of e_o, e_g and of every x_j (transposed, rows on n); the
+        // x_j stay in registers: lane (n, h) holds features fo .. fo + 3 of row n, the layout of qk below
+        const f4 eo = relu_bias4(enc_lds<KSO>(sWo, Dop, sOwn, Dop, Do, 16 * w, n, h), sB + fo);
         const f4 eg = relu_bias4(enc_lds<5>(sWg, ENC_SG, sRad, ENC_SG, 18, 16 * w, n, h), sB + 64 + fo);
         f4 xj[KM];
 #pragma unroll
         for (int j = 0; j < KM; ++j)
             xj[j] = relu_bias4(enc_lds<2>(sWn, ENC_SN, sNei + j * 8, NS, 6, 16 * w, n, h), sB + 128 + fo);
-        // the valid-neighbour mask of row r = lane (wave 0, lanes < 16: they run the softmax), read
-        // before region U is overwritten
+        // the valid-neighbour mask of row n (every lane), read before region U is overwritten
         unsigned valid = 0;
-        if (w == 0 && lane < 16) {
 #pragma unroll
-            for (int j = 0; j < KM; ++j) {
-                const float *pn = sNei + lane * NS + j * 8;
-                const float m = ((((pn[0] + pn[1]) + pn[2]) + pn[3]) + pn[4]) + pn[5];
-                valid |= (j < K && m != 0.0f ? 1u : 0u) << j;
-            }
+        for (int j = 0; j < KM; ++j) {
+            const float *pn = sNei + n * NS + j * 8;
+            const float m = ((((pn[0] + pn[1]) + pn[2]) + pn[3]) + pn[4]) + pn[5];
+            valid |= (j < K && m != 0.0f ? 1u : 0u) << j;
         }
         float *crow = A.cat + (size_t)r * A.ld_cat;
         if (rin) {
@@ -2540,10 +2554,10 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) sE[(fo + j) * TS + n] = eo[j];
+        if (train && rin) {
 #pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            if (train && rin && j < K) *reinterpret_cast<f4 *>(A.xn + ((size_t)r * K + j) * 64 + fo) = xj[j];
-            *reinterpret_cast<f4 *>(sXn + (n * KM + j) * QS + fo) = xj[j];
+            for (int j = 0; j < KM; ++j)
+                if (j < K) *reinterpret_cast<f4 *>(A.xn + ((size_t)r * K + j) * 64 + fo) = xj[j];
         }
         ASTAMP(3);
         __syncthreads();
@@ -2556,38 +2570,32 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
         for (int j = 0; j < 4; ++j) sQ[(fo + j) * TS + n] = acc[j];
         __syncthreads();
         ASTAMP(5);
-        // qk^T = Wk^T q^T
+        ld16w(A.Wv + (16 * w + n) * 64 + 16 * h, av);
+        // qk^T = Wk^T q^T: lane (n, h) holds qk[n][fo .. fo + 3], beside its x_j features
         lds_bfrag(sQ, h, n, b);
         acc = mfma_k64(ak, b);
         if (train && rin) *reinterpret_cast<f4 *>(A.qk + (size_t)r * 64 + fo) = acc;
-        *reinterpret_cast<f4 *>(sQK + n * QS + fo) = acc;
-        __syncthreads();
-        ASTAMP(6);
-        // scores s[r][j] = x_j[r] . qk[r] on MFMA: wave w takes slots j = w (+ 4): the 16 x 16 product
-        // X_j QK^T over the 64 features (k = 16 c + 4 h + t, 16-B LDS reads), whose diagonal is the
-        // 16 scores; lane (n, h) holds rows 4 h .. 4 h + 3 of column n, so lane n, h = n / 4 has s[n][j]
+        // scores s[n][j] = x_j[n] . qk[n]: the lane's 4 features, the wave's 16 over the lane groups h
+        // (xor 16, 32), the four waves' partials through LDS in wave order
 #pragma unroll
-        for (int jj = 0; jj < KM / 4; ++jj) {
-            const int j = w + 4 * jj;
-            f4 sa = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const f4 xa = *reinterpret_cast<const f4 *>(sXn + (n * KM + j) * QS + 16 * c + 4 * h);
-                const f4 qb = *reinterpret_cast<const f4 *>(sQK + n * QS + 16 * c + 4 * h);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) sa = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[t], qb[t], sa, 0, 0, 0);
-            }
-            if ((n >> 2) == h) sS[n * KM + j] = sa[n & 3];
+        for (int j = 0; j < KM; ++j) {
+            float p = xj[j][0] * acc[0];
+            p = fmaf(xj[j][1], acc[1], p);
+            p = fmaf(xj[j][2], acc[2], p);
+            p = fmaf(xj[j][3], acc[3], p);
+            p += __shfl_xor(p, 16);
+            p += __shfl_xor(p, 32);
+            if (h == 0) sP[(w * 16 + n) * KM + j] = p;
         }
         __syncthreads();
-        // masked softmax of row r = lane (wave 0, lanes < 16); alpha to LDS (and the training output)
-        if (w == 0 && lane < 16) {
-            const int row = r0 + lane;
+        ASTAMP(6);
+        // masked softmax of row n in every lane; xb = sum_j alpha_j x_j for the lane's features
+        {
             float sc[KM];
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
-                sc[j] = sS[lane * KM + j] / 8.0f;
+                sc[j] = (((sP[n * KM + j] + sP[(16 + n) * KM + j]) + sP[(32 + n) * KM + j]) + sP[(48 + n) * KM + j]) / 8.0f;
                 mx = ((valid >> j & 1) && sc[j] > mx) ? sc[j] : mx;
             }
             float den = 0.0f;
@@ -2598,23 +2606,13 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(AttnEncBatch P) {
                 den += e;
             }
             const float inv = 1.0f / den;
-#pragma unroll
-            for (int j = 0; j < KM; ++j) {
-                const float a = (valid >> j & 1) ? sc[j] * inv : 0.0f;
-                sA[lane * KM + j] = a;
-                if (train && row < R && j < K) A.alpha[(size_t)row * K + j] = a;
-            }
-        }
-        __syncthreads();
-        // xb = sum_j alpha_j x_j: lane (n, h) = row n, features fo .. fo + 3 (the sX image of the v stage)
-        {
             f4 xb = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
-                const float a = sA[n * KM + j];
-                const f4 xv = *reinterpret_cast<const f4 *>(sXn + (n * KM + j) * QS + fo);
+                const float a = (valid >> j & 1) ? sc[j] * inv : 0.0f;
+                if (train && rin && w == 0 && h == 0 && j < K) A.alpha[(size_t)r * K + j] = a;
 #pragma unroll
-                for (int t = 0; t < 4; ++t) xb[t] = fmaf(a, xv[t], xb[t]);
+                for (int t = 0; t < 4; ++t) xb[t] = fmaf(a, xj[j][t], xb[t]);
             }
             if (train && rin) *reinterpret_cast<f4 *>(A.xb + (size_t)r * 64 + fo) = xb;
 #pragma unroll
@@ -3140,6 +3138,14 @@ static int mfma_attn_grid(int R) {
     return nblk < cap ? nblk : cap;
 }
 
+// riding critic-encoder jobs per agent: every 16-row block its own job up to AAC_RIDE_JOBS jobs in all
+// (then each job walks several blocks, the weights staged once)
+static int ride_jobs(int rows, int n) {
+    static const int cap = std::max(1, env_int("AAC_RIDE_JOBS", 512));
+    const int nrb = (rows + 15) / 16, per = std::max(1, cap / std::max(n, 1));
+    return nrb < per ? nrb : per;
+}
+
 static int attn_grid(int R) {
     static const int rows = std::max(4, env_int("AAC_ATTN_ROWS", 16));
     int wgs = (R + rows - 1) / rows;  // ~4 rows per wave
@@ -3284,15 +3290,18 @@ int aac_attn_enc_fwd_head(const aac_attn_enc_args *args, int32_t nset, const aac
     if (!args || nset < 1 || nset > 2) return ffail("attn_enc_fwd: 1 or 2 argument sets");
     AttnEncBatch P{};
     P.nset = nset;
-    int total = 0, kmax = 1;
+    int total = 0, kmax = 1, dmax = 0;
     for (int s = 0; s < nset; ++s) {
         if (attn_enc_check(args[s])) return -1;
         P.a[s] = args[s];
         P.start[s] = total;
         P.nattn[s] = args[s].R > 0 ? mfma_attn_grid(args[s].R) : 0;
-        P.nride[s] = args[s].c_rows > 0 ? args[s].c_n * ((args[s].c_rows + 15) / 16) : 0;
+        P.rjobs[s] = args[s].c_rows > 0 ? ride_jobs(args[s].c_rows, args[s].c_n) : 1;
+        P.nride[s] = args[s].c_rows > 0 ? args[s].c_n * P.rjobs[s] : 0;
         total += P.nattn[s] + P.nride[s];
         if (args[s].R > 0 && args[s].K > kmax) kmax = args[s].K;
+        if (args[s].R > 0 && args[s].d_own > dmax) dmax = args[s].d_own;
+        if (args[s].c_rows > 0 && args[s].c_din > dmax) dmax = args[s].c_din;
     }
     P.hstart = INT_MAX;
     if (head) {
@@ -3305,8 +3314,13 @@ int aac_attn_enc_fwd_head(const aac_attn_enc_args *args, int32_t nset, const aac
     if (total == 0) return 0;
     const dim3 g(total), b(256);
     hipStream_t st = (hipStream_t)stream;
-    if (kmax > 4) hipLaunchKernelGGL(attn_enc_kernel<8>, g, b, 0, st, P);
-    else hipLaunchKernelGGL(attn_enc_kernel<4>, g, b, 0, st, P);
+    if (kmax > 4) {
+        if (dmax > 24) hipLaunchKernelGGL((attn_enc_kernel<8, ENC_DMAX / 4>), g, b, 0, st, P);
+        else hipLaunchKernelGGL((attn_enc_kernel<8, 6>), g, b, 0, st, P);
+    } else {
+        if (dmax > 24) hipLaunchKernelGGL((attn_enc_kernel<4, ENC_DMAX / 4>), g, b, 0, st, P);
+        else hipLaunchKernelGGL((attn_enc_kernel<4, 6>), g, b, 0, st, P);
+    }
     FHIP(hipGetLastError());
     return 0;
 }

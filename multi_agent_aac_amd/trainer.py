@@ -116,15 +116,23 @@ class Trainer(CheckpointMixin):
         self._sg = {}                                 # parity -> captured whole-step graph
         self.pos_dev = torch.zeros(2, dtype=torch.int64, device="cuda")   # ring position ping-pong
         self._pos_dirty = True       # the host mirror moved outside step_graph: re-seed pos_dev
+        # debug surface: callables run around each eager step --
+        # pre(trainer) before the act launch, post(trainer, act, cur, nxt) after the env step (before
+        # the auto-reset of an unfused tail and before the update).  A step with hooks runs eagerly
+        # (no whole-step graph).  tests/oracle_diff.py hooks the C oracle in this way.
+        self.pre_step_hooks, self.post_step_hooks = [], []
 
     def graph_ok(self):
         """Whole-step graphs: the fused env tail, one rank, the fused learner (ATT: AAC_STEP_GRAPH; the
         GRU step: AAC_STEP_GRAPH_GRU)."""
         if self.gru:
             return (STEP_GRAPH_GRU and self.fused_tail and self.model.world == 1 and not NO_GRAPH
-                    and len(self.replay) > self.B)
+                    and len(self.replay) > self.B and not self.hooked())
         return (STEP_GRAPH and self.fused_tail and self.model.world == 1 and self.model.fused
-                and not NO_GRAPH and len(self.replay) > self.B)
+                and not NO_GRAPH and len(self.replay) > self.B and not self.hooked())
+
+    def hooked(self):
+        return bool(self.pre_step_hooks or self.post_step_hooks)
 
     def _capture_step(self, p):
         """act + env step tail + update_myown of a step whose current buffers are bufs[p], captured
@@ -190,6 +198,8 @@ class Trainer(CheckpointMixin):
     def step(self, update=True, time_env=False):
         self._pos_dirty = True
         c, n = self.cur, self.nxt
+        for f in self.pre_step_hooks:
+            f(self)
         with trace.range("act"):
             if self.gru:
                 hn_buf = self.hp[1] if self.h is self.hp[0] else self.hp[0]
@@ -214,6 +224,8 @@ class Trainer(CheckpointMixin):
             if time_env:
                 ev1.record()
                 self.env_events.append((ev0, ev1))
+            for f in self.post_step_hooks:
+                f(self, act, c, n)
             self.cur, self.nxt = n, c
             if update and len(self.replay) > self.B:
                 with trace.range("update"):
@@ -224,6 +236,8 @@ class Trainer(CheckpointMixin):
         if time_env:
             ev1.record()
             self.env_events.append((ev0, ev1))
+        for f in self.post_step_hooks:
+            f(self, act, c, n)
         with trace.range("replay_push"):
             if self.gru:     # rows keep (cur_hidden, next_hidden) as WGRU/ma_main:636
                 self.replay.push_batch(c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, self.h,
@@ -294,9 +308,12 @@ class UamTrainer(CheckpointMixin):
         self.episode = self.env.use_episode_buffer(torch.zeros(E, dtype=torch.int32, device="cuda"))
         self.env.auto_reset(None, out=self.cur)      # episode counters -> 1
         self.env_events = []
+        self.pre_step_hooks, self.post_step_hooks = [], []      # as Trainer's
 
     def step(self, update=True, time_env=False):
         c, n = self.cur, self.nxt
+        for f in self.pre_step_hooks:
+            f(self)
         with trace.range("act"):
             act = self.model.act(c.own, c.radar, self.episode, noisy=True)
         if time_env:
@@ -307,6 +324,8 @@ class UamTrainer(CheckpointMixin):
         if time_env:
             ev1.record()
             self.env_events.append((ev0, ev1))
+        for f in self.post_step_hooks:
+            f(self, act, c, n)
         with trace.range("replay_push"):
             self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
         self.cur, self.nxt = n, c

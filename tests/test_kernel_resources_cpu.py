@@ -37,7 +37,8 @@ def _usage(src):
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src,pattern", [("aac_fused.hip", "gemm_kernel"), ("aac_env.hip", "step_kernel"),
                                          ("aac_uam.hip", "uam_step_kernel"), ("aac_fused.hip", "actor_dcomb_out_bwd"),
-                                         ("aac_fused.hip", "attn_mfma_bwd_kernel")])
+                                         ("aac_fused.hip", "attn_mfma_bwd_kernel"),
+                                         ("aac_fused.hip", "attn_enc_kernel")])
 def test_hot_kernels_have_no_scratch(src, pattern):
     ks = {k: v for k, v in _usage(src).items() if pattern in k}
     assert ks, f"no {pattern} in {src}"

@@ -61,13 +61,22 @@ def main():
         return fused.GemmLaunch([fused.prob(P(X, n * Din), cp.enc_w[n], P(f, n * 128), rows, 128, Din, N * Din, Din,
                                             128 * N, tb=1, bias=cp.enc_b[n], act=fused.RELU) for n in range(N)])
 
+    def ride_fold(rows):
+        """the target critic's encoders with the target actor's output layer folded in (ha rows)"""
+        X, f = r(rows, N, Din), torch.empty(rows, N * 128, device=dev)
+        ha = torch.relu(r(rows * N, 256))
+        wa, ba = r(2, 256), r(2)
+        keep.append((X, f, ha, wa, ba))
+        return fused.critic_enc_ride(cp, P(X), rows, N, Din, f, fold=(P(ha), SimpleNamespace(Wa=P(wa), ba=P(ba)), D0))
+
     keep = []
     cases = [("target+ride | train (pre)", 1, fused.AttnEnc(actor_set(25 * B, False, ride(B)), actor_set(N * B, True))),
              ("train+ride (iteration)", 4, fused.AttnEnc(actor_set(N * B, True, ride(B)))),
              ("train (last iteration)", 1, fused.AttnEnc(actor_set(N * B, True))),
              ("ride only (actor-step critic)", 4, fused.AttnEnc(fused.ride_only(ride(B)))),
              ("ride pair (iteration 0)", 1, fused.AttnEnc(fused.ride_only(ride(B)), fused.ride_only(ride(B)))),
-             ("act inference E*N rows", 1, fused.AttnEnc(actor_set(4096 * N, False)))]
+             ("act inference E*N rows", 1, fused.AttnEnc(actor_set(4096 * N, False))),
+             ("target critic ride + folded output layer", 1, fused.AttnEnc(fused.ride_only(ride_fold(5 * B))))]
     if os.environ.get("MB_SWEEP"):
         cases = [(f"ride only rows={rows}", 0, fused.AttnEnc(fused.ride_only(ride(rows)))) for rows in (16, 256, 1024, 4096)]
         cases += [(f"train R={R}", 0, fused.AttnEnc(actor_set(R, True))) for R in (16, 1024, 5120, 20480)]
