@@ -1144,7 +1144,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     }
     aacw::lds_barrier();
     ESTAMP(2, __builtin_amdgcn_s_memtime());
-#ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (tools/env_phase_probe.sh)
+#ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (a round-3 probe script, in the git history)
     radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro);
 #endif
     if (A.variant) {

@@ -161,7 +161,7 @@ __device__ unsigned long long g_gemm_st[STAMP_WG][5];
 
 __device__ __forceinline__ void epilogue(const GProb &P, float *C, float *cx, int m, int n, float v) {
     if (m >= P.M || n >= P.N) return;
-#ifdef AAC_DBG_NO_STORE      // timing probes only (tools/gemm_probe.sh): keep the value live, store ~never
+#ifdef AAC_DBG_NO_STORE      // timing probes only (a round-3 probe script, in the git history): keep the value live, store ~never
     if (v != 1234.5678f) return;
 #endif
     if (P.ones && n == P.N - 1) {
@@ -1347,7 +1347,7 @@ __global__ void __launch_bounds__(256) attn_train_bwd_kernel(const float *__rest
 // its neighbour rows are loaded at the start of the block so their latency hides under the
 // projections.
 #ifdef AAC_ATTN_STAMPS
-// phase timestamps of workgroup 0 (probe builds only: tools/attn_stamps.sh)
+// phase timestamps of workgroup 0 (probe builds only: tools/variant_lib.sh + tools/attn_enc_stamps.py)
 __device__ unsigned long long g_attn_st[16];
 #define ASTAMP(i)                                                                                        \
     do {                                                                                                  \

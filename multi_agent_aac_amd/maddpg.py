@@ -76,7 +76,7 @@ class MADDPG:
         if seed is not None:
             torch.manual_seed(seed)
         # rocBLAS picks split-K kernels for the reduction-heavy weight-gradient GEMMs
-        # (dW = G^T X over 5k-20k rows); hipBLASLt ran them on 1-6 workgroups (tools/mb_wgrad.py)
+        # (dW = G^T X over 5k-20k rows); hipBLASLt ran them on 1-6 workgroups (a round-2 microbenchmark, in the git history)
         torch.backends.cuda.preferred_blas_library(blas)
         self.actors = ActorNetwork_ATT_TwoPortion(self.n_actor_dim, dim_act).to(self.device)
         self.critics = CriticCombine(self.n_critic_dim, N, dim_act).to(self.device)

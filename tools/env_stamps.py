@@ -56,8 +56,8 @@ def main():
     # vertices with fp64 cos/sin), goal in the 64-gon band
     stt = env.get_state()
     pp, gl = stt["pre_pos"].cpu().numpy(), stt["goal"].cpu().numpy()
-    from oracle.consts import BOUND, PB
-    r = PB
+    from multi_agent_aac_amd.world import BOUND
+    r = 2.5                   # pB (ATT/env: the drone radius)
     lx, hx = np.minimum(pp[..., 0], pos[..., 0]), np.maximum(pp[..., 0], pos[..., 0])
     ly, hy = np.minimum(pp[..., 1], pos[..., 1]), np.maximum(pp[..., 1], pos[..., 1])
     lo, hi = r + 1e-9, r * np.cos(np.pi / 32) - 1e-9

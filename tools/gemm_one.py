@@ -6,7 +6,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from oracle import learner_ref  # noqa: E402
+from tools import synth  # noqa: E402
 
 
 def main():
@@ -15,9 +15,7 @@ def main():
     m = MADDPG([22, 18, 6], [22, 18, 6], 2, n_agents=5, device="cuda", seed=1, batch_size=1024)
     rep = m.attach_replay(8192, seed=1)
     for p in range(2):
-        tr = learner_ref.random_transitions(4096, 5, p)
-        rep.push_batch(*[tr[q].cuda().contiguous() for q in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
-                                                               "n_own", "n_radar", "n_nei")])
+        rep.push_batch(*synth.transitions(4096, 5, p))
     ops = m._fused_plan(1024).ops()
     for op in ops:
         op()

@@ -9,7 +9,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from oracle import learner_ref  # noqa: E402
+from tools import synth  # noqa: E402
 
 
 def main():
@@ -20,9 +20,7 @@ def main():
     m = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, device="cuda", seed=1, batch_size=B)
     rep = m.attach_replay(8192, seed=1)
     for p in range(2):
-        tr = learner_ref.random_transitions(4096, N, p)
-        rep.push_batch(*[tr[k].cuda().contiguous() for k in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
-                                                               "n_own", "n_radar", "n_nei")])
+        rep.push_batch(*synth.transitions(4096, N, p))
     ops = m._fused_plan(B).ops()
     for op in ops:
         op()

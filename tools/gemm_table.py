@@ -10,7 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from oracle import learner_ref  # noqa: E402
+from tools import synth  # noqa: E402
 
 
 def main():
@@ -26,13 +26,10 @@ def main():
     D0 = 6 + 4 * (N - 1)
     if a.model == "gru":
         from multi_agent_aac_amd.gru import MADDPG
-        from oracle import gru_ref
         m = MADDPG([6, 18, 6], [6, 18, 6], 2, 64, 10, n_agents=N, device="cuda", seed=1, batch_size=B)
         rep = m.attach_replay(8192, seed=1)
-        keys = ("s_own", "s_radar", "s_nei", "act", "rew", "done", "n_own", "n_radar", "n_nei", "h_cur", "h_next")
         for p in range(2):
-            tr = gru_ref.random_gru_transitions(4096, N, p)
-            rep.push_batch(*[tr[k].cuda().contiguous() for k in keys])
+            rep.push_batch(*synth.transitions(4096, N, p, D0=6, H=64))
         fu = m._plan(B)
         ops = fu.ops()
     else:
@@ -40,9 +37,7 @@ def main():
         m = MADDPG([D0, 18, 6], [D0, 18, 6], 2, n_agents=N, device="cuda", seed=1, batch_size=B)
         rep = m.attach_replay(8192, seed=1)
         for p in range(2):
-            tr = learner_ref.random_transitions(4096, N, p)
-            rep.push_batch(*[tr[k].cuda().contiguous() for k in ("s_own", "s_radar", "s_nei", "act", "rew", "done",
-                                                                   "n_own", "n_radar", "n_nei")])
+            rep.push_batch(*synth.transitions(4096, N, p))
         fu = m._fused_plan(B)
         ops = fu.ops()
     for op in ops:
