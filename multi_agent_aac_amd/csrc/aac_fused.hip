@@ -2697,6 +2697,7 @@ const int g_lds_min_k = env_int("AAC_GEMM_LDS_MIN_K", 64);   // ... for products
 int g_lds_min_wg = env_int("AAC_GEMM_LDS_MIN_WG", 256);  // tile choice: largest tile with this many workgroups
 const int g_lds_min_wg_many = env_int("AAC_GEMM_LDS_MIN_WG_MANY", 48);   // ... in launches of >= 12 products
 const long g_lds_min_mn = env_int("AAC_GEMM_LDS_MIN_MN", 64 * 64);
+const int g_lds_pref_wg = env_int("AAC_GEMM_LDS_PREF_WG", 512);   // first choice: largest tile with this many
 int g_lds_small = env_int("AAC_GEMM_LDS_SMALL", 0);         // allow 32x32 LDS workgroup tiles
 const int g_xcd = env_int("AAC_GEMM_XCD", 0);                // XCD-aware order of the LDS tiles
 const int g_xcd_all = env_int("AAC_GEMM_XCD_ALL", 0);        // ... of every workgroup of a launch
@@ -2788,14 +2789,19 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
             // register path's split-K waves on these shapes (tools/mb_lds.py): only with the knob
             // g_lds_min_wg < 0 forces tile -1 - g_lds_min_wg of cand_tall (tests)
             if (g_lds_min_wg < 0) cand = cand_force;
-            for (int c = 0; c < (g_lds_min_wg < 0 ? 0 : (g_lds_small ? 4 : 3)); ++c) {
-                const long nt = (long)((s.M + 32 * cand[c][0] - 1) / (32 * cand[c][0])) *
-                                ((s.N + 32 * cand[c][1] - 1) / (32 * cand[c][1])) * ks;
-                if (nt >= min_wg) {
-                    pick = c;
-                    break;
+            // two passes: the largest tile giving >= g_lds_pref_wg workgroups (two or more per CU: a
+            // product of 320 64x64 tiles left 64 CUs with two workgroups and 192 with one, 30 -> 26 us
+            // for 5120x256x640 as 640 32x64 tiles), else the largest with >= min_wg
+            const int nc = g_lds_min_wg < 0 ? 0 : (g_lds_small ? 4 : 3);
+            for (int pass = (g_lds_pref_wg > min_wg ? 0 : 1); pass < 2 && pick < 0; ++pass)
+                for (int c = 0; c < nc; ++c) {
+                    const long nt = (long)((s.M + 32 * cand[c][0] - 1) / (32 * cand[c][0])) *
+                                    ((s.N + 32 * cand[c][1] - 1) / (32 * cand[c][1])) * ks;
+                    if (nt >= (pass == 0 ? g_lds_pref_wg : min_wg)) {
+                        pick = c;
+                        break;
+                    }
                 }
-            }
             if (pick < 0 && g_lds_small) pick = 3;
             if (g_lds_min_wg < 0) pick = std::min(3, -1 - g_lds_min_wg);
         }
