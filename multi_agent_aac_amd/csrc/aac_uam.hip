@@ -73,6 +73,15 @@ struct UReset {
                               // workgroup b takes envs b*epb ... (mask-filtered)
 };
 
+// the fused step tail (aac_uam_step_tail): the replay push of the step's transitions inside the step
+// launch
+struct UTail {
+    double *ring;             // [cap][54] replay rows (UamReplay); NULL: no push
+    int64_t cap, pos, new_pos, new_size;
+    int64_t *meta;            // the ring's device [pos, size]
+    const double *s_own, *s_radar, *act;    // the transitions' s and a (E*N rows of 7 / 18 / 2)
+};
+
 #ifdef AAC_UAM_STAMPS
 // phase timestamps of the first 64 workgroups of uam_step_kernel (probe builds only)
 __device__ unsigned long long g_uam_st[64][16];
@@ -617,9 +626,85 @@ __device__ inline void lds_agent(Lds &S, int la, double2 pos, double2 vel, doubl
     S.heading[la] = hd;
 }
 
+// the reset of the workgroup's envs with S.active set (local slot -> env: emap, or e0 + slot):
+// episode draw, clouds, aircraft, then the observation (UAM/env:551-771); the step tail and the reset
+// kernel share it.  src: an LDS array of MAXA ints.
+__device__ __attribute__((always_inline)) void reset_envs(const UArgs &A, const UReset &R, Lds &S, int e0, const int32_t *emap,
+                                                     int32_t *src) {
+    const int N = A.N;
+    const int nag = A.epb * N;
+    const int t = threadIdx.x;
+    const auto env_of = [&](int q) { return emap ? emap[q] : e0 + q; };
+    const int le = t / N, i = t - le * N;
+    const int e = env_of(le < A.epb ? le : 0);
+    const bool active = (t < nag) && (e < A.E) && S.active[le];
+    const int base = le * N;
+    const size_t ai = (size_t)e * N + i;
+    // which episode each resetting env takes (bank: a fresh draw per reset)
+    if (t < A.epb && S.active[t]) {
+        const int eq = env_of(t);
+        if (R.mode == 1) {
+            const int ep = A.episode[eq] + 1;
+            A.episode[eq] = ep;
+            src[t] = (int)(mix64(mix64(R.seed ^ (uint64_t)eq) ^ (uint64_t)ep) % (uint64_t)R.bank_n);
+        } else {
+            src[t] = eq;
+        }
+    }
+    __syncthreads();
+    // clouds (UAM/env:576-703)
+    if (t < 2 * A.epb && S.active[t >> 1]) {
+        const int lq = t >> 1, k = t & 1, eq = env_of(lq);
+        const int kind = R.clouds[src[lq] * 2 + k];
+        const double2 c = k == 0 ? make_double2(c_world.cloud_start[kind][0], c_world.cloud_start[kind][1])
+                                 : make_double2(c_world.path[kind][0][0], c_world.path[kind][0][1]);
+        A.clouds[eq * 2 + k] = c;
+        A.cloud_kind[eq * 2 + k] = kind;
+        if (k == 1) A.cloud_tgt[eq] = 1;
+        if (k == 0) A.step[eq] = 0;
+        S.cl[lq][k] = c;
+    }
+    // aircraft (UAM/env:733-771)
+    if (active) {
+        const size_t si = (size_t)src[le] * N + i;
+        const double2 st = R.start[si], g = R.goal[si];
+        const double hd = atan2(g.y - st.y, g.x - st.x);
+        const double2 v = make_double2(0 * cos(hd), 0 * sin(hd));
+        A.pos[ai] = st;
+        A.pre_pos[ai] = st;
+        A.start[ai] = st;
+        A.goal[ai] = g;
+        A.vel[ai] = v;
+        A.pre_vel[ai] = v;
+        A.heading[ai] = hd;
+        A.reach[ai] = 0;
+        lds_agent(S, t, st, v, st, v, g, hd);
+    }
+    __syncthreads();
+    if (active) dist_row(A, S, t, base);
+    __syncthreads();
+    order_phase(A, S, nag);
+    __syncthreads();
+    radar_phase(A, S, e0, nag, emap);
+    __syncthreads();
+    observe_phase(A, S, e0, nag, emap);
+}
+
 // ------------------------------------------------------------------------------- step
-__global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArgs A, const double2 *__restrict__ act) {
+// TAIL: the fused step tail -- after the step, the workgroup's transitions into the replay ring and
+// the bank reset of its finished envs (aac_uam_step_tail: the launches of aac_uam_step, aac_uam_push
+// and aac_uam_auto_reset in one, the same results)
+// TAIL: + the replay push of the workgroup's transitions (aac_uam_step_tail; off in the trainer: the
+// launch grows 188 -> 234 us against the 23-us push launch it replaces).  The bank reset of the
+// finished envs inside this launch as well (each workgroup resetting its own envs after the push) was
+// built, bit-exact, and measured slower: config 5 226 vs 238 M agent-env-steps/s -- ~28 % of the envs
+// finish per step, so ~73 % of the 4-env workgroups ran the whole reset pipeline for ~1 env, where
+// the packed reset launch runs full workgroups of resetting envs only.
+template <bool TAIL>
+__global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArgs A, const double2 *__restrict__ act,
+                                                                           UReset R, UTail T) {
     __shared__ Lds S;
+
     const int N = A.N, K = A.K;
     const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
@@ -885,18 +970,62 @@ __global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArg
         A.env_done[eq] = (uint8_t)((A.episode_length < st) || any_done || all_reach);
     }
     USTAMP(15);
+    if constexpr (TAIL) {
+        __syncthreads();         // the workgroup's rewards, done flags and next observation rows are out
+        const int nv = e0 + A.epb <= A.E ? A.epb : A.E - e0;
+        if (T.ring && nv > 0) {
+            // the transitions (s, a, r, done, s') of the workgroup's aircraft as ring rows
+            // [own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18] (UamReplay; UAM/main:582-603):
+            // consecutive threads write consecutive doubles of the rows
+            if (blockIdx.x == 0 && t == 0 && T.meta) {
+                T.meta[0] = T.new_pos;
+                T.meta[1] = T.new_size;
+            }
+            // every load of the workgroup's rows in flight before the first store (a load-store loop
+            // waited a memory latency per element)
+            const int64_t a0 = (int64_t)e0 * N;
+            const int tot = nv * N * 54;
+            const double *__restrict__ so = T.s_own, *__restrict__ sr = T.s_radar, *__restrict__ sa = T.act;
+            constexpr int PER = (MAXA * 54 + BLOCK - 1) / BLOCK;
+            double v[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int k = t + u * BLOCK;
+                const int kk = k < tot ? k : 0;
+                const int rr = kk / 54, c = kk - rr * 54;
+                const size_t q = (size_t)a0 + rr;
+                if (c < 7) v[u] = so[q * 7 + c];
+                else if (c < 25) v[u] = sr[q * 18 + (c - 7)];
+                else if (c < 27) v[u] = sa[q * 2 + (c - 25)];
+                else if (c == 27) v[u] = A.reward[q];
+                else if (c == 28) v[u] = (double)A.done[q];
+                else if (c < 36) v[u] = A.own[q * 7 + (c - 29)];
+                else v[u] = A.radar[q * 18 + (c - 36)];
+            }
+            double *__restrict__ ring = T.ring;
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int k = t + u * BLOCK;
+                if (k < tot) {
+                    const int rr = k / 54, c = k - rr * 54;
+                    int64_t row = T.pos + a0 + rr;
+                    if (row >= T.cap) row -= T.cap;
+                    ring[row * 54 + c] = v[u];
+                }
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------ reset
 __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     __shared__ Lds S;
-    const int N = A.N;
-    const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
     const int t = threadIdx.x;
     // local env slot -> env: contiguous, or the compacted list of resetting envs (so that every
     // workgroup that runs has epb envs to reset instead of the few of its contiguous range)
     __shared__ int32_t emap[MAXA];
+    __shared__ int32_t src[MAXA];
     if (t < A.epb) {
         if (R.list) {
             const int q = e0 + t;
@@ -913,60 +1042,7 @@ __global__ void __launch_bounds__(BLOCK) uam_reset_kernel(UArgs A, UReset R) {
     int any = 0;
     for (int k = 0; k < A.epb; ++k) any |= S.active[k];
     if (!any) return;
-    const int le = t / N, i = t - le * N;
-    const int e = emap[le < A.epb ? le : 0];
-    const bool active = (t < nag) && (e < A.E) && S.active[le];
-    const int base = le * N;
-    const size_t ai = (size_t)e * N + i;
-    // which episode each resetting env takes (bank: a fresh draw per reset)
-    __shared__ int32_t src[MAXA];
-    if (t < A.epb && S.active[t]) {
-        const int eq = emap[t];
-        if (R.mode == 1) {
-            const int ep = A.episode[eq] + 1;
-            A.episode[eq] = ep;
-            src[t] = (int)(mix64(mix64(R.seed ^ (uint64_t)eq) ^ (uint64_t)ep) % (uint64_t)R.bank_n);
-        } else {
-            src[t] = eq;
-        }
-    }
-    __syncthreads();
-    // clouds (UAM/env:576-703)
-    if (t < 2 * A.epb && S.active[t >> 1]) {
-        const int lq = t >> 1, k = t & 1, eq = emap[lq];
-        const int kind = R.clouds[src[lq] * 2 + k];
-        const double2 c = k == 0 ? make_double2(c_world.cloud_start[kind][0], c_world.cloud_start[kind][1])
-                                 : make_double2(c_world.path[kind][0][0], c_world.path[kind][0][1]);
-        A.clouds[eq * 2 + k] = c;
-        A.cloud_kind[eq * 2 + k] = kind;
-        if (k == 1) A.cloud_tgt[eq] = 1;
-        if (k == 0) A.step[eq] = 0;
-        S.cl[lq][k] = c;
-    }
-    // aircraft (UAM/env:733-771)
-    if (active) {
-        const size_t si = (size_t)src[le] * N + i;
-        const double2 st = R.start[si], g = R.goal[si];
-        const double hd = atan2(g.y - st.y, g.x - st.x);
-        const double2 v = make_double2(0 * cos(hd), 0 * sin(hd));
-        A.pos[ai] = st;
-        A.pre_pos[ai] = st;
-        A.start[ai] = st;
-        A.goal[ai] = g;
-        A.vel[ai] = v;
-        A.pre_vel[ai] = v;
-        A.heading[ai] = hd;
-        A.reach[ai] = 0;
-        lds_agent(S, t, st, v, st, v, g, hd);
-    }
-    __syncthreads();
-    if (active) dist_row(A, S, t, base);
-    __syncthreads();
-    order_phase(A, S, nag);
-    __syncthreads();
-    radar_phase(A, S, e0, nag, emap);
-    __syncthreads();
-    observe_phase(A, S, e0, nag, emap);
+    reset_envs(A, R, S, e0, emap, src);
 }
 
 // ordered list of the done envs for the packed auto-reset (aacw::compact_flags)
@@ -1247,9 +1323,42 @@ int aac_uam_step(aac_uam *h, const double *actions, const aac_uam_out *o, void *
     if (rc) return rc;
     if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return ufail(AAC_E_INVALID, "step outputs");
     UArgs A = make_uargs(h, o);
-    hipLaunchKernelGGL(uam_step_kernel, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A,
-                       reinterpret_cast<const double2 *>(actions));
+    hipLaunchKernelGGL(uam_step_kernel<false>, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A,
+                       reinterpret_cast<const double2 *>(actions), UReset{}, UTail{});
     UCHK(hipGetLastError());
+    return AAC_OK;
+}
+
+int aac_uam_step_tail(aac_uam *h, const double *actions, const aac_uam_out *o, double *ring, int64_t capacity,
+                      int64_t pos, int64_t size, int64_t *meta, const double *s_own, const double *s_radar,
+                      int32_t reset, void *stream) {
+    if (!h || !actions) return ufail(AAC_E_INVALID, "null argument");
+    int rc = check_uout(o);
+    if (rc) return rc;
+    if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return ufail(AAC_E_INVALID, "step outputs");
+    const int64_t M = (int64_t)h->cfg.E * h->cfg.N;
+    UTail T{};
+    if (ring) {
+        if (!s_own || !s_radar || !meta) return ufail(AAC_E_INVALID, "step_tail: push needs s_own, s_radar and meta");
+        if (M > capacity || pos < 0 || pos >= capacity || size < 0 || size > capacity)
+            return ufail(AAC_E_INVALID, "step_tail: E*N > capacity or pos / size out of range");
+        T.ring = ring;
+        T.cap = capacity;
+        T.pos = pos;
+        T.new_pos = (pos + M) % capacity;
+        T.new_size = std::min<int64_t>(size + M, capacity);
+        T.meta = meta;
+        T.s_own = s_own;
+        T.s_radar = s_radar;
+        T.act = actions;
+    }
+    if (reset && !h->bank_n) return ufail(AAC_E_STATE, "step_tail: no episode bank installed (aac_uam_set_bank)");
+    UArgs A = make_uargs(h, o);
+    hipLaunchKernelGGL(uam_step_kernel<true>, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A,
+                       reinterpret_cast<const double2 *>(actions), UReset{}, T);
+    UCHK(hipGetLastError());
+    // the finished envs: the packed bank reset (compaction + reset launches, as aac_uam_auto_reset)
+    if (reset) return aac_uam_auto_reset(h, o->env_done, o, stream);
     return AAC_OK;
 }
 
