@@ -777,7 +777,7 @@ def main():
         out["roofline"] = rf
         if not tr.gru:
             out["attn_roofline"] = attn_roofline(tr.model, a.batch,
-                                                 traffic_file=os.path.join(ROOT, "profiles", "r04_attn_pmc.json"))
+                                                 traffic_file=os.path.join(ROOT, "profiles", "r05_attn_pmc.json"))
     else:
         out["roofline"] = out["env_roofline"]
     if rank == 0 and ws == 1 and a.env_micro:

@@ -8,7 +8,7 @@
 # --pmc pass is its own run with no trace domains.  Summaries: tools/evidence_summary.py.
 export TMPDIR=/tmp
 T="rocprofv3 --kernel-trace --output-format csv"
-SHORT="--steps 10 --warmup 3 --no-cpu-baseline --env-micro 0"
+SHORT="--steps 10 --warmup 3 --no-cpu-baseline --env-micro 0 --no-seg-overhead"
 if [ "$1" = bench ]; then
   bash tools/gpu_job.sh \
     "bench:::300:::python bench.py" \
