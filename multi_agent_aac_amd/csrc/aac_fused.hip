@@ -1990,7 +1990,7 @@ __global__ void __launch_bounds__(256) attn_mfma_fwd_kernel(const float *__restr
 }
 
 template <int KM>
-__global__ void __launch_bounds__(256) attn_mfma_bwd_kernel(const float *__restrict__ dv, int lddv,
+__global__ void __launch_bounds__(256, KM > 4 ? 2 : 3) attn_mfma_bwd_kernel(const float *__restrict__ dv, int lddv,
                                                             const float *__restrict__ xn,
                                                             const float *__restrict__ alpha,
                                                             const float *__restrict__ qk_in,
@@ -2795,7 +2795,8 @@ int plan(const aac_gemm_prob *in, int n, GBatch &g, bool allow_empty = false) {
             // product of 320 64x64 tiles left 64 CUs with two workgroups and 192 with one, 30 -> 26 us
             // for 5120x256x640 as 640 32x64 tiles), else the largest with >= min_wg
             const int nc = g_lds_min_wg < 0 ? 0 : (g_lds_small ? 4 : 3);
-            for (int pass = (g_lds_pref_wg > min_wg ? 0 : 1); pass < 2 && pick < 0; ++pass)
+            // (not in launches of many products, whose tiles fill the chip together: min_wg_many)
+            for (int pass = (g_lds_pref_wg > min_wg && min_wg == g_lds_min_wg ? 0 : 1); pass < 2 && pick < 0; ++pass)
                 for (int c = 0; c < nc; ++c) {
                     const long nt = (long)((s.M + 32 * cand[c][0] - 1) / (32 * cand[c][0])) *
                                     ((s.N + 32 * cand[c][1] - 1) / (32 * cand[c][1])) * ks;
