@@ -1410,20 +1410,24 @@ struct DaobArgs {
     int ldw, din, d0, N, B;
 };
 
+// RT row tiles of 16 samples per workgroup: 2 when one tile per workgroup would put more workgroups
+// than CUs in the launch (B = 1 024, N = 5: 320 -> 160; 64 CUs ran two of the 320 at once, one round
+// more), each workgroup then streams its W_c slice once for 32 samples
+template <int RT>
 __global__ void __launch_bounds__(256) actor_dcomb_out_bwd_kernel(DaobArgs P, int hstart, HeadJob J) {
     if ((int)blockIdx.x >= hstart) {           // the riding critic-head job
         head_rows<false>(J, blockIdx.x - hstart);
         return;
     }
     __shared__ f4 sW4[64 * DAOB_WST / 4];
-    __shared__ float sP[4][16][2];
-    __shared__ float sD[16][2];
+    __shared__ float sP[4][16 * RT][2];
+    __shared__ float sD[16 * RT][2];
     __shared__ f4 sWa4[128];                    // the actor output layer's weights [2][256]
     float *sW = reinterpret_cast<float *>(sW4);
     if (threadIdx.x < 128) sWa4[threadIdx.x] = reinterpret_cast<const f4 *>(P.wa)[threadIdx.x];
     const int N = P.N;
     const int sb = blockIdx.x / N, n = blockIdx.x - sb * N;
-    const int b0 = sb * 16;
+    const int b0 = sb * 16 * RT;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, ln = lane & 15, h = lane >> 4;
     const float *wcol = P.Wc + (size_t)n * 128;       // column block of agent n
     // staging map: item e = t + 256 u (u < 8) -> chunk row e / 32, 4 columns (e % 32) * 4; two chunks
@@ -1445,83 +1449,100 @@ __global__ void __launch_bounds__(256) actor_dcomb_out_bwd_kernel(DaobArgs P, in
     };
     load_chunk(0, pre[0]);
     load_chunk(1, pre[1]);
-    // A fragments: the 16 consecutive dh values of row b0 + ln at k = 64 c + 16 h .. + 15, every chunk
-    const int bl = b0 + ln < P.B ? b0 + ln : P.B - 1;
-    float a[4][16];
+    // A fragments: the 16 consecutive dh values of row b0 + 16 rt + ln at k = 64 c + 16 h .. + 15 (all
+    // chunks for one tile; with two tiles, chunk by chunk)
+    int bl[RT];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) ld16(P.dh + (size_t)bl * 256 + 64 * c + 16 * h, a[c]);
+    for (int rt = 0; rt < RT; ++rt) bl[rt] = b0 + 16 * rt + ln < P.B ? b0 + 16 * rt + ln : P.B - 1;
+    float a[RT == 1 ? 4 : 1][RT][16];
+    if (RT == 1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ld16(P.dh + (size_t)bl[0] * 256 + 64 * c + 16 * h, a[RT == 1 ? c : 0][0]);
+    }
     // the epilogue's operands, in flight across the MFMA chain: mask f, W_enc_n action columns, actions
     const int fo0 = 32 * w + ln, fo1 = fo0 + 16;            // this lane's two features of agent n
-    float fm[2][4];
+    float fm[RT][2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int b = b0 + 4 * h + j, bc = b < P.B ? b : P.B - 1;
-        fm[0][j] = P.f[(size_t)bc * P.ldw + n * 128 + fo0];
-        fm[1][j] = P.f[(size_t)bc * P.ldw + n * 128 + fo1];
-    }
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int b = b0 + 16 * rt + 4 * h + j, bc = b < P.B ? b : P.B - 1;
+            fm[rt][0][j] = P.f[(size_t)bc * P.ldw + n * 128 + fo0];
+            fm[rt][1][j] = P.f[(size_t)bc * P.ldw + n * 128 + fo1];
+        }
     const float *we = P.wenc + (size_t)n * 128 * P.din + P.d0;
     const float we00 = we[(size_t)fo0 * P.din], we01 = we[(size_t)fo0 * P.din + 1];
     const float we10 = we[(size_t)fo1 * P.din], we11 = we[(size_t)fo1 * P.din + 1];
-    // the tail's operands too: this thread's 16 columns of its dh_a row, and (t < 32) its action value
-    const int ts = t >> 4, tc0 = (t & 15) * 16, tb = b0 + ts < P.B ? b0 + ts : P.B - 1;
-    f4 hvp[4];
+    f4 acc0[RT], acc1[RT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) hvp[q] = *reinterpret_cast<const f4 *>(P.ha + ((size_t)tb * N + n) * 256 + tc0 + 4 * q);
-    const int as = t >> 1, aj = t & 1, abc = b0 + as < P.B ? b0 + as : P.B - 1;
-    const float av = t < 32 ? P.X[((size_t)abc * N + n) * P.din + P.d0 + aj] : 0.0f;
-    f4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0;
+    for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
+        if (RT > 1) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) ld16(P.dh + (size_t)bl[rt] * 256 + 64 * c + 16 * h, a[0][rt]);
+        }
         store_chunk(pre[c & 1]);
         __syncthreads();
         if (c + 2 < 4) load_chunk(c + 2, pre[c & 1]);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             const float *rowp = sW + (16 * h + s) * DAOB_WST + 32 * w + ln;
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][s], rowp[0], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][s], rowp[16], acc1, 0, 0, 0);
+            const float w0v = rowp[0], w1v = rowp[16];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const float av_ = a[RT == 1 ? c : 0][rt][s];
+                acc0[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, w0v, acc0[rt], 0, 0, 0);
+                acc1[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, w1v, acc1[rt], 0, 0, 0);
+            }
         }
         __syncthreads();
     }
-    // lane (ln, h): df[b0 + 4h + j][n*128 + fo] = acc[j] (masked); da partials over the lane's features
-    float p0[4], p1[4];
+    // lane (ln, h): df[b0 + 16 rt + 4h + j][n*128 + fo] = acc[rt][j] (masked); da partials over the
+    // lane's features
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const float g0 = fm[0][j] > 0.0f ? acc0[j] : 0.0f;
-        const float g1 = fm[1][j] > 0.0f ? acc1[j] : 0.0f;
-        p0[j] = fmaf(g1, we10, g0 * we00);
-        p1[j] = fmaf(g1, we11, g0 * we01);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {        // over the 16 lanes of the row group (features 0..15 of a tile)
-        p0[j] = aacw::rsum16(p0[j]);
-        p1[j] = aacw::rsum16(p1[j]);
-    }
-    if (ln == 0) {
+    for (int rt = 0; rt < RT; ++rt) {
+        float p0[4], p1[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            sP[w][4 * h + j][0] = p0[j];
-            sP[w][4 * h + j][1] = p1[j];
+            const float g0 = fm[rt][0][j] > 0.0f ? acc0[rt][j] : 0.0f;
+            const float g1 = fm[rt][1][j] > 0.0f ? acc1[rt][j] : 0.0f;
+            p0[j] = fmaf(g1, we10, g0 * we00);
+            p1[j] = fmaf(g1, we11, g0 * we01);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {        // over the 16 lanes of the row group (features 0..15 of a tile)
+            p0[j] = aacw::rsum16(p0[j]);
+            p1[j] = aacw::rsum16(p1[j]);
+        }
+        if (ln == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sP[w][16 * rt + 4 * h + j][0] = p0[j];
+                sP[w][16 * rt + 4 * h + j][1] = p1[j];
+            }
         }
     }
     __syncthreads();
-    if (t < 32) {        // the four waves' partials in wave order, then the tanh backward
-        const int s = as, j = aj, b = b0 + s;
+    if (t < 32 * RT) {   // the four waves' partials in wave order, then the tanh backward
+        const int s = t >> 1, j = t & 1, b = b0 + s, bc = b < P.B ? b : P.B - 1;
+        const float av = P.X[((size_t)bc * N + n) * P.din + P.d0 + j];
         const float da = ((sP[0][s][j] + sP[1][s][j]) + sP[2][s][j]) + sP[3][s][j];
         const float o = da * (1.0f - av * av);
         sD[s][j] = o;
         if (b < P.B) P.dout[((size_t)b * N + n) * 2 + j] = o;
     }
     __syncthreads();
-    {   // dh_a rows: thread (row s, 16 columns)
-        const int s = ts, c0 = tc0, b = b0 + s;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {   // dh_a rows: thread (row s, 16 columns)
+        const int s = 16 * rt + (t >> 4), c0 = (t & 15) * 16, b = b0 + s;
         if (b < P.B) {
             const size_t r = (size_t)b * N + n;
             const float o0 = sD[s][0], o1 = sD[s][1];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int c = c0 + 4 * q;
-                const f4 hv = hvp[q];
+                const f4 hv = *reinterpret_cast<const f4 *>(P.ha + r * 256 + c);
                 const f4 w0 = sWa4[c >> 2];
                 const f4 w1 = sWa4[64 + (c >> 2)];
                 f4 v;
@@ -3115,7 +3136,10 @@ int aac_actor_dcomb_out_bwd(const aac_dcomb_aob_args *a, const aac_head_job *hea
     if (!aligned16(a->dh) || !aligned16(a->Wc) || !aligned16(a->ha) || !aligned16(a->dha) || !aligned16(a->wa))
         return ffail("actor_dcomb_out_bwd: dh, Wc, ha, dha, wa must be 16-B aligned");
     DaobArgs P{a->dh, a->Wc, a->f, a->wenc, a->X, a->wa, a->ha, a->dout, a->dha, a->ldw, a->din, a->d0, a->N, a->B};
-    const int nwg = ((a->B + 15) / 16) * a->N;
+    // two 16-sample tiles per workgroup when one per workgroup would exceed the CUs (AAC_DAOB_RT: force)
+    static const int rt_env = env_int("AAC_DAOB_RT", 0);
+    const int rt = rt_env == 1 || rt_env == 2 ? rt_env : (((a->B + 15) / 16) * a->N > 256 ? 2 : 1);
+    const int nwg = ((a->B + 16 * rt - 1) / (16 * rt)) * a->N;
     HeadJob J{};
     int total = nwg;
     if (head) {
@@ -3124,7 +3148,8 @@ int aac_actor_dcomb_out_bwd(const aac_dcomb_aob_args *a, const aac_head_job *hea
         J = head_job(*head);
         total += (std::max(head->M, 0) + 3) / 4;
     }
-    hipLaunchKernelGGL(actor_dcomb_out_bwd_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, P, nwg, J);
+    if (rt == 2) hipLaunchKernelGGL(actor_dcomb_out_bwd_kernel<2>, dim3(total), dim3(256), 0, (hipStream_t)stream, P, nwg, J);
+    else hipLaunchKernelGGL(actor_dcomb_out_bwd_kernel<1>, dim3(total), dim3(256), 0, (hipStream_t)stream, P, nwg, J);
     FHIP(hipGetLastError());
     return 0;
 }
