@@ -3228,7 +3228,15 @@ static bool attn_bwd_mfma_ok(const float *dv, int32_t lddv, const float *eo, int
            aligned16(dcat_o) && ldd % 4 == 0 && aligned16(dq) && aligned16(deo);
 }
 
-int32_t aac_attn_train_bwd_partials(int32_t R) { return R > 0 ? mfma_attn_grid(R) : 0; }
+// the backward's grid: a 16-row block per workgroup up to AAC_ATTN_BWD_WGS workgroups (default: the
+// forward's cap), then each walks several (160 at B = 1 024, N = 5: -2 %, so off)
+static int attn_bwd_grid(int R) {
+    static const int cap = env_int("AAC_ATTN_BWD_WGS", 0);
+    const int nblk = (R + 15) / 16;
+    return cap > 0 && nblk > cap ? cap : mfma_attn_grid(R);
+}
+
+int32_t aac_attn_train_bwd_partials(int32_t R) { return R > 0 ? attn_bwd_grid(R) : 0; }
 
 int aac_attn_train_bwd_wn(const float *dv, int32_t lddv, const float *xn, const float *alpha, const float *qk,
                           const float *eo, int32_t lde, const float *dcat_o, int32_t ldd, const float *Wq,
@@ -3241,7 +3249,7 @@ int aac_attn_train_bwd_wn(const float *dv, int32_t lddv, const float *xn, const 
     if (pwn && (!nei || !mfma)) return ffail("attn_train_bwd: the dWn partials need nei and the MFMA path (K <= 8)");
     if (!pwn && !dxn) return ffail("attn_train_bwd: dxn (or the dWn partials) required");
     if (mfma) {
-        const dim3 g(mfma_attn_grid(R)), b(256);
+        const dim3 g(attn_bwd_grid(R)), b(256);
         if (K <= 4)
             hipLaunchKernelGGL(attn_mfma_bwd_kernel<4>, g, b, 0, st, dv, lddv, xn, alpha, qk, eo, lde, dcat_o, ldd, Wq,
                                Wk, Wv, dxn, dqk, dq, deo, R, K, nei, pwn);
