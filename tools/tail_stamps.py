@@ -1,6 +1,6 @@
 """Per-workgroup phase timeline of the fused env step tail (aac_env_step_tail: step + replay push +
 auto-reset) in a steady training-like loop, from a stamp build (bash tools/variant_lib.sh estamps
-aac_env.hip -DAAC_ENV_STAMPS; AAC_LIB=tools/variants/lib_estamps.so).
+aac_env.hip -DAAC_ENV_STAMPS; AAC_LIB=ablibs/lib_estamps.so).
 
 python tools/tail_stamps.py [att|wgru]
 
