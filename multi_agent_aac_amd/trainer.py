@@ -20,6 +20,8 @@ Module flags (environment variables read at import):
   AAC_STEP_GRAPH_GRU 0: the GRU training step launched from the host (default: one graph replay;
                    config 4 0.3331 -> 0.3310 ms per step)
   AAC_OVERLAP_RESET 1: separate-launch auto-reset on a side stream (measured slower, off)
+  AAC_UAM_OVERLAP_RESET 0: the UAM loop's packed auto-reset before the update instead of on a side
+                   stream beside it (default on: config 5 0.543 -> 0.519 ms per step)
 """
 import os
 
@@ -46,6 +48,10 @@ STEP_GRAPH_GRU = os.environ.get("AAC_STEP_GRAPH_GRU", "1") == "1"
 # slower, so off: the step launch grows 188 -> 234 us against the 23-us push launch it replaces
 # (226-231 vs 238-240 M agent-env-steps/s; profiles/r05_uam_tail_ab.txt)
 UAM_TAIL = os.environ.get("AAC_UAM_TAIL", "0") == "1"
+# config 5: the packed auto-reset (UAM/env:551-771) on a side stream beside the update, whose small
+# float64 launches leave most CUs idle: 0.543 -> 0.519 ms per step, interleaved
+# (profiles/r05_uam_overlap_reset_ab.txt); AAC_UAM_OVERLAP_RESET=0 runs it before the update
+UAM_OVERLAP_RESET = os.environ.get("AAC_UAM_OVERLAP_RESET", "1") == "1"
 
 
 class CheckpointMixin:
@@ -268,8 +274,8 @@ class side_stream:
     """Run the block on the trainer's side stream, ordered after the main stream's work so far (a
     no-op context when off)."""
 
-    def __init__(self, tr, on):
-        self.tr, self.on = tr, on and OVERLAP_RESET
+    def __init__(self, tr, on, flag=None):
+        self.tr, self.on = tr, on and (OVERLAP_RESET if flag is None else flag)
 
     def __enter__(self):
         if not self.on:
@@ -336,7 +342,7 @@ class UamTrainer(CheckpointMixin):
                 f(self, act, c, n)
             self.cur, self.nxt = n, c
             run_update = update and len(self.replay) > self.B
-            with side_stream(self, run_update), trace.range("auto_reset"):
+            with side_stream(self, run_update, UAM_OVERLAP_RESET), trace.range("auto_reset"):
                 self.env.auto_reset(n.env_done, out=n)
             if run_update:
                 with trace.range("update"):
@@ -354,7 +360,7 @@ class UamTrainer(CheckpointMixin):
             self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar)
         self.cur, self.nxt = n, c
         run_update = update and len(self.replay) > self.B
-        with side_stream(self, run_update), trace.range("auto_reset"):
+        with side_stream(self, run_update, UAM_OVERLAP_RESET), trace.range("auto_reset"):
             self.env.auto_reset(n.env_done, out=n)
         if run_update:
             with trace.range("update"):

@@ -55,6 +55,25 @@ def test_resume_is_bit_identical(native_lib, model, tmp_path):
     assert len(a.replay) == len(b.replay) and a.replay.pos == b.replay.pos
 
 
+def test_uam_overlapped_reset_matches_serial(native_lib, monkeypatch):
+    """UamTrainer's packed auto-reset on the side stream beside the update (trainer.UAM_OVERLAP_RESET,
+    the default) leaves every learner, replay and env tensor bit-identical to the serial order."""
+    from multi_agent_aac_amd import trainer
+    snaps = []
+    for flag in (True, False):
+        monkeypatch.setattr(trainer, "UAM_OVERLAP_RESET", flag)
+        t = _trainer("uam")
+        while len(t.replay) <= t.B:
+            t.step(update=False)
+        for _ in range(6):
+            t.step(update=True)
+        snaps.append(_snapshot(t))
+    a, b = snaps
+    assert set(a) == set(b)
+    bad = [k for k in a if not torch.equal(a[k], b[k])]
+    assert not bad, bad
+
+
 def test_checkpoint_refuses_mismatch(native_lib, tmp_path):
     from multi_agent_aac_amd import checkpoint
     a = _trainer("att")

@@ -12,10 +12,22 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 a, b = idx[-K - 1], idx[-1]
 seg = rows[a:b]
-busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg) / 1e3
+ksum = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg) / 1e3
+# GPU busy = the union of the kernel intervals (kernels on two streams overlap)
+busy, end = 0, None
+for r in seg:
+    s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    if end is None or s0 >= end:
+        busy += e0 - s0
+        end = e0
+    elif e0 > end:
+        busy += e0 - end
+        end = e0
+busy /= 1e3
 wall = (int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
-print(f"last {K} steps: {len(seg) / K:.1f} launches/step, kernel time {busy / K:.1f} us/step, "
-      f"wall {wall / K:.1f} us/step (GPU busy {100 * busy / wall:.1f} %)")
+print(f"last {K} steps: {len(seg) / K:.1f} launches/step, kernel time {ksum / K:.1f} us/step, "
+      f"wall {wall / K:.1f} us/step (GPU busy {100 * busy / wall:.1f} %"
+      + (f", kernels overlapping {ksum - busy:.0f} us over {K} steps)" if ksum > busy + 1 else ")"))
 agg = collections.defaultdict(lambda: [0.0, 0])
 for r in seg:
     agg[r["Kernel_Name"][:100]][0] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 / K
