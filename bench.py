@@ -725,6 +725,9 @@ def main():
                    "maps": 1 if uam else a.maps, "tdcpa": uam,
                    "update_graph": (not a.no_graph) and (ws == 1 or uam or tr.gru or tr.model.fused),
                    "step_graph": graphed,
+                   "auto_reset": ("packed launch on a side stream beside the update" if _trainer.UAM_OVERLAP_RESET
+                                  else "packed launch before the update") if uam else (
+                                  "in the env step launch" if tr.fused_tail else "separate launch"),
                    "graph_segments": "one per update" if (ws == 1 or parallel.capturable(pg)) else
                    "cut at each gradient all-reduce"},
         "updates_per_s": upd_per_s, "grad_iters_per_s": upd_per_s * (1 if (tr.gru or uam) else N),
