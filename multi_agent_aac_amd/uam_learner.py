@@ -252,7 +252,9 @@ class FusedUamUpdate:
     the same weights.  The Adam moments are flat buffers too (``m1`` / ``m2``, one int32 step
     counter), owned by the MADDPG object (``MADDPG._flat_state``) so every plan -- any B, any
     replay -- and the torch-autograd path continue from the same optimiser state."""
-    KS = 8
+    # split-K partial copies of the weight gradients: 4 beat 8 by 0.5 % at config 5 with the reset
+    # overlapped (profiles/r05_uam_ks_ab.txt; 2 and 16 no better); AAC_UAM_KS overrides
+    KS = int(os.environ.get("AAC_UAM_KS", "4"))
 
     def __init__(self, m, B, rep):
         self.m, self.B, self.rep = m, int(B), rep
