@@ -269,6 +269,8 @@ def cpu_baseline_uam(E, N, B, seconds, procs_req=None):
         res = pool.starmap(_cpu_uam_worker, [(N, budget, w) for w in range(procs)])
     steps = sum(r[0] for r in res)
     env_rate = sum(r[0] / r[1] for r in res) * N                 # agent-env-steps/s over all workers
+    one = _cpu_uam_worker(N, budget / 4, 0)                       # one process alone: the scaling ratio
+    rate1 = one[0] / one[1] * N
     torch.set_num_threads(procs)
     a, c = R.RefActor().double(), R.RefCritic().double()
     at, ct = R.RefActor().double(), R.RefCritic().double()
@@ -286,7 +288,9 @@ def cpu_baseline_uam(E, N, B, seconds, procs_req=None):
     t_iter = E * N / env_rate + t_upd
     return {"value": E * N / t_iter, "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
             "physical_cores": phys, "affinity_cores": cores, "cpu_model": cpu_model(),
-            "per_physical_core_extrapolated": _extrapolate(env_rate, procs, phys, t_upd, E, N),
+            "per_physical_core_extrapolated": _extrapolate(env_rate, procs, phys, t_upd, E, N,
+                                                           eff=(env_rate / procs) / rate1),
+            "scalar_env_rate_per_process": {"1_process": rate1, f"{procs}_processes": env_rate / procs},
             "sample": (f"reference-shaped scalar UAM env oracle on {procs} processes x 1 env x {N} aircraft, "
                        f"{steps} env steps ({env_rate:.3g} agent-env-steps/s env-only) + CPU float64 "
                        f"update_myown restatement B={B} x {n_upd} ({t_upd * 1e3:.2f} ms each), {procs} threads; "
@@ -339,13 +343,18 @@ def baseline_procs(requested=None):
     return max(1, min(phys, aff, int(os.environ.get("AAC_CPU_SHARE", "16")))), phys, aff
 
 
-def _extrapolate(env_rate, procs, phys, t_upd, E, N):
+def _extrapolate(env_rate, procs, phys, t_upd, E, N, eff=1.0):
     """The same iteration with the env spread over one process per physical core: the measured
-    per-process env rate x physical cores (envs are independent and the scalar env is compute-bound:
-    no shared state), plus the measured update time."""
-    rate = env_rate / procs * phys
-    return {"value": E * N / (E * N / rate + t_upd), "env_only": rate, "cores": phys,
-            "basis": f"measured per-process env rate x {phys} physical cores + measured update time"}
+    per-process env rate at ``procs`` processes x physical cores, times ``eff`` = the measured
+    per-process rate at ``procs`` over the rate of one process alone (the decline from 1 to ``procs``
+    processes applied once more from ``procs`` to ``phys``: the host does not scale linearly, BENCH_r05
+    212.7 vs 186.7 per process), plus the measured update time.  An extrapolation, not a measurement:
+    the pool caps a job at 16 worker processes."""
+    eff = min(1.0, eff) if eff and eff > 0 else 1.0
+    rate = env_rate / procs * phys * (eff if phys > procs else 1.0)
+    return {"value": E * N / (E * N / rate + t_upd), "env_only": rate, "cores": phys, "scaling_factor": eff,
+            "basis": (f"measured per-process env rate at {procs} processes x {phys} physical cores x {eff:.3f} "
+                      f"(the measured 1 -> {procs}-process per-process ratio) + measured update time")}
 
 
 def cpu_model():
@@ -435,7 +444,8 @@ def cpu_baseline(E, N, B, radar, seconds, model="att", procs_req=None):
     per_proc = {"1_process": modes["scalar_1proc"]["env_only"], f"{procs}_processes": head["env_only"] / procs}
     return {"value": head["value"], "unit": "agent-env-steps/s", "cores": procs, "kind": "port",
             "physical_cores": phys, "affinity_cores": cores, "cpu_model": cpu_model(),
-            "per_physical_core_extrapolated": _extrapolate(head["env_only"], procs, phys, t_upd, E, N),
+            "per_physical_core_extrapolated": _extrapolate(head["env_only"], procs, phys, t_upd, E, N,
+                                                           eff=(head["env_only"] / procs) / modes["scalar_1proc"]["env_only"]),
             "sample": (f"mode 1: reference-shaped scalar env ({sref}, {radar} radar) on {procs} processes "
                        f"x 1 env x {N} agents, {sum(r[0] for r in m1)} env steps in ~{slot:.1f} s "
                        f"({head['env_only']:.3g} agent-env-steps/s env-only) + torch-CPU update_myown restatement "
@@ -661,6 +671,9 @@ def main():
             tr.step(update=True, time_env=True)
         torch.cuda.synchronize()
     env_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in tr.env_events]))
+    # the exact threshold fix-up list never overflowed in this run (else the surplus rays kept their float
+    # decisions): checked once, after the timed region (synchronises)
+    band = None if a.model == "uam" else tr.env.check_band_capacity()
     E_total = a.envs * ws
     N = a.agents
     value = E_total * N * a.steps / dt
@@ -738,7 +751,8 @@ def main():
                          "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": tsrc, "bytes_per_agent_step": bpa, "agents_per_launch": a.envs * N,
-                         "avg_launch_ms": env_ms},
+                         "avg_launch_ms": env_ms,
+                         "exact_band_list": None if band is None else {"most_per_launch": band[0], "capacity": band[1]}},
         "update_roofline": {"bound": "mfma", "unit": "TFLOP/s", "flop_per_update": upd_fl,
                             "achieved": upd_fl * upd_per_s / 1e12, "peak": peak,
                             "frac": upd_fl * upd_per_s / 1e12 / peak, "note": "whole-step rate bound"},

@@ -161,7 +161,8 @@ int aac_env_set_state(aac_env *env, const double *pos, const double *vel, const 
 
 /* Exact radar threshold bands: the most radar rays one launch flagged for the exact fix-up (a ray within
  * ~1e-9 of touching another agent's 64-gon or a cell corner, ATT/env:1089-1164, OM/env:1100-1141) and the
- * list's capacity (more would keep their float values).  Synchronises the stream. */
+ * list's capacity (more would keep their float values); for variant 1 also the most rewards one step
+ * listed for recomputation from the exact radar minimum (the larger of the two).  Synchronises the stream. */
 int aac_env_band_max(aac_env *env, int32_t *out, int32_t *cap, void *stream);
 
 /* Host utilities (no GPU). A* restates ATT/jps_straight.py:17-72 on a grid_w x grid_h x-major

@@ -69,8 +69,21 @@ struct Args {
     // resolved exactly by band_fix_kernel after the launch
     struct BandHdr *band_hdr;
     double2 *band_pos;
-    int32_t *band_cnt;   // [0] entries this launch (zeroed by band_fix_kernel), [1] most ever (overflow check)
+    int32_t *band_cnt;   // [0] entries this launch (zeroed by band_fix_kernel), [1] most ever (overflow check),
+                         // [2] / [3] the same for rfix
     int band_cap;
+    // variant 1 step: agents with a flagged ray, whose reward's near-building penalty (the radar minimum)
+    // band_fix_kernel recomputes from the exact radar (the kernel's minimum is the float one)
+    struct RewFix *rfix;
+};
+
+// a variant-1 agent whose reward band_fix_kernel recomputes: r = rp - nbp(rmin) (kind 1), (rp - nbp) +
+// 0.0 (kind 2, the normal-step branch), rp (kind 0: no penalty term), rmin over the agent's exact rays
+struct RewFix {
+    int32_t e, i, map, kind;
+    double rp;
+    double2 pos;
+    int64_t row;          // ring row of the env's transition (reward column), -1: none
 };
 
 // one flagged radar ray: env, agent, ray, kind (0 step: radar output + ring column, 1 reset: radar
@@ -494,6 +507,9 @@ __device__ __attribute__((always_inline)) void radar_phase(const Args &A, Lds &S
         const int e = emap ? emap[le] : e0 + le;
         const int slot = atomicAdd(A.band_cnt, 1);
         if (slot >= A.band_cap) continue;
+        // variant 1 step: the agent's reward uses its radar minimum -- mark it for the fix-up (S.flags
+        // bit 7, zeroed before the radar phase; the agent phase reads it after the barrier)
+        if (rmin) atomicOr(reinterpret_cast<unsigned *>(&S.flags[la & ~3]), 0x80u << (8 * (la & 3)));
         int64_t row = -1;
         if (ro.ring) {
             row = ro.pos + e;
@@ -575,9 +591,15 @@ struct WpView {
     __device__ double2 operator[](int k) const { return k < WPC ? lds[k] : hbm[k]; }
 };
 
+// the near-building penalty of WGRU/env ss_reward from the radar minimum (bug-compatible band)
+__device__ inline double wgru_nbp(double rmin, double pb) {
+    return (rmin >= pb && rmin <= 5) ? 3 * (((0 - 1) / (5 - pb)) * rmin + 2) : 0;
+}
+
+// rp, rk: the reward before its penalty term and how the term enters (RewFix)
 __device__ __attribute__((always_inline)) double wgru_reward(const Args &A, size_t ai, WpView wp, double2 pp, double2 p, double2 v, uint32_t rm,
                               int cnt, double rmin, int goal, int bnd, int building, int &flag, int &done, int &cg,
-                              uint8_t &fl, double2 start) {
+                              uint8_t &fl, double2 start, double &rp, int &rk) {
     const double px = p.x, py = p.y, pb = A.pb;
     int nrem = cnt - __popc(rm & (cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1u)));
     double smallest = INFINITY;
@@ -680,23 +702,30 @@ __device__ __attribute__((always_inline)) double wgru_reward(const Args &A, size
     const double sp = npnorm(v.x, v.y);
     const double clip = sp < 0 ? 0 : (sp > thr ? thr : sp);
     const double ssp = 3 * ((thr - clip) * (1.0 / thr));
-    const double nbp = (rmin >= pb && rmin <= 5) ? 3 * (((0 - 1) / (5 - pb)) * rmin + 2) : 0;
+    const double nbp = wgru_nbp(rmin, pb);
     double r;
     if (bnd) {
-        r = (((((0.0 + dref) - 5) + dtg) - ssp) + 0.0) - nbp;
+        rp = ((((0.0 + dref) - 5) + dtg) - ssp) + 0.0;
+        r = rp - nbp;
+        rk = 1;
         done = 1;
         fl |= 8;
     } else if (building) {
         done = 1;
         fl |= 16;
-        r = (((((0.0 + dref) - 5) + dtg) - ssp) + 0.0) - nbp;
+        rp = ((((0.0 + dref) - 5) + dtg) - ssp) + 0.0;
+        r = rp - nbp;
+        rk = 1;
     } else if (goal) {
         cg = 1;
-        r = (0.0 + 5) + 0.0;
+        r = rp = (0.0 + 5) + 0.0;
+        rk = 0;
     } else {
         r = 0.0;
         if (flag && nrem > 1) r = r + 3;
-        r = (((((r + dref) + dtg) - ssp) + 0.0) - nbp) + 0.0;
+        rp = (((r + dref) + dtg) - ssp) + 0.0;
+        r = (rp - nbp) + 0.0;
+        rk = 2;
     }
     return r;
 }
@@ -1126,7 +1155,10 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         S.goal[t] = gl;
         if (!A.variant) w0 = A.wp0[ai];     // = wp[cur]; variant 1: cur is a bit mask
     }
-    if (A.variant) S.rmin[t] = 0x7ff0000000000000ull;       // +inf
+    if (A.variant) {
+        S.rmin[t] = 0x7ff0000000000000ull;       // +inf
+        S.flags[t] = 0;                          // bit 7: a ray of this agent is in the band list
+    }
     // variant 1: the first WPC waypoints of every agent of the workgroup, loaded now by all threads
     // (one load each, in flight across the radar phase) and put in LDS after it
     constexpr int WPI = 2;           // items per thread held across the radar (nag <= 64); the rest after it
@@ -1243,11 +1275,26 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
         double r;
         if (A.variant) {
             const WpView wv{wp_cache(A) + t * WPC, A.wp + ai * A.W};
+            const bool fixr = (S.flags[t] & 0x80) != 0;      // read before the flags are rewritten below
+            double rp;
+            int rk;
             r = wgru_reward(A, ai, wv, pp, np, S.vel[t], (uint32_t)cur, wcnt,
-                            __longlong_as_double((long long)S.rmin[t]), goal, bnd, building, wpf, done, cg, fl, st0);
+                            __longlong_as_double((long long)S.rmin[t]), goal, bnd, building, wpf, done, cg, fl, st0,
+                            rp, rk);
             if (cg) {
                 reach = 1;
                 A.reach[ai] = 1;
+            }
+            if (fixr && A.rfix) {      // a ray of this agent is decided exactly after the launch: so is rmin
+                const int slot = atomicAdd(A.band_cnt + 2, 1);
+                if (slot < A.band_cap) {
+                    int64_t row = -1;
+                    if (TAIL && T.ring && T.late[LATE_REW] >= 0) {
+                        row = rpos + e;
+                        if (row >= T.cap) row -= T.cap;
+                    }
+                    A.rfix[slot] = RewFix{e, i, A.map_idx ? A.map_idx[e] : 0, rk, rp, np, row};
+                }
             }
         } else {
             // ATT/env:2266-2603: next waypoint in range, progress toward goal[-1]
@@ -1470,10 +1517,15 @@ struct FixArgs {
                                // the reset observation's radar (its ring row is still fixed)
     float *ring;
     int rw, col;
+    const RewFix *rfix;        // variant 1 step: rewards whose radar minimum is recomputed exactly
+    float *reward;
+    int rcol;                  // the ring's reward column (RewFix.row >= 0)
 };
 
 // The flagged rays of the launch before it (one workgroup; nothing to do in the common case), then the
-// list is emptied for the next launch.
+// list is emptied for the next launch.  Variant 1: the listed agents' rewards from the exact radar
+// minimum (all 18 rays re-run: away from the bands the exact radar is bit-identical to the float one,
+// oracle/aac_oracle.c observe_env takes the minimum over all of them).
 __global__ void __launch_bounds__(256) band_fix_kernel(FixArgs F) {
     const int n = *F.cnt;
     const int m = n < F.cap ? n : F.cap;
@@ -1483,12 +1535,33 @@ __global__ void __launch_bounds__(256) band_fix_kernel(FixArgs F) {
                                          F.occ + (size_t)h.map * F.gw * F.gh, F.gw, F.gh, F.gx0, F.gy0, F.bound);
         const size_t oi = ((size_t)h.e * F.N + h.i) * NRAY + h.r;
         if (h.kind == 1 || !(F.env_done && F.env_done[h.e])) F.radar[oi] = (float)d;
-        if (h.kind == 0 && F.ring && h.row >= 0) F.ring[h.row * F.rw + F.col + h.i * NRAY + h.r] = (float)d;
+        if (h.kind == 0 && F.ring && F.col >= 0 && h.row >= 0) F.ring[h.row * F.rw + F.col + h.i * NRAY + h.r] = (float)d;
+    }
+    const int nr = F.rfix ? F.cnt[2] : 0;
+    const int mr = nr < F.cap ? nr : F.cap;
+    for (int k = threadIdx.x; k < mr; k += 256) {
+        const RewFix x = F.rfix[k];
+        double rmin = INFINITY;
+        for (int r = 0; r < NRAY; ++r) {      // the obstacle radar: the agent's own position and map only
+            const double d = radar_ray_exact(&x.pos, 1, 0, r, F.pb, F.rlen, AAC_RADAR_OBSTACLES,
+                                             F.occ + (size_t)x.map * F.gw * F.gh, F.gw, F.gh, F.gx0, F.gy0, F.bound);
+            rmin = d < rmin ? d : rmin;
+        }
+        const double nbp = wgru_nbp(rmin, F.pb);
+        const double rew = x.kind == 0 ? x.rp : (x.kind == 1 ? x.rp - nbp : (x.rp - nbp) + 0.0);
+        F.reward[(size_t)x.e * F.N + x.i] = (float)rew;
+        if (F.ring && x.row >= 0) F.ring[x.row * F.rw + F.rcol + x.i] = (float)rew;
     }
     __syncthreads();
-    if (threadIdx.x == 0 && n) {
-        if (n > F.cnt[1]) F.cnt[1] = n;
-        F.cnt[0] = 0;
+    if (threadIdx.x == 0) {
+        if (n) {
+            if (n > F.cnt[1]) F.cnt[1] = n;
+            F.cnt[0] = 0;
+        }
+        if (nr) {
+            if (nr > F.cnt[3]) F.cnt[3] = nr;
+            F.cnt[2] = 0;
+        }
     }
 }
 
@@ -1535,6 +1608,7 @@ struct aac_env {
     BandHdr *band_hdr;        // radar threshold-band list (radar_phase, band_fix_kernel)
     double2 *band_pos;
     int32_t *band_cnt;
+    RewFix *rfix;             // variant 1: rewards recomputed from the exact radar minimum
 };
 
 constexpr int BAND_CAP = 16384;   // flagged rays per launch: never more than a few in practice; the
@@ -1605,13 +1679,14 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
     A.band_pos = h->band_pos;
     A.band_cnt = h->band_cnt;
     A.band_cap = BAND_CAP;
+    A.rfix = c.variant ? h->rfix : nullptr;
     return A;
 }
 
 // band_fix_kernel after a step / reset launch on the same stream (ring: the step tail's ring and its
 // late radar column, env_done: skip the radar output of envs the launch reset)
 static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, const uint8_t *env_done = nullptr,
-                            float *ring = nullptr, int rw = 0, int col = -1) {
+                            float *ring = nullptr, int rw = 0, int col = -1, int rcol = -1) {
     FixArgs F;
     F.hdr = h->band_hdr;
     F.pos = h->band_pos;
@@ -1629,9 +1704,12 @@ static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, con
     F.occ = A.occ;
     F.radar = A.radar;
     F.env_done = env_done;
-    F.ring = col >= 0 ? ring : nullptr;
+    F.ring = col >= 0 || rcol >= 0 ? ring : nullptr;
     F.rw = rw;
     F.col = col;
+    F.rfix = A.rfix;
+    F.reward = A.reward;
+    F.rcol = rcol;
     hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, F);
 }
 
@@ -1707,7 +1785,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     ALLOC(wp, EN * h->W) ALLOC(wp0, EN) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
     ALLOC(rlist, (size_t)c.E + 1)
-    ALLOC(band_hdr, (size_t)BAND_CAP) ALLOC(band_pos, (size_t)BAND_CAP * c.N) ALLOC(band_cnt, 2)
+    ALLOC(band_hdr, (size_t)BAND_CAP) ALLOC(band_pos, (size_t)BAND_CAP * c.N) ALLOC(band_cnt, 4) ALLOC(rfix, (size_t)BAND_CAP)
     h->episode_own = h->episode;
     ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
 #undef ALLOC
@@ -1738,7 +1816,7 @@ void aac_env_destroy(aac_env *h) {
     if (!h) return;
     void *ptrs[] = {h->pos, h->vel, h->pre_pos, h->pre_vel, h->goal, h->start, h->wp, h->wp0, h->wp_cur, h->wp_cnt, h->wall,
                     h->reach, h->step, h->map_idx, h->episode_own, h->occ, h->bank_start, h->bank_wp, h->bank_cnt,
-                    h->bank_off, h->rlist, h->occ_rows, h->band_hdr, h->band_pos, h->band_cnt};
+                    h->bank_off, h->rlist, h->occ_rows, h->band_hdr, h->band_pos, h->band_cnt, h->rfix};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -1773,7 +1851,7 @@ static int launch_step(aac_env *h, const float *actions, const aac_step_out *o, 
     else if (A.radar_mode == AAC_RADAR_OBSTACLES) STEP_LAUNCH(0, AAC_RADAR_OBSTACLES);
     else STEP_LAUNCH(0, AAC_RADAR_COMBINED);
 #undef STEP_LAUNCH
-    if (tail) launch_band_fix(h, A, st, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR]);
+    if (tail) launch_band_fix(h, A, st, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR], T.late[LATE_REW]);
     else launch_band_fix(h, A, st);
     HIPCHK(hipGetLastError());
     return AAC_OK;
@@ -1987,8 +2065,10 @@ int aac_env_reset_stamps(unsigned long long *out, int32_t n_wg) {
 
 int aac_env_band_max(aac_env *h, int32_t *out, int32_t *cap, void *stream) {
     if (!h || !out) return fail(AAC_E_INVALID, "null argument");
-    HIPCHK(hipMemcpyAsync(out, h->band_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    int32_t c[4];
+    HIPCHK(hipMemcpyAsync(c, h->band_cnt, sizeof(c), hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    *out = c[1] > c[3] ? c[1] : c[3];     // flagged rays, or (variant 1) rewards to recompute
     if (cap) *cap = BAND_CAP;
     return AAC_OK;
 }

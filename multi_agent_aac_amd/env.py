@@ -227,12 +227,21 @@ class BatchedEnv:
         self.bank_generation = getattr(self, "bank_generation", 0) + 1
 
     def band_max(self):
-        """(most radar rays one launch flagged for the exact threshold fix-up, the list's capacity):
-        aac_env_band_max (synchronises)."""
+        """(most radar rays one launch flagged for the exact threshold fix-up -- variant 1: or rewards
+        listed for the exact radar minimum --, the lists' capacity): aac_env_band_max (synchronises)."""
         n, cap = ctypes.c_int32(0), ctypes.c_int32(0)
         _native.check(_native.lib().aac_env_band_max(self._h, ctypes.byref(n), ctypes.byref(cap), _stream()),
                       "aac_env_band_max")
         return n.value, cap.value
+
+    def check_band_capacity(self):
+        """Raise if any launch flagged more threshold-band rays (or variant-1 rewards) than the fix-up
+        list holds: the surplus would have kept their float decisions.  Synchronises; the trainers call
+        it once at the end of a run."""
+        most, cap = self.band_max()
+        if most > cap:
+            raise RuntimeError(f"exact threshold fix-up list overflowed: {most} entries in one launch, capacity {cap}")
+        return most, cap
 
     def use_episode_buffer(self, episode: torch.Tensor):
         """Keep the per-env episode counter (advanced by every auto-reset) in ``episode`` (int32 [E],

@@ -532,3 +532,40 @@ def test_threshold_states_numpy_env(mode):
     own, radar, nei, reward, done, mask, env_done, bbc = ne.step(act)
     assert np.array_equal(np.asarray(mask, np.uint8), co.mask)
     np.testing.assert_allclose(ne.radar64, co.radar.astype(np.float64), rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("N", [3, 5])
+def test_near_band_ends_oracle(N):
+    """The near-drone band's 2.5 / 10 m ends made observable (tests/thresholds.build_near: a second
+    neighbour at 6 m sets the shortest distance, ATT/env:2420-2432): the C oracle's subject reward (team
+    reward off) is the reference's reward from np.linalg.norm distances, bit for bit in fp32, and the
+    threshold neighbour is in the band on one side of each end and out of it on the other."""
+    from tests import thresholds as T
+    fam, var, st, occ = T.build_near(N)
+    E = len(fam)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=0, team_reward=False)
+    T.oracle_state(co, st)
+    co.step(np.zeros((E, N, 2), np.float32))
+    seen = {}
+    for e, f in enumerate(fam):
+        pos = st["pos"][e]
+        assert co.reward[e, 0] == np.float32(T.near_reward(pos)), (f, var[e])
+        seen.setdefault(f, set()).add(2.5 <= T.float_norm(pos[0], pos[1]) <= 10.0)
+    assert seen == {"near10": {True, False}, "near2.5": {True, False}}, seen
+
+
+def test_wgru_threshold_states_oracle():
+    """The WGRU variant's C oracle on the exact-threshold states (obstacle radar): its integer outputs and
+    radar against the reference's semantics (tests/thresholds.check), the edge_near rays -- the subjects'
+    radar minima, inside the near-building penalty's band -- among them."""
+    from tests import thresholds as T
+    N = 3
+    fam, var, st, occ = T.build(N, seed=5)
+    E = len(fam)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=1, variant="wgru")
+    T.oracle_state(co, st)
+    co.step(np.zeros((E, N, 2), np.float32))
+    post = {"pos": co.pos.copy(), "pre_pos": co.pre_pos.copy(), "goal": co.goal.copy(), "wp": co.wp.copy()}
+    T.check(fam, var, post, occ, 1, co.mask, co.radar, where="c-oracle wgru")
+    near = [e for e, f in enumerate(fam) if f == "edge_near"]
+    assert near and all(2.5 <= co.radar[e, 0].min() <= 5.0 for e in near)

@@ -28,9 +28,15 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
-def _env(E, N, occ, mode):
+def _env(E, N, occ, mode, variant="att", **kw):
     from multi_agent_aac_amd.env import BatchedEnv
-    return BatchedEnv(E, N, occ, radar_mode=mode, max_wp=32)
+    return BatchedEnv(E, N, occ, radar_mode=mode, max_wp=32, variant=variant, **kw)
+
+
+# (variant, radar mode): the ATT env in its three radar modes, the WGRU env (config 4) with its obstacle
+# radar -- its reward's near-building penalty takes the radar minimum, so the exact fix-up recomputes the
+# rewards of agents with a flagged ray
+VARIANTS = [("att", 0), ("att", 1), ("att", 2), ("wgru", 1)]
 
 
 def _install(env, st):
@@ -55,20 +61,20 @@ def _both_ways(seen):
             assert outs == {True, False}, (f, outs)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("variant,mode", VARIANTS)
 @pytest.mark.parametrize("N", [3, 5, 8])
-def test_step_kernel_on_thresholds(native_lib, N, mode):
+def test_step_kernel_on_thresholds(native_lib, N, variant, mode):
     fam, var, st, occ = T.build(N, seed=N)
     E = len(fam)
-    env = _env(E, N, occ, mode)
-    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode)
+    env = _env(E, N, occ, mode, variant)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode, variant=variant)
     _install(env, st)
     T.oracle_state(co, st)
     act = np.zeros((E, N, 2), np.float32)
     env.step(torch.from_numpy(act).cuda())
     co.step(act)
     torch.cuda.synchronize()
-    where = f"step N{N} mode{mode}"
+    where = f"step N{N} {variant} mode{mode}"
     _cmp_oracle(env.bufs, co, where)
     s = env.get_state()
     post = {k: _np(s[k]) for k in ("pos", "pre_pos", "goal", "wp")}
@@ -81,19 +87,20 @@ def test_step_kernel_on_thresholds(native_lib, N, mode):
     assert (mode == 1 or most > 0) and most <= cap, (most, cap)
 
 
-@pytest.mark.parametrize("mode", [0, 2])
-def test_step_tail_on_thresholds(native_lib, mode):
+@pytest.mark.parametrize("variant,mode", [("att", 0), ("att", 2), ("wgru", 1)])
+def test_step_tail_on_thresholds(native_lib, variant, mode):
     """The fused step tail (the bench's launch): the threshold outcomes, and the ring rows' next-radar
-    column carries the exactly-decided radar too."""
+    column carries the exactly-decided radar too (WGRU: and the reward column the exact radar minimum's
+    near-building penalty)."""
     from multi_agent_aac_amd.memory import DeviceReplay
     N = 5
     fam, var, st, occ = T.build(N, seed=11)
     E = len(fam)
-    env = _env(E, N, occ, mode)
+    env = _env(E, N, occ, mode, variant)
     rep = DeviceReplay(2 * E, N, env.D0, seed=0)
     c, n = env.alloc_buffers(), env.alloc_buffers()
     _install(env, st)
-    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=mode, variant=variant)
     T.oracle_state(co, st)
     act = np.zeros((E, N, 2), np.float32)
     a_dev = torch.from_numpy(act).cuda()
@@ -102,7 +109,7 @@ def test_step_tail_on_thresholds(native_lib, mode):
     env.step_tail(a_dev, out=n, replay=rep, srcs=srcs, auto_reset=False)
     co.step(act)
     torch.cuda.synchronize()
-    where = f"tail mode{mode}"
+    where = f"tail {variant} mode{mode}"
     _cmp_oracle(n, co, where)
     s = env.get_state()
     post = {k: _np(s[k]) for k in ("pos", "pre_pos", "goal", "wp")}
@@ -112,6 +119,44 @@ def test_step_tail_on_thresholds(native_lib, mode):
     k = list(rep.fields).index("n_radar")
     ring = _np(rep.ring[pos0:pos0 + E])
     assert np.array_equal(ring[:, off[k]:off[k + 1]], co.radar.reshape(E, -1)), where + " ring n_radar"
+    k = list(rep.fields).index("rew")
+    np.testing.assert_allclose(ring[:, off[k]:off[k + 1]], co.reward, rtol=0, atol=ATOL, err_msg=where + " ring reward")
+    if variant == "wgru":       # agents with a flagged ray had their reward recomputed after the launch
+        most, cap = env.band_max()
+        assert 0 < most <= cap
+
+
+@pytest.mark.parametrize("N", [3, 5])
+def test_near_band_ends_observable(native_lib, N):
+    """The near-drone band's 2.5 / 10 m ends (ATT/env:2420-2432), each on the threshold and +-1-2 ulp,
+    with a second neighbour at 6 m so the in-band term m * shortest + c is non-zero:
+    the kernel's subject reward (team reward off) equals the reference's reward computed from
+    np.linalg.norm distances, the threshold neighbour included exactly when 2.5 <= d <= 10 -- and both
+    outcomes occur at both ends."""
+    fam, var, st, occ = T.build_near(N)
+    E = len(fam)
+    env = _env(E, N, occ, 0, team_reward=False)
+    co = c_oracle.BatchedOracle(E, N, occ, W=32, radar_mode=0, team_reward=False)
+    _install(env, st)
+    T.oracle_state(co, st)
+    act = np.zeros((E, N, 2), np.float32)
+    env.step(torch.from_numpy(act).cuda())
+    co.step(act)
+    torch.cuda.synchronize()
+    _cmp_oracle(env.bufs, co, f"near N{N}")
+    rew = _np(env.bufs.reward)[:, 0]
+    seen = {}
+    for e, f in enumerate(fam):
+        pos = st["pos"][e]
+        d = T.float_norm(pos[0], pos[1])
+        inside = 2.5 <= d <= 10.0
+        want = np.float32(T.near_reward(pos))
+        assert rew[e] == want, (f, var[e], d, rew[e], want)
+        # the two outcomes differ by one penalty term (>= 0.5): the reward decides which one the kernel took
+        other = np.float32(T.near_reward(pos) + (1 if inside else -1) * ((-1 / 7.5) * min(d, 6.0) + 4 / 3))
+        assert abs(float(rew[e]) - float(want)) < abs(float(rew[e]) - float(other))
+        seen.setdefault(f, set()).add(inside)
+    assert seen == {"near10": {True, False}, "near2.5": {True, False}}, seen
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])

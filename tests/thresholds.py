@@ -4,7 +4,8 @@ Each env of a batch puts its agent 0 (the subject) exactly on one predicate thre
 ATT/env:ss_reward or the radar -- and, in sibling envs, one ulp either side of it:
 
   drone      ||p_i - p_j|| = 5 (3-4-5 offsets; ATT/env:2228-2236, np.linalg.norm <= 2 pB)
-  near       neighbour distances 2.5 / 10, the near-drone band's ends (ATT/env:2430-2432)
+  near*      the near-drone band's 2.5 / 10 m ends (ATT/env:2430-2432): build_near, its own batch with a
+             second neighbour setting the shortest distance (else the 10-m end's term is exactly 0)
   wp         waypoint distance 5 (strict <, GEOS point distance; ATT/env:2297-2303)
   goal_apo   goal offset on the 3.5 cos(pi/64) apothem of the Minkowski 64-gon (ATT/env:2266-2269)
   goal_vtx   goal offset on a 3.5 circumradius vertex direction
@@ -18,6 +19,8 @@ ATT/env:ss_reward or the radar -- and, in sibling envs, one ulp either side of i
   corner     a ray through the corner of an isolated occupied cell, touching only that point
              (OM/env:1100-1141)
   edge_run   the 0-degree ray running along an occupied cell's top edge
+  edge_near  the same ray along a top / bottom edge from 3 or 4.5 m: the subject's radar minimum, so the
+             WGRU near-building penalty (WGRU/env ss_reward, pB <= min radar <= 5) rides on it
 
 The subject is stationary (zero velocity, zero action), so the kinematics leave its position bit
 for bit (``bound`` moves along an axis by an exact 2 m).  The other agents sit far away, out of the
@@ -94,7 +97,7 @@ class Batch:
         self.N, self.W = N, W
         self.rows = []          # (family, variant, pos (N,2), pre_pos, vel, goal (N,2), wps (N,W,2), cnt (N,))
 
-    def add(self, family, variant, subject, partner=None, goal=None, wp0=None, vel=None, pre=None):
+    def add(self, family, variant, subject, partner=None, goal=None, wp0=None, vel=None, pre=None, partner2=None):
         N, W = self.N, self.W
         pos = np.zeros((N, 2))
         for k in range(N):                           # fillers along the top, 12 m apart
@@ -102,6 +105,8 @@ class Batch:
         pos[0] = subject
         if partner is not None:
             pos[1] = partner
+        if partner2 is not None:
+            pos[2] = partner2
         goals = pos + np.array([0.0, -100.0])
         goals[0] = goal if goal is not None else (470.0, 262.0)
         wps = np.repeat(goals[:, None, :], W, axis=1).copy()
@@ -130,7 +135,7 @@ def build(N, seed=0):
     B = Batch(N)
     hx, hy = HOME
     # ---- drone contact at exactly 5 m and the near band's ends, with 1-ulp neighbours
-    for fam, (a, b) in (("drone", (3.0, 4.0)), ("near", (1.5, 2.0)), ("near", (6.0, 8.0))):
+    for fam, (a, b) in (("drone", (3.0, 4.0)),):
         for sx, sy, swap in ((1, 1, False), (-1, 1, True), (1, -1, False), (-1, -1, True)):
             ox, oy = (b, a) if swap else (a, b)
             for u in (-1, 0, 1):
@@ -194,8 +199,43 @@ def build(N, seed=0):
                         B.add("corner", u, (c[0], _up(c[1], u)))
         for u in (-1, 0, 1):
             B.add("edge_run", u, (x0 - 6.0, _up(y1, u)))
+            for d in (3.0, 4.5):
+                B.add("edge_near", u, (x0 - d, _up(y1, u)))
+                B.add("edge_near", u, (x0 - d, _up(y0, u)))
     fam, var, st = B.arrays()
     return fam, var, st, threshold_map()
+
+
+def build_near(N):
+    """The near-drone band's two ends made observable: the penalty of every in-band
+    neighbour is m * shortest + c (ATT/env:2420-2432), 0 at shortest = 10, so a second neighbour sets the
+    shortest distance.  Families: near10 (a neighbour at 6 m, the threshold one at 10 m = the 6-8-10
+    offset, +-1 ulp) and near2.5 (a neighbour at 6 m, the threshold one at 2.5 m = 1.5-2-2.5, +-1 ulp: a
+    drone contact too, whose branch still subtracts the penalty).  Needs N >= 3."""
+    assert N >= 3
+    B = Batch(N)
+    hx, hy = HOME
+    for fam, (a, b) in (("near10", (6.0, 8.0)), ("near2.5", (1.5, 2.0))):
+        for sx, sy, swap in ((1, 1, False), (-1, 1, True), (1, -1, False), (-1, -1, True)):
+            ox, oy = (b, a) if swap else (a, b)
+            for u in (-2, -1, 0, 1, 2):
+                B.add(fam, u, (hx, hy), partner=(_up(hx + sx * ox, u), hy + sy * oy), partner2=(hx, hy - sy * 6.0))
+    fam, var, st = B.arrays()
+    return fam, var, st, threshold_map()
+
+
+def near_reward(pos, vmax=5.0):
+    """The subject's own ss_reward (ATT/env:2315-2580; team reward off) for a stationary subject, from
+    np.linalg.norm distances: the near-drone penalty of each neighbour with 2.5 <= d <= 10 uses the
+    shortest distance (ATT/env:2425-2432); a contact (d <= 5) takes the drone branch (:2537-2545)."""
+    ds = [float_norm(pos[0], pos[j]) for j in range(1, len(pos))]
+    shortest = min(ds)
+    c_drone, m_drone = 1 + (2.5 / (10 - 2.5)), (0 - 1) / (10 - 2.5)
+    pen = 0.0
+    for d in ds:
+        pen = pen + (1 * (m_drone * shortest + c_drone)) if 2.5 <= d <= 10 else pen + 0
+    dtg = (1 * (0.0)) / vmax
+    return (((0.0 - 20) - 0.0) - pen) if any(d <= 2 * PB for d in ds) else dtg - pen
 
 
 # ------------------------------------------------------------------ exact expectations (rationals)
@@ -254,7 +294,7 @@ def float_norm(a, b):
     return float(np.linalg.norm(np.asarray(a, dtype=np.float64) - np.asarray(b, dtype=np.float64)))
 
 
-RADAR_FAMILIES = ("tangent", "start_on", "corner", "edge_run")
+RADAR_FAMILIES = ("tangent", "start_on", "corner", "edge_run", "edge_near")
 
 
 def check(families, variants, post, occ, mode, mask, radar, where=""):
@@ -270,9 +310,6 @@ def check(families, variants, post, occ, mode, mask, radar, where=""):
         if fam == "drone":
             want = float_norm(p[0], p[1]) <= 2 * PB
             got = bool(m & 2)
-        elif fam == "near":
-            d = float_norm(p[0], p[1])
-            want, got = (NEAR := (2.5 <= d <= 10.0)), NEAR      # reward-only: compared with the oracle
         elif fam == "wp":
             w = post["wp"][e, 0, 0]
             want = geos.point_dist(p[0, 0], p[0, 1], w[0], w[1]) < 5
