@@ -167,28 +167,6 @@ int aac_critic_head_job(const aac_head_job *job, void *stream);
 int aac_actor_out_bwd(const float *df, int32_t ldf, const float *wenc, int32_t din, int32_t d0, const float *X,
                       const float *wa, const float *ha, int32_t N, int32_t R, float *dout, float *dha, void *stream);
 
-/* CriticCombine.forward (ATT/nets:672-724, R3) over Bs samples in one launch, no intermediate
- * tensor: optionally the actor's tanh output layer first (ha != NULL: a_j = tanh(ha[b*N + n] . wa[j*256]
- * + ba[j]) replaces input columns d0, d0 + 1, and is written to Xout when not NULL), the per-agent
- * encoders f[b][n*128 + c] = relu(wenc[n][c] . X[b][n] + benc[n][c]) (written to f when not NULL), the
- * combine h[b][:] = relu(wc f[b] + bc) ([256][128 N] weights) and optionally the actor-loss head's
- * dual output dh = (h > 0) dscale dvec (dh != NULL).  din % 4 == 0, din <= 40, N <= 8.  nset = 1 or 2
- * independent sets; head (may be NULL, no chained head): a critic-head job as extra workgroups. */
-typedef struct {
-    const float *ha, *wa, *ba;
-    const float *X;
-    float *Xout;
-    const float *wenc, *benc;
-    float *f;
-    const float *wc, *bc;
-    float *h;
-    const float *dvec;
-    float *dh;
-    float dscale;
-    int32_t din, d0, N, Bs;
-} aac_critic_fwd_args;
-int aac_critic_fwd(const aac_critic_fwd_args *args, int32_t nset, const aac_head_job *head, void *stream);
-
 /* The actor step's critic data gradient and aac_actor_out_bwd in one launch (ATT/maddpg:421-425
  * backward): df = (dh Wc) * (f > 0) over B samples (dh [B][256], Wc the combine weight [256][ldw =
  * 128 N], f [B][ldw] the encoder outputs), reduced straight into da_j = df[b][n*128 ..] . W_enc_n[:, d0 + j]

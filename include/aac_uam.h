@@ -64,18 +64,6 @@ int aac_uam_reset(aac_uam *env, const uint8_t *env_mask_dev, const double *start
  * termination of UAM/main:624-637.  actions double[E][N][2] in [-1, 1]. */
 int aac_uam_step(aac_uam *env, const double *actions_dev, const aac_uam_out *out, void *stream);
 
-/* The fused step tail (config 5's training step; UAM/main:582-637): aac_uam_step with -- inside the
- * same launch -- the replay push of the E*N transitions (s_own double[E][N][7], s_radar
- * double[E][N][18] = the step's input observations, actions_dev, and this step's reward / done /
- * next rows) into ring rows [own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18] at
- * (pos + k) % capacity, writing meta = [new pos, new size] (ring NULL: no push); with reset != 0
- * the bank auto-reset of the finished envs follows (aac_uam_auto_reset's launches).  Bit-identical
- * to aac_uam_step + the learner library's aac_uam_push + aac_uam_auto_reset.  Replaces the
- * UAM/main:582-603 push loop (and the reset_world call of UAM/main:637 with reset). */
-int aac_uam_step_tail(aac_uam *env, const double *actions_dev, const aac_uam_out *out, double *ring,
-                      int64_t capacity, int64_t pos, int64_t size, int64_t *meta, const double *s_own_dev,
-                      const double *s_radar_dev, int32_t reset, void *stream);
-
 /* Episode bank for the GPU auto-reset: n whole episodes (start / goal double[n][N][2], clouds
  * int32[n][2]), host pointers.  aac_uam_auto_reset resets every env with env_done_dev[e] != 0
  * to bank entry hash(seed, e, episode[e]) (the reference draws a fresh episode per reset). */

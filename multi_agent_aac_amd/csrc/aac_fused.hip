@@ -1557,314 +1557,6 @@ __global__ void __launch_bounds__(256) actor_dcomb_out_bwd_kernel(DaobArgs P, in
     }
 }
 
-// ------------------------------------------------------------- critic forward on a 16-sample tile
-// CriticCombine.forward (ATT/nets:672-724, R3) for 16 samples x 64 of the 256 combine features per
-// workgroup (aac_critic_fwd): optionally the actor's tanh output layer first (a_j = tanh(ha . Wa[j] +
-// ba[j]) for the 16 N actor rows of the tile, ATT/nets:213; the actions replace the input rows' action
-// columns), the per-agent encoders f = relu(W_n [own_n | a_n] + b_n) for all 128 N features (in LDS:
-// the four column-tile workgroups of a sample block each recompute them, ~1/3 of their MFMA work),
-// then h = relu(Wc f + bc) for the tile's 64 columns, and optionally the actor-loss head's dual output
-// dh = (h > 0) dscale dvec.  Replaces the riding critic-encoder job and the combine's GEMM product.
-// Layout: workgroup b -> set s, sample block sb, column tile ct = local % 4 (the XCD of b % 8 then
-// touches one 64-row block of Wc); the encoders' k order is k = h S + s (S = din / 4: each lane's
-// weights are S consecutive floats), the combine's k = 64 c + 16 h + s (16-B loads of Wc rows).
-struct CfSet {
-    const float *ha, *wa, *ba;      // fold (ha != NULL): actor rows [Bs * N][256], output layer
-    const float *X;                 // input rows [Bs][N][din]
-    float *Xout;                    // fold: the actions are also written to Xout (NULL: not)
-    const float *wenc, *benc;       // [N][128][din], [N][128]
-    float *f;                       // encoder outputs [Bs][128 N] (NULL: kept in LDS only)
-    const float *wc, *bc;           // combine [256][128 N], [256]
-    float *h;                       // [Bs][256]
-    const float *dvec;              // dual output (dh != NULL): dh = (h > 0) dscale dvec
-    float *dh;
-    float dscale;
-    int din, d0, N, Bs;
-};
-struct CfBatch {
-    CfSet s[2];
-    int start[2];
-    int nset;
-    int hstart;
-    int dbg;                        // timing experiments only (AAC_CF_DBG): bit 0 no fold, 1 no encoder
-                                    // MFMA, 2 no combine MFMA
-    HeadJob hj;
-};
-constexpr int CF_DMAX = 40, CF_NMAX = 8;
-
-__device__ __forceinline__ int cf_fstride(int N) { return 128 * N + 4; }
-__device__ __forceinline__ int cf_xstride(int din) { return din + 1; }
-
-#ifdef AAC_CF_STAMPS
-// diagnostic build only (tools/cf_stamps.py): per-workgroup s_memtime at the phase boundaries
-__device__ unsigned long long g_cf_st[4096][8];
-#define CSTAMP(k)                                                                                        \
-    do {                                                                                                \
-        if (threadIdx.x == 0 && blockIdx.x < 4096) g_cf_st[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define CSTAMP(k) \
-    do {          \
-    } while (0)
-#endif
-__device__ __forceinline__ int s_dummy(int c) { return c & 3; }
-constexpr int CF_DS = CF_DMAX / 4;                                 // encoder k steps (max)
-
-// Every global load of a phase is in flight before the phase starts (one wave per SIMD: the phases are
-// latency chains, tools/cf_stamps.py): at entry the folded output layer's actor rows (four passes of
-// 16 rows), the input rows (16-B loads), every encoder weight this lane needs (CF_EB tiles per batch:
-// a lane's k slice of a weight row is Sd consecutive floats) and the loop-invariant vectors; the
-// combine's Wc rows CF_WD chunks ahead, the first ones issued before the encoders.
-constexpr int CF_EB = 10;        // encoder tiles per weight batch (2 N tiles per wave: one batch to N = 5)
-constexpr int CF_WD = 4;         // combine: 64-k chunks of Wc in flight
-__global__ void __launch_bounds__(256) critic_fwd_kernel(CfBatch P) {
-    extern __shared__ f4 cf_smem4[];
-    if ((int)blockIdx.x >= P.hstart) {
-        const HeadJob J = P.hj;
-        head_rows<false>(J, blockIdx.x - P.hstart);
-        return;
-    }
-    CSTAMP(0);
-    const int si = (P.nset > 1 && (int)blockIdx.x >= P.start[1]) ? 1 : 0;
-    const CfSet &S = P.s[si];
-    const int local = blockIdx.x - P.start[si];
-    const int ct = local & 3, sb = local >> 2;
-    const int N = S.N, din = S.din, Sd = din >> 2;
-    const int b0 = sb * 16;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6, ln = lane & 15, hq = lane >> 4;
-    const int FS = cf_fstride(N), XS = cf_xstride(din);
-    float *sF = reinterpret_cast<float *>(cf_smem4);          // [16][FS] encoder outputs
-    float *sX = sF + 16 * FS;                                  // [16 N][XS] input rows
-    float *sA = sX + 16 * N * XS;                              // [16 N][2] folded actions
-    float *sB = sA + 32 * N;                                   // [128 N] encoder biases
-    const int nrow = 16 * N;
-    const int rows_ok = S.Bs - b0 < 16 ? S.Bs - b0 : 16;      // samples of this block
-    const bool fold = S.ha && !(P.dbg & 1);
-    // ---- entry: the first fold round's actor rows (lanes (row rr, 16 columns c): 4 x 16 B per pass)
-    const int rr = t >> 4, cc = t & 15;
-    f4 hv[4][4];
-    auto ha_load = [&](int p0) {
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-            const int q = 16 * (p0 + pp) + rr;
-            const bool ok = fold && p0 + pp < N && q < rows_ok * N;
-            const f4 *hp = reinterpret_cast<const f4 *>(S.ha + ((size_t)b0 * N + (ok ? q : 0)) * 256 + 16 * cc);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) hv[pp][u] = ok ? hp[u] : f4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-    };
-    ha_load(0);
-    // the input rows as 16-B items i4 (row q = i4 / Sd, magic division), rows past the block's samples 0
-    constexpr int XU4 = (16 * CF_NMAX * CF_DMAX / 4 + 255) / 256;
-    const uint64_t msd = ((1ull << 32) + (uint64_t)Sd - 1) / (uint64_t)Sd;   // exact for i4 < 2^16
-    f4 xv[XU4];
-    const int nx4 = nrow * Sd;
-    const f4 *xs4 = reinterpret_cast<const f4 *>(S.X + (size_t)b0 * N * din);
-#pragma unroll
-    for (int u = 0; u < XU4; ++u) {
-        const int i4 = t + 256 * u;
-        const int q = (int)(((uint64_t)i4 * msd) >> 32);
-        xv[u] = (i4 < nx4 && q < rows_ok * N && !(P.dbg & 8)) ? xs4[i4] : f4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
-    // the encoder weights of this wave's tiles tl = w + 4 j (agent tl / 8, features (tl % 8) * 16): a
-    // lane's slice of weight row f0 + ln is k = hq Sd .. hq Sd + Sd - 1
-    const int ntile = 2 * N;
-    float ev[CF_EB][CF_DS];
-    auto enc_load = [&](int j0) {
-#pragma unroll
-        for (int jj = 0; jj < CF_EB; ++jj) {
-            const int j = j0 + jj, tl = w + 4 * j, n = tl >> 3, f0 = (tl & 7) * 16;
-            const bool ok = j < ntile && !(P.dbg & 32);
-            const float *wr = S.wenc + ((size_t)(ok ? n : 0) * 128 + f0 + ln) * din + hq * Sd;
-            if ((Sd & 1) == 0) {
-#pragma unroll
-                for (int s2 = 0; s2 < CF_DS / 2; ++s2) {
-                    const f2 v = (ok && 2 * s2 < Sd) ? reinterpret_cast<const f2 *>(wr)[s2] : f2{0.0f, 0.0f};
-                    ev[jj][2 * s2] = v.x;
-                    ev[jj][2 * s2 + 1] = v.y;
-                }
-            } else {
-#pragma unroll
-                for (int s = 0; s < CF_DS; ++s) ev[jj][s] = (ok && s < Sd) ? wr[s] : 0.0f;
-            }
-        }
-    };
-    enc_load(0);
-    // loop-invariant vectors: encoder biases (to LDS), the combine bias / dual-output vector of this
-    // lane's four columns, the output layer
-    float bz[(CF_NMAX * 128 + 255) / 256];
-#pragma unroll
-    for (int u = 0; u < (CF_NMAX * 128 + 255) / 256; ++u) {
-        const int i = t + 256 * u;
-        bz[u] = i < 128 * N ? S.benc[i] : 0.0f;
-    }
-    const int c4 = 64 * ct + 16 * w + 4 * hq;
-    const f4 bcv = *reinterpret_cast<const f4 *>(S.bc + c4);
-    const f4 dvv = S.dh ? *reinterpret_cast<const f4 *>(S.dvec + c4) : f4{0.0f, 0.0f, 0.0f, 0.0f};
-    f4 wa0[4], wa1[4];
-    float bb0 = 0.0f, bb1 = 0.0f;
-    if (fold) {
-        const f4 *w0 = reinterpret_cast<const f4 *>(S.wa + 16 * cc), *w1 = reinterpret_cast<const f4 *>(S.wa + 256 + 16 * cc);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            wa0[q] = w0[q];
-            wa1[q] = w1[q];
-        }
-        bb0 = S.ba[0];
-        bb1 = S.ba[1];
-    }
-    // ---- input rows and biases to LDS
-#pragma unroll
-    for (int u = 0; u < XU4; ++u) {
-        const int i4 = t + 256 * u;
-        if (i4 < nx4) {
-            const int q = (int)(((uint64_t)i4 * msd) >> 32), k = 4 * (i4 - q * Sd);
-            float *d = sX + q * XS + k;
-            d[0] = xv[u].x;
-            d[1] = xv[u].y;
-            d[2] = xv[u].z;
-            d[3] = xv[u].w;
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < (CF_NMAX * 128 + 255) / 256; ++u) {
-        const int i = t + 256 * u;
-        if (i < 128 * N) sB[i] = bz[u];
-    }
-    CSTAMP(1);
-    if (fold) {
-        // the actor's output layer, as the riding job's fold: lanes (row, c) take columns 16c .. 16c + 15
-        // of the 256-wide row, a 16-lane butterfly sums them (bit-identical to critic_enc_rows' fold)
-        for (int p0 = 0; p0 < N; p0 += 4) {
-            if (p0 > 0) ha_load(p0);
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                if (p0 + pp >= N) break;
-                const int q = 16 * (p0 + pp) + rr;
-                float p0s = 0.0f, p1s = 0.0f;
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        p0s = fmaf(hv[pp][u][e], wa0[u][e], p0s);
-                        p1s = fmaf(hv[pp][u][e], wa1[u][e], p1s);
-                    }
-#pragma unroll
-                for (int o = 8; o >= 1; o >>= 1) {
-                    p0s += __shfl_xor(p0s, o, 16);
-                    p1s += __shfl_xor(p1s, o, 16);
-                }
-                if (cc == 0) {
-                    const float a0 = tanhf(p0s + bb0), a1 = tanhf(p1s + bb1);
-                    sA[2 * q] = a0;
-                    sA[2 * q + 1] = a1;
-                    if (q < rows_ok * N && S.Xout && ct == 0) {
-                        float *xo = S.Xout + ((size_t)b0 * N + q) * din + S.d0;
-                        xo[0] = a0;
-                        xo[1] = a1;
-                    }
-                }
-            }
-        }
-    }
-    // the combine's first Wc chunks (columns 64 ct + 16 w + ln, k = 64 c + 16 hq + s), in flight across
-    // the encoders
-    const int col = 64 * ct + 16 * w + ln;
-    const float *wrow = S.wc + (size_t)col * 128 * N;
-    const int nch = 2 * N;
-    float wq[CF_WD][16];
-#pragma unroll
-    for (int c = 0; c < CF_WD; ++c)
-        if (c < nch && !(P.dbg & 16)) ld16(wrow + 64 * c + 16 * hq, wq[c]);
-        else
-#pragma unroll
-            for (int s = 0; s < 16; ++s) wq[c][s] = 0.0f;
-    CSTAMP(2);
-    __syncthreads();
-    if (fold)
-        for (int q = t; q < nrow; q += 256) {
-            sX[q * XS + S.d0] = sA[2 * q];
-            sX[q * XS + S.d0 + 1] = sA[2 * q + 1];
-        }
-    __syncthreads();
-    CSTAMP(3);
-    // ---- encoders: C[feature][sample] = W_n[f][k] . x[sample][n][k]; lane (ln, hq): features f0 + 4hq
-    // .. + 3 of sample ln
-    for (int j0 = 0; j0 < ntile; j0 += CF_EB) {
-        if (j0 > 0) enc_load(j0);
-#pragma unroll
-        for (int jj = 0; jj < CF_EB; ++jj) {
-            if (j0 + jj >= ntile) break;
-            const int tl = w + 4 * (j0 + jj), n = tl >> 3, f0 = (tl & 7) * 16;
-            const float *xr = sX + (ln * N + n) * XS + hq * Sd;
-            f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (!(P.dbg & 2))
-#pragma unroll
-                for (int s = 0; s < CF_DS; ++s)
-                    if (s < Sd) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ev[jj][s], xr[s], acc, 0, 0, 0);
-            const f4 bv = *reinterpret_cast<const f4 *>(sB + n * 128 + f0 + 4 * hq);
-            f4 v;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float x = acc[e] + bv[e];
-                v[e] = x > 0.0f ? x : 0.0f;
-            }
-            *reinterpret_cast<f4 *>(sF + ln * FS + n * 128 + f0 + 4 * hq) = v;
-            if (S.f && ct == 0 && ln < rows_ok)
-                *reinterpret_cast<f4 *>(S.f + (size_t)(b0 + ln) * 128 * N + n * 128 + f0 + 4 * hq) = v;
-        }
-    }
-    CSTAMP(4);
-    __syncthreads();
-    CSTAMP(5);
-    // ---- combine over K = 128 N in 64-k chunks, CF_WD chunks of Wc in flight
-    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int c = 0; c < nch; ++c) {
-        float cur[16];
-#pragma unroll
-        for (int s = 0; s < 16; ++s) cur[s] = wq[0][s];
-#pragma unroll
-        for (int d = 0; d + 1 < CF_WD; ++d)
-#pragma unroll
-            for (int s = 0; s < 16; ++s) wq[d][s] = wq[d + 1][s];
-        if (c + CF_WD < nch && !(P.dbg & 16)) ld16(wrow + 64 * (c + CF_WD) + 16 * hq, wq[CF_WD - 1]);
-        const float *fr = sF + ln * FS + 64 * c + 16 * hq;
-        float bf[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f4 x = *reinterpret_cast<const f4 *>(fr + 4 * q);
-            bf[4 * q] = x.x;
-            bf[4 * q + 1] = x.y;
-            bf[4 * q + 2] = x.z;
-            bf[4 * q + 3] = x.w;
-        }
-        if (!(P.dbg & 4))
-#pragma unroll
-            for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[s], bf[s], acc, 0, 0, 0);
-        else
-            acc[s_dummy(c)] += cur[c & 15] * bf[c & 15];
-    }
-    CSTAMP(6);
-    // lane (ln, hq): columns 64 ct + 16 w + 4 hq .. + 3 of sample b0 + ln
-    if (ln < rows_ok) {
-        const int b = b0 + ln;
-        f4 hv2;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float x = acc[j] + bcv[j];
-            hv2[j] = x > 0.0f ? x : 0.0f;
-        }
-        *reinterpret_cast<f4 *>(S.h + (size_t)b * 256 + c4) = hv2;
-        if (S.dh) {
-            f4 g;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) g[j] = hv2[j] > 0.0f ? S.dscale * dvv[j] : 0.0f;
-            *reinterpret_cast<f4 *>(S.dh + (size_t)b * 256 + c4) = g;
-        }
-    }
-    CSTAMP(7);
-}
-
 // the six neighbour features of slot `lane` of row `row` (lanes >= K hold zeros), for the mask sum
 __device__ __forceinline__ void ld_nei6(const float *nei, int row, int K, int lane, float (&nb)[6]) {
     if (lane < K) {
@@ -3063,66 +2755,6 @@ int aac_critic_head_job(const aac_head_job *job, void *stream) {
     if (job->M <= 0) return 0;
     if (head_check(*job)) return -1;
     hipLaunchKernelGGL(head_kernel, dim3((job->M + 3) / 4), dim3(256), 0, (hipStream_t)stream, head_job(*job));
-    FHIP(hipGetLastError());
-    return 0;
-}
-
-static int critic_fwd_check(const aac_critic_fwd_args &a) {
-    if (a.Bs <= 0) return 0;
-    if (a.N < 1 || a.N > CF_NMAX) return ffail("critic_fwd: 1 <= N <= 8");
-    if (a.din < 4 || a.din > CF_DMAX || a.din % 4) return ffail("critic_fwd: din % 4 == 0, 4 <= din <= 40");
-    if (!a.X || !a.wenc || !a.benc || !a.wc || !a.bc || !a.h) return ffail("critic_fwd: null operand");
-    if (a.ha && (!a.wa || !a.ba || a.d0 < 0 || a.d0 + 2 > a.din || !aligned16(a.ha) || !aligned16(a.wa)))
-        return ffail("critic_fwd: fold needs wa, ba, d0 + 2 <= din, 16-B aligned ha / wa");
-    if (a.dh && !a.dvec) return ffail("critic_fwd: the dual output needs dvec");
-    if (!aligned16(a.wc) || !aligned16(a.bc) || !aligned16(a.benc) || !aligned16(a.h) || (a.f && !aligned16(a.f)) ||
-        (a.dh && (!aligned16(a.dh) || !aligned16(a.dvec))))
-        return ffail("critic_fwd: wc, bc, benc, h, f, dh, dvec must be 16-B aligned");
-    return 0;
-}
-
-#ifdef AAC_CF_STAMPS
-int aac_cf_stamps(unsigned long long *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cf_st), sizeof(g_cf_st)) == hipSuccess ? 0 : -1;
-}
-#endif
-
-int aac_critic_fwd(const aac_critic_fwd_args *args, int32_t nset, const aac_head_job *head, void *stream) {
-    if (!args || nset < 1 || nset > 2) return ffail("critic_fwd: 1 or 2 argument sets");
-    CfBatch P{};
-    P.nset = nset;
-    static const int dbg = env_int("AAC_CF_DBG", 0);
-    P.dbg = dbg;
-    int total = 0;
-    size_t lds = 0;
-    for (int s = 0; s < nset; ++s) {
-        const aac_critic_fwd_args &a = args[s];
-        if (critic_fwd_check(a)) return -1;
-        P.s[s] = CfSet{a.ha, a.wa, a.ba, a.X, a.Xout, a.wenc, a.benc, a.f, a.wc, a.bc, a.h, a.dvec, a.dh, a.dscale,
-                       a.din, a.d0, a.N, a.Bs};
-        P.start[s] = total;
-        if (a.Bs > 0) {
-            total += 4 * ((a.Bs + 15) / 16);
-            const size_t b = 4 * ((size_t)16 * (128 * a.N + 4) + (size_t)16 * a.N * (a.din + 1) + 32 * (size_t)a.N +
-                                  128 * (size_t)a.N);
-            lds = std::max(lds, b);
-        }
-    }
-    P.hstart = total;
-    if (head) {
-        if (head_check(*head)) return -1;
-        if (head->M2 > 0) return ffail("critic_fwd: a chained head job runs alone (aac_critic_head_job)");
-        P.hj = head_job(*head);
-        total += (std::max(head->M, 0) + 3) / 4;
-    }
-    if (total == 0) return 0;
-    static bool attr = false;      // dynamic LDS beyond 64 KB (N = 8: ~86 KB)
-    if (!attr) {
-        FHIP(hipFuncSetAttribute(reinterpret_cast<const void *>(critic_fwd_kernel),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
-    hipLaunchKernelGGL(critic_fwd_kernel, dim3(total), dim3(256), lds, (hipStream_t)stream, P);
     FHIP(hipGetLastError());
     return 0;
 }

@@ -73,15 +73,6 @@ struct UReset {
                               // workgroup b takes envs b*epb ... (mask-filtered)
 };
 
-// the fused step tail (aac_uam_step_tail): the replay push of the step's transitions inside the step
-// launch
-struct UTail {
-    double *ring;             // [cap][54] replay rows (UamReplay); NULL: no push
-    int64_t cap, pos, new_pos, new_size;
-    int64_t *meta;            // the ring's device [pos, size]
-    const double *s_own, *s_radar, *act;    // the transitions' s and a (E*N rows of 7 / 18 / 2)
-};
-
 #ifdef AAC_UAM_STAMPS
 // phase timestamps of the first 64 workgroups of uam_step_kernel (probe builds only)
 __device__ unsigned long long g_uam_st[64][16];
@@ -691,18 +682,10 @@ __device__ __attribute__((always_inline)) void reset_envs(const UArgs &A, const 
 }
 
 // ------------------------------------------------------------------------------- step
-// TAIL: the fused step tail -- after the step, the workgroup's transitions into the replay ring and
-// the bank reset of its finished envs (aac_uam_step_tail: the launches of aac_uam_step, aac_uam_push
-// and aac_uam_auto_reset in one, the same results)
-// TAIL: + the replay push of the workgroup's transitions (aac_uam_step_tail; off in the trainer: the
-// launch grows 188 -> 234 us against the 23-us push launch it replaces).  The bank reset of the
-// finished envs inside this launch as well (each workgroup resetting its own envs after the push) was
-// built, bit-exact, and measured slower: config 5 226 vs 238 M agent-env-steps/s -- ~28 % of the envs
-// finish per step, so ~73 % of the 4-env workgroups ran the whole reset pipeline for ~1 env, where
-// the packed reset launch runs full workgroups of resetting envs only.
-template <bool TAIL>
-__global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArgs A, const double2 *__restrict__ act,
-                                                                           UReset R, UTail T) {
+// (the replay push inside this launch was built, bit-exact, and measured slower: the launch grew 188 ->
+// 234 us against the 23-us push launch it replaced; so was the bank reset of the finished envs in it,
+// config 5 226 vs 238 M agent-env-steps/s; round 5, removed in round 6)
+__global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArgs A, const double2 *__restrict__ act) {
     __shared__ Lds S;
 
     const int N = A.N, K = A.K;
@@ -970,51 +953,6 @@ __global__ void __launch_bounds__(BLOCK, AAC_UAM_MIN_WAVES) uam_step_kernel(UArg
         A.env_done[eq] = (uint8_t)((A.episode_length < st) || any_done || all_reach);
     }
     USTAMP(15);
-    if constexpr (TAIL) {
-        __syncthreads();         // the workgroup's rewards, done flags and next observation rows are out
-        const int nv = e0 + A.epb <= A.E ? A.epb : A.E - e0;
-        if (T.ring && nv > 0) {
-            // the transitions (s, a, r, done, s') of the workgroup's aircraft as ring rows
-            // [own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18] (UamReplay; UAM/main:582-603):
-            // consecutive threads write consecutive doubles of the rows
-            if (blockIdx.x == 0 && t == 0 && T.meta) {
-                T.meta[0] = T.new_pos;
-                T.meta[1] = T.new_size;
-            }
-            // every load of the workgroup's rows in flight before the first store (a load-store loop
-            // waited a memory latency per element)
-            const int64_t a0 = (int64_t)e0 * N;
-            const int tot = nv * N * 54;
-            const double *__restrict__ so = T.s_own, *__restrict__ sr = T.s_radar, *__restrict__ sa = T.act;
-            constexpr int PER = (MAXA * 54 + BLOCK - 1) / BLOCK;
-            double v[PER];
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int k = t + u * BLOCK;
-                const int kk = k < tot ? k : 0;
-                const int rr = kk / 54, c = kk - rr * 54;
-                const size_t q = (size_t)a0 + rr;
-                if (c < 7) v[u] = so[q * 7 + c];
-                else if (c < 25) v[u] = sr[q * 18 + (c - 7)];
-                else if (c < 27) v[u] = sa[q * 2 + (c - 25)];
-                else if (c == 27) v[u] = A.reward[q];
-                else if (c == 28) v[u] = (double)A.done[q];
-                else if (c < 36) v[u] = A.own[q * 7 + (c - 29)];
-                else v[u] = A.radar[q * 18 + (c - 36)];
-            }
-            double *__restrict__ ring = T.ring;
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int k = t + u * BLOCK;
-                if (k < tot) {
-                    const int rr = k / 54, c = k - rr * 54;
-                    int64_t row = T.pos + a0 + rr;
-                    if (row >= T.cap) row -= T.cap;
-                    ring[row * 54 + c] = v[u];
-                }
-            }
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------ reset
@@ -1323,42 +1261,9 @@ int aac_uam_step(aac_uam *h, const double *actions, const aac_uam_out *o, void *
     if (rc) return rc;
     if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return ufail(AAC_E_INVALID, "step outputs");
     UArgs A = make_uargs(h, o);
-    hipLaunchKernelGGL(uam_step_kernel<false>, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A,
-                       reinterpret_cast<const double2 *>(actions), UReset{}, UTail{});
+    hipLaunchKernelGGL(uam_step_kernel, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A,
+                       reinterpret_cast<const double2 *>(actions));
     UCHK(hipGetLastError());
-    return AAC_OK;
-}
-
-int aac_uam_step_tail(aac_uam *h, const double *actions, const aac_uam_out *o, double *ring, int64_t capacity,
-                      int64_t pos, int64_t size, int64_t *meta, const double *s_own, const double *s_radar,
-                      int32_t reset, void *stream) {
-    if (!h || !actions) return ufail(AAC_E_INVALID, "null argument");
-    int rc = check_uout(o);
-    if (rc) return rc;
-    if (!o->reward || !o->done || !o->mask || !o->env_done || !o->bbc) return ufail(AAC_E_INVALID, "step outputs");
-    const int64_t M = (int64_t)h->cfg.E * h->cfg.N;
-    UTail T{};
-    if (ring) {
-        if (!s_own || !s_radar || !meta) return ufail(AAC_E_INVALID, "step_tail: push needs s_own, s_radar and meta");
-        if (M > capacity || pos < 0 || pos >= capacity || size < 0 || size > capacity)
-            return ufail(AAC_E_INVALID, "step_tail: E*N > capacity or pos / size out of range");
-        T.ring = ring;
-        T.cap = capacity;
-        T.pos = pos;
-        T.new_pos = (pos + M) % capacity;
-        T.new_size = std::min<int64_t>(size + M, capacity);
-        T.meta = meta;
-        T.s_own = s_own;
-        T.s_radar = s_radar;
-        T.act = actions;
-    }
-    if (reset && !h->bank_n) return ufail(AAC_E_STATE, "step_tail: no episode bank installed (aac_uam_set_bank)");
-    UArgs A = make_uargs(h, o);
-    hipLaunchKernelGGL(uam_step_kernel<true>, dim3(h->blocks), dim3(BLOCK), dist_bytes(h), (hipStream_t)stream, A,
-                       reinterpret_cast<const double2 *>(actions), UReset{}, T);
-    UCHK(hipGetLastError());
-    // the finished envs: the packed bank reset (compaction + reset launches, as aac_uam_auto_reset)
-    if (reset) return aac_uam_auto_reset(h, o->env_done, o, stream);
     return AAC_OK;
 }
 

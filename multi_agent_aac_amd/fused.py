@@ -69,14 +69,6 @@ class DaobArgs(ctypes.Structure):
                 ("dha", vp), ("ldw", i32), ("din", i32), ("d0", i32), ("N", i32), ("B", i32)]
 
 
-class CfArgs(ctypes.Structure):
-    """aac_critic_fwd_args (include/aac_fused.h): CriticCombine.forward over Bs samples in one launch
-    (optionally with the actor's output layer folded in first and the actor-loss head's dual output)."""
-    _fields_ = [("ha", vp), ("wa", vp), ("ba", vp), ("X", vp), ("Xout", vp), ("wenc", vp), ("benc", vp), ("f", vp),
-                ("wc", vp), ("bc", vp), ("h", vp), ("dvec", vp), ("dh", vp), ("dscale", f32), ("din", i32),
-                ("d0", i32), ("N", i32), ("Bs", i32)]
-
-
 GEMM_MAX = 16
 HEAD_MAX = 1
 _L = None
@@ -103,7 +95,6 @@ def lib():
         L.aac_attn_block.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
         L.aac_actor_out_bwd.argtypes = [vp, i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp]
         L.aac_actor_dcomb_out_bwd.argtypes = [ctypes.POINTER(DaobArgs), ctypes.POINTER(HeadJob), vp]
-        L.aac_critic_fwd.argtypes = [ctypes.POINTER(CfArgs), i32, ctypes.POINTER(HeadJob), vp]
         L.aac_attn_train_fwd.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]
         L.aac_attn_train_bwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, i32, i32,
                                          vp]
@@ -396,49 +387,6 @@ def adam_at(opt, step_add, gscale=1.0):
          "aac_adam_flat_at_scaled")
 
 
-def critic_fwd_set(cp, X, rows, N, Din, f, h, fold=None, dual=None, write_f=True):
-    """Argument set of aac_critic_fwd: CriticCombine.forward (ATT/nets:672-724, R3) of ``rows``
-    samples with inputs X[b][n][:Din] = [own_n | a_n].  ``fold`` = (ha, ap, d0): the actor's tanh output
-    layer over the actor rows ha[b*N + n] first (ATT/nets:213; the actions land in X's action columns).
-    ``dual`` = (dvec, dh, dscale): the actor-loss head's gradient dh = (h > 0) dscale dvec."""
-    a = CfArgs()
-    a.X, a.wenc, a.benc, a.wc, a.bc, a.h = X, cp.enc_w[0], cp.enc_b[0], cp.Wc, cp.bc, ptr(h)
-    a.f = ptr(f) if (f is not None and write_f) else 0
-    a.din, a.N, a.Bs = Din, N, rows
-    if fold is not None:
-        ha, ap, d0 = fold
-        a.ha, a.wa, a.ba, a.Xout, a.d0 = ha, ap.Wa, ap.ba, X, d0
-    if dual is not None:
-        a.dvec, a.dh, a.dscale = dual[0], ptr(dual[1]), dual[2]
-    return a
-
-
-class CriticFwd:
-    """One aac_critic_fwd launch over one or two independent argument sets (CfArgs), plus an optional
-    critic-head job.  Algorithmic cost per sample: the encoders 2*128*Din per agent, the combine
-    2*256*128 N, the folded output layer 2*2*256 per agent row; bytes: X (and ha) read, f and h
-    (and dh) written, weights read once."""
-
-    def __init__(self, *sets, head=None):
-        assert 1 <= len(sets) <= 2
-        self.n = len(sets)
-        self.arr = (CfArgs * self.n)(*sets)
-        self.head = head
-        self.flops, self.bytes = 0.0, 0.0
-        for a in sets:
-            Bs, N, din = int(a.Bs), int(a.N), int(a.din)
-            self.flops += Bs * (N * 2.0 * 128 * din + 2.0 * 256 * 128 * N + (N * 4.0 * 256 if a.ha else 0.0))
-            self.bytes += 4.0 * (Bs * N * din + (Bs * N * 256 if a.ha else 0) + (Bs * 128 * N if a.f else 0)
-                                 + Bs * 256 * (2 if a.dh else 1) + N * 128 * (din + 1) + 256 * (128 * N + 1))
-        if head is not None:
-            self.flops += 2.0 * 256 * head.M
-            self.bytes += 4.0 * 256 * head.M * (1 if head.mode == 2 else 2)
-
-    def __call__(self):
-        h = ctypes.byref(self.head) if self.head is not None else None
-        _chk(lib().aac_critic_fwd(self.arr, self.n, h, _stream()), "aac_critic_fwd")
-
-
 class DcombAob:
     """One aac_actor_dcomb_out_bwd launch: the actor step's critic data gradient df = (dh Wc) * (f > 0)
     reduced straight into the actor's output-layer backward (dout, dha), plus an optional critic-head
@@ -670,13 +618,6 @@ class FusedUpdate:
     # the actor step's critic data gradient + actor output backward as one launch (DcombAob) instead of
     # a grouped-GEMM product and actor_out_bwd; AAC_DAOB=0 restores the two launches
     DAOB = os.environ.get("AAC_DAOB", "1") == "1"
-    # CriticCombine.forward as one launch (CriticFwd: the folded actor output layer, the encoders, the
-    # combine and the dual output) instead of a riding encoder job + a grouped-GEMM product; needs
-    # DAOB.  Off by default: 0.997 vs 0.863 ms per config-3 step (profiles/r04_cfwd_ab.txt) -- a
-    # 16-sample block re-reads all of Wc from L2 (42 MB per B = 1024 set), the grouped GEMM's larger
-    # tiles do not.  AAC_CFWD=1 selects it (parity-tested either way)
-    CFWD = os.environ.get("AAC_CFWD", "0") == "1"
-
     def __init__(self, model, replay, B):
         self.m, self.rep, self.B = model, replay, B
         N, D0, K = model.n_agents, model.D0, model.n_agents - 1
@@ -750,21 +691,8 @@ class FusedUpdate:
         t_head = lambda: critic_head(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew),  # noqa: E731
                                      done=ptr(self.done), B=B, N=N, gamma=m.GAMMA, q=ptr(self.qn), yout=ptr(self.y))
         self.segs = None
-        self.cfwd = self.CFWD and self.DAOB
         zip0 = not self.OVERLAP and self.MERGED
-        t_cf = critic_fwd_set(Ct, ptr(self.Xt), Bt, N, Din, None, self.h_t, fold=(ptr(self.acts_t.ha), At, D0))
-        if zip0 and self.cfwd:
-            # as below, with the target critic forward (its actor output layer folded in) and critic step
-            # 0's forward as the two sets of one aac_critic_fwd launch
-            cs0 = self._critic_stages(0, C, self.cbuf[1])
-            a0_attn, a0_merge = self._actor_fwd_stages(0, A)
-            self.pre += [AttnEnc(t_attn, a0_attn)] + gemm_launches(t_merge + a0_merge)
-            f0, h0, dq0, dh0, _ = self.cbuf[1]
-            tjob = head_job(ptr(self.h_t), Bt, Ct.Wq, Ct.bq, 2, rew=ptr(self.rew), done=ptr(self.done), B=B, N=N,
-                            gamma=m.GAMMA, q=ptr(self.qn), yout=ptr(self.y),
-                            chain=(ptr(h0), C.Wq, C.bq, ptr(self.q_c), ptr(dq0), ptr(dh0), B))
-            self.pre += [CriticFwd(t_cf, cs0["cfwd"]), lambda: critic_head_job(tjob)]
-        elif zip0:
+        if zip0:
             # the TD-target chain reads only the target networks and the gathered batches: the critic
             # step 0's forward and the actor forward 0 (current weights, their own buffers) share its
             # launches up to the point where the critic step needs the targets y
@@ -778,8 +706,6 @@ class FusedUpdate:
                             gamma=m.GAMMA, q=ptr(self.qn), yout=ptr(self.y),
                             chain=(ptr(h0), C.Wq, C.bq, ptr(self.q_c), ptr(dq0), ptr(dh0), B))
             self.pre += [AttnEnc(ride_only(t_cenc))] + gemm_launches(t_comb) + [lambda: critic_head_job(tjob)]
-        elif self.cfwd:
-            self.pre += [AttnEnc(t_attn)] + gemm_launches(t_merge) + [CriticFwd(t_cf), t_head]
         else:
             self.pre += [AttnEnc(t_attn)] + gemm_launches(t_merge)
             self.pre += [AttnEnc(ride_only(t_cenc))] + gemm_launches(t_comb) + [t_head]
@@ -788,8 +714,6 @@ class FusedUpdate:
         elif self.OVERLAP:
             self.segs = self._overlapped(A, C)
             self.iters = [a + b + j for a, b, j in self.segs]
-        elif self.MERGED and self.cfwd:
-            self.iters = self._merged_cf(A, C, cs0)
         elif self.MERGED:
             self.iters = self._merged(A, C, cs0)
         else:
@@ -834,36 +758,6 @@ class FusedUpdate:
         if adam_pair_ok(self.gc, self.ga):
             return [lambda: adam_sum_pair(ca, aa)]
         return [lambda: adam_sum(*ca[:4], grad_out=ca[4]), lambda: adam_sum(*aa[:4], grad_out=aa[4])]
-
-    def _merged_cf(self, A, C, cs0):
-        """``_merged`` with the critic forwards as aac_critic_fwd launches: segment i+1 runs the actor
-        forward i (attention + merge), then ONE critic-forward launch holding the actor step's critic
-        on the policy actions (output layer folded in, dual output) and critic step i+1's forward, the
-        actor output backward with critic step i+1's head riding along, the weight gradients of both
-        (critic step i+1's data and weight gradients with the actor's), the attention backward and the
-        Adam pair: 8 launches per segment instead of 10, the same arithmetic as the serial order built
-        from the same kernels (``_critic_step`` / ``_actor_step``)."""
-        m, N = self.m, self.N
-        segs = [gemm_launches(cs0["grad"]) + gemm_launches(cs0["encw"])      # its head ran chained in pre
-                + self._adam(m.critic_optimizer, m.fc, self.gc, self.SPLIT_CRITIC, 1)]
-        for i in range(N):
-            cs = self._critic_stages(i + 1, C, self.cbuf[1]) if i + 1 < N else None
-            ac = self._actor_stages(i, A, C)
-            L = []
-            if i > 0:          # iteration 0's actor forward ran in pre
-                a_attn, a_merge = self._actor_fwd_stages(i, A)
-                L += [AttnEnc(a_attn)] + gemm_launches(a_merge)
-            L.append(CriticFwd(ac["cfwd"], *([cs["cfwd"]] if cs is not None else [])))
-            L.append(ac["daob"](cs["head_job"] if cs is not None else None))
-            L += gemm_launches(ac["wgrad1"] + (cs["grad"] if cs is not None else []))
-            L.append(ac["attn_bwd"])
-            L += gemm_launches(ac["wgrad2"] + (cs["encw"] if cs is not None else []) + ac["qstat"])
-            if cs is not None:
-                L += self._adam_pair(i + 1, i)
-            else:
-                L += self._adam(m.actor_optimizer, m.fa, self.ga, self.SPLIT_ACTOR, i + 1)
-            segs.append(L)
-        return segs
 
     def _merged(self, A, C, cs0):
         """Fewer, fuller launches.  The critic step of iteration i+1 reads the critic
@@ -1032,17 +926,6 @@ class FusedUpdate:
         which depends only on the actor weights, changed after the critic step -- shares the
         critic step's launches; the policy actions land in X2 (own columns gathered there too)."""
         cs = self._critic_stages(i, C, cb)
-        if self.cfwd:
-            a_merge = []
-            L = []
-            if fuse_actor_fwd:
-                a_attn, a_merge = self._actor_fwd_stages(i, A)
-                L = [AttnEnc(a_attn)]
-            L.append(CriticFwd(cs["cfwd"]))
-            L.append(cs["head"])
-            L += gemm_launches(cs["grad"] + a_merge)
-            L += gemm_launches(cs["encw"])
-            return L
         if fuse_actor_fwd:
             a_attn, a_merge = self._actor_fwd_stages(i, A)
             L = [AttnEnc(with_ride(a_attn, cs["enc"]))]
@@ -1079,17 +962,12 @@ class FusedUpdate:
                  mact=RELU)]
         encw = [prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din, Din, ta=1, ones=1,
                      cextra=gC.enc_b[n], ksplit=SC, split_stride=nC) for n in range(N)]
-        cfwd = critic_fwd_set(C, X, B, N, Din, f, h)
-        return {"enc": c_enc, "comb": c_comb, "head": head, "head_job": hj, "grad": grad, "encw": encw,
-                "cfwd": cfwd}
+        return {"enc": c_enc, "comb": c_comb, "head": head, "head_job": hj, "grad": grad, "encw": encw}
 
     def _actor_step(self, i, A, C):
         """Actor step of iteration i (ATT/maddpg:389-425) after its forward, up to the weight-
         gradient partials: critic on the policy actions, backward into the actor."""
         st = self._actor_stages(i, A, C)
-        if self.cfwd:
-            return ([CriticFwd(st["cfwd"]), st["daob"]()] + gemm_launches(st["wgrad1"]) + [st["attn_bwd"]]
-                    + gemm_launches(st["wgrad2"] + st["qstat"]))
         L = [AttnEnc(ride_only(st["cenc"]))] + gemm_launches(st["ccomb"])
         if self.DAOB:
             L.append(st["daob"]())
@@ -1132,10 +1010,6 @@ class FusedUpdate:
                           128 * N, Din, D0, N, B)
             st["daob"] = lambda head=None: DcombAob(da, head)
             st["qstat"] = [st["dcomb"][1]]
-        # the critic on the policy actions as one aac_critic_fwd set: the actor's output layer folded in
-        # (actions into X's action columns), encoders, combine, and the actor-loss head's dual output
-        st["cfwd"] = critic_fwd_set(C, X, B, N, Din, f, h, fold=(ptr(c.ha), A, D0),
-                                    dual=(C.Wq, dh, -float(np.float32(1.0) / np.float32(B))))
         st["wgrad1"] = [
             prob(ptr(self.dout), ptr(c.ha), gA.Wa, 2, 256, R, 2, 256, 256, ta=1, ones=1, cextra=gA.ba, ksplit=SA,
                  split_stride=nA),

@@ -43,11 +43,9 @@ STEP_GRAPH = os.environ.get("AAC_STEP_GRAPH", "0") == "1"
 # the GRU training step (config 4) as one graph replay: its host-side launch sequence left the GPU idle
 # ~5 % of a step (act, env tail and update launched from Python); AAC_STEP_GRAPH_GRU=0 keeps it eager
 STEP_GRAPH_GRU = os.environ.get("AAC_STEP_GRAPH_GRU", "1") == "1"
-# config 5: AAC_UAM_TAIL=1 runs the UAM env step and the replay push as one launch
-# (aac_uam_step_tail; bit-exact, tests/test_uam_gpu.py), the packed auto-reset after it.  Measured
-# slower, so off: the step launch grows 188 -> 234 us against the 23-us push launch it replaces
-# (226-231 vs 238-240 M agent-env-steps/s; profiles/r05_uam_tail_ab.txt)
-UAM_TAIL = os.environ.get("AAC_UAM_TAIL", "0") == "1"
+# config 5: the UAM env step and the replay push as one launch was built (bit-exact) and measured
+# slower -- the step launch grew 188 -> 234 us against the 23-us push launch it replaced (226-231 vs
+# 238-240 M agent-env-steps/s; profiles/r05_uam_tail_ab.txt) -- and removed in round 6
 # config 5: the packed auto-reset (UAM/env:551-771) on a side stream beside the update, whose small
 # float64 launches leave most CUs idle: 0.543 -> 0.519 ms per step, interleaved
 # (profiles/r05_uam_overlap_reset_ab.txt); AAC_UAM_OVERLAP_RESET=0 runs it before the update
@@ -330,25 +328,6 @@ class UamTrainer(CheckpointMixin):
         if time_env:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        if UAM_TAIL:
-            # step + replay push in one launch (aac_uam_step_tail): the same results as the separate
-            # launches below
-            with trace.range("env_step"):
-                self.env.step_tail(act, out=n, replay=self.replay, srcs=(c.own, c.radar), auto_reset=False)
-            if time_env:
-                ev1.record()
-                self.env_events.append((ev0, ev1))
-            for f in self.post_step_hooks:
-                f(self, act, c, n)
-            self.cur, self.nxt = n, c
-            run_update = update and len(self.replay) > self.B
-            with side_stream(self, run_update, UAM_OVERLAP_RESET), trace.range("auto_reset"):
-                self.env.auto_reset(n.env_done, out=n)
-            if run_update:
-                with trace.range("update"):
-                    self.model.update(self.B, use_graph=not NO_GRAPH)
-            join_side(self)
-            return
         with trace.range("env_step"):
             self.env.step(act, out=n)
         if time_env:

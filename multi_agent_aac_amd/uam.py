@@ -27,7 +27,7 @@ BOUND = (0.0, 40.0, 0.0, 40.0)               # UAM/params:32-36
 EXPORTS = ("aac_uam_create", "aac_uam_destroy", "aac_uam_last_error", "aac_uam_reset", "aac_uam_step",
            "aac_uam_set_bank", "aac_uam_auto_reset", "aac_uam_bank_build", "aac_uam_get_state",
            "aac_uam_set_state", "aac_uam_actor", "aac_uam_actor_last_error", "aac_uam_set_reset_compact",
-           "aac_uam_use_episode_buffer", "aac_uam_step_tail")
+           "aac_uam_use_episode_buffer")
 
 
 class UamCfg(ctypes.Structure):
@@ -54,8 +54,6 @@ def lib():
         L.aac_uam_destroy.restype = None
         L.aac_uam_reset.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(UamOut), vp]
         L.aac_uam_step.argtypes = [vp, vp, ctypes.POINTER(UamOut), vp]
-        L.aac_uam_step_tail.argtypes = [vp, vp, ctypes.POINTER(UamOut), vp, ctypes.c_int64, ctypes.c_int64,
-                                        ctypes.c_int64, vp, vp, vp, i32, vp]
         L.aac_uam_set_bank.argtypes = [vp, vp, vp, vp, i32, ctypes.c_uint64]
         L.aac_uam_auto_reset.argtypes = [vp, vp, ctypes.POINTER(UamOut), vp]
         L.aac_uam_set_reset_compact.argtypes = [i32]
@@ -211,37 +209,13 @@ class BatchedUAM:
         _chk(lib().aac_uam_step(self._h, _ptr(a), ctypes.byref(o), _stream()), "aac_uam_step")
         return out
 
-    def step_tail(self, actions, out: UamBuffers, replay=None, srcs=None, auto_reset=True):
-        """``step`` + the replay push of the E*N transitions (srcs = (s_own, s_radar): the step's input
-        observation rows) in ONE launch (aac_uam_step_tail; UAM/main:582-603), then with auto_reset
-        the packed bank auto-reset of the finished envs.  The same results as step / push_batch /
-        auto_reset."""
-        a = actions
-        if a.dtype != torch.float64 or not a.is_contiguous() or a.device != self.device:
-            a = a.to(device=self.device, dtype=torch.float64).contiguous()
-        assert a.shape == (self.E, self.N, 2), a.shape
-        o = out.c_struct()
-        ring = cap = pos = size = meta = s_own = s_radar = None
-        if replay is not None:
-            s_own, s_radar = srcs
-            for x, w in ((s_own, 7), (s_radar, 18)):
-                assert x.dtype == torch.float64 and x.is_contiguous() and x.numel() == self.E * self.N * w
-            ring, cap, pos, size, meta = replay.ring, replay.capacity, replay.pos, replay.size, replay.meta
-        _chk(lib().aac_uam_step_tail(self._h, _ptr(a), ctypes.byref(o), _ptr(ring), int(cap or 0), int(pos or 0),
-                                     int(size or 0), _ptr(meta), _ptr(s_own), _ptr(s_radar), int(bool(auto_reset)),
-                                     _stream()), "aac_uam_step_tail")
-        if replay is not None:
-            replay._advance(self.E * self.N, meta=False)      # the kernel wrote meta
-        self._keep_tail = a
-        return out
-
     def set_bank(self, bank: Bank, seed=0):
         assert bank.start.shape[1] == self.N
         _chk(lib().aac_uam_set_bank(self._h, bank.start.ctypes.data, bank.goal.ctypes.data, bank.clouds.ctypes.data,
                                     bank.n, ctypes.c_uint64(seed)), "aac_uam_set_bank")
         self.bank = bank
         self.bank_seed = int(seed)
-        # graphs captured around step_tail / auto_reset bake the bank pointers and seed: owners
+        # graphs captured around auto_reset bake the bank pointers and seed: owners
         # re-capture when this advances (see env.BatchedEnv.set_od_bank)
         self.bank_generation = getattr(self, "bank_generation", 0) + 1
 

@@ -708,75 +708,3 @@ def test_dcomb_out_bwd_matches_reference(native_lib, N, B, with_head):
     if with_head:
         for x, y in zip(*houts):
             assert torch.equal(x, y)
-
-
-@pytest.mark.parametrize("N,Bs,fold,two", [(5, 1024, True, True), (3, 200, False, False), (8, 96, True, False)])
-def test_critic_fwd_matches_reference(native_lib, N, Bs, fold, two):
-    """aac_critic_fwd (CriticCombine.forward, ATT/nets:672-724, R3, in one launch) against fp64 torch:
-    the folded actor output layer (actions into X), the encoders f, the combine h and the actor-loss
-    head's dual output dh; a second independent set and a riding head job in the same launch
-    (the head bit-equal to the standalone aac_critic_head).  Bs = 200 / 96: ragged sample blocks."""
-    from multi_agent_aac_amd import fused
-    from types import SimpleNamespace
-    torch.manual_seed(N * 7 + Bs)
-    P = fused.ptr
-    D0 = 6 + 4 * (N - 1)
-    Din = D0 + 2
-
-    def net():
-        return dict(wenc=torch.randn(N, 128, Din, device=DEV) * 0.2, benc=torch.randn(N, 128, device=DEV) * 0.1,
-                    wc=torch.randn(256, 128 * N, device=DEV) * 0.05, bc=torch.randn(256, device=DEV) * 0.1,
-                    wq=torch.randn(256, device=DEV))
-
-    def cp_of(nt):
-        return SimpleNamespace(enc_w=[P(nt["wenc"], n * 128 * Din) for n in range(N)],
-                               enc_b=[P(nt["benc"], n * 128) for n in range(N)], Wc=P(nt["wc"]), bc=P(nt["bc"]),
-                               Wq=P(nt["wq"]))
-    sets, refs, keep = [], [], []
-    for s in range(2 if two else 1):
-        nt = net()
-        X = torch.rand(Bs, N, Din, device=DEV) * 2 - 1
-        f = torch.full((Bs, 128 * N), 7.0, device=DEV)
-        h = torch.full((Bs, 256), 7.0, device=DEV)
-        dh = torch.full((Bs, 256), 7.0, device=DEV)
-        X0 = X.clone()
-        fo = None
-        if fold and s == 0:
-            ha = torch.relu(torch.randn(Bs * N, 256, device=DEV))
-            wa, ba = torch.randn(2, 256, device=DEV) * 0.1, torch.randn(2, device=DEV) * 0.1
-            ap = SimpleNamespace(Wa=P(wa), ba=P(ba))
-            fo = (P(ha), ap, D0)
-            a = torch.tanh(ha.double() @ wa.double().T + ba.double()).view(Bs, N, 2)
-            X0 = X0.double()
-            X0[:, :, D0:D0 + 2] = a
-            keep += [ha, wa, ba]
-        dscale = -1.0 / Bs
-        sets.append(fused.critic_fwd_set(cp_of(nt), P(X), Bs, N, Din, f, h, fold=fo,
-                                         dual=(P(nt["wq"]), dh, dscale) if s == 0 else None))
-        xe = X0.double()
-        fr = torch.relu(torch.einsum("bnk,nck->bnc", xe, nt["wenc"].double()) + nt["benc"].double()).reshape(Bs, -1)
-        hr = torch.relu(fr @ nt["wc"].double().T + nt["bc"].double())
-        refs.append((X, X0, f, h, dh, fr, hr, nt, s == 0))
-        keep += [X, f, h, dh, nt]
-    head, houts = None, None
-    M = 2 * 64 + 3
-    hh = torch.relu(torch.randn(M, 256, device=DEV))
-    hw, hb, hy = torch.randn(256, device=DEV), torch.randn(1, device=DEV), torch.randn(M, device=DEV)
-    houts = [[torch.full((M,), 7.0, device=DEV), torch.full((M,), 7.0, device=DEV),
-              torch.full((M, 256), 7.0, device=DEV)] for _ in range(2)]
-    q, dq, dhh = houts[0]
-    fused.critic_head(P(hh), M, P(hw), P(hb), 0, y=P(hy), q=P(q), dq=P(dq), dh=P(dhh))
-    q, dq, dhh = houts[1]
-    head = fused.head_job(P(hh), M, P(hw), P(hb), 0, y=P(hy), q=P(q), dq=P(dq), dh=P(dhh))
-    fused.CriticFwd(*sets, head=head)()
-    torch.cuda.synchronize()
-    for X, X0, f, h, dh, fr, hr, nt, first in refs:
-        if fold and first:
-            np.testing.assert_allclose(X[:, :, D0:D0 + 2].cpu().double(), X0[:, :, D0:D0 + 2].cpu(), atol=1e-6)
-        np.testing.assert_allclose(f.cpu().double(), fr.cpu(), rtol=1e-4, atol=1e-5)
-        np.testing.assert_allclose(h.cpu().double(), hr.cpu(), rtol=1e-4, atol=1e-5)
-        if first:
-            want = (torch.from_numpy(h.cpu().numpy()) > 0).double() * (-1.0 / Bs) * nt["wq"].double().cpu()
-            np.testing.assert_allclose(dh.cpu().double(), want, rtol=1e-6, atol=1e-9)
-    for x, y in zip(*houts):
-        assert torch.equal(x, y)

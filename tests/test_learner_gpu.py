@@ -171,15 +171,12 @@ def test_update_matches_cpu_restatement(native_lib, N, B):
     assert learner_ref.check_one_update(MADDPG, device=DEV, N=N, B=B, E=128, tol=1e-5, iters=2)
 
 
-@pytest.mark.parametrize("cfwd,daob", [(True, True), (False, False)])
-def test_update_launch_forms_match_cpu_restatement(native_lib, monkeypatch, cfwd, daob):
-    """The non-default launch forms of the fused update (AAC_CFWD=1: CriticCombine.forward as one
-    critic_fwd launch; AAC_DAOB=0: the critic data gradient and actor output backward as two launches)
-    against the same restatement."""
+def test_update_launch_forms_match_cpu_restatement(native_lib, monkeypatch):
+    """The non-default launch form of the fused update (AAC_DAOB=0: the critic data gradient and actor
+    output backward as two launches) against the same restatement."""
     from multi_agent_aac_amd import fused
     from multi_agent_aac_amd.maddpg import MADDPG
-    monkeypatch.setattr(fused.FusedUpdate, "CFWD", cfwd)
-    monkeypatch.setattr(fused.FusedUpdate, "DAOB", daob)
+    monkeypatch.setattr(fused.FusedUpdate, "DAOB", False)
     assert learner_ref.check_one_update(MADDPG, device=DEV, N=5, B=256, E=128, tol=1e-5, iters=2)
 
 

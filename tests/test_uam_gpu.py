@@ -311,53 +311,3 @@ def test_uam_episode_buffer_counts_resets(native_lib):
         env.auto_reset(env.bufs.env_done)
     torch.cuda.synchronize()
     assert torch.equal(ep, want) and int(want.max()) > 1
-
-
-@pytest.mark.parametrize("N,E,cap,in_launch", [(16, 1003, 40000, True), (16, 8192, 300000, True),
-                                                (5, 2001, 25000, True), (16, 8192, 300000, False)])
-def test_uam_step_tail_bit_exact(native_lib, N, E, cap, in_launch):
-    """aac_uam_step_tail (config 5's launch: step + replay push in one, then with auto_reset the packed
-    bank reset) against the separate aac_uam_step, aac_uam_push and aac_uam_auto_reset from the same
-    bank, state and actions: every output buffer, every state tensor, the episode counters and every
-    ring row bit-identical after each step; the ring wraps (cap not a multiple of E N), E is not a
-    multiple of the 4 envs per workgroup (ragged tail) and many envs reset every step.  in_launch=False:
-    step_tail without reset, then auto_reset (the trainer's form, the reset on its side stream)."""
-    from multi_agent_aac_amd import uam
-    from multi_agent_aac_amd.uam_learner import UamReplay
-    bank = uam.build_bank(2048, N, seed=19)
-    envs, reps, eps, bufs = [], [], [], []
-    for _ in range(2):
-        env = uam.BatchedUAM(E, N, neighbours=True)
-        env.set_bank(bank, seed=7)
-        eps.append(env.use_episode_buffer(torch.zeros(E, dtype=torch.int32, device=DEV)))
-        bb = [env.alloc_buffers(), env.alloc_buffers()]
-        env.auto_reset(None, out=bb[0])
-        envs.append(env)
-        bufs.append(bb)
-        reps.append(UamReplay(cap, DEV, seed=0))
-    rng = np.random.default_rng(8)
-    resets = 0
-    for k in range(10):
-        act = torch.from_numpy(rng.uniform(-1, 1, (E, N, 2))).to(DEV)
-        c0, n0 = bufs[0][k % 2], bufs[0][1 - k % 2]
-        c1, n1 = bufs[1][k % 2], bufs[1][1 - k % 2]
-        envs[0].step_tail(act, out=n0, replay=reps[0], srcs=(c0.own, c0.radar), auto_reset=in_launch)
-        if not in_launch:
-            envs[0].auto_reset(n0.env_done, out=n0)
-        envs[1].step(act, out=n1)
-        reps[1].push_batch(c1.own, c1.radar, act, n1.reward, n1.done, n1.own, n1.radar)
-        envs[1].auto_reset(n1.env_done, out=n1)
-        torch.cuda.synchronize()
-        resets += int(n1.env_done.sum())
-        for name in n0.__dict__:
-            x, y = getattr(n0, name), getattr(n1, name)
-            if isinstance(x, torch.Tensor):
-                assert torch.equal(x, y), (k, name)
-        sa, sb = envs[0].get_state(), envs[1].get_state()
-        for key in sa:
-            assert torch.equal(sa[key], sb[key]), (k, key)
-        assert torch.equal(eps[0], eps[1]), k
-        assert (reps[0].pos, reps[0].size) == (reps[1].pos, reps[1].size)
-        assert torch.equal(reps[0].meta, reps[1].meta), k
-        assert torch.equal(reps[0].ring, reps[1].ring), k
-    assert resets > E // 2, resets
