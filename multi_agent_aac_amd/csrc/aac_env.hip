@@ -70,7 +70,7 @@ struct Args {
     struct BandHdr *band_hdr;
     double2 *band_pos;
     int32_t *band_cnt;   // [0] entries this launch (zeroed by band_fix_kernel), [1] most ever (overflow check),
-                         // [2] / [3] the same for rfix
+                         // [2] / [3] the same for rfix, [4] the folded fix-up's workgroup arrivals
     int band_cap;
     // variant 1 step: agents with a flagged ray, whose reward's near-building penalty (the radar minimum)
     // band_fix_kernel recomputes from the exact radar (the kernel's minimum is the float one)
@@ -302,6 +302,8 @@ struct Lds {
     int32_t idx[BLOCK];
     unsigned long long rmin[BLOCK];   // variant 1: per agent, the smallest radar distance (float64 bits)
     alignas(16) float obs[OBS_STAGE_FLOATS];   // the workgroup's own | nei rows (step kernel, when they fit)
+    int fixflag;            // the workgroup listed a threshold-band ray (or a variant-1 reward) for the fix-up
+    int last;               // step_kernel (folded fix-up): this workgroup arrived last
 };
 // the occupancy maps follow the static LDS image as dynamic LDS: n_maps * gw * gh bytes, then
 // (8-B aligned) the n_maps * gw row masks when the handle has them
@@ -507,6 +509,7 @@ __device__ __attribute__((always_inline)) void radar_phase(const Args &A, Lds &S
         const int e = emap ? emap[le] : e0 + le;
         const int slot = atomicAdd(A.band_cnt, 1);
         if (slot >= A.band_cap) continue;
+        S.fixflag = 1;
         // variant 1 step: the agent's reward uses its radar minimum -- mark it for the fix-up (S.flags
         // bit 7, zeroed before the radar phase; the agent phase reads it after the barrier)
         if (rmin) atomicOr(reinterpret_cast<unsigned *>(&S.flags[la & ~3]), 0x80u << (8 * (la & 3)));
@@ -1066,13 +1069,125 @@ __device__ __attribute__((always_inline)) void tail_copy(const Tail &T, int64_t 
 // One instantiation per (env variant, radar mode): the other variant's reward code and the unused
 // radar path are compiled out, which keeps the kernel inside its 128-VGPR budget (the run-time
 // branches cost ~66 spilled VGPRs / 240 B of scratch per lane).
+// ------------------------------------------------------------------------- exact radar fix-up
+// One radar ray decided exactly (the threshold bands resolved: ray_poly_entry_full / ray_square in mode
+// 2, whose exact tests are the calls seg_gon_meet / seg_square_meet) from an env's positions and map
+// in global memory.  No candidate pre-filter: every other agent's 64-gon gets the full clip, every
+// occupied cell of the segment's box the slab test (the same decisions as the filtered radar loop
+// outside the bands).
+__device__ double radar_ray_exact(const double2 *pos, int N, int i, int r, double pb, double rlen, int mode,
+                                  const uint8_t *occ, int gw, int gh, double gx0, double gy0, const double *b) {
+    const double2 p = pos[i];
+    const double px = p.x, py = p.y;
+    const double ex = px + rlen * c_tab.ray_c[r], ey = py + rlen * c_tab.ray_s[r];
+    const double len = gdist(ex, ey, px, py);
+    bool band = false;
+    double dd = len, dob = len;
+    if (mode != AAC_RADAR_OBSTACLES) {
+        double shortest = INFINITY;
+        for (int j = 0; j < N; ++j) {
+            if (j == i) continue;
+            double t;
+            if (!ray_poly_entry_full<1>(px, py, ex, ey, pos[j].x, pos[j].y, pb, t, band, 2)) continue;
+            const double d = gdist(px + t * (ex - px), py + t * (ey - py), px, py);
+            shortest = d < shortest ? d : shortest;
+        }
+        if (shortest < INFINITY) dd = shortest;
+    }
+    if (mode != AAC_RADAR_DRONES) {
+        double d;
+        int i0 = (int)floor((fmin(px, ex) - 5.0 - gx0) * 0.1), i1 = (int)ceil((fmax(px, ex) + 5.0 - gx0) * 0.1);
+        int j0 = (int)floor((fmin(py, ey) - 5.0 - gy0) * 0.1), j1 = (int)ceil((fmax(py, ey) + 5.0 - gy0) * 0.1);
+        i0 = i0 < 0 ? 0 : i0;
+        j0 = j0 < 0 ? 0 : j0;
+        i1 = i1 > gw - 1 ? gw - 1 : i1;
+        j1 = j1 > gh - 1 ? gh - 1 : j1;
+        for (int ii = i0; ii <= i1; ++ii)
+            for (int jj = j0; jj <= j1; ++jj) {
+                if (!occ[ii * gh + jj]) continue;
+                const double qx = gx0 + 10.0 * ii, qy = gy0 + 10.0 * jj;
+                if (ray_square<1>(px, py, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band, 2) && d <= dob) dob = d;
+            }
+        if (ray_vline(px, py, ex, ey, b[0], d) && d < dob) dob = d;
+        if (ray_vline(px, py, ex, ey, b[1], d) && d < dob) dob = d;
+        if (ray_hline(px, py, ex, ey, b[2], d) && d < dob) dob = d;
+        if (ray_hline(px, py, ex, ey, b[3], d) && d < dob) dob = d;
+    }
+    return mode == AAC_RADAR_DRONES ? dd : (mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
+}
+
+struct FixArgs {
+    const BandHdr *hdr;
+    const double2 *pos;
+    int32_t *cnt;
+    int cap, N, mode, gw, gh;
+    double pb, rlen, gx0, gy0, bound[4];
+    const uint8_t *occ;
+    float *radar;
+    const uint8_t *env_done;   // non-null: a step entry of an env that was auto-reset in the launch keeps
+                               // the reset observation's radar (its ring row is still fixed)
+    float *ring;
+    int rw, col;
+    const RewFix *rfix;        // variant 1 step: rewards whose radar minimum is recomputed exactly
+    float *reward;
+    int rcol;                  // the ring's reward column (RewFix.row >= 0)
+    int fold;                  // step_kernel: the launch's last workgroup runs the fix-up (no launch of its own)
+};
+
+// The flagged rays of the launch before it (one workgroup; nothing to do in the common case), then the
+// list is emptied for the next launch.  Variant 1: the listed agents' rewards from the exact radar
+// minimum (all 18 rays re-run: away from the bands the exact radar is bit-identical to the float one,
+// oracle/aac_oracle.c observe_env takes the minimum over all of them).
+__device__ __attribute__((always_inline)) void band_fix_body(const FixArgs &F) {
+    const int n = *F.cnt;
+    const int m = n < F.cap ? n : F.cap;
+    for (int k = threadIdx.x; k < m; k += 256) {
+        const BandHdr h = F.hdr[k];
+        const double d = radar_ray_exact(F.pos + (size_t)k * F.N, F.N, h.i, h.r, F.pb, F.rlen, F.mode,
+                                         F.occ + (size_t)h.map * F.gw * F.gh, F.gw, F.gh, F.gx0, F.gy0, F.bound);
+        const size_t oi = ((size_t)h.e * F.N + h.i) * NRAY + h.r;
+        if (h.kind == 1 || !(F.env_done && F.env_done[h.e])) F.radar[oi] = (float)d;
+        if (h.kind == 0 && F.ring && F.col >= 0 && h.row >= 0) F.ring[h.row * F.rw + F.col + h.i * NRAY + h.r] = (float)d;
+    }
+    const int nr = F.rfix ? F.cnt[2] : 0;
+    const int mr = nr < F.cap ? nr : F.cap;
+    for (int k = threadIdx.x; k < mr; k += 256) {
+        const RewFix x = F.rfix[k];
+        double rmin = INFINITY;
+        for (int r = 0; r < NRAY; ++r) {      // the obstacle radar: the agent's own position and map only
+            const double d = radar_ray_exact(&x.pos, 1, 0, r, F.pb, F.rlen, AAC_RADAR_OBSTACLES,
+                                             F.occ + (size_t)x.map * F.gw * F.gh, F.gw, F.gh, F.gx0, F.gy0, F.bound);
+            rmin = d < rmin ? d : rmin;
+        }
+        const double nbp = wgru_nbp(rmin, F.pb);
+        const double rew = x.kind == 0 ? x.rp : (x.kind == 1 ? x.rp - nbp : (x.rp - nbp) + 0.0);
+        F.reward[(size_t)x.e * F.N + x.i] = (float)rew;
+        if (F.ring && x.row >= 0) F.ring[x.row * F.rw + F.rcol + x.i] = (float)rew;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (n) {
+            if (n > F.cnt[1]) F.cnt[1] = n;
+            F.cnt[0] = 0;
+        }
+        if (nr) {
+            if (nr > F.cnt[3]) F.cnt[3] = nr;
+            F.cnt[2] = 0;
+        }
+        F.cnt[4] = 0;     // the folded fix-up's arrival counter (step_kernel), for the next launch
+    }
+}
+
+__global__ void __launch_bounds__(256) band_fix_kernel(FixArgs F) { band_fix_body(F); }
+
 template <int VAR, int RM, bool TAIL>
 __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain, const float2 *__restrict__ act,
-                                                                         ResetArgs R, Tail T) {
+                                                                         ResetArgs R, Tail T, FixArgs F) {
     Args A = Ain;
     A.variant = VAR;
     A.radar_mode = RM;
     __shared__ Lds S;
+    if (threadIdx.x == 0) S.fixflag = 0;
     const int N = A.N;
     const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
@@ -1288,6 +1403,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             if (fixr && A.rfix) {      // a ray of this agent is decided exactly after the launch: so is rmin
                 const int slot = atomicAdd(A.band_cnt + 2, 1);
                 if (slot < A.band_cap) {
+                    S.fixflag = 1;
                     int64_t row = -1;
                     if (TAIL && T.ring && T.late[LATE_REW] >= 0) {
                         row = rpos + e;
@@ -1406,6 +1522,32 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             if (T.reset) reset_body(A, R, S, nullptr, e0, true, spec);
         }
     }
+    if (F.fold) {
+        // The exact threshold fix-up (band_fix_body) in this launch: the last workgroup to arrive runs
+        // it.  A workgroup that listed a ray publishes its stores first -- the list entries and the
+        // outputs the fix-up rewrites -- by the agent-scope release before its arrival (the other
+        // workgroups' outputs are not touched); the last one acquires before reading the lists.
+        __syncthreads();
+        if (S.fixflag) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        if (t == 0) {
+            const int prev = __hip_atomic_fetch_add(F.cnt + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.last = prev == (int)gridDim.x - 1;
+        }
+        __syncthreads();
+        if (S.last) {
+            if (t == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            band_fix_body(F);
+        }
+    }
     ESTAMP(5, __builtin_amdgcn_s_memtime());
     ESTAMP(6, __builtin_amdgcn_s_memrealtime());
 }
@@ -1456,113 +1598,6 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Args A, ResetArgs R) {
 // ordered list of the done envs for the packed auto-reset (aacw::compact_flags)
 __global__ void __launch_bounds__(1024) env_compact_kernel(const uint8_t *__restrict__ mask, int E, int32_t *rlist) {
     aacw::compact_flags(mask, E, rlist);
-}
-
-// ------------------------------------------------------------------------- exact radar fix-up
-// One radar ray decided exactly (the threshold bands resolved: ray_poly_entry_full / ray_square in mode
-// 2, whose exact tests are the calls seg_gon_meet / seg_square_meet) from an env's positions and map
-// in global memory.  No candidate pre-filter: every other agent's 64-gon gets the full clip, every
-// occupied cell of the segment's box the slab test (the same decisions as the filtered radar loop
-// outside the bands).
-__device__ double radar_ray_exact(const double2 *pos, int N, int i, int r, double pb, double rlen, int mode,
-                                  const uint8_t *occ, int gw, int gh, double gx0, double gy0, const double *b) {
-    const double2 p = pos[i];
-    const double px = p.x, py = p.y;
-    const double ex = px + rlen * c_tab.ray_c[r], ey = py + rlen * c_tab.ray_s[r];
-    const double len = gdist(ex, ey, px, py);
-    bool band = false;
-    double dd = len, dob = len;
-    if (mode != AAC_RADAR_OBSTACLES) {
-        double shortest = INFINITY;
-        for (int j = 0; j < N; ++j) {
-            if (j == i) continue;
-            double t;
-            if (!ray_poly_entry_full<1>(px, py, ex, ey, pos[j].x, pos[j].y, pb, t, band, 2)) continue;
-            const double d = gdist(px + t * (ex - px), py + t * (ey - py), px, py);
-            shortest = d < shortest ? d : shortest;
-        }
-        if (shortest < INFINITY) dd = shortest;
-    }
-    if (mode != AAC_RADAR_DRONES) {
-        double d;
-        int i0 = (int)floor((fmin(px, ex) - 5.0 - gx0) * 0.1), i1 = (int)ceil((fmax(px, ex) + 5.0 - gx0) * 0.1);
-        int j0 = (int)floor((fmin(py, ey) - 5.0 - gy0) * 0.1), j1 = (int)ceil((fmax(py, ey) + 5.0 - gy0) * 0.1);
-        i0 = i0 < 0 ? 0 : i0;
-        j0 = j0 < 0 ? 0 : j0;
-        i1 = i1 > gw - 1 ? gw - 1 : i1;
-        j1 = j1 > gh - 1 ? gh - 1 : j1;
-        for (int ii = i0; ii <= i1; ++ii)
-            for (int jj = j0; jj <= j1; ++jj) {
-                if (!occ[ii * gh + jj]) continue;
-                const double qx = gx0 + 10.0 * ii, qy = gy0 + 10.0 * jj;
-                if (ray_square<1>(px, py, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band, 2) && d <= dob) dob = d;
-            }
-        if (ray_vline(px, py, ex, ey, b[0], d) && d < dob) dob = d;
-        if (ray_vline(px, py, ex, ey, b[1], d) && d < dob) dob = d;
-        if (ray_hline(px, py, ex, ey, b[2], d) && d < dob) dob = d;
-        if (ray_hline(px, py, ex, ey, b[3], d) && d < dob) dob = d;
-    }
-    return mode == AAC_RADAR_DRONES ? dd : (mode == AAC_RADAR_OBSTACLES ? dob : (dd < dob ? dd : dob));
-}
-
-struct FixArgs {
-    const BandHdr *hdr;
-    const double2 *pos;
-    int32_t *cnt;
-    int cap, N, mode, gw, gh;
-    double pb, rlen, gx0, gy0, bound[4];
-    const uint8_t *occ;
-    float *radar;
-    const uint8_t *env_done;   // non-null: a step entry of an env that was auto-reset in the launch keeps
-                               // the reset observation's radar (its ring row is still fixed)
-    float *ring;
-    int rw, col;
-    const RewFix *rfix;        // variant 1 step: rewards whose radar minimum is recomputed exactly
-    float *reward;
-    int rcol;                  // the ring's reward column (RewFix.row >= 0)
-};
-
-// The flagged rays of the launch before it (one workgroup; nothing to do in the common case), then the
-// list is emptied for the next launch.  Variant 1: the listed agents' rewards from the exact radar
-// minimum (all 18 rays re-run: away from the bands the exact radar is bit-identical to the float one,
-// oracle/aac_oracle.c observe_env takes the minimum over all of them).
-__global__ void __launch_bounds__(256) band_fix_kernel(FixArgs F) {
-    const int n = *F.cnt;
-    const int m = n < F.cap ? n : F.cap;
-    for (int k = threadIdx.x; k < m; k += 256) {
-        const BandHdr h = F.hdr[k];
-        const double d = radar_ray_exact(F.pos + (size_t)k * F.N, F.N, h.i, h.r, F.pb, F.rlen, F.mode,
-                                         F.occ + (size_t)h.map * F.gw * F.gh, F.gw, F.gh, F.gx0, F.gy0, F.bound);
-        const size_t oi = ((size_t)h.e * F.N + h.i) * NRAY + h.r;
-        if (h.kind == 1 || !(F.env_done && F.env_done[h.e])) F.radar[oi] = (float)d;
-        if (h.kind == 0 && F.ring && F.col >= 0 && h.row >= 0) F.ring[h.row * F.rw + F.col + h.i * NRAY + h.r] = (float)d;
-    }
-    const int nr = F.rfix ? F.cnt[2] : 0;
-    const int mr = nr < F.cap ? nr : F.cap;
-    for (int k = threadIdx.x; k < mr; k += 256) {
-        const RewFix x = F.rfix[k];
-        double rmin = INFINITY;
-        for (int r = 0; r < NRAY; ++r) {      // the obstacle radar: the agent's own position and map only
-            const double d = radar_ray_exact(&x.pos, 1, 0, r, F.pb, F.rlen, AAC_RADAR_OBSTACLES,
-                                             F.occ + (size_t)x.map * F.gw * F.gh, F.gw, F.gh, F.gx0, F.gy0, F.bound);
-            rmin = d < rmin ? d : rmin;
-        }
-        const double nbp = wgru_nbp(rmin, F.pb);
-        const double rew = x.kind == 0 ? x.rp : (x.kind == 1 ? x.rp - nbp : (x.rp - nbp) + 0.0);
-        F.reward[(size_t)x.e * F.N + x.i] = (float)rew;
-        if (F.ring && x.row >= 0) F.ring[x.row * F.rw + F.rcol + x.i] = (float)rew;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (n) {
-            if (n > F.cnt[1]) F.cnt[1] = n;
-            F.cnt[0] = 0;
-        }
-        if (nr) {
-            if (nr > F.cnt[3]) F.cnt[3] = nr;
-            F.cnt[2] = 0;
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -1685,8 +1720,8 @@ static Args make_args(const aac_env *h, const aac_step_out *o) {
 
 // band_fix_kernel after a step / reset launch on the same stream (ring: the step tail's ring and its
 // late radar column, env_done: skip the radar output of envs the launch reset)
-static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, const uint8_t *env_done = nullptr,
-                            float *ring = nullptr, int rw = 0, int col = -1, int rcol = -1) {
+static FixArgs fix_args(const aac_env *h, const Args &A, const uint8_t *env_done = nullptr, float *ring = nullptr,
+                        int rw = 0, int col = -1, int rcol = -1) {
     FixArgs F;
     F.hdr = h->band_hdr;
     F.pos = h->band_pos;
@@ -1710,8 +1745,21 @@ static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, con
     F.rfix = A.rfix;
     F.reward = A.reward;
     F.rcol = rcol;
-    hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, F);
+    F.fold = 0;
+    return F;
 }
+
+static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, const uint8_t *env_done = nullptr,
+                            float *ring = nullptr, int rw = 0, int col = -1, int rcol = -1) {
+    hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, fix_args(h, A, env_done, ring, rw, col, rcol));
+}
+
+// the step launches run the exact fix-up in their last workgroup (1) or launch band_fix_kernel after them
+// (0; AAC_ENV_FOLD_FIX)
+static int g_fold_fix = [] {
+    const char *v = getenv("AAC_ENV_FOLD_FIX");
+    return v ? atoi(v) : 1;
+}();
 
 static ResetArgs bank_reset_args(const aac_env *h) {
     ResetArgs R{};
@@ -1785,7 +1833,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     ALLOC(wp, EN * h->W) ALLOC(wp0, EN) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
     ALLOC(rlist, (size_t)c.E + 1)
-    ALLOC(band_hdr, (size_t)BAND_CAP) ALLOC(band_pos, (size_t)BAND_CAP * c.N) ALLOC(band_cnt, 4) ALLOC(rfix, (size_t)BAND_CAP)
+    ALLOC(band_hdr, (size_t)BAND_CAP) ALLOC(band_pos, (size_t)BAND_CAP * c.N) ALLOC(band_cnt, 5) ALLOC(rfix, (size_t)BAND_CAP)
     h->episode_own = h->episode;
     ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
 #undef ALLOC
@@ -1841,18 +1889,20 @@ static int launch_step(aac_env *h, const float *actions, const aac_step_out *o, 
     if (A.variant) lds = ((lds + 15) & ~(size_t)15) + sizeof(double2) * WPC * (size_t)h->epb * h->cfg.N;
     const hipStream_t st = (hipStream_t)stream;
     const float2 *a2 = reinterpret_cast<const float2 *>(actions);
+    FixArgs F = tail ? fix_args(h, A, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR], T.late[LATE_REW])
+                     : fix_args(h, A);
+    F.fold = g_fold_fix;
 #define STEP_LAUNCH(V, M)                                                                                        \
     do {                                                                                                         \
-        if (tail) hipLaunchKernelGGL((step_kernel<V, M, true>), grid, block, lds, st, A, a2, R, T);              \
-        else hipLaunchKernelGGL((step_kernel<V, M, false>), grid, block, lds, st, A, a2, R, T);                  \
+        if (tail) hipLaunchKernelGGL((step_kernel<V, M, true>), grid, block, lds, st, A, a2, R, T, F);           \
+        else hipLaunchKernelGGL((step_kernel<V, M, false>), grid, block, lds, st, A, a2, R, T, F);               \
     } while (0)
     if (A.variant) STEP_LAUNCH(1, AAC_RADAR_OBSTACLES);
     else if (A.radar_mode == AAC_RADAR_DRONES) STEP_LAUNCH(0, AAC_RADAR_DRONES);
     else if (A.radar_mode == AAC_RADAR_OBSTACLES) STEP_LAUNCH(0, AAC_RADAR_OBSTACLES);
     else STEP_LAUNCH(0, AAC_RADAR_COMBINED);
 #undef STEP_LAUNCH
-    if (tail) launch_band_fix(h, A, st, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR], T.late[LATE_REW]);
-    else launch_band_fix(h, A, st);
+    if (!F.fold) hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, F);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }
@@ -1914,7 +1964,7 @@ int aac_env_step_tail(aac_env *h, const float *actions, const aac_step_out *o, c
             }
             col += w;
         }
-        if (col != T.rw) return fail(AAC_E_INVALID, "step tail: field widths must sum to row_width");
+        if (col > T.rw) return fail(AAC_E_INVALID, "step tail: field widths exceed row_width (the ring's row stride)");
         for (int q = T.nf; q < TAIL_MAX_FIELDS; ++q) {     // unused descriptor slots: harmless values
             T.src[q] = t->srcs[0];
             T.width[q] = 1;

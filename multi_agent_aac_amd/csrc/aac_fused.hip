@@ -894,17 +894,21 @@ __device__ __forceinline__ void adam4_body(const Adam4 &P, int64_t blk, int64_t 
     const float b2 = P.b2, eps = P.eps;
     for (int64_t base = wave * 64; base < P.n; base += nwaves * 64) {
         const int64_t i = base + 4 * e4;
-        const f4 acc = copy_sum4(P.gpart, P.ns, P.gs, i < P.n ? i : 0, g);
         const int64_t k = i + g;
+        // the element's optimiser state loads first (clamped index, unconditional): in flight with the
+        // copy loads instead of after their sum
+        const int64_t kc = k < P.n ? k : P.n - 1;
+        const float m0 = P.m[kc], v0 = P.v[kc], p0 = P.p[kc];
+        const f4 acc = copy_sum4(P.gpart, P.ns, P.gs, i < P.n ? i : 0, g);
         if (k < P.n) {
             const float gi = g == 0 ? acc.x : (g == 1 ? acc.y : (g == 2 ? acc.z : acc.w));
             if (P.gout) P.gout[k] = gi;
-            float mi = P.m[k];
+            float mi = m0;
             mi = mi + w1 * (gi - mi);
-            float vi = P.v[k] * b2;
+            float vi = v0 * b2;
             vi = vi + w2 * (gi * gi);
             const float den = sqrtf(vi) / bc2s + eps;
-            P.p[k] = P.p[k] + (-step_size) * (mi / den);
+            P.p[k] = p0 + (-step_size) * (mi / den);
             P.m[k] = mi;
             P.v[k] = vi;
         }

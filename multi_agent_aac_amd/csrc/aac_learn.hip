@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(LEARN_BLOCK) push_kernel(float *ring, int rw, 
     const int e = blockIdx.x;
     const int64_t row = (meta[0] + e) % cap;
     float *dst = ring + row * rw;
-    for (int c = threadIdx.x; c < rw; c += LEARN_BLOCK) {
+    for (int c = threadIdx.x; c < F.offset[F.n]; c += LEARN_BLOCK) {      // data columns (rw may be padded)
         int f = 0;
         while (c >= F.offset[f + 1]) ++f;
         const int w = F.width[f], cc = c - F.offset[f];
@@ -187,6 +187,8 @@ __global__ void __launch_bounds__(LEARN_BLOCK) push_rows_kernel(float *ring, int
             for (int k = threadIdx.x; k < n; k += LEARN_BLOCK) rows[(k / w) * rw + off + k % w] = src[k];
         }
     }
+    const int dw = F.offset[F.n], pad = rw - dw;      // a padded row's tail: zeros
+    for (int k = threadIdx.x; k < pt * pad; k += LEARN_BLOCK) rows[(k / pad) * rw + dw + k % pad] = 0.0f;
     __syncthreads();
     if ((rw & 3) == 0) {
         const int r4 = rw >> 2;
@@ -298,7 +300,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(const int64_t *meta, int B
 __global__ void __launch_bounds__(LEARN_BLOCK) gather_kernel(const float *ring, int rw, const int32_t *idx, Fields F) {
     const int b = blockIdx.x;
     const float *src = ring + (int64_t)idx[b] * rw;
-    for (int c = threadIdx.x; c < rw; c += LEARN_BLOCK) {
+    for (int c = threadIdx.x; c < F.offset[F.n]; c += LEARN_BLOCK) {      // data columns (rw may be padded)
         int f = 0;
         while (c >= F.offset[f + 1]) ++f;
         const int w = F.width[f];
@@ -718,7 +720,8 @@ static int make_fields(Fields &F, int n, const int32_t *widths, int rw) {
         F.offset[f + 1] = F.offset[f] + widths[f];
     }
     for (int f = n; f < AAC_MAX_FIELDS; ++f) F.offset[f + 1] = INT_MAX;
-    if (F.offset[n] != rw) return lfail("replay: field widths must sum to row_width");
+    // rw: the ring's row stride, the field widths' sum or more (rows padded to whole cache lines)
+    if (F.offset[n] > rw) return lfail("replay: field widths exceed row_width");
     return 0;
 }
 

@@ -132,6 +132,27 @@ def prob(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, bias=None, act=NONE, adden
                     ta, tb, act, mact, ones, ksplit, dvec, C2, dscale)
 
 
+# weight gradients whose real output width fills whole tiles take their bias gradient (the virtual
+# ones column, which would cost a tile column of its own for one real column) as a separate M x 1
+# product against a ones vector: dWm 4 -> 3 column tiles, dWc 11 -> 10, dWa / dWq 9 -> 8 (round 6);
+# AAC_BIAS_SPLIT=0 keeps the ones column
+BIAS_SPLIT = os.environ.get("AAC_BIAS_SPLIT", "1") == "1"
+
+
+def split_bias(p, ones_vec):
+    """[p] or, for a weight-gradient product with a ones column whose real width is a multiple of 32
+    (BIAS_SPLIT), [p without it, the bias gradient op(A) . ones as an M x 1 product into cextra] --
+    the same sums, the bias's in another order."""
+    nreal = p.N - p.ones
+    if not (BIAS_SPLIT and p.ones and nreal % 32 == 0 and ones_vec is not None):
+        return [p]
+    w = GemmProb.from_buffer_copy(p)
+    w.N, w.ones, w.cextra = nreal, 0, None
+    b = GemmProb(p.A, ones_vec, p.cextra, None, None, None, None, p.split_stride, p.M, 1, p.K, p.lda, 1, 1, 0, 0,
+                 p.ta, 0, NONE, NONE, 0, p.ksplit, None, None, 0.0)
+    return [w, b]
+
+
 def head_job(h, M, w, b, mode, y=None, rew=None, done=None, B=0, N=0, gamma=0.0, q=None, dq=None, dh=None,
              yout=None, chain=None):
     """aac_critic_head's arguments as a job for a grouped GEMM launch (``GemmLaunch(heads=...)``).
@@ -608,6 +629,10 @@ class FusedUpdate:
     # or B*N*K rows, critic K = B rows.  AAC_SPLIT_ACTOR / AAC_SPLIT_CRITIC override (tuning).
     SPLIT_ACTOR = int(os.environ.get("AAC_SPLIT_ACTOR", "20"))
     SPLIT_CRITIC = int(os.environ.get("AAC_SPLIT_CRITIC", "4"))
+    # the merge layer's weight gradient dWm | dbm (256 x 192 + 1 over K = B N) takes fewer split copies
+    # than the actor's others: its LDS tiles then fill one round of the launch (the copies past it stay
+    # zero); tools/mb_split.py, round 6
+    SPLIT_DWM = int(os.environ.get("AAC_SPLIT_DWM", "10"))
     # world == 1: run the critic step of iteration i+1 beside the actor step of iteration i on a
     # second stream of the captured graph (AAC_OVERLAP=1; measured slower, off: DESIGN section 4)
     OVERLAP = os.environ.get("AAC_OVERLAP", "0") == "1"
@@ -661,6 +686,8 @@ class FusedUpdate:
             P = max(attn_bwd_partials(R), self.SPLIT_ACTOR)
             self.pwn = torch.zeros(P, 448, device=dev)
             self.ones_p = torch.ones(P, device=dev)
+        # the bias gradients' ones vector (split_bias; K <= B N rows)
+        self.ones_k = torch.ones(max(B * N, B), device=dev)
         # weight-gradient partial copies (summed by the Adam kernel)
         self.ga = torch.zeros(self.SPLIT_ACTOR, padded(model.fa.numel), device=dev)
         self.gc = torch.zeros(self.SPLIT_CRITIC, padded(model.fc.numel), device=dev)
@@ -953,11 +980,12 @@ class FusedUpdate:
         hj = head_job(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq), dh=ptr(dh))
         head = lambda: critic_head(ptr(h), B, C.Wq, C.bq, 0, y=y, q=ptr(self.q_c, i * B), dq=ptr(dq),  # noqa: E731
                                    dh=ptr(dh))
-        grad = [
+        ov = ptr(self.ones_k)
+        grad = split_bias(
             prob(ptr(dq), ptr(h), gC.Wq, 1, 256, B, 1, 256, 256, ta=1, ones=1, cextra=gC.bq, ksplit=SC,
-                 split_stride=nC),
+                 split_stride=nC), ov) + split_bias(
             prob(ptr(dh), ptr(f), gC.Wc, 256, 128 * N, B, 256, 128 * N, 128 * N, ta=1, ones=1, cextra=gC.bc,
-                 ksplit=SC, split_stride=nC),
+                 ksplit=SC, split_stride=nC), ov) + [
             prob(ptr(dh), C.Wc, ptr(df), B, 128 * N, 256, 256, 128 * N, 128 * N, mask=ptr(f), ldmask=128 * N,
                  mact=RELU)]
         encw = [prob(ptr(df, n * 128), X + 4 * n * Din, gC.enc_w[n], 128, Din, B, 128 * N, N * Din, Din, ta=1, ones=1,
@@ -1010,11 +1038,13 @@ class FusedUpdate:
                           128 * N, Din, D0, N, B)
             st["daob"] = lambda head=None: DcombAob(da, head)
             st["qstat"] = [st["dcomb"][1]]
-        st["wgrad1"] = [
+        ov = ptr(self.ones_k)
+        wout = split_bias(
             prob(ptr(self.dout), ptr(c.ha), gA.Wa, 2, 256, R, 2, 256, 256, ta=1, ones=1, cextra=gA.ba, ksplit=SA,
-                 split_stride=nA),
+                 split_stride=nA), ov) + split_bias(
             prob(ptr(self.dha), ptr(c.cat), gA.Wm, 256, 192, R, 256, 192, 192, ta=1, ones=1, cextra=gA.bm,
-                 ksplit=SA, split_stride=nA),
+                 ksplit=min(self.SPLIT_DWM, SA), split_stride=nA), ov)
+        st["wgrad1"] = wout + [
             prob(ptr(self.dha), A.Wm, ptr(self.dcat_o), R, 64, 256, 256, 192, 64),
             prob(ptr(self.dha), A.Wm + 4 * 64, ptr(self.dcat_g), R, 64, 256, 256, 192, 64, mask=ptr(c.cat, 64),
                  ldmask=192, mact=RELU),

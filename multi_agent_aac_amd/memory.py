@@ -2,7 +2,7 @@
 
 ``DeviceReplay`` stores one transition per fixed-width fp32 row
     [s_own (N*D0) | s_radar (N*18) | s_nei (N*K*6) | a (N*2) | r (N) | done (N) | s'_own | s'_radar | s'_nei]
-(660 floats = 2 640 B at N = 5) in a ring of ``capacity`` rows; with ``hidden = H`` (the GRU-actor
+(660 floats = 2 640 B at N = 5, padded to 672 = 21 whole 128-B lines) in a ring of ``capacity`` rows; with ``hidden = H`` (the GRU-actor
 learner) the row also carries the actor hidden states before and after
 the step, ``| h_cur (N*H) | h_next (N*H)`` (the ``cur_hidden`` / ``next_hidden`` fields of
 MADDPG_ownENV_randomOD_Wgru_radar/ma_main_randomOD_Wgru_radar.py:636).  Push is one HIP launch for all E
@@ -14,6 +14,7 @@ position / size and the RNG counter live in device memory).
 an unchanged ``ma_main`` (E = 1); its rows land in the same device ring.
 """
 import ctypes
+import os
 from collections import namedtuple
 
 import numpy as np
@@ -25,6 +26,8 @@ Experience = namedtuple("Experience", ("states", "actions", "next_states", "rewa
                                        "cur_hidden", "next_hidden"))
 
 FIELDS = ("s_own", "s_radar", "s_nei", "act", "rew", "done", "n_own", "n_radar", "n_nei")
+# ring rows padded to a multiple of this many bytes (0: unpadded); AAC_RING_PAD overrides
+ROW_PAD = int(os.environ.get("AAC_RING_PAD", "128"))
 HIDDEN_FIELDS = ("h_cur", "h_next")
 
 
@@ -40,12 +43,17 @@ class DeviceReplay:
             self.dtypes += [0, 0]
             self.fields = FIELDS + HIDDEN_FIELDS
         self.widths = [int(torch.Size(s).numel()) for s in self.shapes]
-        self.row_width = sum(self.widths)
+        self.row_width = sum(self.widths)          # data floats per transition
+        # the ring's row stride: rounded up to whole 128-B lines (ROW_PAD), so that no line holds the
+        # end of one transition and the start of the next (the fused env tail writes each row's fields
+        # from one workgroup); the pad columns stay zero
+        q = ROW_PAD // 4 if ROW_PAD else 1
+        self.stride = (self.row_width + q - 1) // q * q
         self.capacity = int(capacity)
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        self.ring = torch.zeros(self.capacity, self.row_width, dtype=torch.float32, device=self.device)
+        self.ring = torch.zeros(self.capacity, self.stride, dtype=torch.float32, device=self.device)
         self.meta = torch.zeros(2, dtype=torch.int64, device=self.device)       # [next pos, size]
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)    # sampler RNG counter
         self.seed = int(seed)
@@ -79,7 +87,7 @@ class DeviceReplay:
         for t in srcs:
             assert t.is_contiguous() and t.device == self.device and t.shape[0] == E
         n = len(srcs)
-        d = dict(ring=self.ring.data_ptr(), row_width=self.row_width, capacity=self.capacity, pos=self.pos,
+        d = dict(ring=self.ring.data_ptr(), row_width=self.stride, capacity=self.capacity, pos=self.pos,
                  size=self.size, meta=self.meta.data_ptr(), n_fields=n,
                  srcs=(ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs]),
                  widths=(ctypes.c_int32 * n)(*self.widths[:n]), dtypes=(ctypes.c_int32 * n)(*self.dtypes[:n]))

@@ -75,7 +75,7 @@ class CheckpointMixin:
             # whole-step graphs bake the noise seed and the ring position word: re-capture / re-seed
             # them whatever the load did (a refused file changes nothing, but re-capturing is cheap)
             if hasattr(self, "_sg"):
-                self._sg = {}
+                self._sg, self._sg2 = {}, {}
             self._pos_dirty = True
 
 
@@ -143,61 +143,95 @@ class Trainer(CheckpointMixin):
     def hooked(self):
         return bool(self.pre_step_hooks or self.post_step_hooks)
 
-    def _capture_step(self, p):
-        """act + env step tail + update_myown of a step whose current buffers are bufs[p], captured
-        as one HIP graph.  Nothing runs during the capture; the replay's host mirror is restored."""
+    def _step_body(self, p, side=None):
+        """The launches of one training step whose current buffers are bufs[p] (act + env step tail +
+        update_myown), for capture: the ring position is read from / advanced in pos_dev[p] /
+        pos_dev[1 - p]."""
         c, n = self.bufs[p], self.bufs[1 - p]
-        saved = (self.replay.pos, self.replay.size)
         if self.gru:
             # the hidden-state pair flips with the buffer pair: parity p reads hp[p ^ hoff]
             hin, hout = self.hp[p ^ self._hoff], self.hp[1 - (p ^ self._hoff)]
-            plan = self.model._plan(self.B)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                act, hn = self.model.act(c.own, c.radar, hin, self.episode, noisy=True, h_out=hout)
-                srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, hin, hn]
-                self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs, zero_rows=hn,
-                                   pos_io=(self.pos_dev[p], self.pos_dev[1 - p]))
-                plan.run()
-            self.replay.pos, self.replay.size = saved
-            self._sg[p] = (g, None)
+            act, hn = self.model.act(c.own, c.radar, hin, self.episode, noisy=True, h_out=hout)
+            srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei, hin, hn]
+            self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs, zero_rows=hn,
+                               pos_io=(self.pos_dev[p], self.pos_dev[1 - p]))
+            self.model._plan(self.B).run()
             return
-        fu = self.model._fused_plan(self.B)
-        side = torch.cuda.Stream()
+        act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
+        srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei]
+        self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs, pos_io=(self.pos_dev[p], self.pos_dev[1 - p]))
+        self.model._fused_plan(self.B).run_streams(side)
+
+    def _capture_step(self, p, steps=1):
+        """``steps`` consecutive training steps from parity p (act + env step tail + update_myown
+        each, parities alternating), captured as one HIP graph.  Nothing runs during the capture; the
+        replay's host mirror is restored."""
+        saved = (self.replay.pos, self.replay.size)
+        side = None if self.gru else torch.cuda.Stream()
+        if not self.gru:
+            self.model._fused_plan(self.B)        # built outside the capture
+        else:
+            self.model._plan(self.B)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            act = self.model.act(c.own, c.radar, c.nei, self.episode, noisy=True)
-            srcs = [c.own, c.radar, c.nei, act, n.reward, n.done, n.own, n.radar, n.nei]
-            self.env.step_tail(act, out=n, replay=self.replay, srcs=srcs, pos_io=(self.pos_dev[p], self.pos_dev[1 - p]))
-            fu.run_streams(side)
+            for k in range(steps):
+                self._step_body(p ^ (k & 1), side)
         self.replay.pos, self.replay.size = saved
-        self._sg[p] = (g, side)
+        return g, side
+
+    def _graphs_current(self):
+        gen = getattr(self.env, "bank_generation", 0)
+        if (self._sg or getattr(self, "_sg2", None)) and getattr(self, "_sg_bank_gen", gen) != gen:
+            self._sg, self._sg2 = {}, {}      # the env's OD bank / seed changed under the captured graphs
+        self._sg_bank_gen = gen
+        if self.gru and not self._sg and not getattr(self, "_sg2", None):
+            # (re)capture: the hidden-state pair's offset against the buffer parity, as of now
+            p = 0 if self.cur is self.bufs[0] else 1
+            self._hoff = (0 if self.h is self.hp[0] else 1) ^ p
+
+    def _advance_mirror(self, steps):
+        if self._pos_dirty:
+            # eager steps / a checkpoint load moved the host mirror: the graph reads pos_dev[p]
+            p = 0 if self.cur is self.bufs[0] else 1
+            self.pos_dev[p].fill_(self.replay.pos)
+            self._pos_dirty = False
+        rep = self.replay
+        for _ in range(steps):
+            rep.pos = (rep.pos + self.E) % rep.capacity
+            rep.size = min(rep.size + self.E, rep.capacity)
+            p = 0 if self.cur is self.bufs[0] else 1
+            self.cur, self.nxt = self.nxt, self.cur
+            if self.gru:
+                self.h = self.hp[1 - (p ^ self._hoff)]
 
     def step_graph(self):
         """One training step as one graph replay (the same launches as ``step(update=True)``; the
         ring position lives in device words, the host keeps its mirror)."""
         p = 0 if self.cur is self.bufs[0] else 1
-        gen = getattr(self.env, "bank_generation", 0)
-        if self._sg and getattr(self, "_sg_bank_gen", gen) != gen:
-            self._sg = {}             # the env's OD bank / seed changed under the captured graphs
+        self._graphs_current()
         if not self._sg:
-            self._sg_bank_gen = gen
-            if self.gru:
-                self._hoff = (0 if self.h is self.hp[0] else 1) ^ p
             for q in (0, 1):
-                self._capture_step(q)
-        if self._pos_dirty:
-            # eager steps / a checkpoint load moved the host mirror: the graph reads pos_dev[p]
-            self.pos_dev[p].fill_(self.replay.pos)
-            self._pos_dirty = False
+                self._sg[q] = self._capture_step(q)
+        self._advance_mirror(0)
         with trace.range("step_graph"):
             self._sg[p][0].replay()
-        rep = self.replay
-        rep.pos = (rep.pos + self.E) % rep.capacity
-        rep.size = min(rep.size + self.E, rep.capacity)
-        self.cur, self.nxt = self.nxt, self.cur
-        if self.gru:
-            self.h = self.hp[1 - (p ^ self._hoff)]
+        self._advance_mirror(1)
+
+    def step_graph_pair(self):
+        """Two training steps as ONE graph replay (both buffer parities in sequence): the GPU idles at
+        each graph launch boundary (~6-9 us between the end of one replay and the first kernel of the
+        next), so two steps per replay halve those gaps.  The same launches and results as two
+        ``step_graph`` calls."""
+        p = 0 if self.cur is self.bufs[0] else 1
+        self._graphs_current()
+        if not getattr(self, "_sg2", None):
+            self._sg2 = {}
+        if p not in self._sg2:
+            self._sg2[p] = self._capture_step(p, steps=2)
+        self._advance_mirror(0)
+        with trace.range("step_graph_pair"):
+            self._sg2[p][0].replay()
+        self._advance_mirror(2)
 
     def env_episode_view(self):
         # the env's own per-env episode counter (advanced by each auto-reset; 1 after the first)

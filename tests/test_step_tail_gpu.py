@@ -117,13 +117,13 @@ def test_step_tail_rejects_bad_fields(native_lib, occ):
     t.ring, t.row_width, t.capacity, t.pos, t.size, t.meta = ring.data_ptr(), 10, 64, 0, 0, meta.data_ptr()
     t.n_fields = 2
     t.srcs = (ctypes.c_void_p * 2)(src.data_ptr(), src.data_ptr())
-    t.widths = (ctypes.c_int32 * 2)(4, 4)          # 8 != row_width
+    t.widths = (ctypes.c_int32 * 2)(8, 4)          # 12 > row_width
     act = torch.zeros(E, N, 2, device="cuda")
     o = env.bufs.c_struct()
     rc = _native.lib().aac_env_step_tail(env._h, ctypes.c_void_p(act.data_ptr()), ctypes.byref(o), ctypes.byref(t),
                                          None)
     assert rc != 0 and b"row_width" in _native.lib().aac_last_error()
-    t.widths = (ctypes.c_int32 * 2)(4, 6)
+    t.widths = (ctypes.c_int32 * 2)(4, 6)            # (a row stride past the fields' sum: padding, allowed)
     t.capacity = 8                                  # < E
     rc = _native.lib().aac_env_step_tail(env._h, ctypes.c_void_p(act.data_ptr()), ctypes.byref(o), ctypes.byref(t),
                                          None)
@@ -144,7 +144,8 @@ def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, st
     eagerly: bit-identical networks, optimiser state, replay ring and env state.  The second case is
     config 3 (4096 envs x 5 agents, B = 1024); the GRU step (config 4: 4096 x 8, B = 512) carries the
     hidden-state pair through the replays.  An eager step between graph replays re-seeds the device
-    ring-position word."""
+    ring-position word.  Then two steps per replay (step_graph_pair, both parities in one
+    graph: the bench's timed form) from either starting parity."""
     from multi_agent_aac_amd import trainer
     monkeypatch.setattr(trainer, "STEP_GRAPH", True)        # off by default in the bench (measured neutral)
     tr = [trainer.Trainer(E, N, B, mem, "combined", seed=0, model=model) for _ in range(2)]
@@ -160,6 +161,17 @@ def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, st
             tr[1].step(update=True)         # eager step between replays: pos_dev re-seeded
         else:
             tr[1].step_graph()
+    # two steps per replay (the bench's form), from either parity, after the single-step replays
+    for _ in range(2):
+        tr[0].step(update=True)
+        tr[0].step(update=True)
+        tr[1].step_graph_pair()
+    tr[0].step(update=True)
+    tr[1].step_graph()
+    for _ in range(2):
+        tr[0].step(update=True)
+        tr[0].step(update=True)
+        tr[1].step_graph_pair()
     torch.cuda.synchronize()
     a, b = tr[0], tr[1]
     for x, y in ((a.model.fa.data, b.model.fa.data), (a.model.fc.data, b.model.fc.data),
