@@ -1522,7 +1522,11 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             if (T.reset) reset_body(A, R, S, nullptr, e0, true, spec);
         }
     }
-    if (F.fold) {
+    if constexpr (VAR == 0) {
+      if (F.fold) {
+        // Variant 0 only: compiled into the variant-1 (WGRU) kernel the fold's cold code cost config 4
+        // 16 us per step (0.3344 -> 0.3509 ms; the variant-1 step launch 89 -> 105 us), so WGRU keeps the
+        // separate band_fix_kernel launch.
         // The exact threshold fix-up (band_fix_body) in this launch: the last workgroup to arrive runs
         // it.  A workgroup that listed a ray publishes its stores first -- the list entries and the
         // outputs the fix-up rewrites -- by the agent-scope release before its arrival (the other
@@ -1547,6 +1551,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             __syncthreads();
             band_fix_body(F);
         }
+      }
     }
     ESTAMP(5, __builtin_amdgcn_s_memtime());
     ESTAMP(6, __builtin_amdgcn_s_memrealtime());
@@ -1891,7 +1896,7 @@ static int launch_step(aac_env *h, const float *actions, const aac_step_out *o, 
     const float2 *a2 = reinterpret_cast<const float2 *>(actions);
     FixArgs F = tail ? fix_args(h, A, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR], T.late[LATE_REW])
                      : fix_args(h, A);
-    F.fold = g_fold_fix;
+    F.fold = g_fold_fix && !A.variant;
 #define STEP_LAUNCH(V, M)                                                                                        \
     do {                                                                                                         \
         if (tail) hipLaunchKernelGGL((step_kernel<V, M, true>), grid, block, lds, st, A, a2, R, T, F);           \
