@@ -61,6 +61,14 @@ int aac_uam_push(double *ring, int64_t capacity, int64_t pos, int64_t M, const d
                  const double *act, const double *rew, const void *done, int32_t done_u8, const double *nown,
                  const double *nradar, int64_t *meta, int64_t size, void *stream);
 
+/* aac_uam_push with the ring position on the device (graph replays of whole training steps): the
+ * position is read from *pos_in and the advanced one, (pos + M) % capacity, stored to *pos_out (a
+ * different word); meta (required) receives [new pos, min(meta[1] + M, capacity)].  Alternate the
+ * two words between consecutive pushes. */
+int aac_uam_push_io(double *ring, int64_t capacity, int64_t M, const double *own, const double *radar,
+                    const double *act, const double *rew, const void *done, int32_t done_u8, const double *nown,
+                    const double *nradar, int64_t *meta, const int64_t *pos_in, int64_t *pos_out, void *stream);
+
 /* Replay rows ring[idx[b]] (row width 54: own 7 | radar 18 | a 2 | r | done | own' 7 | radar' 18,
  * uam_learner.ROW) -> rows[b][54], xc[b] = [own | a] (9), xt[b][0:7] = own', xp[b][0:7] = own. */
 int aac_uam_gather(const double *ring, const int32_t *idx, int32_t B, double *rows, double *xc, double *xt,

@@ -70,7 +70,7 @@ struct Args {
     struct BandHdr *band_hdr;
     double2 *band_pos;
     int32_t *band_cnt;   // [0] entries this launch (zeroed by band_fix_kernel), [1] most ever (overflow check),
-                         // [2] / [3] the same for rfix, [4] the folded fix-up's workgroup arrivals
+                         // [2] / [3] the same for rfix
     int band_cap;
     // variant 1 step: agents with a flagged ray, whose reward's near-building penalty (the radar minimum)
     // band_fix_kernel recomputes from the exact radar (the kernel's minimum is the float one)
@@ -302,8 +302,6 @@ struct Lds {
     int32_t idx[BLOCK];
     unsigned long long rmin[BLOCK];   // variant 1: per agent, the smallest radar distance (float64 bits)
     alignas(16) float obs[OBS_STAGE_FLOATS];   // the workgroup's own | nei rows (step kernel, when they fit)
-    int fixflag;            // the workgroup listed a threshold-band ray (or a variant-1 reward) for the fix-up
-    int last;               // step_kernel (folded fix-up): this workgroup arrived last
 };
 // the occupancy maps follow the static LDS image as dynamic LDS: n_maps * gw * gh bytes, then
 // (8-B aligned) the n_maps * gw row masks when the handle has them
@@ -509,7 +507,6 @@ __device__ __attribute__((always_inline)) void radar_phase(const Args &A, Lds &S
         const int e = emap ? emap[le] : e0 + le;
         const int slot = atomicAdd(A.band_cnt, 1);
         if (slot >= A.band_cap) continue;
-        S.fixflag = 1;
         // variant 1 step: the agent's reward uses its radar minimum -- mark it for the fix-up (S.flags
         // bit 7, zeroed before the radar phase; the agent phase reads it after the barrier)
         if (rmin) atomicOr(reinterpret_cast<unsigned *>(&S.flags[la & ~3]), 0x80u << (8 * (la & 3)));
@@ -1131,7 +1128,6 @@ struct FixArgs {
     const RewFix *rfix;        // variant 1 step: rewards whose radar minimum is recomputed exactly
     float *reward;
     int rcol;                  // the ring's reward column (RewFix.row >= 0)
-    int fold;                  // step_kernel: the launch's last workgroup runs the fix-up (no launch of its own)
 };
 
 // The flagged rays of the launch before it (one workgroup; nothing to do in the common case), then the
@@ -1174,7 +1170,6 @@ __device__ __attribute__((always_inline)) void band_fix_body(const FixArgs &F) {
             if (nr > F.cnt[3]) F.cnt[3] = nr;
             F.cnt[2] = 0;
         }
-        F.cnt[4] = 0;     // the folded fix-up's arrival counter (step_kernel), for the next launch
     }
 }
 
@@ -1182,12 +1177,11 @@ __global__ void __launch_bounds__(256) band_fix_kernel(FixArgs F) { band_fix_bod
 
 template <int VAR, int RM, bool TAIL>
 __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain, const float2 *__restrict__ act,
-                                                                         ResetArgs R, Tail T, FixArgs F) {
+                                                                         ResetArgs R, Tail T) {
     Args A = Ain;
     A.variant = VAR;
     A.radar_mode = RM;
     __shared__ Lds S;
-    if (threadIdx.x == 0) S.fixflag = 0;
     const int N = A.N;
     const int nag = A.epb * N;
     const int e0 = blockIdx.x * A.epb;
@@ -1403,7 +1397,6 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             if (fixr && A.rfix) {      // a ray of this agent is decided exactly after the launch: so is rmin
                 const int slot = atomicAdd(A.band_cnt + 2, 1);
                 if (slot < A.band_cap) {
-                    S.fixflag = 1;
                     int64_t row = -1;
                     if (TAIL && T.ring && T.late[LATE_REW] >= 0) {
                         row = rpos + e;
@@ -1521,37 +1514,6 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
             }
             if (T.reset) reset_body(A, R, S, nullptr, e0, true, spec);
         }
-    }
-    if constexpr (VAR == 0) {
-      if (F.fold) {
-        // Variant 0 only: compiled into the variant-1 (WGRU) kernel the fold's cold code cost config 4
-        // 16 us per step (0.3344 -> 0.3509 ms; the variant-1 step launch 89 -> 105 us), so WGRU keeps the
-        // separate band_fix_kernel launch.
-        // The exact threshold fix-up (band_fix_body) in this launch: the last workgroup to arrive runs
-        // it.  A workgroup that listed a ray publishes its stores first -- the list entries and the
-        // outputs the fix-up rewrites -- by the agent-scope release before its arrival (the other
-        // workgroups' outputs are not touched); the last one acquires before reading the lists.
-        __syncthreads();
-        if (S.fixflag) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (t == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-        if (t == 0) {
-            const int prev = __hip_atomic_fetch_add(F.cnt + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            S.last = prev == (int)gridDim.x - 1;
-        }
-        __syncthreads();
-        if (S.last) {
-            if (t == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            band_fix_body(F);
-        }
-      }
     }
     ESTAMP(5, __builtin_amdgcn_s_memtime());
     ESTAMP(6, __builtin_amdgcn_s_memrealtime());
@@ -1750,7 +1712,6 @@ static FixArgs fix_args(const aac_env *h, const Args &A, const uint8_t *env_done
     F.rfix = A.rfix;
     F.reward = A.reward;
     F.rcol = rcol;
-    F.fold = 0;
     return F;
 }
 
@@ -1758,13 +1719,6 @@ static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, con
                             float *ring = nullptr, int rw = 0, int col = -1, int rcol = -1) {
     hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, fix_args(h, A, env_done, ring, rw, col, rcol));
 }
-
-// the step launches run the exact fix-up in their last workgroup (1) or launch band_fix_kernel after them
-// (0; AAC_ENV_FOLD_FIX)
-static int g_fold_fix = [] {
-    const char *v = getenv("AAC_ENV_FOLD_FIX");
-    return v ? atoi(v) : 1;
-}();
 
 static ResetArgs bank_reset_args(const aac_env *h) {
     ResetArgs R{};
@@ -1838,7 +1792,7 @@ int aac_env_create(const aac_env_cfg *cfg, int device, aac_env **out) {
     ALLOC(wp, EN * h->W) ALLOC(wp0, EN) ALLOC(wp_cur, EN) ALLOC(wp_cnt, EN) ALLOC(wall, EN) ALLOC(reach, EN)
     ALLOC(step, (size_t)c.E) ALLOC(map_idx, (size_t)c.E) ALLOC(episode, (size_t)c.E)
     ALLOC(rlist, (size_t)c.E + 1)
-    ALLOC(band_hdr, (size_t)BAND_CAP) ALLOC(band_pos, (size_t)BAND_CAP * c.N) ALLOC(band_cnt, 5) ALLOC(rfix, (size_t)BAND_CAP)
+    ALLOC(band_hdr, (size_t)BAND_CAP) ALLOC(band_pos, (size_t)BAND_CAP * c.N) ALLOC(band_cnt, 4) ALLOC(rfix, (size_t)BAND_CAP)
     h->episode_own = h->episode;
     ALLOC(occ, (size_t)c.n_maps * c.grid_w * c.grid_h)
 #undef ALLOC
@@ -1896,18 +1850,17 @@ static int launch_step(aac_env *h, const float *actions, const aac_step_out *o, 
     const float2 *a2 = reinterpret_cast<const float2 *>(actions);
     FixArgs F = tail ? fix_args(h, A, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR], T.late[LATE_REW])
                      : fix_args(h, A);
-    F.fold = g_fold_fix && !A.variant;
 #define STEP_LAUNCH(V, M)                                                                                        \
     do {                                                                                                         \
-        if (tail) hipLaunchKernelGGL((step_kernel<V, M, true>), grid, block, lds, st, A, a2, R, T, F);           \
-        else hipLaunchKernelGGL((step_kernel<V, M, false>), grid, block, lds, st, A, a2, R, T, F);               \
+        if (tail) hipLaunchKernelGGL((step_kernel<V, M, true>), grid, block, lds, st, A, a2, R, T);              \
+        else hipLaunchKernelGGL((step_kernel<V, M, false>), grid, block, lds, st, A, a2, R, T);                  \
     } while (0)
     if (A.variant) STEP_LAUNCH(1, AAC_RADAR_OBSTACLES);
     else if (A.radar_mode == AAC_RADAR_DRONES) STEP_LAUNCH(0, AAC_RADAR_DRONES);
     else if (A.radar_mode == AAC_RADAR_OBSTACLES) STEP_LAUNCH(0, AAC_RADAR_OBSTACLES);
     else STEP_LAUNCH(0, AAC_RADAR_COMBINED);
 #undef STEP_LAUNCH
-    if (!F.fold) hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, F);
+    hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, F);
     HIPCHK(hipGetLastError());
     return AAC_OK;
 }

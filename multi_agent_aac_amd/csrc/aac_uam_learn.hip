@@ -336,7 +336,9 @@ __global__ void uam_polyak_kernel(double *tgt, const double *__restrict__ src, i
 // one replay row per aircraft (UamReplay.push_batch): a workgroup assembles 64 rows in LDS from
 // coalesced reads of the seven sources, then writes them as 64 x 54 contiguous doubles (two ring
 // segments at the wrap); thread 0 of workgroup 0 stores the ring's new [pos, size] (meta).
-// done is uint8 (env output) or float64.
+// done is uint8 (env output) or float64.  pos_in non-null (graph replays): the position is read from
+// that device word and the advanced one stored to pos_out (another word: every workgroup reads pos_in),
+// the size advanced in meta[1] by workgroup 0 alone.
 constexpr int PR = 64;            // rows per workgroup
 __global__ void __launch_bounds__(256) uam_push_kernel(double *ring, int64_t capacity, int64_t pos, int M,
                                                        const double *__restrict__ own, const double *__restrict__ radar,
@@ -344,12 +346,22 @@ __global__ void __launch_bounds__(256) uam_push_kernel(double *ring, int64_t cap
                                                        const void *__restrict__ done, int done_u8,
                                                        const double *__restrict__ nown,
                                                        const double *__restrict__ nradar, int64_t *meta,
-                                                       int64_t new_pos, int64_t new_size) {
+                                                       int64_t new_pos, int64_t new_size,
+                                                       const int64_t *__restrict__ pos_in, int64_t *pos_out) {
     __shared__ double t[PR * 54];
     const int r0 = blockIdx.x * PR, nr = min(PR, M - r0), tid = threadIdx.x;
-    if (blockIdx.x == 0 && tid == 0 && meta) {
-        meta[0] = new_pos;
-        meta[1] = new_size;
+    if (pos_in) pos = *pos_in;
+    if (blockIdx.x == 0 && tid == 0) {
+        if (pos_in) {
+            const int64_t np = pos + M >= capacity ? pos + M - capacity : pos + M;
+            const int64_t ns = meta[1] + M;
+            *pos_out = np;
+            meta[0] = np;
+            meta[1] = ns < capacity ? ns : capacity;
+        } else if (meta) {
+            meta[0] = new_pos;
+            meta[1] = new_size;
+        }
     }
     auto stage = [&](const double *src, int w, int c0) {
         for (int e = tid; e < nr * w; e += 256) {
@@ -454,7 +466,24 @@ int aac_uam_push(double *ring, int64_t capacity, int64_t pos, int64_t M, const d
     if (M >= (int64_t)1 << 30) return lfail("uam_push: too many rows in one push");
     const int64_t np = (pos + M) % capacity, ns = std::min<int64_t>(size + M, capacity);
     hipLaunchKernelGGL(uam_push_kernel, dim3((unsigned)((M + PR - 1) / PR)), dim3(256), 0, (hipStream_t)stream, ring,
-                       capacity, pos, (int)M, own, radar, act, rew, done, done_u8, nown, nradar, meta, np, ns);
+                       capacity, pos, (int)M, own, radar, act, rew, done, done_u8, nown, nradar, meta, np, ns,
+                       (const int64_t *)nullptr, (int64_t *)nullptr);
+    LHIP(hipGetLastError());
+    return 0;
+}
+
+int aac_uam_push_io(double *ring, int64_t capacity, int64_t M, const double *own, const double *radar,
+                    const double *act, const double *rew, const void *done, int32_t done_u8, const double *nown,
+                    const double *nradar, int64_t *meta, const int64_t *pos_in, int64_t *pos_out, void *stream) {
+    if (M <= 0) return 0;
+    if (!ring || !own || !radar || !act || !rew || !done || !nown || !nradar || !meta || !pos_in || !pos_out)
+        return lfail("uam_push_io: NULL argument");
+    if (pos_in == pos_out) return lfail("uam_push_io: pos_in and pos_out must be two distinct words");
+    if (M > capacity) return lfail("uam_push_io: M > capacity");
+    if (M >= (int64_t)1 << 30) return lfail("uam_push_io: too many rows in one push");
+    hipLaunchKernelGGL(uam_push_kernel, dim3((unsigned)((M + PR - 1) / PR)), dim3(256), 0, (hipStream_t)stream, ring,
+                       capacity, (int64_t)0, (int)M, own, radar, act, rew, done, done_u8, nown, nradar, meta,
+                       (int64_t)0, (int64_t)0, pos_in, pos_out);
     LHIP(hipGetLastError());
     return 0;
 }

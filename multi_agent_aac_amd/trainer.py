@@ -16,12 +16,14 @@ per agent and zeroed at episode start, ``WGRU/ma_main:476-647``); ``UamTrainer``
 
 Module flags (environment variables read at import):
   AAC_FUSED_TAIL   0 / 1 forces the separate / fused env tail (default fused)
-  AAC_STEP_GRAPH   1: each ATT training step replays one captured graph (measured neutral, off)
+  AAC_STEP_GRAPH   0: the ATT training step launched from the host (default: graph replays, two
+                   steps per replay in bench.py; config 3 0.818 -> 0.812 ms per step)
   AAC_STEP_GRAPH_GRU 0: the GRU training step launched from the host (default: one graph replay;
                    config 4 0.3331 -> 0.3310 ms per step)
   AAC_OVERLAP_RESET 1: separate-launch auto-reset on a side stream (measured slower, off)
   AAC_UAM_OVERLAP_RESET 0: the UAM loop's packed auto-reset before the update instead of on a side
                    stream beside it (default on: config 5 0.543 -> 0.519 ms per step)
+  AAC_UAM_STEP_GRAPH 1: the UAM training step as graph replays (measured slower, off)
 """
 import os
 
@@ -36,10 +38,12 @@ OVERLAP_RESET = os.environ.get("AAC_OVERLAP_RESET", "0") == "1"   # measured slo
 # workgroups since the 4-env workgroups) 0.378 -> 0.371 ms per step.  AAC_FUSED_TAIL=0 / 1 forces it.
 _FT = os.environ.get("AAC_FUSED_TAIL")
 FUSED_TAIL = None if _FT is None else _FT == "1"
-# config 3: each timed step (act + fused env tail + update) replays one captured HIP graph (one per
-# buffer parity; AAC_STEP_GRAPH=1).  Measured neutral (0.8926 vs 0.8929 ms per step: the host already
-# runs ahead of the device), so the steps are launched from the host by default
-STEP_GRAPH = os.environ.get("AAC_STEP_GRAPH", "0") == "1"
+# config 3: the timed steps (act + fused env tail + update) replay captured HIP graphs, two steps per
+# replay in bench.py (both buffer parities in one graph).  One step per replay measured neutral in
+# rounds 3-5 (0.8173 vs 0.8178 ms); two per replay halve the ~6-9 us GPU idle at each graph-launch
+# boundary: 0.8102-0.8119 vs 0.8167-0.8184 ms interleaved (profiles/r06_step_graph_ab.txt).
+# AAC_STEP_GRAPH=0 launches the steps from the host
+STEP_GRAPH = os.environ.get("AAC_STEP_GRAPH", "1") == "1"
 # the GRU training step (config 4) as one graph replay: its host-side launch sequence left the GPU idle
 # ~5 % of a step (act, env tail and update launched from Python); AAC_STEP_GRAPH_GRU=0 keeps it eager
 STEP_GRAPH_GRU = os.environ.get("AAC_STEP_GRAPH_GRU", "1") == "1"
@@ -50,6 +54,12 @@ STEP_GRAPH_GRU = os.environ.get("AAC_STEP_GRAPH_GRU", "1") == "1"
 # float64 launches leave most CUs idle: 0.543 -> 0.519 ms per step, interleaved
 # (profiles/r05_uam_overlap_reset_ab.txt); AAC_UAM_OVERLAP_RESET=0 runs it before the update
 UAM_OVERLAP_RESET = os.environ.get("AAC_UAM_OVERLAP_RESET", "1") == "1"
+# config 5: the whole UAM training step (act, env step, replay push with the ring position in device
+# words, auto-reset beside the update) as graph replays, two steps per replay in bench.py
+# (AAC_UAM_STEP_GRAPH=1; bit-identical, test_uam_whole_step_graph_equals_eager).  Measured slower than
+# the host-launched step (0.5167 / 0.5189 vs 0.5115 / 0.5144 ms interleaved, profiles/r06_uam_step_graph_ab.txt),
+# so off by default
+UAM_STEP_GRAPH = os.environ.get("AAC_UAM_STEP_GRAPH", "0") == "1"
 
 
 class CheckpointMixin:
@@ -352,8 +362,97 @@ class UamTrainer(CheckpointMixin):
         self.env.auto_reset(None, out=self.cur)      # episode counters -> 1
         self.env_events = []
         self.pre_step_hooks, self.post_step_hooks = [], []      # as Trainer's
+        self.bufs = [self.cur, self.nxt]
+        self._sg, self._sg2 = {}, {}                  # parity -> captured whole-step graph (1 / 2 steps)
+        self.pos_dev = torch.zeros(2, dtype=torch.int64, device="cuda")   # ring position ping-pong
+        self._pos_dirty = True
+
+    def graph_ok(self):
+        """Whole-step graphs: one rank, the fused learner, the replay past one batch, no hooks."""
+        m = self.model
+        return (UAM_STEP_GRAPH and m.world == 1 and m.fused_learner and not NO_GRAPH
+                and len(self.replay) > self.B and not self.hooked())
+
+    def hooked(self):
+        return bool(self.pre_step_hooks or self.post_step_hooks)
+
+    def _step_body(self, p, side):
+        """The launches of ``step(update=True)`` from buffer parity p, for capture: the push reads /
+        advances the ring position in pos_dev[p] / pos_dev[1 - p] (aac_uam_push_io); the update is the
+        fused learner's raw launches."""
+        c, n = self.bufs[p], self.bufs[1 - p]
+        act = self.model.act(c.own, c.radar, self.episode, noisy=True)
+        self.env.step(act, out=n)
+        self.replay.push_batch(c.own, c.radar, act, n.reward, n.done, n.own, n.radar,
+                               pos_io=(self.pos_dev[p], self.pos_dev[1 - p]))
+        fu = self.model.fused(self.B, self.replay)
+        if side is not None:
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.env.auto_reset(n.env_done, out=n)
+            fu.run()
+            main.wait_stream(side)
+        else:
+            self.env.auto_reset(n.env_done, out=n)
+            fu.run()
+
+    def _capture_step(self, p, steps=1):
+        saved = (self.replay.pos, self.replay.size)
+        side = torch.cuda.Stream() if UAM_OVERLAP_RESET else None
+        self.model.fused(self.B, self.replay)        # built outside the capture
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for k in range(steps):
+                self._step_body(p ^ (k & 1), side)
+        self.replay.pos, self.replay.size = saved
+        return g, side
+
+    def _advance_mirror(self, steps):
+        if self._pos_dirty:
+            p = 0 if self.cur is self.bufs[0] else 1
+            self.pos_dev[p].fill_(self.replay.pos)
+            self._pos_dirty = False
+        rep, M = self.replay, self.E * self.N
+        for _ in range(steps):
+            rep.pos = (rep.pos + M) % rep.capacity
+            rep.size = min(rep.size + M, rep.capacity)
+            self.cur, self.nxt = self.nxt, self.cur
+
+    def _graphs_current(self):
+        gen = getattr(self.env, "bank_generation", 0)
+        if (self._sg or self._sg2) and (getattr(self, "_sg_bank_gen", gen) != gen
+                                        or getattr(self, "_sg_fu", None) is not self.model._fu):
+            # the episode bank / seed changed, or the fused learner was rebuilt (new buffers), under
+            # the captured graphs
+            self._sg, self._sg2 = {}, {}
+        self._sg_bank_gen = gen
+        self._sg_fu = self.model.fused(self.B, self.replay)
+
+    def step_graph(self):
+        """One training step (``step(update=True)``'s launches) as one graph replay."""
+        p = 0 if self.cur is self.bufs[0] else 1
+        self._graphs_current()
+        if p not in self._sg:
+            self._sg[p] = self._capture_step(p)
+        self._advance_mirror(0)
+        with trace.range("step_graph"):
+            self._sg[p][0].replay()
+        self._advance_mirror(1)
+
+    def step_graph_pair(self):
+        """Two training steps as one graph replay (both buffer parities): half the graph-launch gaps."""
+        p = 0 if self.cur is self.bufs[0] else 1
+        self._graphs_current()
+        if p not in self._sg2:
+            self._sg2[p] = self._capture_step(p, steps=2)
+        self._advance_mirror(0)
+        with trace.range("step_graph_pair"):
+            self._sg2[p][0].replay()
+        self._advance_mirror(2)
 
     def step(self, update=True, time_env=False):
+        self._pos_dirty = True
         c, n = self.cur, self.nxt
         for f in self.pre_step_hooks:
             f(self)

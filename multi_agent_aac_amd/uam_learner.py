@@ -100,23 +100,38 @@ class UamReplay:
     def __len__(self):
         return self.size
 
-    def push_batch(self, own, radar, act, rew, done, n_own, n_radar):
+    def push_batch(self, own, radar, act, rew, done, n_own, n_radar, pos_io=None):
         """E x N transitions (leading dims flattened): one aac_uam_push launch for contiguous device
-        float64 inputs (done uint8 or float64), else a row-assembly launch per ring segment."""
+        float64 inputs (done uint8 or float64), else a row-assembly launch per ring segment.
+        ``pos_io`` = (pos_in, pos_out) int64 device words (graph replays, aac_uam_push_io): the kernel
+        reads the position from pos_in and advances it into pos_out and meta; the host mirror
+        advances as usual."""
         M = own.numel() // 7
         if M > self.capacity:
             raise ValueError("one push larger than the replay capacity")
+        if pos_io is not None and self.device.type != "cuda":
+            raise ValueError("pos_io needs the device ring")
         ts = (own, radar, act, rew, n_own, n_radar)
         if (self.device.type == "cuda" and all(t.is_cuda and t.dtype == F64 and t.is_contiguous() for t in ts)
                 and done.is_cuda and done.is_contiguous() and done.dtype in (torch.uint8, F64)
                 and rew.numel() == M and done.numel() == M):
             from . import fused
             p = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
+            if pos_io is not None:
+                pin, pout = pos_io
+                assert pin.dtype == torch.int64 and pout.dtype == torch.int64 and pin.data_ptr() != pout.data_ptr()
+                _ok(_learn_lib().aac_uam_push_io(p(self.ring), self.capacity, M, p(own), p(radar), p(act), p(rew),
+                                                 p(done), int(done.dtype == torch.uint8), p(n_own), p(n_radar),
+                                                 p(self.meta), p(pin), p(pout), fused._stream()), "aac_uam_push_io")
+                self._advance(M, meta=False)
+                return
             _ok(_learn_lib().aac_uam_push(p(self.ring), self.capacity, self.pos, M, p(own), p(radar), p(act), p(rew),
                                           p(done), int(done.dtype == torch.uint8), p(n_own), p(n_radar),
                                           p(self.meta), self.size, fused._stream()), "aac_uam_push")
             self._advance(M, meta=False)       # the kernel wrote meta
             return
+        if pos_io is not None:
+            raise ValueError("pos_io needs contiguous device float64 sources (the aac_uam_push_io launch)")
         cols = [own.reshape(-1, 7), radar.reshape(-1, 18), act.reshape(-1, 2), rew.reshape(-1, 1),
                 done.reshape(-1, 1), n_own.reshape(-1, 7), n_radar.reshape(-1, 18)]
         cols = [c if c.dtype == F64 else c.to(F64) for c in cols]
@@ -197,6 +212,7 @@ def _learn_lib():
         L.aac_adam64_sum_scaled.argtypes = [vp, vp, i32, vp, vp, i64, dbl, dbl, dbl, dbl, vp, i32, dbl, vp]
         L.aac_uam_polyak.argtypes = [vp, vp, i64, dbl, vp, vp, vp, i32, vp, vp]
         L.aac_uam_push.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp, i64, vp]
+        L.aac_uam_push_io.argtypes = [vp, i64, i64, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]
         L.aac_sum64_partials.argtypes = [vp, vp, i32, i64, vp]
         _LL = L
     return _LL

@@ -74,6 +74,46 @@ def test_uam_overlapped_reset_matches_serial(native_lib, monkeypatch):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("overlap", [True, False])
+def test_uam_whole_step_graph_equals_eager(native_lib, monkeypatch, overlap):
+    """UamTrainer.step_graph / step_graph_pair (act + env step + replay push with the ring position in
+    device words (aac_uam_push_io) + auto-reset beside the update, replayed from captured graphs)
+    against the same steps launched eagerly: every learner, replay and env tensor bit-identical, the
+    host mirror of the ring position too, across ring wraps (8192 rows, 1536 per push), an eager step
+    between replays (the device word re-seeded) and both starting parities."""
+    from multi_agent_aac_amd import trainer
+    monkeypatch.setattr(trainer, "UAM_OVERLAP_RESET", overlap)
+    monkeypatch.setattr(trainer, "UAM_STEP_GRAPH", True)     # off by default in the bench (measured slower)
+    tr = [_trainer("uam") for _ in range(2)]
+    for t in tr:
+        while len(t.replay) <= t.B:
+            t.step(update=False)
+        t.step(update=True)
+    assert tr[1].graph_ok()
+    for k in range(5):
+        tr[0].step(update=True)
+        if k == 2:
+            tr[1].step(update=True)
+        else:
+            tr[1].step_graph()
+    for _ in range(3):
+        tr[0].step(update=True)
+        tr[0].step(update=True)
+        tr[1].step_graph_pair()
+    tr[0].step(update=True)
+    tr[1].step(update=True)
+    for _ in range(2):
+        tr[0].step(update=True)
+        tr[0].step(update=True)
+        tr[1].step_graph_pair()
+    a, b = _snapshot(tr[0]), _snapshot(tr[1])
+    assert set(a) == set(b)
+    bad = [k for k in a if not torch.equal(a[k], b[k])]
+    assert not bad, bad
+    assert (tr[0].replay.pos, tr[0].replay.size) == (tr[1].replay.pos, tr[1].replay.size)
+    assert torch.equal(tr[0].episode, tr[1].episode)
+
+
 def test_checkpoint_refuses_mismatch(native_lib, tmp_path):
     from multi_agent_aac_amd import checkpoint
     a = _trainer("att")
@@ -115,13 +155,12 @@ def test_resume_into_running_loop_with_other_seeds(native_lib, model, tmp_path, 
         b.step(update=False)
     for _ in range(2):
         b.step(update=True)
-    if model == "att":
-        b.step_graph()
-        assert b._sg
+    b.step_graph()
+    assert b._sg
     assert b.model.has_graph()
     b.load_checkpoint(path)
     for k in range(4):
-        if model == "att" and k % 2:
+        if k % 2:
             b.step_graph()
         else:
             b.step(update=True)

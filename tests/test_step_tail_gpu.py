@@ -147,7 +147,7 @@ def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, st
     ring-position word.  Then two steps per replay (step_graph_pair, both parities in one
     graph: the bench's timed form) from either starting parity."""
     from multi_agent_aac_amd import trainer
-    monkeypatch.setattr(trainer, "STEP_GRAPH", True)        # off by default in the bench (measured neutral)
+    monkeypatch.setattr(trainer, "STEP_GRAPH", True)
     tr = [trainer.Trainer(E, N, B, mem, "combined", seed=0, model=model) for _ in range(2)]
     for t in tr:
         while len(t.replay) <= 3 * B:
