@@ -42,7 +42,9 @@ def _init(rank, ws, port):
                       LOCAL_RANK="0")
     import torch.distributed as dist
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    # AAC_TEST_BACKEND=nccl: one GPU per rank (each process sees only its own, set before the first
+    # HIP call by _worker), the collectives captured in the update graph (parallel.capturable)
+    dist.init_process_group(os.environ.get("AAC_TEST_BACKEND", "gloo"), rank=rank, world_size=ws)
     return dist
 
 
@@ -295,7 +297,10 @@ def _unpack(blob):
     return torch.load(io.BytesIO(blob), weights_only=True)
 
 
-def _worker(rank, ws, port, q, kind):
+def _worker(rank, ws, port, q, kind, backend="gloo"):
+    os.environ["AAC_TEST_BACKEND"] = backend
+    if backend == "nccl":
+        os.environ["HIP_VISIBLE_DEVICES"] = str(rank)      # before this process's first HIP call
     try:
         q.put((rank, _pack(WORK[kind](rank, ws, port))))
     except BaseException as e:      # report instead of leaving the peer blocked in a collective
@@ -303,11 +308,11 @@ def _worker(rank, ws, port, q, kind):
         raise
 
 
-def _run_two(kind):
+def _run_two(kind, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, kind)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, kind, backend)) for r in range(2)]
     for p in procs:
         p.start()
     out = {r: _unpack(b) for r, b in (q.get(timeout=240) for _ in procs)}
@@ -338,6 +343,23 @@ def test_two_rank_shards_match_mean_gradient_oracle(native_lib, kind):
     for r in range(2):
         assert out[r]["n_segments"] > 1 and (SEGMENTS[kind] is None or out[r]["n_segments"] == SEGMENTS[kind]), out[r][
             "n_segments"]
+        assert out[r]["graph_equal"], r
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="two GPUs needed (one rank per GPU over RCCL)")
+@pytest.mark.parametrize("kind", ["att", "gru", "uam"])
+def test_two_rank_rccl_matches_mean_gradient_oracle(native_lib, kind):
+    """the world > 1 default over RCCL -- two ranks on two GPUs, the all-reduces captured
+    inside the update graph -- against the same mean-gradient restatement, ranks bit-identical, the
+    one-graph replay equal to the eager launch list.  Skipped on one-GPU boxes (this pool's): there
+    the captured-collective schedule is pinned by test_rccl_collectives_captured_in_graph (one rank)
+    and the mean-gradient arithmetic by the gloo test above; AAC_GRAPH_COLL=0 is the fallback
+    (segments with eager RCCL collectives)."""
+    out = _run_two(kind, "nccl")
+    for x, y in zip(out[0]["flat"], out[1]["flat"]):
+        assert torch.equal(x, y)
+    CHECK[kind](out)
+    for r in range(2):
         assert out[r]["graph_equal"], r
 
 
