@@ -1,6 +1,7 @@
 """Per-step kernel time of the last K steps of a rocprofv3 kernel trace, steps delimited by a
 marker kernel (default the env step kernel): python tools/trace_window.py run_kernel_trace.csv
-[K] [marker]"""
+[K] [marker] [skip].  skip: trailing steps left out -- bench.py runs 10 eager env-timing steps after
+a graph-replayed timed region, so the timed steps of configs 3 and 4 are the ones before those."""
 import collections
 import csv
 import sys
@@ -9,8 +10,9 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 marker = sys.argv[3] if len(sys.argv) > 3 else "::step_kernel("
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
-a, b = idx[-K - 1], idx[-1]
+a, b = idx[-K - 1 - skip], idx[-1 - skip]
 seg = rows[a:b]
 ksum = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg) / 1e3
 # GPU busy = the union of the kernel intervals (kernels on two streams overlap)
@@ -25,7 +27,7 @@ for r in seg:
         end = e0
 busy /= 1e3
 wall = (int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
-print(f"last {K} steps: {len(seg) / K:.1f} launches/step, kernel time {ksum / K:.1f} us/step, "
+print(f"{'last' if not skip else f'{skip} eager steps skipped, then the last'} {K} steps: {len(seg) / K:.1f} launches/step, kernel time {ksum / K:.1f} us/step, "
       f"wall {wall / K:.1f} us/step (GPU busy {100 * busy / wall:.1f} %"
       + (f", kernels overlapping {ksum - busy:.0f} us over {K} steps)" if ksum > busy + 1 else ")"))
 agg = collections.defaultdict(lambda: [0.0, 0])
