@@ -1,7 +1,7 @@
 """Sub-phase timeline of the env step kernel's agent phase (thread 0 = agent 0 of the workgroup's
 first env) from a stamp build with agent stamps:
   bash tools/variant_lib.sh astamps aac_env.hip -DAAC_ENV_STAMPS -DAAC_ENV_AGENT_STAMPS
-  AAC_LIB=tools/variants/lib_astamps.so python tools/agent_stamps.py [E] [N] [att|wgru]
+  AAC_LIB=tools/vlib/lib_astamps.so python tools/agent_stamps.py [E] [N] [att|wgru]
 Phases (cycles): observe_agent (obs rows + tdCPA), neighbour loops (collisions, penalty), building
 cells, goal + bound predicates, reward + writes (WGRU: wgru_reward); with the step phases around them."""
 import ctypes

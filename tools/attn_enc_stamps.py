@@ -1,6 +1,6 @@
 """Phase timestamps (s_memtime) of workgroup 0 of aac_attn_enc_fwd (training set, config-3 shapes),
 from a probe build: bash tools/variant_lib.sh astamp aac_fused.hip -DAAC_ATTN_STAMPS, then
-AAC_LIB=tools/variants/lib_astamp.so python tools/attn_enc_stamps.py [R ...].  Phases: issue of the
+AAC_LIB=tools/vlib/lib_astamp.so python tools/attn_enc_stamps.py [R ...].  Phases: issue of the
 staging + weight-fragment loads, staging barrier, encoders + stores, barrier, q, qk, softmax, v."""
 import ctypes
 import os

@@ -1,5 +1,5 @@
 """Per-workgroup phase timeline of the env step kernel at config 3 (4096 x 5, combined radar) from a
-stamp build (bash tools/variant_lib.sh estamps aac_env.hip -DAAC_ENV_STAMPS; AAC_LIB=...)."""
+stamp build (bash tools/variant_lib.sh estamps aac_env.hip -DAAC_ENV_STAMPS; AAC_LIB=tools/vlib/lib_estamps.so)."""
 import ctypes
 import os
 import sys

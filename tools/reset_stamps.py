@@ -1,6 +1,6 @@
 """Phase timeline of the env auto-reset kernel (reset_kernel) in the training loop's steady state,
 from a stamp build (bash tools/variant_lib.sh estamps multi_agent_aac_amd/csrc/aac_env.hip
--DAAC_ENV_STAMPS; AAC_LIB=tools/variants/lib_estamps.so).  Default: config 4 (WGRU env, 8 agents x
+-DAAC_ENV_STAMPS; AAC_LIB=tools/vlib/lib_estamps.so).  Default: config 4 (WGRU env, 8 agents x
 4096 envs); ``att`` for config 3 (5 x 4096, combined radar).  Phases: OD draw, state writes, radar,
 observation (cycles), per resetting workgroup."""
 import ctypes
