@@ -21,6 +21,7 @@
 
 #include "../../include/aac_uam.h"
 #include "aac_noise.h"
+#include "aac_wave.h"
 
 namespace {
 
@@ -202,11 +203,27 @@ __device__ __forceinline__ double row_noise(const ActorArgs &A, int r, uint64_t 
 // k step, so the block's latency chain (loads, two barriers, the 32-step merge chain, the output
 // reduction, the noise) is paid once per 16 NT rows.  NT = 1 was the first form: ~10 k cycles per
 // 16 rows at one wave per SIMD.  Every row's arithmetic is the same for any NT (bit-identical).
+// AAC_UAM_ACT_PF (default 1): the next block's own / radar rows are loaded while this block's merge
+// chain runs (spare registers of the one-wave-per-SIMD launch; LDS-only barriers keep them in flight),
+// and the exploration noise of the workgroup's first NBN blocks is drawn up front into LDS by all 256
+// threads (the fp64 Box-Muller off the per-block output stage, which one wave ran after the chain).
+// Same arithmetic per row: bit-identical to the form without either.
+#ifndef AAC_UAM_ACT_PF
+#define AAC_UAM_ACT_PF 1
+#endif
+#if AAC_UAM_ACT_PF
+#define UACT_BARRIER() aacw::lds_barrier()
+#else
+#define UACT_BARRIER() __syncthreads()
+#endif
+constexpr int NBN = 8;       // blocks per workgroup whose noise is drawn up front (config 5: 8 per workgroup)
+
 template <int NT>
 __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
     constexpr int ROWS = 16 * NT, TS = ROWS + 1;       // TS: row stride of the [feature][rows] image
     __shared__ double sH[128 * TS];          // [h_o | h_r] of the block, [feature][row]
     __shared__ double sP[4][ROWS][2];        // per-wave partial output dots
+    __shared__ double2 sN[AAC_UAM_ACT_PF ? NBN * ROWS : 1];     // up-front noise, [block of the wg][row]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
     // A fragments (lane: output row 16 t + n of the tile, k slot kq of each 4-step)
     double a1[2], a2[5], a3[2][32];
@@ -242,9 +259,8 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
     // the launch's noise epoch (one atomic per workgroup), after the weight loads are in flight
     const uint64_t ctr = A.noisy ? aacn::take_epoch(A.counter) : 0;
     const int nblk = (A.R + ROWS - 1) / ROWS;
-    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    auto load_rows = [&](int blk, double (&bo)[NT][2], double (&br)[NT][5]) {
         const int r0 = blk * ROWS;
-        double bo[NT][2], br[NT][5];
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             const int r = r0 + 16 * q + n;
@@ -260,6 +276,25 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
                 br[q][s] = A.radar[(size_t)rc * 18 + (k < 18 ? k : 17)];
             }
         }
+    };
+    double bo[NT][2], br[NT][5];
+    if (AAC_UAM_ACT_PF && (int)blockIdx.x < nblk) load_rows(blockIdx.x, bo, br);
+    if (AAC_UAM_ACT_PF && A.noisy) {
+        for (int i = threadIdx.x; i < NBN * ROWS; i += 256) {
+            const int bi = i / ROWS, x = i - bi * ROWS;
+            const int rr = (blockIdx.x + bi * gridDim.x) * ROWS + x;
+            if (rr < A.R) {
+                double e1;
+                const double e0 = row_noise(A, rr, ctr, e1);
+                sN[i] = make_double2(e0, e1);
+            }
+        }
+    }
+    for (int blk = blockIdx.x, bi = 0; blk < nblk; blk += gridDim.x, ++bi) {
+        const int r0 = blk * ROWS;
+        double nbo[NT][2], nbr[NT][5];
+        if (!AAC_UAM_ACT_PF) load_rows(blk, bo, br);
+        else if (blk + (int)gridDim.x < nblk) load_rows(blk + gridDim.x, nbo, nbr);
         // h_o^T = relu(W1 own^T + b1), h_r^T = relu(W2 radar^T + b2): padded k slots have a zero A
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
@@ -277,7 +312,7 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
                 sH[(64 + 16 * w + kq + 4 * j) * TS + 16 * q + n] = u > 0.0 ? u : 0.0;
             }
         }
-        __syncthreads();
+        UACT_BARRIER();
         // h^T = relu(W3 [h_o | h_r]^T + b3), two output tiles per wave and NT row tiles, then this
         // lane's share of the 128 -> 2 output layer
         d4 h0[NT], h1[NT];
@@ -322,7 +357,7 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
                 sP[w][16 * q + n][1] = p1;
             }
         }
-        __syncthreads();
+        UACT_BARRIER();
         for (int x = threadIdx.x; x < ROWS; x += 256) {
             const int rr = r0 + x;
             if (rr < A.R) {
@@ -330,13 +365,28 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
                 const double s1 = ((sP[0][x][1] + sP[1][x][1]) + sP[2][x][1]) + sP[3][x][1];
                 double x0 = tanh(s0 + b40), x1 = tanh(s1 + b41);
                 if (A.noisy) {
-                    double e1;
-                    const double e0 = row_noise(A, rr, ctr, e1);
+                    double e0, e1;
+                    if (AAC_UAM_ACT_PF && bi < NBN) {
+                        const double2 z = sN[bi * ROWS + x];
+                        e0 = z.x;
+                        e1 = z.y;
+                    } else {
+                        e0 = row_noise(A, rr, ctr, e1);
+                    }
                     x0 = fmin(fmax(x0 + e0, -1.0), 1.0);
                     x1 = fmin(fmax(x1 + e1, -1.0), 1.0);
                 }
                 A.out[2 * (size_t)rr] = x0;
                 A.out[2 * (size_t)rr + 1] = x1;
+            }
+        }
+        if (AAC_UAM_ACT_PF) {
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s) bo[q][s] = nbo[q][s];
+#pragma unroll
+                for (int s = 0; s < 5; ++s) br[q][s] = nbr[q][s];
             }
         }
     }
