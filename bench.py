@@ -645,22 +645,28 @@ def main():
     tr.env_events.clear()
     t0 = time.perf_counter()
     graphed = hasattr(tr, "graph_ok") and tr.graph_ok()
-    # two steps per graph replay (both buffer parities in one graph: half the graph-launch gaps) when
-    # the step count is even; AAC_STEP_PAIR=0 replays one step per graph
-    pairs = graphed and a.steps % 2 == 0 and os.environ.get("AAC_STEP_PAIR", "1") == "1"
+    # several steps per graph replay (the buffer parities in sequence: fewer graph-launch gaps): the
+    # largest of AAC_STEP_GROUP (default 2: 4 measured slower, profiles/r06_step_group_ab.txt) and 2 that
+    # divides the step count; AAC_STEP_PAIR=0 replays
+    # one step per graph
+    group = 1
+    if graphed and os.environ.get("AAC_STEP_PAIR", "1") == "1":
+        group = next((g for g in (int(os.environ.get("AAC_STEP_GROUP", "2")), 2) if g >= 2 and g % 2 == 0
+                      and a.steps % g == 0), 1)
+    pairs = group > 1
     if graphed:
         for _ in range(2):        # capture (untimed) and replay once
             if pairs:
-                tr.step_graph_pair()
+                tr.step_graph_pair(group)
             else:
                 tr.step_graph()
         torch.cuda.synchronize()
         barrier(ws)
         t0 = time.perf_counter()
     with trace.range("timed_steps"):
-        for k in range(a.steps // 2 if pairs else a.steps):
+        for k in range(a.steps // group):
             if pairs:
-                tr.step_graph_pair()
+                tr.step_graph_pair(group)
             elif graphed:
                 tr.step_graph()
             else:
@@ -745,7 +751,7 @@ def main():
                    "parallelism": f"env-shard x{ws}" + (" + RCCL grad all-reduce" if ws > 1 else ""),
                    "maps": 1 if uam else a.maps, "tdcpa": uam,
                    "update_graph": (not a.no_graph) and (ws == 1 or uam or tr.gru or tr.model.fused),
-                   "step_graph": ("two steps per graph replay" if pairs else graphed),
+                   "step_graph": (f"{group} steps per graph replay" if pairs else graphed),
                    "auto_reset": ("packed launch on a side stream beside the update" if _trainer.UAM_OVERLAP_RESET
                                   else "packed launch before the update") if uam else (
                                   "in the env step launch" if tr.fused_tail else "separate launch"),

@@ -227,21 +227,22 @@ class Trainer(CheckpointMixin):
             self._sg[p][0].replay()
         self._advance_mirror(1)
 
-    def step_graph_pair(self):
-        """Two training steps as ONE graph replay (both buffer parities in sequence): the GPU idles at
-        each graph launch boundary (~6-9 us between the end of one replay and the first kernel of the
-        next), so two steps per replay halve those gaps.  The same launches and results as two
-        ``step_graph`` calls."""
+    def step_graph_pair(self, steps=2):
+        """``steps`` (even) training steps as ONE graph replay (the buffer parities in sequence): the
+        GPU idles at each graph launch boundary (~6-9 us between the end of one replay and the first
+        kernel of the next), so k steps per replay cut those gaps k-fold.  The same launches and
+        results as ``steps`` ``step_graph`` calls."""
+        assert steps >= 2 and steps % 2 == 0
         p = 0 if self.cur is self.bufs[0] else 1
         self._graphs_current()
         if not getattr(self, "_sg2", None):
             self._sg2 = {}
-        if p not in self._sg2:
-            self._sg2[p] = self._capture_step(p, steps=2)
+        if (p, steps) not in self._sg2:
+            self._sg2[(p, steps)] = self._capture_step(p, steps=steps)
         self._advance_mirror(0)
         with trace.range("step_graph_pair"):
-            self._sg2[p][0].replay()
-        self._advance_mirror(2)
+            self._sg2[(p, steps)][0].replay()
+        self._advance_mirror(steps)
 
     def env_episode_view(self):
         # the env's own per-env episode counter (advanced by each auto-reset; 1 after the first)
@@ -440,16 +441,17 @@ class UamTrainer(CheckpointMixin):
             self._sg[p][0].replay()
         self._advance_mirror(1)
 
-    def step_graph_pair(self):
-        """Two training steps as one graph replay (both buffer parities): half the graph-launch gaps."""
+    def step_graph_pair(self, steps=2):
+        """``steps`` (even) training steps as one graph replay (the buffer parities in sequence)."""
+        assert steps >= 2 and steps % 2 == 0
         p = 0 if self.cur is self.bufs[0] else 1
         self._graphs_current()
-        if p not in self._sg2:
-            self._sg2[p] = self._capture_step(p, steps=2)
+        if (p, steps) not in self._sg2:
+            self._sg2[(p, steps)] = self._capture_step(p, steps=steps)
         self._advance_mirror(0)
         with trace.range("step_graph_pair"):
-            self._sg2[p][0].replay()
-        self._advance_mirror(2)
+            self._sg2[(p, steps)][0].replay()
+        self._advance_mirror(steps)
 
     def step(self, update=True, time_env=False):
         self._pos_dirty = True

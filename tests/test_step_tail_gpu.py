@@ -144,8 +144,8 @@ def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, st
     eagerly: bit-identical networks, optimiser state, replay ring and env state.  The second case is
     config 3 (4096 envs x 5 agents, B = 1024); the GRU step (config 4: 4096 x 8, B = 512) carries the
     hidden-state pair through the replays.  An eager step between graph replays re-seeds the device
-    ring-position word.  Then two steps per replay (step_graph_pair, both parities in one
-    graph: the bench's timed form) from either starting parity."""
+    ring-position word.  Then two and four steps per replay (step_graph_pair, the parities
+    in sequence in one graph: the bench's timed forms) from either starting parity."""
     from multi_agent_aac_amd import trainer
     monkeypatch.setattr(trainer, "STEP_GRAPH", True)
     tr = [trainer.Trainer(E, N, B, mem, "combined", seed=0, model=model) for _ in range(2)]
@@ -172,6 +172,10 @@ def test_whole_step_graph_equals_eager(native_lib, monkeypatch, E, N, B, mem, st
         tr[0].step(update=True)
         tr[0].step(update=True)
         tr[1].step_graph_pair()
+    # four steps per replay (the bench's form when the step count allows it)
+    for _ in range(4):
+        tr[0].step(update=True)
+    tr[1].step_graph_pair(4)
     torch.cuda.synchronize()
     a, b = tr[0], tr[1]
     for x, y in ((a.model.fa.data, b.model.fa.data), (a.model.fc.data, b.model.fc.data),
