@@ -135,10 +135,6 @@ int aac_env_auto_reset(aac_env *env, const uint8_t *env_done_dev, const aac_step
  * (the default, or AAC_ENV_RESET_PACKED=0 / 1) packs for the WGRU variant only, where a large
  * share of the envs ends every step.  Results are identical either way. */
 void aac_env_set_reset_compact(int32_t on);
-/* Process-wide: on != 0 (the default, or AAC_ENV_RADAR_WL=0 / 1) the variant-0 step launches clip
- * their radar candidate cells as one workgroup-wide list (balanced over the threads) when the items
- * fit; 0 runs every (agent, ray) item on its own thread.  Results are identical either way. */
-void aac_env_set_radar_work_list(int32_t on);
 /* Diagnostic builds only (-DAAC_ENV_STAMPS): per-workgroup phase stamps of the last step launch
  * (7 uint64 per workgroup); returns an error in a normal build. */
 int aac_env_stamps(unsigned long long *out, int32_t n_wg);

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("AAC_LIB") or os.path.join(_HERE, "libaac_env.so")
 
 EXPORTS = (
     "aac_env_create", "aac_env_destroy", "aac_last_error", "aac_env_reset", "aac_env_step", "aac_env_step_tail",
-    "aac_env_set_od_bank", "aac_env_set_od_banks", "aac_env_auto_reset", "aac_env_set_reset_compact", "aac_env_set_radar_work_list", "aac_env_use_episode_buffer", "aac_env_get_state", "aac_env_set_state",
+    "aac_env_set_od_bank", "aac_env_set_od_banks", "aac_env_auto_reset", "aac_env_set_reset_compact", "aac_env_use_episode_buffer", "aac_env_get_state", "aac_env_set_state",
     "aac_env_band_max", "aac_astar", "aac_od_bank_build",
 )
 
@@ -69,9 +69,6 @@ def lib():
     L.aac_env_auto_reset.argtypes = [vp, vp, ctypes.POINTER(StepOut), vp]
     L.aac_env_set_reset_compact.argtypes = [ctypes.c_int32]
     L.aac_env_set_reset_compact.restype = None
-    if hasattr(L, "aac_env_set_radar_work_list") or not os.environ.get("AAC_LIB"):
-        L.aac_env_set_radar_work_list.argtypes = [ctypes.c_int32]
-        L.aac_env_set_radar_work_list.restype = None
     L.aac_env_use_episode_buffer.argtypes = [vp, vp, vp]
     if hasattr(L, "aac_env_band_max") or not os.environ.get("AAC_LIB"):   # (older A/B builds lack it)
         L.aac_env_band_max.argtypes = [vp, vp, vp, vp]

@@ -520,260 +520,6 @@ __device__ __attribute__((always_inline)) void radar_phase(const Args &A, Lds &S
     }
 }
 
-// ---------------------------------------------------------------- work-list radar (variant 0)
-// The radar phase with its cell clips balanced over the workgroup (AAC_ENV_RADAR_WL): one pass
-// collects every (agent, ray) item's candidate cells (the 8 x 8-cell box's row masks and the line
-// filter of radar_obstacles) and its drone / boundary-line minimum; the workgroup's candidates are
-// then clipped as one list, thread c taking candidates c, c + 256, ... -- a ray with many candidate
-// cells no longer holds its wave while the others idle -- and each hit lowers its item's minimum with
-// an LDS atomic min on an order key of the distance.  The minimum of the same hit distances as
-// radar_ray (no pruning: the skipped squares could not lower it, so the result is the same), the
-// band flags of mode 1 as there (a square the pruning skipped may add a flag: band_fix_kernel then
-// re-runs a ray whose answer cannot change).  The lists alias the observation staging area
-// (S.obs), dead during the radar phase; the host picks this path when the items fit, the map has row
-// masks and the radar's box stays within 8 x 8 cells.
-#ifndef AAC_ENV_RADAR_WL
-#define AAC_ENV_RADAR_WL 1
-#endif
-constexpr int WL_ITEMS = 432;          // (agent, ray) items: nag * NRAY <= WL_ITEMS (24 agents)
-struct WlLds {
-    unsigned long long key[WL_ITEMS];  // the item's minimum so far, as an order key (dkey)
-    unsigned long long cand[WL_ITEMS]; // candidate cells of the item's box, bit (i - i0) * 8 + (j - j0)
-    int ij[WL_ITEMS];                  // the box's first cell, i0 << 16 | j0
-    int16_t pre[WL_ITEMS + 1];         // exclusive prefix of the candidate counts (<= 64 WL_ITEMS < 2^15)
-    unsigned band[(WL_ITEMS + 31) / 32];   // items with a threshold-band case
-    int wtot[BLOCK / 64];              // the scan's wave totals
-};
-static_assert(sizeof(WlLds) <= sizeof(float) * OBS_STAGE_FLOATS, "the work lists fit the staging area");
-static_assert(64 * WL_ITEMS < 32768, "candidate prefix in int16");
-
-// a total order on doubles as unsigned keys (-0 < +0; every distance here is >= 0)
-__device__ inline unsigned long long dkey(double d) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(d);
-    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-__device__ inline double dfromkey(unsigned long long k) {
-    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
-}
-
-// the k-th (0-based) set bit of m (k < popcount(m))
-__device__ inline int select_bit(unsigned long long m, int k) {
-    const int lo = __popcll(m & 0xffffffffull);
-    int base = 0;
-    if (k >= lo) {
-        k -= lo;
-        m >>= 32;
-        base = 32;
-    }
-    unsigned x = (unsigned)m;
-#pragma unroll 1
-    for (int b = 0; b < 4; ++b) {
-        const int c = __popc(x & 0xffu);
-        if (k < c) break;
-        k -= c;
-        x >>= 8;
-        base += 8;
-    }
-#pragma unroll 1
-    for (; k > 0; --k) x &= x - 1;
-    return base + __builtin_ctz(x);
-}
-
-// the item's ray geometry, as radar_ray computes it
-__device__ __attribute__((always_inline)) void wl_ray(const Args &A, const Lds &S, int w, int &le, int &i, int &r,
-                                                      double &px, double &py, double &ex, double &ey) {
-    const int la = w / NRAY;
-    r = w - la * NRAY;
-    le = la / A.N;
-    i = la - le * A.N;
-    const double2 p = S.pos[le * A.N + i];
-    px = p.x;
-    py = p.y;
-    ex = px + A.radar_len * c_tab.ray_c[r];
-    ey = py + A.radar_len * c_tab.ray_s[r];
-}
-
-__device__ __attribute__((always_inline)) void radar_phase_wl(const Args &A, Lds &S, int e0, int nagents,
-                                                              RingOut ro) {
-    WlLds &W = *reinterpret_cast<WlLds *>(S.obs);
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nitems = nagents * NRAY;
-    static_assert(WL_ITEMS <= 2 * BLOCK, "two items per thread");
-    if (t < (WL_ITEMS + 31) / 32) W.band[t] = 0u;
-    aacw::lds_barrier();
-    // (1) per item: candidate cells, the drone / boundary-line minimum
-    int cnt[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int w = t + k * BLOCK;
-        cnt[k] = 0;
-        if (w >= WL_ITEMS) continue;
-        unsigned long long cnd = 0;
-        int ij = 0;
-        double pre = 0.0;
-        bool band = false;
-        int le, i, r;
-        double px, py, ex, ey;
-        wl_ray(A, S, w < nitems ? w : 0, le, i, r, px, py, ex, ey);
-        const int e = e0 + le;
-        if (w < nitems && e < A.E) {
-            const int mi = A.map_idx ? A.map_idx[e] : 0;
-            const unsigned long long *rows = map_rows(A, mi);
-            const double len = gdist(ex, ey, px, py);
-            double dd = len;
-            if (A.radar_mode != AAC_RADAR_OBSTACLES) {     // drones: as radar_ray
-                const int N = A.N, base = le * N;
-                const double pb = A.pb;
-                const double reach2 = (pb + 1e-6) * (pb + 1e-6);
-                const double ddx = ex - px, ddy = ey - py;
-                const double inv = 1.0 / (ddx * ddx + ddy * ddy);
-                double shortest = INFINITY;
-                for (int j0 = 0; j0 < N; j0 += 64) {
-                    const int jn = N - j0 < 64 ? N - j0 : 64;
-                    unsigned long long cand = 0;
-                    for (int jj = 0; jj < jn; ++jj) {
-                        const double2 q = S.pos[base + j0 + jj];
-                        const double wx = q.x - px, wy = q.y - py;
-                        double tt = (wx * ddx + wy * ddy) * inv;
-                        tt = tt < 0.0 ? 0.0 : (tt > 1.0 ? 1.0 : tt);
-                        const double qx = tt * ddx - wx, qy = tt * ddy - wy;
-                        if (j0 + jj != i && qx * qx + qy * qy <= reach2) cand |= 1ull << jj;
-                    }
-                    while (cand) {
-                        const int j = j0 + __builtin_ctzll(cand);
-                        cand &= cand - 1;
-                        const double2 q = S.pos[base + j];
-                        double tq;
-                        if (!ray_poly_entry<1>(px, py, ex, ey, q.x, q.y, pb, tq, band, 1)) continue;
-                        const double ix = px + tq * (ex - px), iy = py + tq * (ey - py);
-                        const double d = gdist(ix, iy, px, py);
-                        shortest = d < shortest ? d : shortest;
-                    }
-                }
-                if (shortest < INFINITY) dd = shortest;
-            }
-            pre = dd;
-            if (A.radar_mode != AAC_RADAR_DRONES) {
-                // the candidate cells of radar_obstacles' row-mask path (the host guarantees it: row
-                // masks, a box within 8 x 8 cells) and the boundary lines; the cells are clipped in (2)
-                int i0 = (int)floor((fmin(px, ex) - 5.0 - A.gx0) * 0.1), i1 = (int)ceil((fmax(px, ex) + 5.0 - A.gx0) * 0.1);
-                int j0 = (int)floor((fmin(py, ey) - 5.0 - A.gy0) * 0.1), j1 = (int)ceil((fmax(py, ey) + 5.0 - A.gy0) * 0.1);
-                i0 = i0 < 0 ? 0 : i0;
-                j0 = j0 < 0 ? 0 : j0;
-                i1 = i1 > A.gw - 1 ? A.gw - 1 : i1;
-                j1 = j1 > A.gh - 1 ? A.gh - 1 : j1;
-                const double ddx = ex - px, ddy = ey - py;
-                const double L2 = ddx * ddx + ddy * ddy;
-                const double reach = 5.0 * (fabs(ddx) + fabs(ddy)) * (1.0 + 1e-9) + 1e-12;
-                if (i1 >= i0 && j1 >= j0) {
-                    const unsigned long long span = (2ull << (j1 - j0)) - 1;
-                    for (int di = 0; di <= i1 - i0; ++di) {
-                        unsigned long long row = (rows[i0 + di] >> j0) & span;
-                        const double wx = A.gx0 + 10.0 * (i0 + di) - px;
-                        while (row) {
-                            const int b = __builtin_ctzll(row);
-                            row &= row - 1;
-                            const double wy = A.gy0 + 10.0 * (j0 + b) - py;
-                            const double cr = wx * ddy - wy * ddx, al = wx * ddx + wy * ddy;
-                            if (fabs(cr) <= reach && al >= -reach && al <= L2 + reach) cnd |= 1ull << (di * 8 + b);
-                        }
-                    }
-                    ij = (i0 << 16) | j0;
-                }
-                double mind = len, d;
-                if (ray_vline(px, py, ex, ey, A.bound[0], d) && d < mind) mind = d;
-                if (ray_vline(px, py, ex, ey, A.bound[1], d) && d < mind) mind = d;
-                if (ray_hline(px, py, ex, ey, A.bound[2], d) && d < mind) mind = d;
-                if (ray_hline(px, py, ex, ey, A.bound[3], d) && d < mind) mind = d;
-                pre = A.radar_mode == AAC_RADAR_OBSTACLES ? mind : (dd < mind ? dd : mind);
-            }
-        }
-        W.key[w] = dkey(pre);
-        W.cand[w] = cnd;
-        W.ij[w] = ij;
-        cnt[k] = __popcll(cnd);
-        if (band) atomicOr(&W.band[w >> 5], 1u << (w & 31));
-    }
-    aacw::lds_barrier();
-    // (1b) exclusive prefix of the counts in item order (items t, then 256 + t)
-    int run = 0;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        int x = cnt[k];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) W.wtot[wv] = x;
-        aacw::lds_barrier();
-        int off = run;
-#pragma unroll
-        for (int q = 0; q < BLOCK / 64; ++q) off += q < wv ? W.wtot[q] : 0;
-        int tot = 0;
-#pragma unroll
-        for (int q = 0; q < BLOCK / 64; ++q) tot += W.wtot[q];
-        const int w = t + k * BLOCK;
-        if (w < WL_ITEMS) W.pre[w] = (int16_t)(off + x - cnt[k]);
-        run += tot;
-        aacw::lds_barrier();
-    }
-    if (t == 0) W.pre[WL_ITEMS] = (int16_t)run;
-    aacw::lds_barrier();
-    // (2) the workgroup's candidate cells, clipped in one list
-    const int total = run;
-    for (int c = t; c < total; c += BLOCK) {
-        int lo = 0, hi = WL_ITEMS - 1;       // the item: the last with pre[w] <= c
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (W.pre[mid] <= c) lo = mid;
-            else hi = mid - 1;
-        }
-        const int w = lo;
-        const int b = select_bit(W.cand[w], c - W.pre[w]);
-        int le, i, r;
-        double px, py, ex, ey;
-        wl_ray(A, S, w, le, i, r, px, py, ex, ey);
-        const int ij = W.ij[w];
-        const double qx = A.gx0 + 10.0 * ((ij >> 16) + (b >> 3)), qy = A.gy0 + 10.0 * ((ij & 0xffff) + (b & 7));
-        bool band = false;
-        double d;
-        if (ray_square<1>(px, py, ex, ey, qx - 5.0, qx + 5.0, qy - 5.0, qy + 5.0, d, band, 1))
-            atomicMin(&W.key[w], dkey(d));
-        if (band) atomicOr(&W.band[w >> 5], 1u << (w & 31));
-    }
-    aacw::lds_barrier();
-    // (3) outputs, and the flagged rays into the band list (as radar_phase)
-    uint32_t flagged = 0;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int w = t + k * BLOCK;
-        if (w >= nitems) continue;
-        const int la = w / NRAY, r = w - la * NRAY;
-        const int le = la / A.N, i = la - le * A.N;
-        const int e = e0 + le;
-        if (e >= A.E) continue;
-        radar_out(A, S, e, i, r, la, false, ro, dfromkey(W.key[w]));
-        if ((W.band[w >> 5] >> (w & 31)) & 1u) flagged |= 1u << k;
-    }
-    aacw::lds_barrier();      // the agent phase stages its observation rows over the lists
-    while (flagged && A.band_cnt) {
-        const int w = t + __builtin_ctz(flagged) * BLOCK;
-        flagged &= flagged - 1;
-        const int la = w / NRAY, r = w - la * NRAY;
-        const int le = la / A.N, i = la - le * A.N;
-        const int e = e0 + le;
-        const int slot = atomicAdd(A.band_cnt, 1);
-        if (slot >= A.band_cap) continue;
-        int64_t row = -1;
-        if (ro.ring) {
-            row = ro.pos + e;
-            if (row >= ro.cap) row -= ro.cap;
-        }
-        A.band_hdr[slot] = BandHdr{e, i, r, 0, A.map_idx ? A.map_idx[e] : 0, 0, row};
-        for (int j = 0; j < A.N; ++j) A.band_pos[(size_t)slot * A.N + j] = S.pos[le * A.N + j];
-    }
-}
-
 #ifndef AAC_ENV_AGENT_STAMPS
 #define ASTAMP(k) \
     do {          \
@@ -1429,7 +1175,7 @@ __device__ __attribute__((always_inline)) void band_fix_body(const FixArgs &F) {
 
 __global__ void __launch_bounds__(256) band_fix_kernel(FixArgs F) { band_fix_body(F); }
 
-template <int VAR, int RM, bool TAIL, bool WLR = false>
+template <int VAR, int RM, bool TAIL>
 __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain, const float2 *__restrict__ act,
                                                                          ResetArgs R, Tail T) {
     Args A = Ain;
@@ -1540,8 +1286,7 @@ __global__ void __launch_bounds__(BLOCK, AAC_ENV_MIN_WAVES) step_kernel(Args Ain
     aacw::lds_barrier();
     ESTAMP(2, __builtin_amdgcn_s_memtime());
 #ifndef AAC_DBG_SKIP_RADAR      // timing experiments only (a round-3 probe script, in the git history)
-    if constexpr (VAR == 0 && WLR) radar_phase_wl(A, S, e0, nag, ro);
-    else radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro);
+    radar_phase(A, S, e0, nag, false, nullptr, A.variant != 0, ro);
 #endif
     if (A.variant) {
         double2 *wc = wp_cache(A);
@@ -1975,12 +1720,6 @@ static void launch_band_fix(const aac_env *h, const Args &A, hipStream_t st, con
     hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, fix_args(h, A, env_done, ring, rw, col, rcol));
 }
 
-// AAC_ENV_RADAR_WL=0: the per-item radar phase everywhere (A/B of radar_phase_wl)
-static int g_radar_wl = [] {
-    const char *v = getenv("AAC_ENV_RADAR_WL");
-    return v ? atoi(v) : AAC_ENV_RADAR_WL;
-}();
-
 static ResetArgs bank_reset_args(const aac_env *h) {
     ResetArgs R{};
     R.mode = 1;
@@ -2111,24 +1850,15 @@ static int launch_step(aac_env *h, const float *actions, const aac_step_out *o, 
     const float2 *a2 = reinterpret_cast<const float2 *>(actions);
     FixArgs F = tail ? fix_args(h, A, T.reset ? o->env_done : nullptr, T.ring, T.rw, T.late[LATE_RADAR], T.late[LATE_REW])
                      : fix_args(h, A);
-#define STEP_LAUNCH(V, M, WL)                                                                                    \
+#define STEP_LAUNCH(V, M)                                                                                        \
     do {                                                                                                         \
-        if (tail) hipLaunchKernelGGL((step_kernel<V, M, true, WL>), grid, block, lds, st, A, a2, R, T);          \
-        else hipLaunchKernelGGL((step_kernel<V, M, false, WL>), grid, block, lds, st, A, a2, R, T);              \
+        if (tail) hipLaunchKernelGGL((step_kernel<V, M, true>), grid, block, lds, st, A, a2, R, T);              \
+        else hipLaunchKernelGGL((step_kernel<V, M, false>), grid, block, lds, st, A, a2, R, T);                  \
     } while (0)
-    // the work-list radar (radar_phase_wl): the items fit its lists, the map has row masks, the radar's
-    // box stays within 8 x 8 cells (i1 - i0 <= radar_len / 10 + 3), the lists leave the tail's column
-    // table alone
-    const bool wl = g_radar_wl && !A.variant && A.radar_mode != AAC_RADAR_DRONES && h->occ_rows &&
-                    h->epb * h->cfg.N * NRAY <= WL_ITEMS && A.radar_len <= 40.0 &&
-                    (!tail || !T.ring || (size_t)T.tab_off * sizeof(float) >= sizeof(WlLds));
-    if (A.variant) STEP_LAUNCH(1, AAC_RADAR_OBSTACLES, false);
-    else if (A.radar_mode == AAC_RADAR_DRONES) STEP_LAUNCH(0, AAC_RADAR_DRONES, false);
-    else if (A.radar_mode == AAC_RADAR_OBSTACLES) {
-        if (wl) STEP_LAUNCH(0, AAC_RADAR_OBSTACLES, true);
-        else STEP_LAUNCH(0, AAC_RADAR_OBSTACLES, false);
-    } else if (wl) STEP_LAUNCH(0, AAC_RADAR_COMBINED, true);
-    else STEP_LAUNCH(0, AAC_RADAR_COMBINED, false);
+    if (A.variant) STEP_LAUNCH(1, AAC_RADAR_OBSTACLES);
+    else if (A.radar_mode == AAC_RADAR_DRONES) STEP_LAUNCH(0, AAC_RADAR_DRONES);
+    else if (A.radar_mode == AAC_RADAR_OBSTACLES) STEP_LAUNCH(0, AAC_RADAR_OBSTACLES);
+    else STEP_LAUNCH(0, AAC_RADAR_COMBINED);
 #undef STEP_LAUNCH
     hipLaunchKernelGGL(band_fix_kernel, dim3(1), dim3(256), 0, st, F);
     HIPCHK(hipGetLastError());
@@ -2316,8 +2046,6 @@ int aac_env_auto_reset(aac_env *h, const uint8_t *env_done, const aac_step_out *
 }
 
 void aac_env_set_reset_compact(int32_t on) { g_env_compact = on < 0 ? -1 : (on != 0); }
-
-void aac_env_set_radar_work_list(int32_t on) { g_radar_wl = on != 0; }
 
 int aac_env_stamps(unsigned long long *out, int32_t n_wg) {
 #ifdef AAC_ENV_STAMPS

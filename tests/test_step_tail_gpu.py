@@ -83,47 +83,6 @@ def test_step_tail_equals_separate_launches(native_lib, occ, variant, N, E, rada
     assert ra.size == cap and ra.pos == (14 * E) % cap
 
 
-@pytest.mark.parametrize("radar,N,E,maps", [("combined", 5, 4096, 1), ("obstacles", 5, 1001, 1), ("combined", 3, 777, 2),
-                                              ("combined", 4, 600, 1)])
-def test_radar_work_list_bit_exact(native_lib, occ, radar, N, E, maps):
-    """The variant-0 step's work-list radar (radar_phase_wl: every item's candidate cells clipped as one
-    workgroup-wide list, aac_env_set_radar_work_list(1), the default) against the per-item radar phase
-    (0): every output, the state and every ring row bit-identical over steps with resets (config 3's
-    shape first, ragged last workgroups, a map stack), with the ring's late radar column written by
-    either."""
-    from multi_agent_aac_amd import _native
-    from multi_agent_aac_amd.memory import DeviceReplay
-    L = _native.lib()
-    ea, eb = _pair(E, N, occ, "att", radar, maps, 6)
-    cap = 3 * E
-    ra = DeviceReplay(cap, N, ea.D0, seed=1)
-    rb = DeviceReplay(cap, N, eb.D0, seed=1)
-    bufs = [[e.alloc_buffers(), e.alloc_buffers()] for e in (ea, eb)]
-    ea.auto_reset(None, out=bufs[0][0])
-    eb.auto_reset(None, out=bufs[1][0])
-    rng = np.random.default_rng(5)
-    try:
-        for t in range(10):
-            act = torch.from_numpy(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)).cuda()
-            k = t % 2
-            outs = []
-            for on, env, rep, b in ((1, ea, ra, bufs[0]), (0, eb, rb, bufs[1])):
-                L.aac_env_set_radar_work_list(on)
-                c, n = b[k], b[1 - k]
-                env.step_tail(act, out=n, replay=rep, srcs=[c.own, c.radar, c.nei, act, n.reward, n.done, n.own,
-                                                            n.radar, n.nei])
-                torch.cuda.synchronize()
-                outs.append(n)
-            na, nb = outs
-            for f in ("own", "radar", "nei", "reward", "done", "mask", "env_done", "bbc"):
-                assert torch.equal(getattr(na, f), getattr(nb, f)), (t, f)
-            sa, sb = ea.get_state(), eb.get_state()
-            assert all(torch.equal(sa[key], sb[key]) for key in sa), t
-            assert torch.equal(ra.ring, rb.ring), t
-    finally:
-        L.aac_env_set_radar_work_list(1)
-
-
 def test_step_tail_without_push_or_reset(native_lib, occ):
     """Each part is optional: no ring and no reset is the plain step; reset without a push is step +
     auto-reset."""
