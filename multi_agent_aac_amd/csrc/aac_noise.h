@@ -33,6 +33,24 @@ __device__ inline uint64_t take_epoch(uint64_t *word) {
     return ep;
 }
 
+// The same counter with the arrival moved to the end of the launch, off the start of its chain:
+// every thread reads the epoch with one load (the word holds epoch | 0 between launches), and
+// end_epoch -- reached by every workgroup after its last use of the epoch -- counts the arrival;
+// the last workgroup stores epoch + 1.  Every workgroup has read the epoch before it arrives, so
+// none reads the advanced word.  The counter's sequence is take_epoch's.
+__device__ inline uint64_t read_epoch(const uint64_t *word) {
+    return __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffull;
+}
+
+__device__ inline void end_epoch(uint64_t *word, uint64_t ep) {
+    __syncthreads();      // (its fence completes this workgroup's reads of the word)
+    if (threadIdx.x == 0) {
+        const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long *>(word), 1ull << 32);
+        if ((old >> 32) == (uint64_t)(gridDim.x * gridDim.y * gridDim.z) - 1)
+            atomicExch(reinterpret_cast<unsigned long long *>(word), (unsigned long long)((ep + 1) & 0xffffffffull));
+    }
+}
+
 // the exploration noise of agent row `row` (env row / N): var from the env's episode (linear
 // schedule to eps_end, then noise_end), Box-Muller pair from the hash of (seed, epoch, row)
 __device__ __forceinline__ void row_noise(int64_t row, int N, const int32_t *episode, int eps_end, float noise_start,

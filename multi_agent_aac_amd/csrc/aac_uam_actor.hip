@@ -216,7 +216,13 @@ __device__ __forceinline__ double row_noise(const ActorArgs &A, int r, uint64_t 
 #else
 #define UACT_BARRIER() __syncthreads()
 #endif
-constexpr int NBN = 8;       // blocks per workgroup whose noise is drawn up front (config 5: 8 per workgroup)
+// AAC_UAM_ACT_EPOCH_END: the noise epoch read with one load at the start and the launch's arrival
+// counted at its end (aacn::read_epoch / end_epoch) instead of an atomic round trip before the
+// first block (aacn::take_epoch); the same counter sequence
+#ifndef AAC_UAM_ACT_EPOCH_END
+#define AAC_UAM_ACT_EPOCH_END 1
+#endif
+constexpr int NBN = 8;      // blocks per workgroup whose noise is drawn up front (config 5: 8 per workgroup)
 
 template <int NT>
 __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
@@ -257,7 +263,7 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
     }
     const double b40 = A.b4[0], b41 = A.b4[1];
     // the launch's noise epoch (one atomic per workgroup), after the weight loads are in flight
-    const uint64_t ctr = A.noisy ? aacn::take_epoch(A.counter) : 0;
+    const uint64_t ctr = !A.noisy ? 0 : (AAC_UAM_ACT_EPOCH_END ? aacn::read_epoch(A.counter) : aacn::take_epoch(A.counter));
     const int nblk = (A.R + ROWS - 1) / ROWS;
     auto load_rows = [&](int blk, double (&bo)[NT][2], double (&br)[NT][5]) {
         const int r0 = blk * ROWS;
@@ -390,6 +396,7 @@ __global__ void __launch_bounds__(256) uam_actor_ws_kernel(ActorArgs A) {
             }
         }
     }
+    if (AAC_UAM_ACT_EPOCH_END && A.noisy) aacn::end_epoch(A.counter, ctr);
 }
 
 }  // namespace

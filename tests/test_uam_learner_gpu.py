@@ -183,6 +183,42 @@ def test_act_and_noise_schedule(native_lib):
     assert int(m.noise_counter.item()) == 3
 
 
+def _mix64(x):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def test_actor_noise_epoch_per_launch(native_lib):
+    """The config-5 act launch (8192 envs x 16 aircraft: 256 workgroups) over several noisy calls:
+    every row's noise is the Box-Muller pair of hash(seed, epoch, row) with the launch's epoch (one
+    per call, whichever workgroup reads it), the counter advances by exactly one per launch with the
+    arrival field back at 0 -- restated here in numpy for a sample of rows, 1e-12."""
+    m, _ = _model()
+    E, N = 8192, 16
+    g = torch.Generator(device=DEV).manual_seed(5)
+    own = torch.rand(E, N, 7, dtype=torch.float64, device=DEV, generator=g) * 2 - 1
+    radar = torch.rand(E, N, 18, dtype=torch.float64, device=DEV, generator=g) * 5
+    ep = torch.randint(1, 12000, (E,), dtype=torch.int32, device=DEV, generator=g)
+    plain = m.act(own, radar, ep, noisy=False).view(-1, 2).cpu().numpy()
+    rows = np.unique(np.concatenate([np.arange(0, E * N, 61), np.arange(E * N - 64, E * N)])).astype(np.uint64)
+    epn = ep.cpu().numpy()[(rows // N).astype(np.int64)].astype(np.float64)
+    var = np.where(epn <= 10000, 1.0 + (0.0 - 1.0) / 9999.0 * (epn - 1), 0.0)
+    with np.errstate(over="ignore"):
+        for k in range(4):
+            out = m.act(own, radar, ep, noisy=True).view(-1, 2).cpu().numpy()
+            assert int(m.noise_counter.item()) == k + 1
+            h1 = _mix64(_mix64(_mix64(np.uint64(m.noise_seed)) ^ np.uint64(k)) ^ (np.uint64(2) * rows))
+            h2 = _mix64(h1 ^ np.uint64(0xD1B54A32D192ED03))
+            u1 = ((h1 >> np.uint64(11)).astype(np.float64) + 1.0) * (1.0 / 9007199254740992.0)
+            u2 = (h2 >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+            rr = np.sqrt(-2.0 * np.log(u1))
+            want = np.stack([rr * np.cos(6.283185307179586 * u2) * var, rr * np.sin(6.283185307179586 * u2) * var], 1)
+            want = np.clip(plain[rows.astype(np.int64)] + want, -1.0, 1.0)
+            np.testing.assert_allclose(out[rows.astype(np.int64)], want, rtol=0, atol=1e-12)
+
+
 @pytest.mark.parametrize("R", [1, 15, 16, 17, 1000, 131072])
 def test_actor_kernel_rows(native_lib, R):
     """aac_uam_actor over ragged row counts (partial 16-row blocks, one row, the config-5 size)
