@@ -86,6 +86,60 @@ def test_replay_push_gather_sample(native_lib):
     assert torch.equal(first, rep.batch_buffers(512)[0])
 
 
+def _mix64(x):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def _draw_rounds(seed, ctr, block, B, size):
+    """The redraw sampler of aac_replay_sample (size >= 2B) restated: B draws of hash(seed, epoch,
+    workgroup, index, attempt) mod size; every round the least index holding a value keeps it and
+    the others draw again with the next attempt, until the B values are distinct."""
+    idx = np.arange(B, dtype=np.uint64)
+    att = np.zeros(B, dtype=np.uint64)
+    base = _mix64(_mix64(np.uint64(seed)) ^ np.uint64(ctr))
+
+    def draw(i, a):
+        key = (np.uint64(block) << np.uint64(44)) | (i << np.uint64(20)) | a
+        return (_mix64(base ^ key) % np.uint64(size)).astype(np.int64)
+
+    val = draw(idx, att)
+    for _ in range(64):
+        order = np.lexsort((np.arange(B), val))          # by value, then index
+        first = np.ones(B, dtype=bool)
+        first[1:] = val[order][1:] != val[order][:-1]
+        lose = np.zeros(B, dtype=bool)
+        lose[order[~first]] = True
+        if not lose.any():
+            break
+        att[lose] += np.uint64(1)
+        val[lose] = draw(idx[lose], att[lose])
+    return val
+
+
+@pytest.mark.parametrize("B,size,nb", [(1024, 2048, 1), (1024, 3000, 1), (1024, 200000, 2), (512, 1000000, 1),
+                                       (4096, 8192, 1), (100, 250, 3)])
+def test_sampler_rows_match_restatement(native_lib, B, size, nb):
+    """aac_replay_sample's rows against the numpy restatement of its draw, bit for bit, over several
+    epochs (the counter advancing once per launch) and batches (one workgroup each); ring sizes from
+    2B (many redraw rounds) up."""
+    from multi_agent_aac_amd import ops
+    meta = torch.tensor([0, size], dtype=torch.int64, device=DEV)
+    counter = torch.zeros(1, dtype=torch.int64, device=DEV)
+    idx = torch.zeros(nb * B, dtype=torch.int32, device=DEV)
+    with np.errstate(over="ignore"):
+        for ctr in range(3):
+            ops.replay_sample(meta, B, 12345, counter, idx)
+            got = idx.cpu().numpy().reshape(nb, B)
+            assert int(counter.item()) == ctr + 1
+            for blk in range(nb):
+                want = _draw_rounds(12345, ctr, blk, B, size)
+                assert np.array_equal(got[blk], want), (ctr, blk)
+                assert len(np.unique(got[blk])) == B
+
+
 @pytest.mark.parametrize("extra", [0, 1, 7, 1023, 1024])
 def test_sampler_distinct_on_small_ring(native_lib, extra):
     """size = B + extra rows (the first updates after the len(memory) > B guard): every batch holds
