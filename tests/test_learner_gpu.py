@@ -219,6 +219,39 @@ def test_noise_clamp_schedule(native_lib):
     assert act.abs().max() == 0
 
 
+def test_noise_rows_match_restatement(native_lib):
+    """aac_noise_clamp's per-row noise (choose_action's N(0, var^2), ATT/maddpg:476-500) against the
+    numpy restatement of aacn::row_noise: the Box-Muller pair of hash(seed, epoch, row) in float64,
+    var from each env's episode on the linear schedule, rounded to float32; every row of 3 launches
+    with ragged episodes (both sides of eps_end), 1 float32 ulp."""
+    from multi_agent_aac_amd import ops
+    E, N, eps_end, seed = 3001, 5, 8000, 99
+    g = torch.Generator(device=DEV).manual_seed(4)
+    ep = torch.randint(1, 9000, (E,), dtype=torch.int32, device=DEV, generator=g)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    noise = torch.empty(E, N, 2, device=DEV)
+    rows = np.arange(E * N, dtype=np.uint64)
+    epn = ep.cpu().numpy()[(rows // N).astype(np.int64)].astype(np.float64)
+    ns, ne = float(np.float32(1.0)), float(np.float32(0.05))
+    var = np.where(epn <= eps_end, ns + (ne - ns) / (eps_end - 1) * (epn - 1), ne)
+    with np.errstate(over="ignore"):
+        for k in range(3):
+            act = torch.rand(E, N, 2, device=DEV, generator=g) * 2 - 1
+            a0 = act.cpu().numpy().reshape(-1, 2)
+            ops.noise_clamp(act, ep, eps_end, 1.0, seed, ctr, noise, noise_end=0.05)
+            assert int(ctr.item()) == k + 1
+            h1 = _mix64(_mix64(_mix64(np.uint64(seed)) ^ np.uint64(k)) ^ (np.uint64(2) * rows))
+            h2 = _mix64(h1 ^ np.uint64(0xD1B54A32D192ED03))
+            u1 = ((h1 >> np.uint64(11)).astype(np.float64) + 1.0) * (1.0 / 9007199254740992.0)
+            u2 = (h2 >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+            rr = np.sqrt(-2.0 * np.log(u1))
+            want = np.stack([rr * np.cos(6.283185307179586 * u2) * var,
+                             rr * np.sin(6.283185307179586 * u2) * var], 1).astype(np.float32)
+            got = noise.cpu().numpy().reshape(-1, 2)
+            np.testing.assert_array_max_ulp(got, want, maxulp=1)
+            np.testing.assert_array_equal(act.cpu().numpy().reshape(-1, 2), np.clip(a0 + got, -1, 1))
+
+
 @pytest.mark.parametrize("N,B", [(3, 64), (5, 256)])
 def test_update_matches_cpu_restatement(native_lib, N, B):
     from multi_agent_aac_amd.maddpg import MADDPG
